@@ -1,0 +1,281 @@
+// irt_common.h -- numerics shared by the host build (g++) and the gfx950 kernels (hipcc).
+//
+// Everything here is pure IEEE-754 single-precision arithmetic (+ - * / sqrt, compares,
+// integer ops), which gfx950 and x86-64 SSE evaluate identically when compiled with
+// -ffp-contract=off and correctly rounded f32 divide/sqrt (hipcc's default).  That is what
+// makes the MI355X path bit-exact against the reference's CPU build: the reference calls
+// glibc's asinf/atan2f/logf/powf, so this header restates glibc's (fdlibm-derived)
+// algorithms where a device version is needed, and the host tabulates the rest
+// (logf over the 2^24 values 1-k/2^24 it can ever see; the sRGB byte thresholds).
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define IRT_HD __host__ __device__ __forceinline__
+#else
+#include <string.h>
+#define IRT_HD inline
+#endif
+
+namespace irt {
+
+// Bit casts.
+IRT_HD uint32_t f2u(float f) {
+#if defined(__HIPCC__)
+  return __builtin_bit_cast(uint32_t, f);
+#else
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return u;
+#endif
+}
+IRT_HD float u2f(uint32_t u) {
+#if defined(__HIPCC__)
+  return __builtin_bit_cast(float, u);
+#else
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+#endif
+}
+
+// float -> int with x86-64 cvttss2si semantics (the reference's g++ build): truncate
+// toward zero; NaN or out of int range -> INT_MIN.  (gfx950 v_cvt_i32_f32 saturates and
+// maps NaN to 0, so the conversion must be spelled out.)
+IRT_HD int f2i_x86(float f) {
+  if (!(f > -2147483904.0f && f < 2147483648.0f)) return (int)0x80000000u;
+  return (int)f;
+}
+
+// LCG<4> of common/dvr_course-common-both.h:41-86: 4 TEA-like seeding rounds, then
+// state = 1664525*state + 1013904223, sample = (state & 0xFFFFFF) / 2^24.
+IRT_HD uint32_t lcg_seed(uint32_t v0, uint32_t v1) {
+  uint32_t s0 = 0;
+  for (int n = 0; n < 4; n++) {
+    s0 += 0x9e3779b9u;
+    v0 += ((v1 << 4) + 0xa341316cu) ^ (v1 + s0) ^ ((v1 >> 5) + 0xc8013ea4u);
+    v1 += ((v0 << 4) + 0xad90777du) ^ (v0 + s0) ^ ((v0 >> 5) + 0x7e95761eu);
+  }
+  return v0;
+}
+IRT_HD uint32_t lcg_next(uint32_t s) { return 1664525u * s + 1013904223u; }
+IRT_HD float lcg_float(uint32_t s) { return (float)(s & 0x00FFFFFFu) / (float)0x01000000; }
+
+// ---------------------------------------------------------------------------------
+// glibc 2.35 flt-32 asinf / atanf / atan2f (fdlibm lineage: Sun Microsystems 1993,
+// float conversion by Ian Lance Taylor, Cygnus; asinf polynomial by Naohiko Shimizu).
+// Restated for the device so toSpherical() (icon_rt/ICONGrid.h:36-42), which sdda()
+// evaluates per ray segment (ShellAccel.h:134-135), rounds exactly as the reference's
+// glibc calls do.  Verified bit-exact against the host glibc: asinf and atanf over every
+// float, atan2f over 2e8 samples (tests/test_math_restatement.py re-checks a sample).
+
+IRT_HD float glibc_asinf(float x) {
+  const float one = 1.0f, huge = 1.0e30f;
+  const float pio2_hi = 1.57079637050628662109375f;
+  const float pio2_lo = -4.37113900018624283e-8f;
+  const float pio4_hi = 0.785398185253143310546875f;
+  const float p0 = 1.666675248e-1f, p1 = 7.495297643e-2f, p2 = 4.547037598e-2f,
+              p3 = 2.417951451e-2f, p4 = 4.216630880e-2f;
+  float t, w, p, q, c, r, s;
+  const int32_t hx = (int32_t)f2u(x);
+  const int32_t ix = hx & 0x7fffffff;
+  if (ix == 0x3f800000) return x * pio2_hi + x * pio2_lo;
+  if (ix > 0x3f800000) return (x - x) / (x - x);
+  if (ix < 0x3f000000) {
+    if (ix < 0x32000000) {
+      if (huge + x > one) return x;
+    } else {
+      t = x * x;
+      w = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+      return x + x * w;
+    }
+  }
+  w = one - __builtin_fabsf(x);
+  t = w * 0.5f;
+  p = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+  s = __builtin_sqrtf(t);
+  if (ix >= 0x3F79999A) {
+    t = pio2_hi - (2.0f * (s + s * p) - pio2_lo);
+  } else {
+    w = u2f(f2u(s) & 0xfffff000u);
+    c = (t - w * w) / (s + w);
+    r = p;
+    p = 2.0f * s * r - (pio2_lo - 2.0f * c);
+    q = pio4_hi - 2.0f * w;
+    t = pio4_hi - (p - q);
+  }
+  return hx > 0 ? t : -t;
+}
+
+IRT_HD float glibc_atanf(float x) {
+  const float one = 1.0f, huge = 1.0e30f;
+  const float atanhi0 = 4.6364760399e-01f, atanhi1 = 7.8539812565e-01f,
+              atanhi2 = 9.8279368877e-01f, atanhi3 = 1.5707962513e+00f;
+  const float atanlo0 = 5.0121582440e-09f, atanlo1 = 3.7748947079e-08f,
+              atanlo2 = 3.4473217170e-08f, atanlo3 = 7.5497894159e-08f;
+  const float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
+              aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
+              aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
+              aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
+  float w, s1, s2, z, hi, lo;
+  const int32_t hx = (int32_t)f2u(x);
+  const int32_t ix = hx & 0x7fffffff;
+  int id;
+  if (ix >= 0x4c000000) {
+    if (ix > 0x7f800000) return x + x;
+    return hx > 0 ? atanhi3 + atanlo3 : -atanhi3 - atanlo3;
+  }
+  if (ix < 0x3ee00000) {
+    if (ix < 0x31000000) {
+      if (huge + x > one) return x;
+    }
+    id = -1;
+  } else {
+    x = __builtin_fabsf(x);
+    if (ix < 0x3f980000) {
+      if (ix < 0x3f300000) {
+        id = 0;
+        x = (2.0f * x - one) / (2.0f + x);
+      } else {
+        id = 1;
+        x = (x - one) / (x + one);
+      }
+    } else {
+      if (ix < 0x401c0000) {
+        id = 2;
+        x = (x - 1.5f) / (one + 1.5f * x);
+      } else {
+        id = 3;
+        x = -1.0f / x;
+      }
+    }
+  }
+  z = x * x;
+  w = z * z;
+  s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+  s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+  if (id < 0) return x - x * (s1 + s2);
+  hi = id == 0 ? atanhi0 : id == 1 ? atanhi1 : id == 2 ? atanhi2 : atanhi3;
+  lo = id == 0 ? atanlo0 : id == 1 ? atanlo1 : id == 2 ? atanlo2 : atanlo3;
+  z = hi - ((x * (s1 + s2) - lo) - x);
+  return hx < 0 ? -z : z;
+}
+
+IRT_HD float glibc_atan2f(float y, float x) {
+  const float tiny = 1.0e-30f, zero = 0.0f;
+  const float pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f,
+              pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+  float z;
+  const int32_t hx = (int32_t)f2u(x), ix = hx & 0x7fffffff;
+  const int32_t hy = (int32_t)f2u(y), iy = hy & 0x7fffffff;
+  if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+  if (hx == 0x3f800000) return glibc_atanf(y);
+  const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+  if (iy == 0) {
+    switch (m) {
+      case 0:
+      case 1: return y;
+      case 2: return pi + tiny;
+      default: return -pi - tiny;
+    }
+  }
+  if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  if (ix == 0x7f800000) {
+    if (iy == 0x7f800000) {
+      switch (m) {
+        case 0: return pi_o_4 + tiny;
+        case 1: return -pi_o_4 - tiny;
+        case 2: return 3.0f * pi_o_4 + tiny;
+        default: return -3.0f * pi_o_4 - tiny;
+      }
+    }
+    switch (m) {
+      case 0: return zero;
+      case 1: return -zero;
+      case 2: return pi + tiny;
+      default: return -pi - tiny;
+    }
+  }
+  if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  const int32_t k = (iy - ix) >> 23;
+  if (k > 60)
+    z = pi_o_2 + 0.5f * pi_lo;
+  else if (hx < 0 && k < -60)
+    z = 0.0f;
+  else
+    z = glibc_atanf(__builtin_fabsf(y / x));
+  switch (m) {
+    case 0: return z;
+    case 1: return u2f(f2u(z) ^ 0x80000000u);
+    case 2: return pi - (z - pi_lo);
+    default: return (z - pi_lo) - pi;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Cube-map point locator: the MI355X replacement for the OptiX / cuBQL cell location
+// (icon_rt/deviceCode.cu:58-125).  A direction is mapped to one of 6*G*G cells of a
+// gnomonic cube map; each cell lists (conservatively, see host/irt_scene.cpp) every
+// record that can contain a point in that direction, sorted by record index, so the first
+// record passing sample() is the reference's "lowest index wins" answer.
+IRT_HD uint32_t cubemap_cell(float px, float py, float pz, int G) {
+  const float ax = __builtin_fabsf(px), ay = __builtin_fabsf(py), az = __builtin_fabsf(pz);
+  int face;
+  float u, v;
+  if (ax >= ay && ax >= az) {
+    face = px >= 0.f ? 0 : 1;
+    u = py / ax;
+    v = pz / ax;
+  } else if (ay >= az) {
+    face = py >= 0.f ? 2 : 3;
+    u = px / ay;
+    v = pz / ay;
+  } else {
+    face = pz >= 0.f ? 4 : 5;
+    u = px / az;
+    v = py / az;
+  }
+  const float fg = (float)G;
+  int i = (int)((u + 1.f) * 0.5f * fg);
+  int j = (int)((v + 1.f) * 0.5f * fg);
+  // NaN / non-finite directions fall into cell 0 of face 0 after clamping; callers
+  // reject them earlier (a sample point is always finite).
+  i = i < 0 ? 0 : (i >= G ? G - 1 : i);
+  j = j < 0 ? 0 : (j >= G ? G - 1 : j);
+  return (uint32_t)face * (uint32_t)G * (uint32_t)G + (uint32_t)j * (uint32_t)G + (uint32_t)i;
+}
+
+// One candidate-list entry: the record's radial extent (for the cheap first test of
+// sample(), ICONGrid.h:184) and its index.
+struct LocEntry {
+  float h0, hN;
+  uint32_t idx;
+  uint32_t pad;
+};
+
+// Per-record height/value block: 64 floats = 256 B, two 128-B lines.
+//   [0..31]  height[0..31]   (ICONCell::height)
+//   [32..62] value[0..30]    (ICONCell::value; value[31] is never read by the render
+//                             path -- findHeight() < numLayers <= 31 after the radial test)
+//   [63]     numLayers (int bits)
+constexpr int kHV = 64;
+
+// ICONCell::findHeight (ICONGrid.h:117-145): lower_bound over height[1..numLayers].
+IRT_HD int find_height(const float *height, int numLayers, float hpos) {
+  int first = 0, count = numLayers;
+  while (count > 0) {
+    const int step = count / 2;
+    const int it = first + step;
+    if (!(hpos <= height[it + 1])) {
+      first = it + 1;
+      count -= step + 1;
+    } else {
+      count = step;
+    }
+  }
+  return first;
+}
+
+}  // namespace irt

@@ -1,0 +1,385 @@
+// irt_context.hip -- the C ABI of include/icon_rt_hip.h on the HIP runtime: context
+// lifetime, HBM layout, accelerator builds, and frame launches.  Host-side preparation
+// (planes, locator, tables) lives in host/*.cpp (compiled by g++).
+
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <cfloat>
+#include <vector>
+
+#include "irt_internal.h"
+#include "irt_kernels.h"
+
+using namespace irt;
+
+#define IRT_HIP(call)                                                             \
+  do {                                                                            \
+    hipError_t e_ = (call);                                                       \
+    if (e_ != hipSuccess) {                                                       \
+      set_error("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__,  \
+                __LINE__);                                                        \
+      return IRT_E_HIP;                                                           \
+    }                                                                             \
+  } while (0)
+
+struct irt_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  irt_volume_info info{};
+  uint32_t n = 0;
+  int G = 0;
+  // HBM
+  float *d_hv = nullptr;
+  float4 *d_planes = nullptr;
+  uint32_t *d_offsets = nullptr;
+  uint4 *d_entries = nullptr;
+  float *d_logtab = nullptr;
+  float *d_srgb = nullptr;
+  float *d_valueRanges = nullptr;
+  float *d_maxOp = nullptr;
+  size_t numMCs = 0;
+  float4 *d_lut = nullptr;
+  int lutCap = 0;
+  int lutSize = 0;
+  float tfLo = 0.f, tfHi = 1.f, opScale = 1.f;
+  bool tfSet = false;
+  unsigned long long *d_counters = nullptr;
+  unsigned long long *h_counters = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool pending = false;
+  irt_render_stats stats{};
+  size_t bytes = 0;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(irt_context *c, T **p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  IRT_HIP(hipMalloc((void **)p, count * sizeof(T)));
+  c->bytes += count * sizeof(T);
+  return IRT_OK;
+}
+
+template <typename T>
+int upload(irt_context *c, T **p, const T *src, size_t count) {
+  int rc = dalloc(c, p, count);
+  if (rc) return rc;
+  if (count) IRT_HIP(hipMemcpyAsync(*p, src, count * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  return IRT_OK;
+}
+
+void free_all(irt_context *c) {
+  if (c->device >= 0) (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void *ptrs[] = {c->d_hv,     c->d_planes,        c->d_offsets, c->d_entries,
+                  c->d_logtab, c->d_srgb,          c->d_valueRanges, c->d_maxOp,
+                  c->d_lut,    c->d_counters};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  if (c->h_counters) (void)hipHostFree(c->h_counters);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+int finish_stats(irt_context *c) {
+  if (!c->pending) return IRT_OK;
+  IRT_HIP(hipEventSynchronize(c->ev1));
+  float ms = 0.f;
+  IRT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  c->stats.raysLaunched = c->h_counters[0];
+  c->stats.raysInBox = c->h_counters[1];
+  c->stats.locateCalls = c->h_counters[2];
+  c->stats.samplesFound = c->h_counters[3];
+  c->stats.candidatesTested = c->h_counters[4];
+  c->stats.kernelMs = ms;
+  c->pending = false;
+  return IRT_OK;
+}
+
+int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int packed,
+                int tileBegin, int tileStride, uint32_t *fb, irt_vec4f *accum, int *numTilesOut,
+                void *stream) {
+  if (!c || !lp || W <= 0 || H <= 0 || !fb || !accum || tileStride <= 0 || tileBegin < 0) {
+    set_error("irt_render: bad argument");
+    return IRT_E_INVALID;
+  }
+  if (!c->tfSet) {
+    set_error("irt_render: no transfer function set (irt_set_transfunc)");
+    return IRT_E_INVALID;
+  }
+  if (lp->raygen != IRT_RAYGEN_WITH_ACCEL && lp->raygen != IRT_RAYGEN_AE) {
+    set_error("irt_render: unknown raygen %d", lp->raygen);
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  const int tilesX = (W + 63) / 64, tilesY = (H + 63) / 64;
+  const int total = tilesX * tilesY;
+  int numTiles = tileBegin < total ? (total - tileBegin + tileStride - 1) / tileStride : 0;
+  if (numTilesOut) *numTilesOut = numTiles;
+
+  RenderArgs A;
+  memset(&A, 0, sizeof(A));
+  A.org = make_float3(lp->org.x, lp->org.y, lp->org.z);
+  A.dir00 = make_float3(lp->dir_00.x, lp->dir_00.y, lp->dir_00.z);
+  A.du = make_float3(lp->dir_du.x, lp->dir_du.y, lp->dir_du.z);
+  A.dv = make_float3(lp->dir_dv.x, lp->dir_dv.y, lp->dir_dv.z);
+  A.accumID = lp->accumID;
+  A.amb = make_float3(lp->ambientColor.x, lp->ambientColor.y, lp->ambientColor.z);
+  A.ambRad = lp->ambientRadiance;
+  A.unitDistance = lp->unitDistance;
+  A.raygen = lp->raygen;
+  const irt_volume_info &I = c->info;
+  A.bmin = make_float3(I.bounds.lower.x, I.bounds.lower.y, I.bounds.lower.z);
+  A.bmax = make_float3(I.bounds.upper.x, I.bounds.upper.y, I.bounds.upper.z);
+  A.dims = make_int3(I.shellDims[0], I.shellDims[1], I.shellDims[2]);
+  A.sbLo = make_float3(I.sphericalBounds.lower.x, I.sphericalBounds.lower.y, I.sphericalBounds.lower.z);
+  A.sbHi = make_float3(I.sphericalBounds.upper.x, I.sphericalBounds.upper.y, I.sphericalBounds.upper.z);
+  A.maxOp = c->d_maxOp;
+  A.tfLo = c->tfLo;
+  A.tfHi = c->tfHi;
+  A.opacityScale = c->opScale;
+  A.lut = c->d_lut;
+  A.lutSize = c->lutSize;
+  A.numCells = c->n;
+  A.G = c->G;
+  A.offsets = c->d_offsets;
+  A.entries = c->d_entries;
+  A.planes = c->d_planes;
+  A.hv = c->d_hv;
+  A.logtab = c->d_logtab;
+  A.srgbTh = c->d_srgb;
+  A.W = W;
+  A.H = H;
+  A.fb = fb;
+  A.accum = (float4 *)accum;
+  A.packed = packed;
+  A.tileBegin = tileBegin;
+  A.tileStride = tileStride;
+  A.numTiles = numTiles;
+  A.tilesX = tilesX;
+  A.counters = c->d_counters;
+
+  if (c->pending) {
+    int rc = finish_stats(c);
+    if (rc) return rc;
+  }
+  IRT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), s));
+  IRT_HIP(hipEventRecord(c->ev0, s));
+  if (numTiles > 0) launch_render(A, numTiles * 16, s);
+  IRT_HIP(hipGetLastError());
+  IRT_HIP(hipEventRecord(c->ev1, s));
+  IRT_HIP(hipMemcpyAsync(c->h_counters, c->d_counters, 8 * sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost, s));
+  c->pending = true;
+  return IRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_context **out) {
+  if (!out || (numCells && !cells)) {
+    set_error("irt_create: null argument");
+    return IRT_E_INVALID;
+  }
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    set_error("irt_create: no HIP device visible (this product has no CPU fallback)");
+    return IRT_E_HIP;
+  }
+  if (device < 0 || device >= ndev) {
+    set_error("irt_create: device %d out of range (%d devices)", device, ndev);
+    return IRT_E_INVALID;
+  }
+  HostScene S;
+  int rc = build_scene(cells, numCells, S);
+  if (rc) return rc;
+  const std::vector<float> &logtab = logf_table();
+  float th[256];
+  srgb_thresholds(th);
+
+  irt_context *c = new irt_context();
+  c->device = device;
+  auto fail = [&](int code) {
+    free_all(c);
+    delete c;
+    return code;
+  };
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    set_error("irt_create: cannot initialise device %d", device);
+    return fail(IRT_E_HIP);
+  }
+  c->info = S.info;
+  c->n = (uint32_t)S.n;
+  c->G = S.G;
+  if ((rc = upload(c, &c->d_hv, S.hv.data(), S.hv.size()))) return fail(rc);
+  if ((rc = upload(c, &c->d_planes, (const float4 *)S.planes.data(), S.planes.size()))) return fail(rc);
+  if ((rc = upload(c, &c->d_offsets, S.offsets.data(), S.offsets.size()))) return fail(rc);
+  if ((rc = upload(c, &c->d_entries, (const uint4 *)S.entries.data(), S.entries.size()))) return fail(rc);
+  if ((rc = upload(c, &c->d_logtab, logtab.data(), logtab.size()))) return fail(rc);
+  if ((rc = upload(c, &c->d_srgb, th, 256))) return fail(rc);
+  if ((rc = dalloc(c, &c->d_counters, 8))) return fail(rc);
+  if (hipHostMalloc((void **)&c->h_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    set_error("irt_create: event/pinned allocation failed");
+    return fail(IRT_E_HIP);
+  }
+  memset(c->h_counters, 0, 8 * sizeof(unsigned long long));
+
+  // ShellAccel{vec3i(1,1024,1024), sphericalBounds} + initGrid + buildShell_ICON
+  // (hostCode.cu:652-666), majorants zero until a transfer function arrives
+  const int dims[3] = {S.info.shellDims[0], S.info.shellDims[1], S.info.shellDims[2]};
+  c->numMCs = (size_t)dims[0] * dims[1] * dims[2];
+  if ((rc = dalloc(c, &c->d_valueRanges, 2 * c->numMCs))) return fail(rc);
+  if ((rc = dalloc(c, &c->d_maxOp, c->numMCs))) return fail(rc);
+  if (hipMemsetAsync(c->d_maxOp, 0, c->numMCs * sizeof(float), c->stream) != hipSuccess) {
+    set_error("irt_create: memset failed");
+    return fail(IRT_E_HIP);
+  }
+  launch_shell_init(c->d_valueRanges, c->numMCs, c->stream);
+  if (numCells) {
+    irt_icon_cell *d_cells = nullptr;
+    if (hipMalloc((void **)&d_cells, numCells * sizeof(irt_icon_cell)) != hipSuccess ||
+        hipMemcpyAsync(d_cells, cells, numCells * sizeof(irt_icon_cell), hipMemcpyHostToDevice,
+                       c->stream) != hipSuccess) {
+      set_error("irt_create: cell upload failed");
+      if (d_cells) (void)hipFree(d_cells);
+      return fail(IRT_E_HIP);
+    }
+    const irt_box3f &sb = S.info.sphericalBounds;
+    launch_shell_build(d_cells, numCells, make_int3(dims[0], dims[1], dims[2]),
+                       make_float3(sb.lower.x, sb.lower.y, sb.lower.z),
+                       make_float3(sb.upper.x, sb.upper.y, sb.upper.z), c->d_valueRanges, c->stream);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_cells);
+    if (e != hipSuccess || hipGetLastError() != hipSuccess) {
+      set_error("irt_create: shell build failed: %s", hipGetErrorString(e));
+      return fail(IRT_E_HIP);
+    }
+  }
+  if (hipStreamSynchronize(c->stream) != hipSuccess) {
+    set_error("irt_create: upload failed");
+    return fail(IRT_E_HIP);
+  }
+  c->info.deviceBytes = c->bytes;
+  *out = c;
+  return IRT_OK;
+}
+
+void irt_destroy(irt_context *c) {
+  if (!c) return;
+  free_all(c);
+  delete c;
+}
+
+int irt_get_volume_info(const irt_context *c, irt_volume_info *info) {
+  if (!c || !info) {
+    set_error("irt_get_volume_info: null argument");
+    return IRT_E_INVALID;
+  }
+  *info = c->info;
+  return IRT_OK;
+}
+
+int irt_set_transfunc(irt_context *c, const irt_vec4f *lut, int size, irt_box1f valueRange,
+                      float opacityScale) {
+  if (!c || !lut || size <= 0) {
+    set_error("irt_set_transfunc: bad argument");
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(c->device));
+  if (size > c->lutCap) {
+    if (c->d_lut) {
+      IRT_HIP(hipStreamSynchronize(c->stream));
+      IRT_HIP(hipFree(c->d_lut));
+      c->bytes -= c->lutCap * sizeof(float4);
+      c->d_lut = nullptr;
+    }
+    int rc = dalloc(c, &c->d_lut, (size_t)size);
+    if (rc) return rc;
+    c->lutCap = size;
+  }
+  IRT_HIP(hipMemcpyAsync(c->d_lut, lut, size * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  c->lutSize = size;
+  c->tfLo = valueRange.lower;
+  c->tfHi = valueRange.upper;
+  c->opScale = opacityScale;
+  // transfuncUpdateHandler -> computeMaxOpacities (hostCode.cu:878-909); the majorants
+  // ignore opacityScale exactly like the reference kernel (hostCode.cu:362-397)
+  launch_max_opacities(c->d_valueRanges, c->numMCs, c->d_lut, size, valueRange.lower,
+                       valueRange.upper, c->d_maxOp, c->stream);
+  IRT_HIP(hipGetLastError());
+  IRT_HIP(hipStreamSynchronize(c->stream));
+  c->tfSet = true;
+  c->info.deviceBytes = c->bytes;
+  return IRT_OK;
+}
+
+int irt_clear_frame(irt_context *c, uint32_t *fb, irt_vec4f *accum, size_t n, void *stream) {
+  if (!c) {
+    set_error("irt_clear_frame: null context");
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(c->device));
+  launch_clear(fb, (float4 *)accum, n, stream ? (hipStream_t)stream : c->stream);
+  IRT_HIP(hipGetLastError());
+  return IRT_OK;
+}
+
+int irt_render(irt_context *c, const irt_launch_params *lp, int W, int H, uint32_t *fb,
+               irt_vec4f *accum, void *stream) {
+  return render_impl(c, lp, W, H, 0, 0, 1, fb, accum, nullptr, stream);
+}
+
+int irt_render_tiles(irt_context *c, const irt_launch_params *lp, int W, int H, int tileBegin,
+                     int tileStride, uint32_t *fb, irt_vec4f *accum, int *numTiles,
+                     void *stream) {
+  return render_impl(c, lp, W, H, 1, tileBegin, tileStride, fb, accum, numTiles, stream);
+}
+
+int irt_unpack_tiles(irt_context *c, const uint32_t *g, int numRanks, int maxTiles, int W, int H,
+                     uint32_t *fb, void *stream) {
+  if (!c || !g || !fb || numRanks <= 0 || maxTiles < 0 || W <= 0 || H <= 0) {
+    set_error("irt_unpack_tiles: bad argument");
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(c->device));
+  if (maxTiles > 0) launch_unpack(g, numRanks, maxTiles, W, H, fb, stream ? (hipStream_t)stream : c->stream);
+  IRT_HIP(hipGetLastError());
+  return IRT_OK;
+}
+
+int irt_get_render_stats(const irt_context *cc, irt_render_stats *st) {
+  irt_context *c = const_cast<irt_context *>(cc);
+  if (!c || !st) {
+    set_error("irt_get_render_stats: null argument");
+    return IRT_E_INVALID;
+  }
+  int rc = finish_stats(c);
+  if (rc) return rc;
+  *st = c->stats;
+  return IRT_OK;
+}
+
+int irt_get_shell(const irt_context *c, float *valueRanges, float *maxOpacities) {
+  if (!c) {
+    set_error("irt_get_shell: null context");
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(c->device));
+  IRT_HIP(hipStreamSynchronize(c->stream));
+  if (valueRanges)
+    IRT_HIP(hipMemcpy(valueRanges, c->d_valueRanges, 2 * c->numMCs * sizeof(float), hipMemcpyDeviceToHost));
+  if (maxOpacities)
+    IRT_HIP(hipMemcpy(maxOpacities, c->d_maxOp, c->numMCs * sizeof(float), hipMemcpyDeviceToHost));
+  return IRT_OK;
+}
+
+}  // extern "C"

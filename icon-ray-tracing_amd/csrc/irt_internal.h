@@ -1,0 +1,56 @@
+// irt_internal.h -- C++ internals shared by the host build (host/*.cpp, g++) and the HIP
+// runtime layer (csrc/*.hip, hipcc).  No HIP types here.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "icon_rt_hip.h"
+#include "irt_common.h"
+
+namespace irt {
+
+void set_error(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+void clear_error();
+
+struct Plane4 {
+  float x, y, z, w;
+};
+
+// Everything the GPU needs, prepared on the host.
+struct HostScene {
+  size_t n = 0;
+  irt_volume_info info{};
+  std::vector<float> hv;          // n * kHV floats (see irt_common.h)
+  std::vector<Plane4> planes;     // n * 3 side planes of sample() (ICONGrid.h:197-199)
+  int G = 0;                      // cube-map cells per face edge
+  std::vector<uint32_t> offsets;  // 6*G*G + 1 CSR offsets
+  std::vector<LocEntry> entries;  // candidate lists, each sorted by record index
+};
+
+// Validate, compute volume facts, per-record planes/heights, and the locator.
+int build_scene(const irt_icon_cell *cells, size_t n, HostScene &out, int threads = 0);
+
+// Volume facts only (hostCode.cu:792-808, 838-840).
+void compute_volume_info(const irt_icon_cell *cells, size_t n, irt_volume_info &info);
+
+// glibc logf(1 - k/2^24) for k in [0, 2^24): the only arguments woodcockTracking's
+// `logf(1.f - rnd())` (deviceCode.cu:165) can ever see.
+const std::vector<float> &logf_table();
+
+// th[b] (b = 1..255) = smallest float x with make_8bit(linear_to_srgb(x)) >= b, under the
+// host glibc powf (dvr_course-common-both.h:30-35, 89-92); th[0] = -inf.
+void srgb_thresholds(float th[256]);
+
+// Host restatement of the scalar reference functions the kernels rely on, for checks.
+int sample_host(const HostScene &s, uint32_t rec, float px, float py, float pz, float &value);
+// Reference-semantics point location over the locator (host side, for CPU tests).
+int locate_host(const HostScene &s, float px, float py, float pz, float &value,
+                uint32_t *record);
+
+int default_threads();
+
+}  // namespace irt

@@ -1,0 +1,380 @@
+// irt_scene.cpp -- host preparation of the HBM-resident scene for the gfx950 kernels.
+//
+//  1. per record: the three side planes sample() builds on every call
+//     (icon_rt/ICONGrid.h:187-199), computed ONCE here with the same glibc cosf/sinf and
+//     the same float expression order, so the kernel's plane tests are bit-identical to
+//     the reference's -- and the 12 sin/cos per cell test disappear from the hot loop;
+//  2. per record: a 256-B height/value block for findHeight/getValue (ICONGrid.h:117-164);
+//  3. the point locator replacing the reference's cell location (CPU: linear scan,
+//     deviceCode.cu:116-123; GPU: OptiX/cuBQL, 58-115): a gnomonic cube map with G x G
+//     cells per face, each cell listing every record whose column can contain a point of
+//     that direction, sorted by record index.  Conservative by construction:
+//       - the region sample() accepts is {r in [h0,hN]} x the cone of its three side
+//         planes, i.e. the geodesic triangle of the corners (or, for clockwise corners,
+//         its antipode -- handled);
+//       - geodesic triangles are straight-edged under the gnomonic projection, so each is
+//         rasterised per face by a separating-axis test against every grid cell, padded by
+//         1e-5 in face coordinates (~60 m on the Earth; float error of the kernel's
+//         direction->cell mapping and of the plane rounding is < 1e-6);
+//       - triangles with an angular radius > 15 degrees (R1B00/R2B00-class grids) use a
+//         cone-vs-cell test; degenerate records go into every list.
+//     With lists sorted by index, the first list entry passing sample() IS the
+//     reference's "lowest index wins" answer (deviceCode.cu:119-122).
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "irt_internal.h"
+
+namespace irt {
+
+namespace {
+
+struct V3 {
+  float x, y, z;
+};
+inline V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline V3 cross(V3 u, V3 v) {
+  return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+}
+// toCartesian (ICONGrid.h:44-54)
+inline V3 toCartesian(float r, float lat, float lon) {
+  float x = r * cosf(lat) * cosf(lon);
+  float y = r * cosf(lat) * sinf(lon);
+  float z = r * sinf(lat);
+  return {x, y, z};
+}
+// makePlane (ICONGrid.h:170-174)
+inline Plane4 makePlane(V3 a, V3 b, V3 c) {
+  V3 N = cross(b - a, c - a);
+  return {N.x, N.y, N.z, dot(a, N)};
+}
+// evalPlane (ICONGrid.h:176-179)
+inline float evalPlane(const Plane4 &p, float px, float py, float pz) {
+  return (px * p.x + py * p.y + pz * p.z) - p.w;
+}
+
+struct D3 {
+  double x, y, z;
+};
+inline double dotd(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline D3 unitd(D3 a) {
+  double l = sqrt(dotd(a, a));
+  return {a.x / l, a.y / l, a.z / l};
+}
+inline double comp(const D3 &d, int a) { return a == 0 ? d.x : a == 1 ? d.y : d.z; }
+
+constexpr double kPadUV = 1e-5;          // face-coordinate padding
+constexpr double kBigCap = 0.2617993878;  // 15 degrees
+
+// Face f: axis f/2, sign +1 for even f; (u, v) axes as in cubemap_cell (irt_common.h).
+inline void face_axes(int f, int &ax, int &ua, int &va, double &s) {
+  ax = f / 2;
+  s = (f % 2 == 0) ? 1.0 : -1.0;
+  ua = ax == 0 ? 1 : 0;
+  va = ax == 2 ? 1 : 2;
+}
+
+// Direction of the centre / corners of grid cell (i,j) of face f.
+inline D3 face_dir(int f, double u, double v) {
+  int ax, ua, va;
+  double s;
+  face_axes(f, ax, ua, va, s);
+  double c[3];
+  c[ax] = s;
+  c[ua] = u;
+  c[va] = v;
+  return unitd({c[0], c[1], c[2]});
+}
+
+// Triangle (grid coordinates) vs axis-aligned box, separating axis test.
+inline bool tri_box_overlap(const double tx[3], const double ty[3], double bx0, double by0,
+                            double bx1, double by1) {
+  // box axes
+  double mnx = std::min(tx[0], std::min(tx[1], tx[2])), mxx = std::max(tx[0], std::max(tx[1], tx[2]));
+  double mny = std::min(ty[0], std::min(ty[1], ty[2])), mxy = std::max(ty[0], std::max(ty[1], ty[2]));
+  if (mxx < bx0 || mnx > bx1 || mxy < by0 || mny > by1) return false;
+  const double cx = 0.5 * (bx0 + bx1), cy = 0.5 * (by0 + by1);
+  const double hx = 0.5 * (bx1 - bx0), hy = 0.5 * (by1 - by0);
+  for (int k = 0; k < 3; ++k) {
+    const int k1 = (k + 1) % 3;
+    const double nx = -(ty[k1] - ty[k]), ny = tx[k1] - tx[k];
+    double p0 = nx * tx[0] + ny * ty[0], p1 = nx * tx[1] + ny * ty[1], p2 = nx * tx[2] + ny * ty[2];
+    double tmin = std::min(p0, std::min(p1, p2)), tmax = std::max(p0, std::max(p1, p2));
+    double bc = nx * cx + ny * cy, br = hx * fabs(nx) + hy * fabs(ny);
+    if (tmax < bc - br || tmin > bc + br) return false;
+  }
+  return true;
+}
+
+struct Rasterizer {
+  int G;
+  // Append grid cells overlapped by the geodesic triangle with unit corner directions d[3].
+  void triangle(const D3 d[3], std::vector<uint32_t> &cells) const {
+    const D3 c = unitd({d[0].x + d[1].x + d[2].x, d[0].y + d[1].y + d[2].y,
+                        d[0].z + d[1].z + d[2].z});
+    double rho = 0;
+    for (int k = 0; k < 3; ++k) rho = std::max(rho, acos(std::max(-1.0, std::min(1.0, dotd(c, d[k])))));
+    if (!(rho < kBigCap)) {
+      cap(c, rho, cells);
+      return;
+    }
+    const double padG = kPadUV * 0.5 * G;
+    for (int f = 0; f < 6; ++f) {
+      int ax, ua, va;
+      double s;
+      face_axes(f, ax, ua, va, s);
+      double tx[3], ty[3];
+      bool front = true;
+      for (int k = 0; k < 3; ++k) {
+        const double w = s * comp(d[k], ax);
+        if (!(w > 1e-6)) {
+          front = false;
+          break;
+        }
+        tx[k] = (comp(d[k], ua) / w + 1.0) * 0.5 * G;
+        ty[k] = (comp(d[k], va) / w + 1.0) * 0.5 * G;
+      }
+      if (!front) continue;
+      double mnx = std::min(tx[0], std::min(tx[1], tx[2])) - padG;
+      double mxx = std::max(tx[0], std::max(tx[1], tx[2])) + padG;
+      double mny = std::min(ty[0], std::min(ty[1], ty[2])) - padG;
+      double mxy = std::max(ty[0], std::max(ty[1], ty[2])) + padG;
+      int i0 = std::max(0, (int)floor(mnx)), i1 = std::min(G - 1, (int)floor(mxx));
+      int j0 = std::max(0, (int)floor(mny)), j1 = std::min(G - 1, (int)floor(mxy));
+      for (int j = j0; j <= j1; ++j)
+        for (int i = i0; i <= i1; ++i)
+          if (tri_box_overlap(tx, ty, i - padG, j - padG, i + 1 + padG, j + 1 + padG))
+            cells.push_back((uint32_t)f * G * G + (uint32_t)j * G + (uint32_t)i);
+    }
+  }
+  // Cone of half-angle rho around c versus every grid cell's bounding cone.
+  void cap(const D3 &c, double rho, std::vector<uint32_t> &cells) const {
+    const double padA = 3 * kPadUV;
+    for (int f = 0; f < 6; ++f)
+      for (int j = 0; j < G; ++j)
+        for (int i = 0; i < G; ++i) {
+          const double u0 = 2.0 * i / G - 1, u1 = 2.0 * (i + 1) / G - 1;
+          const double v0 = 2.0 * j / G - 1, v1 = 2.0 * (j + 1) / G - 1;
+          const D3 g = face_dir(f, 0.5 * (u0 + u1), 0.5 * (v0 + v1));
+          double delta = 0;
+          const double us[2] = {u0, u1}, vs[2] = {v0, v1};
+          for (double uu : us)
+            for (double vv : vs)
+              delta = std::max(delta, acos(std::max(-1.0, std::min(1.0, dotd(g, face_dir(f, uu, vv))))));
+          const double ang = acos(std::max(-1.0, std::min(1.0, dotd(c, g))));
+          if (ang <= rho + delta + padA) cells.push_back((uint32_t)f * G * G + (uint32_t)j * G + (uint32_t)i);
+        }
+  }
+  void all(std::vector<uint32_t> &cells) const {
+    for (uint32_t k = 0; k < 6u * G * G; ++k) cells.push_back(k);
+  }
+};
+
+inline bool finite_geometry(const irt_icon_cell &c) {
+  for (int k = 0; k < 3; ++k)
+    if (!std::isfinite(c.lat[k]) || !std::isfinite(c.lon[k])) return false;
+  for (int j = 0; j <= c.numLayers; ++j)
+    if (!std::isfinite(c.height[j])) return false;
+  return true;
+}
+
+inline bool same_column(const irt_icon_cell &a, const irt_icon_cell &b) {
+  return memcmp(a.lat, b.lat, sizeof(a.lat)) == 0 && memcmp(a.lon, b.lon, sizeof(a.lon)) == 0;
+}
+
+}  // namespace
+
+int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads) {
+  if (n > 0xFFFFFFF0ull) {
+    set_error("too many cells (%zu)", n);
+    return IRT_E_INVALID;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    if (cells[i].numLayers < 0 || cells[i].numLayers > 31) {
+      set_error("cell %zu: numLayers %d outside [0,31] (MAX_LAYERS 32, ICONGrid.h:57)", i,
+                cells[i].numLayers);
+      return IRT_E_DATA;
+    }
+    if (!finite_geometry(cells[i])) {
+      set_error("cell %zu: non-finite lat/lon/height", i);
+      return IRT_E_DATA;
+    }
+  }
+  if (threads <= 0) threads = default_threads();
+  S = HostScene();
+  S.n = n;
+  compute_volume_info(cells, n, S.info);
+
+  // --- per-record planes and height/value blocks
+  S.hv.assign(n * kHV, 0.f);
+  S.planes.resize(n * 3);
+  {
+    std::vector<std::thread> ts;
+    const size_t chunk = (n + threads - 1) / std::max(threads, 1);
+    for (int t = 0; t < threads; ++t) {
+      const size_t b = t * chunk, e = std::min(n, b + chunk);
+      if (b >= e) break;
+      ts.emplace_back([&, b, e] {
+        for (size_t i = b; i < e; ++i) {
+          const irt_icon_cell &c = cells[i];
+          const float h0 = c.height[0], hN = c.height[c.numLayers];
+          V3 bv[3], tv[3];
+          for (int k = 0; k < 3; ++k) {
+            bv[k] = toCartesian(h0, c.lat[k], c.lon[k]);
+            tv[k] = toCartesian(hN, c.lat[k], c.lon[k]);
+          }
+          S.planes[3 * i + 0] = makePlane(bv[0], bv[1], tv[1]);
+          S.planes[3 * i + 1] = makePlane(bv[1], bv[2], tv[2]);
+          S.planes[3 * i + 2] = makePlane(bv[2], bv[0], tv[0]);
+          float *hv = &S.hv[i * kHV];
+          memcpy(hv, c.height, 32 * sizeof(float));
+          memcpy(hv + 32, c.value, 31 * sizeof(float));
+          int32_t nl = c.numLayers;
+          memcpy(hv + 63, &nl, 4);
+        }
+      });
+    }
+    for (auto &t : ts) t.join();
+  }
+
+  // --- columns: runs of consecutive records with identical corners
+  std::vector<size_t> runStart;
+  for (size_t i = 0; i < n; ++i)
+    if (i == 0 || !same_column(cells[i], cells[i - 1])) runStart.push_back(i);
+  const size_t numRuns = runStart.size();
+  runStart.push_back(n);
+
+  double scale = 1.5;
+  if (const char *e = getenv("IRT_LOCATOR_SCALE")) scale = atof(e);
+  int G = (int)llround(sqrt((double)std::max<size_t>(numRuns, 1) / 6.0) * scale);
+  G = std::max(4, std::min(G, 2048));
+  if (const char *e = getenv("IRT_LOCATOR_G")) G = std::max(1, std::min(4096, atoi(e)));
+  S.G = G;
+  const uint32_t numGridCells = 6u * G * G;
+  Rasterizer R{G};
+
+  // --- rasterise runs in parallel; each thread owns a contiguous range of runs so the
+  //     concatenated (cell, record) pairs stay in record order
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> parts(threads);
+  {
+    std::vector<std::thread> ts;
+    const size_t chunk = (numRuns + threads - 1) / std::max(threads, 1);
+    for (int t = 0; t < threads; ++t) {
+      const size_t b = t * chunk, e = std::min(numRuns, b + chunk);
+      if (b >= e) break;
+      ts.emplace_back([&, t, b, e] {
+        std::vector<uint32_t> gc;
+        auto &out = parts[t];
+        for (size_t r = b; r < e; ++r) {
+          const size_t i0 = runStart[r], i1 = runStart[r + 1];
+          const irt_icon_cell &c = cells[i0];
+          D3 d[3];
+          for (int k = 0; k < 3; ++k) {
+            const double la = c.lat[k], lo = c.lon[k];
+            d[k] = {cos(la) * cos(lo), cos(la) * sin(lo), sin(la)};
+          }
+          // Which cone do the float planes carve out?  Probe the centroid direction
+          // (and its antipode) at the record's mid radius.
+          const D3 cd = unitd({d[0].x + d[1].x + d[2].x, d[0].y + d[1].y + d[2].y,
+                               d[0].z + d[1].z + d[2].z});
+          gc.clear();
+          int mode = 2;  // 0 normal, 1 antipodal, 2 degenerate
+          for (size_t i = i0; i < i1 && mode == 2; ++i) {
+            const irt_icon_cell &ci = cells[i];
+            const double rm = 0.5 * ((double)ci.height[0] + (double)ci.height[ci.numLayers]);
+            for (int sgn = 0; sgn < 2 && mode == 2; ++sgn) {
+              const double s = sgn ? -rm : rm;
+              const float px = (float)(cd.x * s), py = (float)(cd.y * s), pz = (float)(cd.z * s);
+              bool in = true;
+              for (int k = 0; k < 3; ++k)
+                if (evalPlane(S.planes[3 * i + k], px, py, pz) > 0.f) in = false;
+              if (in) mode = sgn;
+            }
+          }
+          if (std::isnan(cd.x) || std::isnan(cd.y) || std::isnan(cd.z)) mode = 2;
+          if (mode == 2) {
+            R.all(gc);
+          } else {
+            D3 dd[3] = {d[0], d[1], d[2]};
+            if (mode == 1)
+              for (auto &q : dd) q = {-q.x, -q.y, -q.z};
+            R.triangle(dd, gc);
+          }
+          std::sort(gc.begin(), gc.end());
+          gc.erase(std::unique(gc.begin(), gc.end()), gc.end());
+          for (size_t i = i0; i < i1; ++i) {
+            const irt_icon_cell &ci = cells[i];
+            if (ci.height[0] > ci.height[ci.numLayers]) continue;  // radial test never passes
+            for (uint32_t g : gc) out.emplace_back(g, (uint32_t)i);
+          }
+        }
+      });
+    }
+    for (auto &t : ts) t.join();
+  }
+
+  // --- stable counting sort by grid cell -> CSR
+  S.offsets.assign(numGridCells + 1, 0);
+  size_t total = 0;
+  for (auto &p : parts) {
+    total += p.size();
+    for (auto &e : p) S.offsets[e.first + 1]++;
+  }
+  for (uint32_t k = 0; k < numGridCells; ++k) S.offsets[k + 1] += S.offsets[k];
+  if (total > 0xFFFFFFF0ull) {
+    set_error("locator too large (%zu entries)", total);
+    return IRT_E_INVALID;
+  }
+  S.entries.resize(total);
+  {
+    std::vector<uint32_t> cursor(S.offsets.begin(), S.offsets.end() - 1);
+    for (auto &p : parts)
+      for (auto &e : p) {
+        const irt_icon_cell &c = cells[e.second];
+        S.entries[cursor[e.first]++] = {c.height[0], c.height[c.numLayers], e.second, 0u};
+      }
+  }
+  S.info.locatorFaceRes = G;
+  S.info.locatorEntries = total;
+  return IRT_OK;
+}
+
+// sample() (ICONGrid.h:181-208) with the precomputed planes; lat/lon of toSpherical are
+// dead in sample() and skipped.
+int sample_host(const HostScene &s, uint32_t rec, float px, float py, float pz, float &value) {
+  const float r = sqrtf(px * px + py * py + pz * pz);
+  const float *hv = &s.hv[(size_t)rec * kHV];
+  int32_t nl;
+  memcpy(&nl, hv + 63, 4);
+  if (r < hv[0] || r > hv[nl]) return 0;
+  for (int k = 0; k < 3; ++k)
+    if (evalPlane(s.planes[3 * (size_t)rec + k], px, py, pz) > 0.f) return 0;
+  value = hv[32 + find_height(hv, nl, r)];
+  return 1;
+}
+
+int locate_host(const HostScene &s, float px, float py, float pz, float &value,
+                uint32_t *record) {
+  if (s.n == 0 || s.G == 0) return 0;
+  const float r = sqrtf(px * px + py * py + pz * pz);
+  const uint32_t cell = cubemap_cell(px, py, pz, s.G);
+  for (uint32_t e = s.offsets[cell]; e < s.offsets[cell + 1]; ++e) {
+    const LocEntry &E = s.entries[e];
+    if (r < E.h0 || r > E.hN) continue;
+    if (sample_host(s, E.idx, px, py, pz, value)) {
+      if (record) *record = E.idx;
+      return 1;
+    }
+  }
+  return 0;
+}
+
+}  // namespace irt

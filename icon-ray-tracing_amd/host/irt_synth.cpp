@@ -1,0 +1,171 @@
+// irt_synth.cpp -- synthetic RnBk icosahedral ICON grids in the `.ic` record format.
+//
+// Real DWD ICON data (netCDF grid + HHL + fields) is not available offline and the
+// reference's converter (tools/convert_icon/convert_icon.cpp) needs netCDF, so benches and
+// tests use this generator.  Construction (deterministic, double precision, then rounded
+// to float like convert_icon.cpp:356-358 does for clat/clon):
+//  - icosahedron from (0,+-1,+-phi) and its cyclic permutations, normalised; faces oriented
+//    counter-clockwise seen from outside (the orientation sample()'s "> 0 => outside"
+//    plane tests expect, ICONGrid.h:201-203);
+//  - root split: every face into rootN^2 triangles on a barycentric lattice, vertices
+//    projected to the unit sphere; then `bisections` rounds of 4-way edge-midpoint
+//    splitting (midpoints normalised).  20*rootN^2*4^bisections triangles (R2B07: 1.31 M);
+//  - corners: lat = asin(z), lon = atan2(y, x) (toSpherical, ICONGrid.h:36-42);
+//  - levels: H_l = R + top*(l/L)^2, R = 6.371229e6 m (convert_icon.cpp:359), HSURF = 0;
+//  - value of layer l of a column with centre c: 0.5 + 0.35 sin(4cx+3cy) cos(5cz)(1-h)
+//    + 0.1 h + noise*(hash(column,l)-0.5), h = (l+0.5)/L, normalised to [0,1] over the
+//    grid (convert_icon.cpp:317-328 normalises its fields the same way);
+//  - records of <= 31 layers (MAX_LAYERS 32, ICONGrid.h:57), bottom to top, consecutive
+//    per column, the layer boundary height shared by neighbouring records
+//    (convert_icon.cpp:362-388).
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "irt_internal.h"
+
+namespace {
+
+struct D3 {
+  double x, y, z;
+};
+inline D3 add(D3 a, D3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline D3 sub(D3 a, D3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline D3 mul(D3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+inline double dotd(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline D3 crossd(D3 u, D3 v) {
+  return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+}
+inline D3 unit(D3 a) { return mul(a, 1.0 / sqrt(dotd(a, a))); }
+
+struct Tri {
+  D3 a, b, c;
+};
+
+void bisect(const Tri &t, int depth, std::vector<Tri> &out) {
+  if (depth == 0) {
+    out.push_back(t);
+    return;
+  }
+  D3 ab = unit(add(t.a, t.b)), bc = unit(add(t.b, t.c)), ca = unit(add(t.c, t.a));
+  bisect({t.a, ab, ca}, depth - 1, out);
+  bisect({ab, t.b, bc}, depth - 1, out);
+  bisect({ca, bc, t.c}, depth - 1, out);
+  bisect({ab, bc, ca}, depth - 1, out);
+}
+
+inline uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+}  // namespace
+
+extern "C" int irt_synth_grid(int rootN, int bisections, int levels, float topHeight,
+                              float noise, uint32_t seed, irt_icon_cell *out, size_t capacity,
+                              size_t *count) {
+  using irt::set_error;
+  if (!count || rootN < 1 || bisections < 0 || bisections > 12 || levels < 1 ||
+      levels > 100000) {
+    set_error("irt_synth_grid: bad argument");
+    return IRT_E_INVALID;
+  }
+  const size_t numTris = 20ull * rootN * rootN * (1ull << (2 * bisections));
+  const int recsPerCol = (levels + 30) / 31;
+  const size_t total = numTris * recsPerCol;
+  *count = total;
+  if (!out) return IRT_OK;
+  if (capacity < total) {
+    set_error("irt_synth_grid: capacity %zu < %zu", capacity, total);
+    return IRT_E_INVALID;
+  }
+
+  const double phi = (1.0 + sqrt(5.0)) / 2.0;
+  const D3 V[12] = {{-1, phi, 0}, {1, phi, 0}, {-1, -phi, 0}, {1, -phi, 0},
+                    {0, -1, phi}, {0, 1, phi}, {0, -1, -phi}, {0, 1, -phi},
+                    {phi, 0, -1}, {phi, 0, 1}, {-phi, 0, -1}, {-phi, 0, 1}};
+  const int F[20][3] = {{0, 11, 5}, {0, 5, 1},  {0, 1, 7},   {0, 7, 10}, {0, 10, 11},
+                        {1, 5, 9},  {5, 11, 4}, {11, 10, 2}, {10, 7, 6}, {7, 1, 8},
+                        {3, 9, 4},  {3, 4, 2},  {3, 2, 6},   {3, 6, 8},  {3, 8, 9},
+                        {4, 9, 5},  {2, 4, 11}, {6, 2, 10},  {8, 6, 7},  {9, 8, 1}};
+  std::vector<Tri> roots;
+  roots.reserve(20 * rootN * rootN);
+  for (int f = 0; f < 20; ++f) {
+    D3 a = unit(V[F[f][0]]), b = unit(V[F[f][1]]), c = unit(V[F[f][2]]);
+    if (dotd(crossd(sub(b, a), sub(c, a)), add(add(a, b), c)) < 0) std::swap(b, c);
+    auto P = [&](int i, int j) {  // barycentric lattice point, on the sphere
+      double s = (double)i / rootN, t = (double)j / rootN;
+      return unit(add(a, add(mul(sub(b, a), s), mul(sub(c, a), t))));
+    };
+    for (int j = 0; j < rootN; ++j)
+      for (int i = 0; i + j < rootN; ++i) {
+        roots.push_back({P(i, j), P(i + 1, j), P(i, j + 1)});
+        if (i + j + 1 < rootN) roots.push_back({P(i + 1, j), P(i + 1, j + 1), P(i, j + 1)});
+      }
+  }
+  std::vector<Tri> tris;
+  tris.reserve(numTris);
+  for (const Tri &t : roots) bisect(t, bisections, tris);
+  if (tris.size() != numTris) {
+    set_error("irt_synth_grid: internal triangle count mismatch");
+    return IRT_E_INVALID;
+  }
+
+  const float R = 6.371229E6f;
+  std::vector<float> H(levels + 1);
+  for (int l = 0; l <= levels; ++l) {
+    double f = (double)l / levels;
+    H[l] = (float)((double)R + (double)topHeight * f * f);
+  }
+
+  // values (double), then normalise to [0,1]
+  std::vector<double> val(numTris * (size_t)levels);
+  double vmin = INFINITY, vmax = -INFINITY;
+  for (size_t t = 0; t < numTris; ++t) {
+    D3 c = unit(add(add(tris[t].a, tris[t].b), tris[t].c));
+    double base = sin(4 * c.x + 3 * c.y) * cos(5 * c.z);
+    for (int l = 0; l < levels; ++l) {
+      double h = (l + 0.5) / levels;
+      double v = 0.5 + 0.35 * base * (1 - h) + 0.1 * h;
+      if (noise != 0.f) {
+        uint32_t k = hash32((uint32_t)t * 2654435761u ^ hash32((uint32_t)l + seed * 97u));
+        v += (double)noise * ((k >> 8) * (1.0 / 16777216.0) - 0.5);
+      }
+      val[t * levels + l] = v;
+      vmin = std::min(vmin, v);
+      vmax = std::max(vmax, v);
+    }
+  }
+  const double vscale = vmax > vmin ? 1.0 / (vmax - vmin) : 0.0;
+
+  size_t r = 0;
+  for (size_t t = 0; t < numTris; ++t) {
+    const D3 cs[3] = {tris[t].a, tris[t].b, tris[t].c};
+    float lat[3], lon[3];
+    for (int k = 0; k < 3; ++k) {
+      double z = std::max(-1.0, std::min(1.0, cs[k].z));
+      lat[k] = (float)asin(z);
+      lon[k] = (float)atan2(cs[k].y, cs[k].x);
+    }
+    for (int rc = 0; rc < recsPerCol; ++rc) {
+      irt_icon_cell &cell = out[r++];
+      memset(&cell, 0, sizeof(cell));
+      memcpy(cell.lat, lat, sizeof(lat));
+      memcpy(cell.lon, lon, sizeof(lon));
+      const int l0 = rc * 31;
+      const int nl = std::min(31, levels - l0);
+      cell.numLayers = nl;
+      for (int j = 0; j <= nl; ++j) cell.height[j] = H[l0 + j];
+      for (int j = 0; j < nl; ++j)
+        cell.value[j] = (float)((val[t * levels + l0 + j] - vmin) * vscale);
+    }
+  }
+  return IRT_OK;
+}

@@ -1,0 +1,388 @@
+"""irt -- Python binding of the MI355X ICON renderer's C ABI (include/icon_rt_hip.h).
+
+Thin ctypes layer over ``icon-ray-tracing_amd/libicon_rt_hip.so`` (built in-tree by
+``make -C icon-ray-tracing_amd``).  It mirrors the host flow of the reference app
+``icon_rt`` (szellmann/icon-ray-tracing, icon_rt/hostCode.cu:703-968): load ``.ic``
+records, lat/lon filter, volume facts, default transfer function, camera, then frame
+launches on the GPU.  There is no CPU fallback: without the library or a HIP device the
+calls raise ``IrtError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libicon_rt_hip.so")
+
+# icon_rt::ICONCell (icon_rt/ICONGrid.h:59-76), 284 bytes, the `.ic` record
+CELL_DTYPE = np.dtype(
+    [("lat", "<f4", (3,)), ("lon", "<f4", (3,)), ("numLayers", "<i4"),
+     ("height", "<f4", (32,)), ("value", "<f4", (32,))], align=False)
+assert CELL_DTYPE.itemsize == 284
+
+RAYGEN_WITH_ACCEL = 0  # woodcockTrackingWithAccel (deviceCode.cu:281-341)
+RAYGEN_AE = 1          # woodcockTrackingAE (deviceCode.cu:239-275)
+
+
+class IrtError(RuntimeError):
+    pass
+
+
+class Vec3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+    def tolist(self):
+        return [self.x, self.y, self.z]
+
+
+class Vec4(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float), ("w", C.c_float)]
+
+
+class Box1(C.Structure):
+    _fields_ = [("lower", C.c_float), ("upper", C.c_float)]
+
+
+class Box3(C.Structure):
+    _fields_ = [("lower", Vec3), ("upper", Vec3)]
+
+
+class LaunchParams(C.Structure):
+    """Per-frame part of icon_rt::LaunchParams (icon_rt/Params.h:92-119)."""
+    _fields_ = [("org", Vec3), ("dir_00", Vec3), ("dir_du", Vec3), ("dir_dv", Vec3),
+                ("accumID", C.c_int32), ("ambientColor", Vec3), ("ambientRadiance", C.c_float),
+                ("unitDistance", C.c_float), ("raygen", C.c_int32)]
+
+    def camera12(self) -> np.ndarray:
+        return np.array(self.org.tolist() + self.dir_00.tolist() + self.dir_du.tolist()
+                        + self.dir_dv.tolist(), dtype=np.float32)
+
+
+class VolumeInfo(C.Structure):
+    _fields_ = [("numCells", C.c_uint64), ("bounds", Box3), ("sphericalBounds", Box3),
+                ("dataRange", Box1), ("unitDistance", C.c_float), ("shellDims", C.c_int32 * 3),
+                ("locatorFaceRes", C.c_int32), ("locatorEntries", C.c_uint64),
+                ("deviceBytes", C.c_uint64)]
+
+
+class RenderStats(C.Structure):
+    _fields_ = [("raysLaunched", C.c_uint64), ("raysInBox", C.c_uint64),
+                ("locateCalls", C.c_uint64), ("samplesFound", C.c_uint64),
+                ("candidatesTested", C.c_uint64), ("kernelMs", C.c_float)]
+
+    def asdict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load the in-tree product library (fails loudly if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise IrtError(f"{LIB_PATH} not built; run `make -C icon-ray-tracing_amd` "
+                           "(or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        P, I, F, S = C.c_void_p, C.c_int, C.c_float, C.c_size_t
+        L.irt_last_error.restype = C.c_char_p
+        sig = {
+            "irt_create": [P, S, I, C.POINTER(P)],
+            "irt_destroy": [P],
+            "irt_get_volume_info": [P, C.POINTER(VolumeInfo)],
+            "irt_set_transfunc": [P, P, I, Box1, F],
+            "irt_clear_frame": [P, P, P, S, P],
+            "irt_render": [P, C.POINTER(LaunchParams), I, I, P, P, P],
+            "irt_render_tiles": [P, C.POINTER(LaunchParams), I, I, I, I, P, P,
+                                 C.POINTER(C.c_int), P],
+            "irt_unpack_tiles": [P, P, I, I, I, I, P, P],
+            "irt_get_render_stats": [P, C.POINTER(RenderStats)],
+            "irt_get_shell": [P, P, P],
+            "irt_num_tiles": [I, I],
+            "irt_load_ic": [C.c_char_p, C.c_long, P, S, C.POINTER(S)],
+            "irt_save_ic": [C.c_char_p, P, S],
+            "irt_filter_cells": [P, S, Box1, Box1, C.POINTER(S)],
+            "irt_compute_volume_info": [P, S, C.POINTER(VolumeInfo)],
+            "irt_default_transfunc": [Box1, P, C.POINTER(Box1)],
+            "irt_resample_lut": [P, I, P, I],
+            "irt_camera_view_all": [Box3, F, I, I, C.POINTER(LaunchParams)],
+            "irt_camera_look_at": [Vec3, Vec3, Vec3, F, I, I, C.POINTER(LaunchParams)],
+            "irt_synth_grid": [I, I, I, F, F, C.c_uint32, P, S, C.POINTER(S)],
+            # host-only inspection (include/icon_rt_hip_debug.h)
+            "irt_debug_asinf": [F],
+            "irt_debug_atan2f": [F, F],
+            "irt_debug_f2i": [F],
+            "irt_debug_logf_entry": [C.c_uint32],
+            "irt_debug_srgb_thresholds": [P],
+            "irt_debug_scene_build": [P, S, C.POINTER(P)],
+            "irt_debug_scene_info": [P, C.POINTER(VolumeInfo)],
+            "irt_debug_scene_locate": [P, Vec3, C.POINTER(C.c_float), C.POINTER(C.c_uint32)],
+            "irt_debug_scene_candidates": [P, Vec3, P, I],
+            "irt_debug_scene_planes": [P, C.c_uint32, P],
+            "irt_debug_scene_free": [P],
+        }
+        for name, args in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            if name not in ("irt_last_error",):
+                fn.restype = C.c_int
+        L.irt_debug_asinf.restype = F
+        L.irt_debug_atan2f.restype = F
+        L.irt_debug_logf_entry.restype = F
+        L.irt_destroy.restype = None
+        L.irt_debug_scene_free.restype = None
+        L.irt_debug_srgb_thresholds.restype = None
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().irt_last_error().decode(errors="replace")
+        raise IrtError(f"{what} failed ({rc}): {msg}")
+
+
+def _ptr(a: np.ndarray) -> C.c_void_p:
+    return C.c_void_p(a.ctypes.data)
+
+
+def vec3(v) -> Vec3:
+    return Vec3(float(v[0]), float(v[1]), float(v[2]))
+
+
+def box1(lo, hi) -> Box1:
+    return Box1(float(lo), float(hi))
+
+
+# ----------------------------------------------------------------------- host helpers
+def synth_grid(root_n: int, bisections: int, levels: int, top_height: float = 75e3,
+               noise: float = 0.0, seed: int = 1234) -> np.ndarray:
+    """Synthetic RnBk ICON grid as `.ic` records (host/irt_synth.cpp)."""
+    n = C.c_size_t()
+    _check(lib().irt_synth_grid(root_n, bisections, levels, top_height, noise, seed, None, 0,
+                                C.byref(n)), "irt_synth_grid")
+    cells = np.zeros(n.value, dtype=CELL_DTYPE)
+    _check(lib().irt_synth_grid(root_n, bisections, levels, top_height, noise, seed,
+                                _ptr(cells), n.value, C.byref(n)), "irt_synth_grid")
+    return cells
+
+
+def load_ic(path: str, max_num_cells: int = -1) -> np.ndarray:
+    n = C.c_size_t()
+    _check(lib().irt_load_ic(path.encode(), max_num_cells, None, 0, C.byref(n)), "irt_load_ic")
+    cells = np.zeros(n.value, dtype=CELL_DTYPE)
+    _check(lib().irt_load_ic(path.encode(), max_num_cells, _ptr(cells), n.value, C.byref(n)),
+           "irt_load_ic")
+    return cells
+
+
+def save_ic(path: str, cells: np.ndarray):
+    cells = np.ascontiguousarray(cells, dtype=CELL_DTYPE)
+    _check(lib().irt_save_ic(path.encode(), _ptr(cells), cells.size), "irt_save_ic")
+
+
+def filter_cells(cells: np.ndarray, lat_range=(-np.inf, np.inf), lon_range=(-np.inf, np.inf)):
+    """--lat-range / --lon-range filter in degrees (hostCode.cu:736-758); returns a copy."""
+    out = np.array(cells, dtype=CELL_DTYPE, copy=True)
+    n = C.c_size_t()
+    _check(lib().irt_filter_cells(_ptr(out), out.size, box1(*lat_range), box1(*lon_range),
+                                  C.byref(n)), "irt_filter_cells")
+    return out[: n.value].copy()
+
+
+def volume_info(cells: np.ndarray) -> VolumeInfo:
+    cells = np.ascontiguousarray(cells, dtype=CELL_DTYPE)
+    info = VolumeInfo()
+    _check(lib().irt_compute_volume_info(_ptr(cells), cells.size, C.byref(info)),
+           "irt_compute_volume_info")
+    return info
+
+
+def default_transfunc(data_range) -> tuple[np.ndarray, tuple[float, float]]:
+    """hostCode.cu:823-836 + Pipeline::setTransfunc resampling (pipeline.cu:469-473)."""
+    lut = np.zeros((300, 4), dtype=np.float32)
+    vr = Box1()
+    _check(lib().irt_default_transfunc(box1(*data_range), _ptr(lut), C.byref(vr)),
+           "irt_default_transfunc")
+    return lut, (vr.lower, vr.upper)
+
+
+def resample_lut(src: np.ndarray, n: int) -> np.ndarray:
+    src = np.ascontiguousarray(src, dtype=np.float32).reshape(-1, 4)
+    dst = np.zeros((n, 4), dtype=np.float32)
+    _check(lib().irt_resample_lut(_ptr(src), src.shape[0], _ptr(dst), n), "irt_resample_lut")
+    return dst
+
+
+def camera_view_all(bounds: Box3, img_w: int, img_h: int, fovy_deg: float = 90.0) -> LaunchParams:
+    lp = LaunchParams()
+    _check(lib().irt_camera_view_all(bounds, fovy_deg, img_w, img_h, C.byref(lp)),
+           "irt_camera_view_all")
+    return lp
+
+
+def camera_look_at(vp, vi, vu, fovy_deg: float, img_w: int, img_h: int) -> LaunchParams:
+    lp = LaunchParams()
+    _check(lib().irt_camera_look_at(vec3(vp), vec3(vi), vec3(vu), fovy_deg, img_w, img_h,
+                                    C.byref(lp)), "irt_camera_look_at")
+    return lp
+
+
+def num_tiles(w: int, h: int) -> int:
+    return lib().irt_num_tiles(w, h)
+
+
+@dataclass
+class FrameSetup:
+    """What icon_rt's main() derives before the first launch (hostCode.cu:736-958)."""
+    lp: LaunchParams
+    lut: np.ndarray
+    value_range: tuple[float, float]
+    opacity_scale: float
+    info: VolumeInfo
+
+
+# The survey's framing camera: --camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60
+FRAMING_CAMERA = ((0.0, 0.0, 1.4e7), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0)
+
+
+def setup_frame(cells: np.ndarray, width: int, height: int, camera=None,
+                camera_div=None, raygen: int = RAYGEN_WITH_ACCEL) -> FrameSetup:
+    """Mirror hostCode.cu main(): volume facts, default TF, unitDistance, camera.
+
+    camera: None -> Camera::viewAll(volbounds) with fovy 90 (hostCode.cu:819-821);
+            (vp, vi, vu, fovyDeg) -> Pipeline --camera/-fovy (pipeline.cu:444-454).
+    camera_div: the image size dir_du/dir_dv are divided by; the reference hard-codes
+            512 (hostCode.cu:815,944-945); default: the real (width, height).
+    """
+    info = volume_info(cells)
+    lut, vr = default_transfunc((info.dataRange.lower, info.dataRange.upper))
+    dw, dh = camera_div if camera_div is not None else (width, height)
+    if camera is None:
+        lp = camera_view_all(info.bounds, dw, dh)
+    else:
+        vp, vi, vu, fovy = camera
+        lp = camera_look_at(vp, vi, vu, fovy, dw, dh)
+    lp.accumID = 0
+    lp.ambientColor = Vec3(1.0, 1.0, 1.0)
+    lp.ambientRadiance = 1.0
+    lp.unitDistance = info.unitDistance
+    lp.raygen = raygen
+    return FrameSetup(lp=lp, lut=lut, value_range=vr, opacity_scale=1.0, info=info)
+
+
+# ----------------------------------------------------------------------- GPU context
+class Context:
+    """One renderer context on one HIP device (irt_create ... irt_destroy)."""
+
+    def __init__(self, cells: np.ndarray, device: int = 0):
+        cells = np.ascontiguousarray(cells, dtype=CELL_DTYPE)
+        h = C.c_void_p()
+        _check(lib().irt_create(_ptr(cells), cells.size, device, C.byref(h)), "irt_create")
+        self._h = h
+        self.device = device
+        self.info = VolumeInfo()
+        _check(lib().irt_get_volume_info(self._h, C.byref(self.info)), "irt_get_volume_info")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().irt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_transfunc(self, lut: np.ndarray, value_range, opacity_scale: float = 1.0):
+        lut = np.ascontiguousarray(lut, dtype=np.float32).reshape(-1, 4)
+        _check(lib().irt_set_transfunc(self._h, _ptr(lut), lut.shape[0], box1(*value_range),
+                                       float(opacity_scale)), "irt_set_transfunc")
+
+    def clear(self, fb_ptr: int, accum_ptr: int, num_pixels: int, stream: int = 0):
+        _check(lib().irt_clear_frame(self._h, C.c_void_p(fb_ptr), C.c_void_p(accum_ptr),
+                                     num_pixels, C.c_void_p(stream)), "irt_clear_frame")
+
+    def render(self, lp: LaunchParams, width: int, height: int, fb_ptr: int, accum_ptr: int,
+               stream: int = 0):
+        _check(lib().irt_render(self._h, C.byref(lp), width, height, C.c_void_p(fb_ptr),
+                                C.c_void_p(accum_ptr), C.c_void_p(stream)), "irt_render")
+
+    def render_tiles(self, lp: LaunchParams, width: int, height: int, tile_begin: int,
+                     tile_stride: int, fb_ptr: int, accum_ptr: int, stream: int = 0) -> int:
+        n = C.c_int()
+        _check(lib().irt_render_tiles(self._h, C.byref(lp), width, height, tile_begin,
+                                      tile_stride, C.c_void_p(fb_ptr), C.c_void_p(accum_ptr),
+                                      C.byref(n), C.c_void_p(stream)), "irt_render_tiles")
+        return n.value
+
+    def unpack_tiles(self, gathered_ptr: int, num_ranks: int, max_tiles: int, width: int,
+                     height: int, fb_ptr: int, stream: int = 0):
+        _check(lib().irt_unpack_tiles(self._h, C.c_void_p(gathered_ptr), num_ranks, max_tiles,
+                                      width, height, C.c_void_p(fb_ptr), C.c_void_p(stream)),
+               "irt_unpack_tiles")
+
+    def stats(self) -> RenderStats:
+        st = RenderStats()
+        _check(lib().irt_get_render_stats(self._h, C.byref(st)), "irt_get_render_stats")
+        return st
+
+    def shell(self) -> tuple[np.ndarray, np.ndarray]:
+        n = int(np.prod(list(self.info.shellDims)))
+        vr = np.zeros((n, 2), dtype=np.float32)
+        mo = np.zeros(n, dtype=np.float32)
+        _check(lib().irt_get_shell(self._h, _ptr(vr), _ptr(mo)), "irt_get_shell")
+        return vr, mo
+
+
+class DebugScene:
+    """Host-side locator (include/icon_rt_hip_debug.h), for CPU checks."""
+
+    def __init__(self, cells: np.ndarray):
+        cells = np.ascontiguousarray(cells, dtype=CELL_DTYPE)
+        h = C.c_void_p()
+        _check(lib().irt_debug_scene_build(_ptr(cells), cells.size, C.byref(h)),
+               "irt_debug_scene_build")
+        self._h = h
+        self.info = VolumeInfo()
+        lib().irt_debug_scene_info(self._h, C.byref(self.info))
+
+    def locate(self, p):
+        v = C.c_float()
+        r = C.c_uint32()
+        hit = lib().irt_debug_scene_locate(self._h, vec3(p), C.byref(v), C.byref(r))
+        return (True, v.value, r.value) if hit == 1 else (False, 0.0, None)
+
+    def candidates(self, p):
+        n = lib().irt_debug_scene_candidates(self._h, vec3(p), None, 0)
+        out = np.zeros(max(n, 1), dtype=np.uint32)
+        lib().irt_debug_scene_candidates(self._h, vec3(p), _ptr(out), n)
+        return out[:n]
+
+    def planes(self, rec: int) -> np.ndarray:
+        out = np.zeros(12, dtype=np.float32)
+        _check(lib().irt_debug_scene_planes(self._h, rec, _ptr(out)), "irt_debug_scene_planes")
+        return out.reshape(3, 4)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().irt_debug_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

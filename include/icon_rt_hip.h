@@ -1,0 +1,200 @@
+/*
+ * icon_rt_hip.h -- C ABI of the MI355X-native ICON volume renderer.
+ *
+ * Drop-in boundary for the hot path of szellmann/icon-ray-tracing `icon_rt`:
+ * the reference renders one frame with
+ *     SET_LAUNCH_PARAMS(parms); pl.launch();            (icon_rt/hostCode.cu:961-963)
+ * which runs the raygen `woodcockTrackingWithAccel` (icon_rt/deviceCode.cu:281-341)
+ * once per pixel -- on the CPU through parallel::for_each (common/pipeline.cu:1066-1071),
+ * on NVIDIA through owlLaunch2D (common/pipeline.cu:1064).  This library replaces that
+ * launch (and the accelerator builds that feed it) with hand-written HIP kernels for
+ * gfx950.  Plain C types, plain pointers and sizes; no C++ or torch types.
+ *
+ * Conventions
+ *  - Every function returns IRT_OK (0) or a negative IRT_E_* code; irt_last_error()
+ *    returns a thread-local message for the last failure.  (The reference prints and
+ *    continues or abort()s; pipeline.cu:992-995, hostCode.cu:19-34.)
+ *  - Input arrays are copied; the context never retains caller pointers beyond a call
+ *    (the reference's LaunchParams borrow pointers owned by Buffer/Frame/Transfunc).
+ *  - Framebuffer pointers passed to irt_render* are DEVICE pointers on the context's
+ *    device (HBM-resident, as the reference's fbPointer/accumBuffer in RTCORE builds).
+ *  - `stream` is a hipStream_t passed as void* (NULL = the context's own stream).
+ *  - A context is single-caller.  Multi-GPU = one process (one context) per GPU.
+ */
+#ifndef ICON_RT_HIP_H
+#define ICON_RT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IRT_OK 0
+#define IRT_E_INVALID (-1)   /* bad argument */
+#define IRT_E_HIP (-2)       /* HIP runtime error (no device, OOM, launch failure) */
+#define IRT_E_DATA (-3)      /* unusable cell data (numLayers out of [0,31], non-finite) */
+#define IRT_E_IO (-4)        /* file I/O */
+
+/* == icon_rt::ICONCell (icon_rt/ICONGrid.h:59-76); 284 bytes; the `.ic` record. */
+typedef struct irt_icon_cell {
+  float lat[3];        /* radians, per triangle corner, ccw */
+  float lon[3];        /* radians */
+  int32_t numLayers;   /* <= 31 (MAX_LAYERS 32, ICONGrid.h:57) */
+  float height[32];    /* metres from the Earth centre, [0:numLayers] used */
+  float value[32];     /* per layer, [0:numLayers) used */
+} irt_icon_cell;
+
+typedef struct irt_vec3f { float x, y, z; } irt_vec3f;
+typedef struct irt_vec4f { float x, y, z, w; } irt_vec4f;
+typedef struct irt_box1f { float lower, upper; } irt_box1f;
+typedef struct irt_box3f { irt_vec3f lower, upper; } irt_box3f;
+
+/* Raygen selector == Pipeline::setRayGen(...) choice (hostCode.cu:138-149, 863). */
+#define IRT_RAYGEN_WITH_ACCEL 0 /* woodcockTrackingWithAccel, deviceCode.cu:281-341 */
+#define IRT_RAYGEN_AE 1         /* woodcockTrackingAE, deviceCode.cu:239-275 */
+
+/* Per-frame part of icon_rt::LaunchParams (icon_rt/Params.h:92-119).  The volume,
+ * accelerator and transfer-function members live in the context (set by irt_create /
+ * irt_set_transfunc); the framebuffer pointers are arguments of irt_render. */
+typedef struct irt_launch_params {
+  irt_vec3f org;            /* camera.org    (Params.h:101; hostCode.cu:942) */
+  irt_vec3f dir_00;         /* camera.dir_00 (Params.h:102; hostCode.cu:943) */
+  irt_vec3f dir_du;         /* camera.dir_du (Params.h:103; hostCode.cu:944) */
+  irt_vec3f dir_dv;         /* camera.dir_dv (Params.h:104; hostCode.cu:945) */
+  int32_t accumID;          /* Params.h:111; hostCode.cu:958 */
+  irt_vec3f ambientColor;   /* Params.h:114; hostCode.cu:925 */
+  float ambientRadiance;    /* Params.h:115; hostCode.cu:926 */
+  float unitDistance;       /* Params.h:118; hostCode.cu:956 */
+  int32_t raygen;           /* IRT_RAYGEN_* */
+} irt_launch_params;
+
+/* Scene facts computed at irt_create exactly as hostCode.cu:792-808, 838-840. */
+typedef struct irt_volume_info {
+  uint64_t numCells;            /* Volume::numCells (Params.h:63) */
+  irt_box3f bounds;             /* Volume::bounds = union of ICONCell::getBounds() */
+  irt_box3f sphericalBounds;    /* ShellAccel::sphericalBounds (r, lat, lon) */
+  irt_box1f dataRange;          /* min/max of value[0:numLayers) */
+  float unitDistance;           /* 10^(floor(log10(sphericalBounds.lower.x))-3) */
+  int32_t shellDims[3];         /* ShellAccel::dims = (1,1024,1024) (hostCode.cu:654) */
+  /* locator facts (MI355X point-location structure replacing OptiX/cuBQL) */
+  int32_t locatorFaceRes;       /* cube-map cells per face edge */
+  uint64_t locatorEntries;      /* candidate-list entries */
+  uint64_t deviceBytes;         /* HBM held by the context */
+} irt_volume_info;
+
+/* Statistics of the most recent irt_render* call on a context. */
+typedef struct irt_render_stats {
+  uint64_t raysLaunched;        /* pixels the raygen ran for */
+  uint64_t raysInBox;           /* rays that passed boxTest (deviceCode.cu:294) */
+  uint64_t locateCalls;         /* sampleVolume calls (deviceCode.cu:173) */
+  uint64_t samplesFound;        /* sampleVolume calls that found a cell */
+  uint64_t candidatesTested;    /* locator candidate-list entries examined */
+  float kernelMs;               /* render kernel time, HIP events on the launch stream */
+} irt_render_stats;
+
+typedef struct irt_context irt_context;
+
+/* ---------------------------------------------------------------- errors */
+const char *irt_last_error(void);
+
+/* ---------------------------------------------------------------- context
+ * irt_create: validate and copy `cells` (already lat/lon-filtered, see irt_filter_cells),
+ * compute the volume facts (hostCode.cu:792-808), build the cell locator that replaces the
+ * OptiX/cuBQL accelerators (hostCode.cu:440-650), upload to HBM on `device`, and build the
+ * spherical-shell accelerator on the GPU: initGrid + buildShell_ICON
+ * (hostCode.cu:216-225, 299-336, 652-666).  Majorants stay zero until irt_set_transfunc. */
+int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_context **out);
+void irt_destroy(irt_context *ctx);
+int irt_get_volume_info(const irt_context *ctx, irt_volume_info *info);
+
+/* == Pipeline::setTransfunc -> transfuncUpdateHandler -> computeMaxOpacities
+ * (pipeline.cu:456-478; hostCode.cu:878-909, 362-397).  `rgbaLUT` is the final LUT
+ * (the reference resamples to 300 entries first when size < 300; irt_resample_lut). */
+int irt_set_transfunc(irt_context *ctx, const irt_vec4f *rgbaLUT, int size,
+                      irt_box1f valueRange, float opacityScale);
+
+/* == clearFramebuffer (common/pipeline.cu:171-199): fb = make_rgba(0), accum = 0. */
+int irt_clear_frame(irt_context *ctx, uint32_t *d_fb, irt_vec4f *d_accum, size_t numPixels,
+                    void *stream);
+
+/* == one Pipeline::launch() of the raygen over the full width x height launch
+ * (pipeline.cu:1061-1074 / owlLaunch2D 1064).  d_fb / d_accum are device arrays of
+ * width*height, pixel (x,y) at x + width*y (deviceCode.cu:286). */
+int irt_render(irt_context *ctx, const irt_launch_params *lp, int width, int height,
+               uint32_t *d_fb, irt_vec4f *d_accum, void *stream);
+
+/* Frame-tile subset of the same launch, for multi-GPU frame splitting: renders the
+ * 64x64 tiles t = tileBegin, tileBegin+tileStride, ... (row-major tile ids over
+ * ceil(width/64) x ceil(height/64)) into PACKED buffers: tile k of this subset at
+ * d_fb_tiles[k*4096 + ly*64 + lx].  Pixel seeds/cameras use the full-launch (x,y,width,
+ * height), so every pixel is bit-identical to irt_render's.  Returns the tile count in
+ * *numTiles when non-NULL. */
+int irt_render_tiles(irt_context *ctx, const irt_launch_params *lp, int width, int height,
+                     int tileBegin, int tileStride, uint32_t *d_fb_tiles,
+                     irt_vec4f *d_accum_tiles, int *numTiles, void *stream);
+
+/* Scatter packed tiles (as produced by irt_render_tiles on `numRanks` ranks and gathered
+ * rank-major into d_gathered[rank][maxTilesPerRank][4096]) into a linear framebuffer. */
+int irt_unpack_tiles(irt_context *ctx, const uint32_t *d_gathered, int numRanks,
+                     int maxTilesPerRank, int width, int height, uint32_t *d_fb, void *stream);
+
+int irt_get_render_stats(const irt_context *ctx, irt_render_stats *stats);
+
+/* Download the shell accelerator (for checking): valueRanges as 2 floats per
+ * macrocell, maxOpacities as 1 float per macrocell; either may be NULL. */
+int irt_get_shell(const irt_context *ctx, float *valueRanges, float *maxOpacities);
+
+/* Number of tiles of a width x height launch. */
+int irt_num_tiles(int width, int height);
+
+/* ---------------------------------------------------------------- host helpers
+ * (no GPU needed) -- the host-side setup of icon_rt's main() and common/, so a host
+ * program (the C++ Pipeline mirror under icon-ray-tracing_amd/host, or Python) can
+ * reproduce the reference's frame setup bit for bit. */
+
+/* Load a raw `.ic` file (hostCode.cu:717-734): N = filesize/284; the first
+ * min(N, maxNumCells) records if maxNumCells >= 0.  Call with out == NULL to get the
+ * count in *count; then with capacity >= count. */
+int irt_load_ic(const char *path, long maxNumCells, irt_icon_cell *out, size_t capacity,
+                size_t *count);
+int irt_save_ic(const char *path, const irt_icon_cell *cells, size_t count);
+
+/* Lat/lon filter in degrees (hostCode.cu:736-758); stable, in place; returns the kept
+ * count in *count. */
+int irt_filter_cells(irt_icon_cell *cells, size_t n, irt_box1f latRangeDeg,
+                     irt_box1f lonRangeDeg, size_t *count);
+
+/* Volume facts without a GPU (same values irt_get_volume_info reports). */
+int irt_compute_volume_info(const irt_icon_cell *cells, size_t n, irt_volume_info *info);
+
+/* Default transfer function of hostCode.cu:823-836 after Pipeline::setTransfunc's
+ * resampling to 300 entries (pipeline.cu:469-473): writes 300 entries to out300 and the
+ * value range (dataRange, or [0,1] if empty) to *valueRange. */
+int irt_default_transfunc(irt_box1f dataRange, irt_vec4f *out300, irt_box1f *valueRange);
+
+/* resampleLUT (common/dvr_course-common.h:44-70). */
+int irt_resample_lut(const irt_vec4f *src, int nsrc, irt_vec4f *dst, int ndst);
+
+/* Camera (common/camera.h) -> LaunchParams.camera as hostCode.cu:939-945 computes it:
+ * org = getPosition(), dir_00 = lower_left, dir_du = horizontal/imgW, dir_dv =
+ * vertical/imgH.  irt_camera_view_all: Camera::viewAll (camera.h:98-104) with the
+ * default fovy of 90 degrees; irt_camera_look_at: Pipeline's --camera vp vi vu / -fovy
+ * path (pipeline.cu:444-454; fovy in degrees, <1e-3 -> 90). */
+int irt_camera_view_all(irt_box3f bounds, float fovyDeg, int imgW, int imgH,
+                        irt_launch_params *lp);
+int irt_camera_look_at(irt_vec3f vp, irt_vec3f vi, irt_vec3f vu, float fovyDeg, int imgW,
+                       int imgH, irt_launch_params *lp);
+
+/* Synthetic RnBk icosahedral ICON grid (no netCDF offline): 20*rootN^2*4^bisections
+ * triangles, `levels` layers with heights R + topHeight*(l/levels)^2, a smooth value
+ * field normalised to [0,1] (plus `noise` * hash noise, seeded), stored as `.ic` records
+ * of <= 31 layers, bottom to top, consecutive per column.  out == NULL -> count only. */
+int irt_synth_grid(int rootN, int bisections, int levels, float topHeight, float noise,
+                   uint32_t seed, irt_icon_cell *out, size_t capacity, size_t *count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ICON_RT_HIP_H */

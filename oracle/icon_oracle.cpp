@@ -1,0 +1,812 @@
+// icon_oracle.cpp -- CPU ORACLE for the ICON Woodcock-tracking hot path.
+//
+// TEST INFRASTRUCTURE ONLY.  This file restates, in plain C++, the reference's
+// CPU render path (szellmann/icon-ray-tracing, non-RTCORE build) so the MI355X
+// product can be checked against it.  It is compiled into oracle/liboracle.so and
+// may only be loaded by tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg.  Nothing under icon-ray-tracing_amd/ uses it.
+//
+// Pinning: oracle/ref_harness.cpp compiles the reference's own headers
+// (vecmath.h, dvr_course-common-both.h, ICONGrid.h, ShellAccel.h, DDA.h,
+// camera.h) and pipeline.cu/fb.cu/transfunc.cu from /root/reference into
+// oracle/_ref/; tests/golden/ holds fixtures generated from it and
+// tests/test_oracle_*.py check this restatement against them bit for bit.
+//
+// Numerics: every float expression keeps the reference's evaluation order;
+// libm calls (asinf, atan2f, sinf, cosf, logf, powf, tanf, atanf, log10f) go to
+// the host glibc exactly where the reference calls them; build with
+// -ffp-contract=off.  float->int conversions use x86 cvttss2si semantics
+// (out-of-range / NaN -> INT_MIN), which is what the reference's g++ build does.
+
+#include "icon_oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+namespace {
+
+struct V3 { float x, y, z; };
+struct V4 { float x, y, z, w; };
+struct I3 { int x, y, z; };
+struct B1 { float lower, upper; };
+struct B3 { V3 lower, upper; };
+
+inline V3 v3(float s) { return {s, s, s}; }
+inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
+inline V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+inline V3 operator*(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+inline V3 operator/(V3 a, V3 b) { return {a.x / b.x, a.y / b.y, a.z / b.z}; }
+inline V3 operator/(V3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+// vecmath.h:536-538
+inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// vecmath.h:541-548
+inline V3 cross(V3 u, V3 v) {
+  return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+}
+// vecmath.h:550-557
+inline V3 normalize(V3 u) { return u / sqrtf(dot(u, u)); }
+inline float length(V3 u) { return sqrtf(dot(u, u)); }
+inline V3 vmin(V3 a, V3 b) { return {fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z)}; }
+inline V3 vmax(V3 a, V3 b) { return {fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z)}; }
+// vecmath.h:512-533
+inline float reduce_min(V3 u) { return fminf(fminf(u.x, u.y), u.z); }
+inline float reduce_max(V3 u) { return fmaxf(fmaxf(u.x, u.y), u.z); }
+// vecmath.h:46-54
+inline int imin(int a, int b) { return a < b ? a : b; }
+inline int imax(int a, int b) { return b < a ? a : b; }
+// vecmath.h:1338-1341
+inline int iclamp(int x, int a, int b) { return imax(a, imin(x, b)); }
+
+// float -> int the way the reference's x86-64 g++ build converts (cvttss2si):
+// truncation toward zero, INT_MIN for NaN and for anything outside int range.
+inline int f2i(float f) {
+  if (!(f > -2147483904.0f && f < 2147483648.0f)) return INT32_MIN;
+  return (int)f;
+}
+
+inline V3 toV3(oc_vec3 v) { return {v.x, v.y, v.z}; }
+inline oc_vec3 toOc(V3 v) { return {v.x, v.y, v.z}; }
+inline B3 toB3(oc_box3 b) { return {toV3(b.lower), toV3(b.upper)}; }
+
+// ---------------------------------------------------------------- RNG
+// LCG<4> (common/dvr_course-common-both.h:41-86)
+struct LCG {
+  uint32_t state;
+  uint64_t draws = 0;
+  LCG(uint32_t val0, uint32_t val1) {
+    uint32_t v0 = val0, v1 = val1, s0 = 0;
+    for (unsigned n = 0; n < 4; n++) {
+      s0 += 0x9e3779b9u;
+      v0 += ((v1 << 4) + 0xa341316cu) ^ (v1 + s0) ^ ((v1 >> 5) + 0xc8013ea4u);
+      v1 += ((v0 << 4) + 0xad90777du) ^ (v0 + s0) ^ ((v0 >> 5) + 0x7e95761eu);
+    }
+    state = v0;
+  }
+  float operator()() {
+    state = 1664525u * state + 1013904223u;
+    ++draws;
+    return (state & 0x00FFFFFFu) / (float)0x01000000;
+  }
+};
+
+// ---------------------------------------------------------------- geometry
+// ICONGrid.h:36-42
+inline V3 toSpherical(V3 c) {
+  float r = length(c);
+  float lat = asinf(c.z / r);
+  float lon = atan2f(c.y, c.x);
+  return {r, lat, lon};
+}
+// ICONGrid.h:44-54
+inline V3 toCartesian(V3 s) {
+  const float r = s.x, lat = s.y, lon = s.z;
+  float x = r * cosf(lat) * cosf(lon);
+  float y = r * cosf(lat) * sinf(lon);
+  float z = r * sinf(lat);
+  return {x, y, z};
+}
+// ICONGrid.h:170-179 (Plane == vec4f(N, dot(a,N)))
+inline V4 makePlane(V3 a, V3 b, V3 c) {
+  V3 N = cross(b - a, c - a);
+  return {N.x, N.y, N.z, dot(a, N)};
+}
+inline float evalPlane(const V4 &p, V3 pos) { return dot(pos, V3{p.x, p.y, p.z}) - p.w; }
+
+// ICONGrid.h:117-145 (std::lower_bound over height[1..numLayers])
+inline int findHeight(const oc_cell &c, float hpos) {
+  int first = 0;
+  int count = c.numLayers;
+  while (count > 0) {
+    int it = first;
+    int step = count / 2;
+    it = it + step;
+    if (!(hpos <= c.height[it + 1])) {
+      first = ++it;
+      count -= step + 1;
+    } else {
+      count = step;
+    }
+  }
+  return first;
+}
+// ICONGrid.h:147-164
+inline float getValue(const oc_cell &c, float hpos) { return c.value[findHeight(c, hpos)]; }
+
+// The six corners of a cell column (ICONGrid.h:188-195).
+inline void corners(const oc_cell &cell, V3 b[3], V3 t[3]) {
+  const float h0 = cell.height[0], hN = cell.height[cell.numLayers];
+  for (int k = 0; k < 3; ++k) {
+    b[k] = toCartesian({h0, cell.lat[k], cell.lon[k]});
+    t[k] = toCartesian({hN, cell.lat[k], cell.lon[k]});
+  }
+}
+
+struct CellPlanes { V4 p[3]; };
+inline CellPlanes cellPlanes(const oc_cell &cell) {
+  V3 b[3], t[3];
+  corners(cell, b, t);
+  CellPlanes P;
+  P.p[0] = makePlane(b[0], b[1], t[1]);
+  P.p[1] = makePlane(b[1], b[2], t[2]);
+  P.p[2] = makePlane(b[2], b[0], t[0]);
+  return P;
+}
+
+// sample(cell,pos,value) (ICONGrid.h:181-208), literal: toSpherical first,
+// corners and planes recomputed per call.
+inline bool sampleLiteral(const oc_cell &cell, V3 pos, float &value) {
+  const V3 spherical = toSpherical(pos);
+  if (spherical.x < cell.height[0] || spherical.x > cell.height[cell.numLayers]) return false;
+  CellPlanes P = cellPlanes(cell);
+  if (evalPlane(P.p[0], pos) > 0.f) return false; /* ccw */
+  if (evalPlane(P.p[1], pos) > 0.f) return false;
+  if (evalPlane(P.p[2], pos) > 0.f) return false;
+  value = getValue(cell, spherical.x);
+  return true;
+}
+// Same predicate, same result: lat/lon of toSpherical are dead in sample(), and
+// the planes depend only on the cell, so they can be precomputed.
+inline bool sampleFast(const oc_cell &cell, const CellPlanes &P, V3 pos, float &value) {
+  const float r = length(pos);
+  if (r < cell.height[0] || r > cell.height[cell.numLayers]) return false;
+  if (evalPlane(P.p[0], pos) > 0.f) return false;
+  if (evalPlane(P.p[1], pos) > 0.f) return false;
+  if (evalPlane(P.p[2], pos) > 0.f) return false;
+  value = getValue(cell, r);
+  return true;
+}
+
+// ICONGrid.h:78-115
+inline B3 getBounds(const oc_cell &c) {
+  B3 bounds{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
+  V3 bv1 = toCartesian({c.height[0], c.lat[0], c.lon[0]});
+  V3 bv2 = toCartesian({c.height[0], c.lat[1], c.lon[1]});
+  V3 bv3 = toCartesian({c.height[0], c.lat[2], c.lon[2]});
+  bounds.lower = vmin(bounds.lower, bv1); bounds.upper = vmax(bounds.upper, bv1);
+  bounds.lower = vmin(bounds.lower, bv2); bounds.upper = vmax(bounds.upper, bv2);
+  bounds.lower = vmin(bounds.lower, bv3); bounds.upper = vmax(bounds.upper, bv3);
+  V3 tv1 = toCartesian({c.height[c.numLayers], c.lat[0], c.lon[0]});
+  V3 tv2 = toCartesian({c.height[c.numLayers], c.lat[1], c.lon[1]});
+  V3 tv3 = toCartesian({c.height[c.numLayers], c.lat[2], c.lon[2]});
+  V3 bary = (tv1 + tv2 + tv3) / 3.f;
+  float R = c.height[c.numLayers];
+  float D = R - length(bary);
+  float off = D / R;
+  tv1 = tv1 + tv1 * off;
+  tv2 = tv2 + tv2 * off;
+  tv3 = tv3 + tv3 * off;
+  bounds.lower = vmin(bounds.lower, tv1); bounds.upper = vmax(bounds.upper, tv1);
+  bounds.lower = vmin(bounds.lower, tv2); bounds.upper = vmax(bounds.upper, tv2);
+  bounds.lower = vmin(bounds.lower, tv3); bounds.upper = vmax(bounds.upper, tv3);
+  return bounds;
+}
+
+// ---------------------------------------------------------------- ray / shell
+struct Ray { V3 org; float tmin; V3 dir; float tmax; };
+inline V3 eval(const Ray &r, float t) { return r.org + r.dir * t; }
+
+// vecmath.h:1926-1937
+inline bool boxTest(const Ray &ray, const B3 &box, float &t0, float &t1) {
+  const V3 t_lo = (box.lower - ray.org) / ray.dir;
+  const V3 t_hi = (box.upper - ray.org) / ray.dir;
+  const V3 t_nr = vmin(t_lo, t_hi);
+  const V3 t_fr = vmax(t_lo, t_hi);
+  t0 = fmaxf(ray.tmin, reduce_max(t_nr));
+  t1 = fminf(ray.tmax, reduce_min(t_fr));
+  return t0 < t1;
+}
+
+// ShellAccel.h:34-53
+inline bool intersectSphere(const Ray &ray, float radius, float &tnear, float &tfar) {
+  float A = dot(ray.dir, ray.dir);
+  float B = dot(ray.dir, ray.org) * 2.f;
+  float C = dot(ray.org, ray.org) - radius * radius;
+  float d = B * B - 4.f * A * C;
+  if (d < 0.f) return false;
+  d = sqrtf(d);
+  float q = B < 0.f ? -0.5f * (B - d) : -0.5f * (B + d);
+  float t1 = q / A;
+  float t2 = C / q;
+  tnear = fminf(t1, t2);
+  tfar = fmaxf(t1, t2);
+  return true;
+}
+
+// ShellAccel.h:57-68 (note dims-1)
+inline I3 projectToSphericalGrid(V3 sph, const int dims[3], const B3 &sb) {
+  const float radSize = sb.upper.x - sb.lower.x;
+  const float latSize = sb.upper.y - sb.lower.y;
+  const float lonSize = sb.upper.z - sb.lower.z;
+  return {f2i((sph.x - sb.lower.x) / radSize * (dims[0] - 1)),
+          f2i((sph.y - sb.lower.y) / latSize * (dims[1] - 1)),
+          f2i((sph.z - sb.lower.z) / lonSize * (dims[2] - 1))};
+}
+// ShellAccel.h:71-80
+inline I3 normalizeGridCoord(I3 c, const int dims[3]) {
+  while (c.x < 0) c.x += dims[0];
+  while (c.x >= dims[0]) c.x -= dims[0];
+  while (c.y < 0) c.y += dims[1];
+  while (c.y >= dims[1]) c.y -= dims[1];
+  while (c.z < 0) c.z += dims[2];
+  while (c.z >= dims[2]) c.z -= dims[2];
+  return c;
+}
+// DDA.h:15-21
+inline size_t linearIndex(I3 i, const int dims[3]) {
+  return i.z * size_t(dims[0]) * dims[1] + i.y * dims[0] + i.x;
+}
+
+// sdda (ShellAccel.h:82-229), literal -- including the degenerate r=0 planes.
+template <typename Func>
+inline void sdda(Ray ray, const int dims[3], const B3 &sb, const Func &func) {
+  const float sceneEPS = sb.lower.x * 1e-6f;
+  float t1 = 0.f, t2 = 0.f, t3 = 0.f, t4 = 0.f;
+  bool s1 = intersectSphere(ray, sb.upper.x, t1, t4);
+  bool s2 = intersectSphere(ray, sb.lower.x, t2, t3);
+  if (!s1 && !s2) return;
+  if (t4 < ray.tmin) return;
+  B1 ranges[2] = {{INFINITY, -INFINITY}, {INFINITY, -INFINITY}};
+  if (s1 && !s2) {
+    ranges[0] = {t1, t4};
+  } else if (ray.tmin < t2) {
+    ranges[0] = {t1, t2};
+    ranges[1] = {t3, t4};
+  } else {
+    ranges[0] = {t3, t4};
+  }
+  for (int i = 0; i < 2; ++i) {
+    if (ranges[i].upper <= ranges[i].lower) break;  // box1f::empty (vecmath.h:981)
+    V3 P1 = eval(ray, ranges[i].lower + sceneEPS);
+    V3 P2 = eval(ray, ranges[i].upper - sceneEPS);
+    V3 SP1 = toSpherical(P1);
+    V3 SP2 = toSpherical(P2);
+    const B1 radBounds{sb.lower.x, sb.upper.x};
+    const B1 latBounds{sb.lower.y, sb.upper.y};
+    const B1 lonBounds{sb.lower.z, sb.upper.z};
+    const float radInc = (radBounds.upper - radBounds.lower) / float(dims[0]);
+    const float latInc = (latBounds.upper - latBounds.lower) / float(dims[1]);
+    const float lonInc = (lonBounds.upper - lonBounds.lower) / float(dims[2]);
+    I3 cellID = projectToSphericalGrid(SP1, dims, sb);
+    const I3 step = {SP1.x < SP2.x ? 1 : -1, SP1.y < SP2.y ? 1 : -1, SP1.z < SP2.z ? 1 : -1};
+    I3 stop = projectToSphericalGrid(SP2, dims, sb);
+    stop = {stop.x + step.x, stop.y + step.y, stop.z + step.z};
+    float radOff = (cellID.x + step.x) * radInc;
+    float latOff = (cellID.y + step.y) * latInc;
+    float lonOff = (cellID.z + step.z) * lonInc;
+    float radius = step.x == 1 ? sb.lower.x + radOff : sb.upper.x + radOff;
+    float sphereT1, sphereT2;
+    bool sphereHit = intersectSphere(ray, radius, sphereT1, sphereT2);
+    if (!sphereHit) sphereT1 = ranges[i].upper;
+    (void)sphereT1;
+    V4 latPlane = makePlane(v3(0.f), toCartesian({0.f, latOff, latBounds.lower}),
+                            toCartesian({0.f, latOff, latBounds.upper}));
+    V4 lonPlane = makePlane(v3(0.f), toCartesian({0.f, lonBounds.lower, lonOff}),
+                            toCartesian({0.f, lonBounds.upper, lonOff}));
+    V3 tnext = {ranges[i].upper, evalPlane(latPlane, eval(ray, ranges[i].lower)),
+                evalPlane(lonPlane, eval(ray, ranges[i].lower))};
+    float t = ranges[i].lower;
+    while (1) {
+      V3 P = ray.org + ray.dir * t;
+      float tt1 = FLT_MAX;
+      if (tnext.x < tt1 && tnext.x >= t) tt1 = tnext.x;
+      if (tnext.y < tt1 && tnext.y >= t) tt1 = tnext.y;
+      if (tnext.z < tt1 && tnext.z >= t) tt1 = tnext.z;
+      int leafID = (int)linearIndex(normalizeGridCoord(cellID, dims), dims);
+      if (!func(leafID, t, tt1)) return;
+      const float t_closest = reduce_min(tnext);
+      if (tnext.x == t_closest) {
+        cellID.x += step.x;
+        if (cellID.x == stop.x) break;
+      }
+      if (tnext.y == t_closest) {
+        cellID.y += step.y;
+        if (cellID.y == stop.y) break;
+        V4 plane = makePlane(v3(0.f), toCartesian({0.f, cellID.y * latInc, latBounds.lower}),
+                             toCartesian({0.f, cellID.y * latInc, latBounds.upper}));
+        tnext.y = evalPlane(plane, P);
+      }
+      if (tnext.z == t_closest) {
+        cellID.z += step.z;
+        if (cellID.z == stop.z) break;
+        V4 plane = makePlane(v3(0.f), toCartesian({0.f, lonBounds.lower, cellID.z * lonInc}),
+                             toCartesian({0.f, lonBounds.upper, cellID.z * lonInc}));
+        tnext.z = evalPlane(plane, P);
+      }
+      t = t_closest;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- shading
+// dvr_course-common-both.h:30-35
+inline float linear_to_srgb(float x) {
+  if (x <= 0.0031308f) return 12.92f * x;
+  return 1.055f * powf(x, 1.f / 2.4f) - 0.055f;
+}
+// dvr_course-common-both.h:89-92
+inline uint32_t make_8bit(const float f) {
+  return (uint32_t)fminf(255, fmaxf(0, (float)f2i(f * 256.f)));
+}
+// dvr_course-common-both.h:103-110
+inline uint32_t make_rgba(V4 c) {
+  return (make_8bit(c.x) << 0) + (make_8bit(c.y) << 8) + (make_8bit(c.z) << 16) +
+         (make_8bit(c.w) << 24);
+}
+
+// postClassify (deviceCode.cu:127-135)
+inline V4 postClassify(const oc_params &p, float v) {
+  v = (v - p.tf_lower) / (p.tf_upper - p.tf_lower);
+  int idx = f2i(v * (p.lut_size));
+  float frac = (v * p.lut_size) - idx;
+  const float *v1 = p.lut + 4 * iclamp(idx, 0, p.lut_size - 1);
+  const float *v2 = p.lut + 4 * iclamp(idx + 1, 0, p.lut_size - 1);
+  const float om = 1.f - frac;
+  return {v1[0] * frac + v2[0] * om * 1.f, v1[1] * frac + v2[1] * om * 1.f,
+          v1[2] * frac + v2[2] * om * 1.f, v1[3] * frac + v2[3] * om * p.opacityScale};
+}
+
+// ---------------------------------------------------------------- renderer
+struct Scene {
+  const oc_cell *cells;
+  size_t n;
+  bool fast;
+  std::vector<CellPlanes> planes;  // fast mode only
+};
+
+struct ThreadStats {
+  uint64_t launched = 0, inBox = 0, locate = 0, found = 0, draws = 0, leaves = 0;
+};
+
+// sampleVolume, CPU branch: first cell index wins (deviceCode.cu:116-123)
+inline bool sampleVolume(const Scene &S, V3 pos, float &value) {
+  if (S.fast) {
+    for (size_t i = 0; i < S.n; ++i)
+      if (sampleFast(S.cells[i], S.planes[i], pos, value)) return true;
+  } else {
+    for (size_t i = 0; i < S.n; ++i)
+      if (sampleLiteral(S.cells[i], pos, value)) return true;
+  }
+  return false;
+}
+
+// woodcockTracking (deviceCode.cu:149-186)
+inline float woodcockTracking(const Scene &S, const oc_params &p, const Ray &ray, LCG &rnd,
+                              float majorant, V3 &albedo, float &extinction, ThreadStats &ts) {
+  float t = ray.tmin;
+  while (1) {
+    if (majorant <= 0.f) break;
+    t -= (logf(1.f - rnd()) / (majorant / p.unitDistance));
+    if (t > ray.tmax) break;
+    V3 P = ray.org + ray.dir * t;
+    float value{0.f};
+    ++ts.locate;
+    if (!sampleVolume(S, P, value)) continue;
+    ++ts.found;
+    V4 sample = postClassify(p, value);
+    float u = rnd();
+    if (sample.w >= u * majorant) {
+      albedo = {sample.x, sample.y, sample.z};
+      extinction = sample.w;
+      break;
+    }
+  }
+  return fminf(t, ray.tmax);
+}
+
+// generateRay (deviceCode.cu:36-49).  The reference's expression
+//   dir_00 + (screen.u+rnd())*dir_du + (screen.v+rnd())*dir_dv
+// leaves the two rnd() calls unsequenced; g++ (the reference's CPU compiler)
+// evaluates the dir_dv operand's rnd() first.  oracle/ref_harness.cpp pins this.
+inline Ray generateRay(const oc_params &p, float su, float sv, LCG &rnd) {
+  const float jv = rnd();
+  const float ju = rnd();
+  V3 dir = toV3(p.dir_00) + v3(su + ju) * toV3(p.dir_du) + v3(sv + jv) * toV3(p.dir_dv);
+  dir = normalize(dir);
+  if (fabsf(dir.x) < 1e-5f) dir.x = 1e-5f;
+  if (fabsf(dir.y) < 1e-5f) dir.y = 1e-5f;
+  if (fabsf(dir.z) < 1e-5f) dir.z = 1e-5f;
+  return Ray{toV3(p.org), 0.f, dir, 1e10f};
+}
+
+// lerp (vecmath.h:1333-1336): x*a + (1-x)*b, then srgb + RGBA8 (deviceCode.cu:333-340)
+inline void accumulate(const oc_params &p, V3 color, float alpha, float *acc, uint32_t *fbp) {
+  const float a = 1.f / (p.accumID + 1);
+  V4 old{acc[0], acc[1], acc[2], acc[3]};
+  V4 nv{color.x, color.y, color.z, alpha};
+  V4 r{a * nv.x + (1.f - a) * old.x, a * nv.y + (1.f - a) * old.y, a * nv.z + (1.f - a) * old.z,
+       a * nv.w + (1.f - a) * old.w};
+  acc[0] = r.x; acc[1] = r.y; acc[2] = r.z; acc[3] = r.w;
+  V4 c = r;
+  c.x = linear_to_srgb(c.x);
+  c.y = linear_to_srgb(c.y);
+  c.z = linear_to_srgb(c.z);
+  *fbp = make_rgba(c);
+}
+
+// RAYGEN woodcockTrackingWithAccel (deviceCode.cu:281-341) and
+// woodcockTrackingAE (deviceCode.cu:239-275) for one pixel.
+void raygen(const Scene &S, const oc_params &p, int x, int y, int W, int H, float *accum,
+            uint32_t *fb, ThreadStats &ts) {
+  const int pixelID = x + W * y;
+  ++ts.launched;
+  LCG rnd((uint32_t)p.accumID * (uint32_t)W * (uint32_t)H + (uint32_t)x, (uint32_t)y);
+  Ray ray = generateRay(p, (float)x + .5f, (float)y + .5f, rnd);
+  float t0, t1;
+  const B3 bounds = toB3(p.bounds);
+  if (!boxTest(ray, bounds, t0, t1)) {
+    ts.draws += rnd.draws;
+    return;
+  }
+  ++ts.inBox;
+  ray.tmin = t0;
+  ray.tmax = t1;
+  V3 color = v3(0.f);
+  float alpha = 0.f;
+  const V3 amb = toV3(p.ambientColor);
+  if (p.raygen == 1) {
+    V3 albedo = v3(0.f);
+    float extinction = 0.f;
+    woodcockTracking(S, p, ray, rnd, 1.f, albedo, extinction, ts);
+    color = albedo * amb * p.ambientRadiance;
+    alpha = extinction > 0.f ? 1.f : 0.f;
+  } else {
+    const B3 sb = toB3(p.sphericalBounds);
+    auto woodcockFunc = [&](const int leafID, float tt0, float tt1) {
+      ++ts.leaves;
+      V3 albedo = v3(0.f);
+      float extinction = 0.f;
+      const float majorant = p.maxOpacities[leafID];
+      ray.tmin = tt0;
+      ray.tmax = tt1;
+      float t = woodcockTracking(S, p, ray, rnd, majorant, albedo, extinction, ts);
+      if (t > tt0 && t < tt1) {
+        color = albedo * amb * p.ambientRadiance;
+        alpha = extinction > 0.f ? 1.f : 0.f;
+        return false;
+      }
+      return true;
+    };
+    sdda(ray, p.dims, sb, woodcockFunc);
+  }
+  accumulate(p, color, alpha, accum + 4 * (size_t)pixelID, fb + pixelID);
+  ts.draws += rnd.draws;
+}
+
+}  // namespace
+
+// ======================================================================== C API
+
+extern "C" {
+
+size_t oracle_filter_cells(oc_cell *cells, size_t n, float latLo, float latHi, float lonLo,
+                           float lonHi) {
+  // deg2rad (ICONGrid.h:26-29): d*float(M_PI)/180.f
+  auto d2r = [](float d) { return d * float(M_PI) / 180.f; };
+  const float la0 = d2r(latLo), la1 = d2r(latHi), lo0 = d2r(lonLo), lo1 = d2r(lonHi);
+  size_t k = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const oc_cell &c = cells[i];
+    bool drop = (c.lat[0] < la0 || c.lat[1] < la0 || c.lat[2] < la0) ||
+                (c.lat[0] > la1 || c.lat[1] > la1 || c.lat[2] > la1) ||
+                (c.lon[0] < lo0 || c.lon[1] < lo0 || c.lon[2] < lo0) ||
+                (c.lon[0] > lo1 || c.lon[1] > lo1 || c.lon[2] > lo1);
+    if (!drop) {
+      if (k != i) cells[k] = cells[i];
+      ++k;
+    }
+  }
+  return k;
+}
+
+void oracle_compute_bounds(const oc_cell *cells, size_t n, oc_box3 *sphericalBounds,
+                           oc_box3 *volbounds, float *dataRange) {
+  B3 vb{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
+  B3 sb{v3(INFINITY), v3(-INFINITY)};
+  B1 dr{INFINITY, -INFINITY};
+  for (size_t i = 0; i < n; ++i) {
+    const oc_cell &cell = cells[i];
+    float minLat = fminf(cell.lat[0], fminf(cell.lat[1], cell.lat[2]));
+    float maxLat = fmaxf(cell.lat[0], fmaxf(cell.lat[1], cell.lat[2]));
+    float minLon = fminf(cell.lon[0], fminf(cell.lon[1], cell.lon[2]));
+    float maxLon = fmaxf(cell.lon[0], fmaxf(cell.lon[1], cell.lon[2]));
+    sb.lower.x = fminf(sb.lower.x, cell.height[0]);
+    sb.upper.x = fmaxf(sb.upper.x, cell.height[cell.numLayers]);
+    sb.lower.y = fminf(sb.lower.y, minLat);
+    sb.upper.y = fmaxf(sb.upper.y, maxLat);
+    sb.lower.z = fminf(sb.lower.z, minLon);
+    sb.upper.z = fmaxf(sb.upper.z, maxLon);
+    B3 b = getBounds(cell);
+    vb.lower = vmin(vb.lower, b.lower);
+    vb.upper = vmax(vb.upper, b.upper);
+    for (int j = 0; j < cell.numLayers; ++j) {
+      dr.lower = fminf(dr.lower, cell.value[j]);
+      dr.upper = fmaxf(dr.upper, cell.value[j]);
+    }
+  }
+  *sphericalBounds = {toOc(sb.lower), toOc(sb.upper)};
+  *volbounds = {toOc(vb.lower), toOc(vb.upper)};
+  dataRange[0] = dr.lower;
+  dataRange[1] = dr.upper;
+}
+
+float oracle_unit_distance(float innerRadius) {
+  float magnitude = floorf(log10f(innerRadius));
+  float scale = powf(10.f, magnitude - 3);
+  return 1.0f * scale;
+}
+
+void oracle_default_lut5(float *out) {
+  static const float lut[20] = {0.149f, 0.015f, 0.705f, 1.0f,  0.486f, 0.603f, 0.956f,
+                                0.75f,  0.866f, 0.866f, 0.866f, 0.5f, 0.996f, 0.690f,
+                                0.552f, 0.25f,  0.752f, 0.298f, 0.231f, 0.0f};
+  memcpy(out, lut, sizeof(lut));
+}
+
+void oracle_resample_lut(const float *src, int nsrc, float *dst, int ndst) {
+  for (int i = 0; i < ndst; ++i) {
+    float indexf = i / (float)(ndst) * (nsrc - 1);
+    int indexa = (int)indexf;
+    int indexb = std::min(indexa + 1, nsrc - 1);
+    float frac = indexf - indexa;
+    float x = 1.f - frac;
+    for (int c = 0; c < 4; ++c)
+      dst[4 * i + c] = x * src[4 * indexa + c] + (1.f - x) * src[4 * indexb + c];
+  }
+}
+
+static void cameraFrame(V3 origin, V3 poi, V3 up, float fovy, float aspect, oc_vec3 *out4) {
+  // Camera::setOrientation (camera.h:34-54) + forceUpFrame (56-64) + getScreen (86-96)
+  V3 vz = (poi.x == origin.x && poi.y == origin.y && poi.z == origin.z)
+              ? V3{0, 0, 1}
+              : -normalize(poi - origin);
+  V3 vx = cross(up, vz);
+  if (dot(vx, vx) < 1e-8f)
+    vx = {0, 1, 0};
+  else
+    vx = normalize(vx);
+  V3 vy = normalize(cross(vz, vx));
+  if (!(fabsf(dot(vz, up)) < 1e-6f)) {
+    vx = normalize(cross(up, vz));
+    vy = normalize(cross(vz, vx));
+  }
+  float screen_height = 2.f * tanf(0.5f * fovy);
+  V3 vertical = v3(screen_height) * vy;
+  V3 horizontal = v3(screen_height * aspect) * vx;
+  V3 lower_left = -vz - v3(0.5f) * vertical - v3(0.5f) * horizontal;
+  out4[0] = toOc(origin);
+  out4[1] = toOc(lower_left);
+  out4[2] = toOc(horizontal);
+  out4[3] = toOc(vertical);
+}
+
+void oracle_camera_view_all(oc_box3 box, float fovy_deg, float aspect, oc_vec3 *out4) {
+  // camera.h:108 (member default) / pipeline.cu:451 conversion
+  const float fovy = fovy_deg * M_PI / 180.f;
+  B3 b = toB3(box);
+  V3 up{0, 1, 0};
+  float diagonal = length(b.upper - b.lower);
+  float r = diagonal * 0.5f;
+  V3 center = (b.lower + b.upper) / 2.f;
+  V3 eye = center + V3{0, 0, r + r / std::atan(fovy)};
+  cameraFrame(eye, center, up, fovy, aspect, out4);
+}
+
+void oracle_camera_orient(oc_vec3 vp, oc_vec3 vi, oc_vec3 vu, float fovy_deg, float aspect,
+                          oc_vec3 *out4) {
+  // Pipeline::Impl::setCamera (pipeline.cu:444-454)
+  float f = fovy_deg;
+  if (f < 1e-3f) f = 90.f;
+  const float fovy = f * M_PI / 180.f;
+  cameraFrame(toV3(vp), toV3(vi), toV3(vu), fovy, aspect, out4);
+}
+
+void oracle_build_shell(const oc_cell *cells, size_t n, const int32_t dims[3],
+                        oc_box3 sphericalBounds, float *valueRanges) {
+  const int d[3] = {dims[0], dims[1], dims[2]};
+  const size_t numMCs = (size_t)d[0] * d[1] * d[2];
+  // initGrid(ShellAccel) (hostCode.cu:216-225)
+  for (size_t i = 0; i < numMCs; ++i) {
+    valueRanges[2 * i] = FLT_MAX;
+    valueRanges[2 * i + 1] = -FLT_MAX;
+  }
+  const B3 sb = toB3(sphericalBounds);
+  // buildShell_ICON (hostCode.cu:299-336); float atomicMin/Max (36-56) only
+  // store when strictly smaller/larger.
+  for (size_t ci = 0; ci < n; ++ci) {
+    const oc_cell &cell = cells[ci];
+    for (int i = 0; i < cell.numLayers; ++i) {
+      I3 c1 = projectToSphericalGrid({cell.height[i], cell.lat[0], cell.lon[0]}, d, sb);
+      I3 c2 = projectToSphericalGrid({cell.height[i], cell.lat[1], cell.lon[1]}, d, sb);
+      I3 c3 = projectToSphericalGrid({cell.height[i], cell.lat[2], cell.lon[2]}, d, sb);
+      I3 c4 = projectToSphericalGrid({cell.height[i + 1], cell.lat[0], cell.lon[0]}, d, sb);
+      I3 c5 = projectToSphericalGrid({cell.height[i + 1], cell.lat[1], cell.lon[1]}, d, sb);
+      I3 c6 = projectToSphericalGrid({cell.height[i + 1], cell.lat[2], cell.lon[2]}, d, sb);
+      I3 lo{imin(c1.x, imin(c2.x, c3.x)), imin(c1.y, imin(c2.y, c3.y)),
+            imin(c1.z, imin(c2.z, c3.z))};
+      I3 up{imax(c4.x, imax(c5.x, c6.x)), imax(c4.y, imax(c5.y, c6.y)),
+            imax(c4.z, imax(c5.z, c6.z))};
+      B1 range{getValue(cell, cell.height[i]), getValue(cell, cell.height[i + 1])};
+      for (int mcz = lo.z; mcz <= up.z; ++mcz)
+        for (int mcy = lo.y; mcy <= up.y; ++mcy)
+          for (int mcx = lo.x; mcx <= up.x; ++mcx) {
+            size_t id = linearIndex({mcx, mcy, mcz}, d);
+            float *vr = valueRanges + 2 * id;
+            if (range.lower < vr[0]) vr[0] = range.lower;
+            if (range.upper > vr[1]) vr[1] = range.upper;
+          }
+    }
+  }
+}
+
+void oracle_max_opacities(const float *valueRanges, size_t numMCs, const float *lut, int size,
+                          float tfLo, float tfHi, float *maxOpacities) {
+  for (size_t mc = 0; mc < numMCs; ++mc) {
+    B1 vr{valueRanges[2 * mc], valueRanges[2 * mc + 1]};
+    if (vr.upper < vr.lower) {
+      maxOpacities[mc] = 0.f;
+      continue;
+    }
+    vr.lower -= tfLo;
+    vr.lower /= tfHi - tfLo;
+    vr.upper -= tfLo;
+    vr.upper /= tfHi - tfLo;
+    int lo = iclamp(f2i(vr.lower * (size - 1)), 0, size - 1);
+    int hi = iclamp(f2i(vr.upper * (size - 1)) + 1, 0, size - 1);
+    float maxOpacity = 0.f;
+    for (int i = lo; i <= hi; ++i) maxOpacity = fmaxf(maxOpacity, lut[4 * i + 3]);
+    maxOpacities[mc] = maxOpacity;
+  }
+}
+
+void oracle_clear(uint32_t *fb, float *accum, size_t numPixels) {
+  V4 zero{0.f, 0.f, 0.f, 0.f};
+  uint32_t c = make_rgba(zero);
+  for (size_t i = 0; i < numPixels; ++i) {
+    if (fb) fb[i] = c;
+    if (accum) accum[4 * i] = accum[4 * i + 1] = accum[4 * i + 2] = accum[4 * i + 3] = 0.f;
+  }
+}
+
+int oracle_render(const oc_cell *cells, size_t n, const oc_params *p, int W, int H, int x0,
+                  int y0, int x1, int y1, float *accum, uint32_t *fb, int nthreads, int fast,
+                  oc_stats *stats) {
+  if (!p || W <= 0 || H <= 0 || x0 < 0 || y0 < 0 || x1 > W || y1 > H) return -1;
+  if (x1 <= x0 || y1 <= y0) return 0;
+  Scene S{cells, n, fast != 0, {}};
+  if (S.fast) {
+    S.planes.resize(n);
+    for (size_t i = 0; i < n; ++i) S.planes[i] = cellPlanes(cells[i]);
+  }
+  // parallel::for_each over 64x64 tiles (common/for_each.h:70-85,
+  // parallel_for.h:62-82), dynamic via an atomic counter (thread_pool.h:146-161)
+  const int tw = 64, th = 64;
+  const int ntx = (x1 - x0 + tw - 1) / tw, nty = (y1 - y0 + th - 1) / th;
+  const long numTiles = (long)ntx * nty;
+  std::atomic<long> counter{0};
+  if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
+  if (nthreads <= 0) nthreads = 1;
+  std::vector<ThreadStats> tstats(nthreads);
+  auto worker = [&](int tid) {
+    ThreadStats &ts = tstats[tid];
+    for (;;) {
+      long tile = counter.fetch_add(1);
+      if (tile >= numTiles) break;
+      int fx = (int)(tile % ntx) * tw + x0, lx = std::min(fx + tw, x1);
+      int fy = (int)(tile / ntx) * th + y0, ly = std::min(fy + th, y1);
+      for (int y = fy; y < ly; ++y)
+        for (int x = fx; x < lx; ++x) raygen(S, *p, x, y, W, H, accum, fb, ts);
+    }
+  };
+  std::vector<std::thread> threads;
+  for (int t = 1; t < nthreads; ++t) threads.emplace_back(worker, t);
+  worker(0);
+  for (auto &t : threads) t.join();
+  if (stats) {
+    memset(stats, 0, sizeof(*stats));
+    for (auto &ts : tstats) {
+      stats->rays_launched += ts.launched;
+      stats->rays_in_box += ts.inBox;
+      stats->locate_calls += ts.locate;
+      stats->samples_found += ts.found;
+      stats->rng_draws += ts.draws;
+      stats->leaves += ts.leaves;
+    }
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ KATs
+void oracle_lcg(uint32_t seed0, uint32_t seed1, int n, float *out) {
+  LCG r(seed0, seed1);
+  for (int i = 0; i < n; ++i) out[i] = r();
+}
+
+int oracle_sample(const oc_cell *cell, oc_vec3 pos, float *value) {
+  float v = 0.f;
+  bool ok = sampleLiteral(*cell, toV3(pos), v);
+  if (ok) *value = v;
+  return ok ? 1 : 0;
+}
+
+int oracle_find_height(const oc_cell *cell, float h) { return findHeight(*cell, h); }
+
+int oracle_intersect_sphere(oc_vec3 org, oc_vec3 dir, float radius, float *tn, float *tf) {
+  Ray r{toV3(org), 0.f, toV3(dir), 1e10f};
+  return intersectSphere(r, radius, *tn, *tf) ? 1 : 0;
+}
+
+int oracle_box_test(oc_vec3 org, oc_vec3 dir, float tmin, float tmax, oc_box3 box, float *t0,
+                    float *t1) {
+  Ray r{toV3(org), tmin, toV3(dir), tmax};
+  return boxTest(r, toB3(box), *t0, *t1) ? 1 : 0;
+}
+
+int oracle_sdda_trace(oc_vec3 org, oc_vec3 dir, float tmin, float tmax, const int32_t dims[3],
+                      oc_box3 sphericalBounds, int maxOut, int32_t *leaf, float *t0, float *t1) {
+  Ray r{toV3(org), tmin, toV3(dir), tmax};
+  const int d[3] = {dims[0], dims[1], dims[2]};
+  int count = 0;
+  sdda(r, d, toB3(sphericalBounds), [&](int l, float a, float b) {
+    if (count < maxOut) {
+      leaf[count] = l;
+      t0[count] = a;
+      t1[count] = b;
+    }
+    ++count;
+    return count < 100000;
+  });
+  return count;
+}
+
+float oracle_linear_to_srgb(float x) { return linear_to_srgb(x); }
+
+uint32_t oracle_make_rgba(const float *c) { return make_rgba({c[0], c[1], c[2], c[3]}); }
+
+void oracle_to_spherical(oc_vec3 c, oc_vec3 *out) { *out = toOc(toSpherical(toV3(c))); }
+void oracle_to_cartesian(oc_vec3 s, oc_vec3 *out) { *out = toOc(toCartesian(toV3(s))); }
+
+void oracle_get_bounds(const oc_cell *cell, oc_box3 *out) {
+  B3 b = getBounds(*cell);
+  *out = {toOc(b.lower), toOc(b.upper)};
+}
+
+void oracle_post_classify(const float *lut, int size, float lo, float hi, float opacityScale,
+                          float v, float *out4) {
+  oc_params p{};
+  p.lut = lut;
+  p.lut_size = size;
+  p.tf_lower = lo;
+  p.tf_upper = hi;
+  p.opacityScale = opacityScale;
+  V4 r = postClassify(p, v);
+  out4[0] = r.x; out4[1] = r.y; out4[2] = r.z; out4[3] = r.w;
+}
+
+}  // extern "C"

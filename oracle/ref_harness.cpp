@@ -1,0 +1,406 @@
+// ref_harness.cpp -- builds oracle/_ref/libiconref.so from the REFERENCE's own
+// headers under /root/reference (TEST INFRASTRUCTURE ONLY; see oracle/Makefile).
+//
+// Compiled as-is from /root/reference (no stand-in headers): common/vecmath.h,
+// common/dvr_course-common-both.h (LCG, linear_to_srgb, make_rgba),
+// common/dvr_course-common.h (resampleLUT), common/camera.h (Camera),
+// common/thread_pool.h + common/for_each.h (the CPU parallel_for),
+// icon_rt/ICONGrid.h (ICONCell, sample, toSpherical/toCartesian),
+// icon_rt/ShellAccel.h (intersectSphere, sdda), icon_rt/DDA.h (linearIndex).
+//
+// icon_rt/deviceCode.cu itself cannot be compiled here: it includes Params.h,
+// which includes cuBQL/traversal/fixedBoxQuery.h from the un-vendored cuBQL
+// submodule (empty in the snapshot).  So the ~60 lines of raygen glue from
+// deviceCode.cu (generateRay 36-49, the CPU sampleVolume loop 116-123,
+// postClassify 127-135, woodcockTracking 149-186, the two raygens 239-341) and
+// the host setup / shell build from hostCode.cu (CUDA-only) are restated below
+// with the reference's own vector types and operators -- in particular the
+// unsequenced `dir_00 + (u+rnd())*dir_du + (v+rnd())*dir_dv` expression is kept
+// verbatim so the draw order is whatever g++ does for the reference.
+//
+// oracle/icon_oracle.cpp is an independent restatement; tests compare the two.
+
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include <dvr_course-common.h>
+#include <dvr_course-common.cuh>
+#include <for_each.h>
+#include <thread_pool.h>
+
+#include "DDA.h"
+#include "ICONGrid.h"
+#include "ShellAccel.h"
+
+using namespace dvr_course;
+using namespace icon_rt;
+
+static_assert(sizeof(ICONCell) == 284, "ICONCell layout");
+
+namespace {
+
+struct RefParams {
+  vec3f org, dir_00, dir_du, dir_dv;
+  int accumID;
+  vec3f ambientColor;
+  float ambientRadiance;
+  float unitDistance;
+  int raygen;
+  box3f bounds;
+  ShellAccel accel;
+  box1f tfRange;
+  float opacityScale;
+  const vec4f *lut;
+  int lutSize;
+  const ICONCell *cells;
+  int numCells;
+};
+
+struct Counters {
+  unsigned long long locate = 0, found = 0;
+};
+
+// deviceCode.cu:36-49 (expression kept as in the reference)
+inline Ray generateRay(const RefParams &lp, const vec2f screen, Random &rnd) {
+  vec3f org = lp.org;
+  vec3f dir = lp.dir_00 + (screen.u + rnd()) * lp.dir_du + (screen.v + rnd()) * lp.dir_dv;
+  dir = normalize(dir);
+  if (fabsf(dir.x) < 1e-5f) dir.x = 1e-5f;
+  if (fabsf(dir.y) < 1e-5f) dir.y = 1e-5f;
+  if (fabsf(dir.z) < 1e-5f) dir.z = 1e-5f;
+  return Ray(org, dir, 0.f, 1e10f);
+}
+
+// deviceCode.cu:116-123 (non-RTCORE branch)
+inline bool sampleVolume(const RefParams &lp, vec3f pos, float &value) {
+  for (unsigned i = 0; i < (unsigned)lp.numCells; ++i) {
+    if (sample(lp.cells[i], pos, value)) return true;
+  }
+  return false;
+}
+
+// deviceCode.cu:127-135
+inline vec4f postClassify(const RefParams &lp, float v) {
+  v = (v - lp.tfRange.lower) / (lp.tfRange.upper - lp.tfRange.lower);
+  int idx = v * (lp.lutSize);
+  float frac = (v * lp.lutSize) - idx;
+  vec4f v1 = lp.lut[clamp(idx, 0, lp.lutSize - 1)];
+  vec4f v2 = lp.lut[clamp(idx + 1, 0, lp.lutSize - 1)];
+  return v1 * frac + v2 * (1.f - frac) * vec4f(1, 1, 1, lp.opacityScale);
+}
+
+// deviceCode.cu:149-186
+inline float woodcockTracking(const RefParams &lp, const Ray &ray, Random &rnd, float majorant,
+                              vec3f &albedo, float &extinction, Counters &cnt) {
+  float t = ray.tmin;
+  while (1) {
+    if (majorant <= 0.f) break;
+    t -= (logf(1.f - rnd()) / (majorant / lp.unitDistance));
+    if (t > ray.tmax) break;
+    vec3f P = ray.org + ray.dir * t;
+    float value{0.f};
+    ++cnt.locate;
+    if (!sampleVolume(lp, P, value)) continue;
+    ++cnt.found;
+    vec4f s = postClassify(lp, value);
+    float u = rnd();
+    if (s.w >= u * majorant) {
+      albedo = vec3f(s.x, s.y, s.z);
+      extinction = s.w;
+      break;
+    }
+  }
+  return fminf(t, ray.tmax);
+}
+
+// deviceCode.cu:239-275 and 281-341, one pixel
+void raygen(const RefParams &lp, int x, int y, int W, int H, vec4f *accumBuffer,
+            uint32_t *fbPointer, Counters &cnt) {
+  const vec2i threadIndex(x, y);
+  const vec2i launchDim(W, H);
+  const int pixelID = threadIndex.x + launchDim.x * threadIndex.y;
+  Random rnd(lp.accumID * launchDim.x * launchDim.y + (unsigned)threadIndex.x,
+             (unsigned)threadIndex.y);
+  Ray ray = generateRay(lp, vec2f(threadIndex) + vec2f(.5f), rnd);
+  float t0, t1;
+  if (!boxTest(ray, lp.bounds, t0, t1)) return;
+  ray.tmin = t0, ray.tmax = t1;
+  vec3f color{0.f};
+  float alpha{0.f};
+  if (lp.raygen == 1) {
+    vec3f albedo = 0.f;
+    float extinction = 0.f;
+    woodcockTracking(lp, ray, rnd, 1.f, albedo, extinction, cnt);
+    color = albedo * lp.ambientColor * lp.ambientRadiance;
+    alpha = extinction > 0.f ? 1.f : 0.f;
+  } else {
+    const float *maxOpacities = lp.accel.maxOpacities;
+    auto woodcockFunc = [&](const int leafID, float t0, float t1) {
+      vec3f albedo = 0.f;
+      float extinction = 0.f;
+      const float majorant = maxOpacities[leafID];
+      ray.tmin = t0;
+      ray.tmax = t1;
+      float t = woodcockTracking(lp, ray, rnd, majorant, albedo, extinction, cnt);
+      if (t > t0 && t < t1) {
+        color = albedo * lp.ambientColor * lp.ambientRadiance;
+        alpha = extinction > 0.f ? 1.f : 0.f;
+        return false;
+      }
+      return true;
+    };
+    sdda(ray, lp.accel, woodcockFunc, false);
+  }
+  float accum = 1.f / (lp.accumID + 1);
+  accumBuffer[pixelID] = lerp(vec4f(color, alpha), accumBuffer[pixelID], accum);
+  vec4f accumColor = accumBuffer[pixelID];
+  accumColor.r = linear_to_srgb(accumColor.r);
+  accumColor.g = linear_to_srgb(accumColor.g);
+  accumColor.b = linear_to_srgb(accumColor.b);
+  fbPointer[pixelID] = make_rgba(accumColor);
+}
+
+// float atomicMin/Max semantics of hostCode.cu:36-56 (store only when strictly
+// smaller / larger), sequential.
+inline void fmin_store(float *a, float v) { if (v < *a) *a = v; }
+inline void fmax_store(float *a, float v) { if (v > *a) *a = v; }
+
+}  // namespace
+
+extern "C" {
+
+// ---- full frame on the reference's CPU parallel_for (64x64 tiles, thread_pool)
+int ref_render(const void *cells, int numCells, const float *camera12, int accumID,
+               const float *ambient4, float unitDistance, int raygenKind,
+               const float *bounds6, const int *dims, const float *sphericalBounds6,
+               const float *maxOpacities, const float *tf3, const float *lut, int lutSize,
+               int W, int H, int x0, int y0, int x1, int y1, float *accum, uint32_t *fb,
+               int nthreads, unsigned long long *counters2) {
+  RefParams lp;
+  lp.org = vec3f(camera12[0], camera12[1], camera12[2]);
+  lp.dir_00 = vec3f(camera12[3], camera12[4], camera12[5]);
+  lp.dir_du = vec3f(camera12[6], camera12[7], camera12[8]);
+  lp.dir_dv = vec3f(camera12[9], camera12[10], camera12[11]);
+  lp.accumID = accumID;
+  lp.ambientColor = vec3f(ambient4[0], ambient4[1], ambient4[2]);
+  lp.ambientRadiance = ambient4[3];
+  lp.unitDistance = unitDistance;
+  lp.raygen = raygenKind;
+  lp.bounds = box3f(vec3f(bounds6[0], bounds6[1], bounds6[2]),
+                    vec3f(bounds6[3], bounds6[4], bounds6[5]));
+  lp.accel.dims = vec3i(dims[0], dims[1], dims[2]);
+  lp.accel.sphericalBounds =
+      box3f(vec3f(sphericalBounds6[0], sphericalBounds6[1], sphericalBounds6[2]),
+            vec3f(sphericalBounds6[3], sphericalBounds6[4], sphericalBounds6[5]));
+  lp.accel.valueRanges = nullptr;
+  lp.accel.maxOpacities = const_cast<float *>(maxOpacities);
+  lp.tfRange = box1f(tf3[0], tf3[1]);
+  lp.opacityScale = tf3[2];
+  lp.lut = (const vec4f *)lut;
+  lp.lutSize = lutSize;
+  lp.cells = (const ICONCell *)cells;
+  lp.numCells = numCells;
+
+  if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
+  thread_pool pool((unsigned)nthreads);
+  std::vector<Counters> perThread(nthreads);
+  std::mutex mtx;
+  Counters total;
+  parallel::for_each(pool, x0, x1, y0, y1, [&](int x, int y) {
+    Counters c;
+    raygen(lp, x, y, W, H, (vec4f *)accum, fb, c);
+    std::lock_guard<std::mutex> g(mtx);
+    total.locate += c.locate;
+    total.found += c.found;
+  });
+  if (counters2) {
+    counters2[0] = total.locate;
+    counters2[1] = total.found;
+  }
+  return 0;
+}
+
+// ---- host setup restated from hostCode.cu:792-808 with the reference's types
+void ref_compute_bounds(const void *cellsv, int n, float *sb6, float *vb6, float *dr2) {
+  const ICONCell *cells = (const ICONCell *)cellsv;
+  box3f volbounds({INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY});
+  box1f dataRange(INFINITY, -INFINITY);
+  box3f sphericalBounds{vec3f(INFINITY), vec3f(-INFINITY)};
+  for (int i = 0; i < n; ++i) {
+    const ICONCell &cell = cells[i];
+    float minLat = fminf(cells[i].lat.x, fminf(cells[i].lat.y, cells[i].lat.z));
+    float maxLat = fmaxf(cells[i].lat.x, fmaxf(cells[i].lat.y, cells[i].lat.z));
+    float minLon = fminf(cells[i].lon.x, fminf(cells[i].lon.y, cells[i].lon.z));
+    float maxLon = fmaxf(cells[i].lon.x, fmaxf(cells[i].lon.y, cells[i].lon.z));
+    sphericalBounds.lower.x = fminf(sphericalBounds.lower.x, cell.height[0]);
+    sphericalBounds.upper.x = fmaxf(sphericalBounds.upper.x, cell.height[cell.numLayers]);
+    sphericalBounds.lower.y = fminf(sphericalBounds.lower.y, minLat);
+    sphericalBounds.upper.y = fmaxf(sphericalBounds.upper.y, maxLat);
+    sphericalBounds.lower.z = fminf(sphericalBounds.lower.z, minLon);
+    sphericalBounds.upper.z = fmaxf(sphericalBounds.upper.z, maxLon);
+    volbounds.extend(cell.getBounds());
+    for (int j = 0; j < cell.numLayers; ++j) dataRange.extend(cell.value[j]);
+  }
+  const float s[6] = {sphericalBounds.lower.x, sphericalBounds.lower.y, sphericalBounds.lower.z,
+                      sphericalBounds.upper.x, sphericalBounds.upper.y, sphericalBounds.upper.z};
+  const float v[6] = {volbounds.lower.x, volbounds.lower.y, volbounds.lower.z,
+                      volbounds.upper.x, volbounds.upper.y, volbounds.upper.z};
+  memcpy(sb6, s, sizeof(s));
+  memcpy(vb6, v, sizeof(v));
+  dr2[0] = dataRange.lower;
+  dr2[1] = dataRange.upper;
+}
+
+// ---- initGrid + buildShell_ICON (hostCode.cu:216-225, 299-336), sequential
+void ref_build_shell(const void *cellsv, int n, const int *dimsi, const float *sb6,
+                     float *valueRanges) {
+  const ICONCell *cells = (const ICONCell *)cellsv;
+  ShellAccel shell;
+  shell.dims = vec3i(dimsi[0], dimsi[1], dimsi[2]);
+  shell.sphericalBounds = box3f(vec3f(sb6[0], sb6[1], sb6[2]), vec3f(sb6[3], sb6[4], sb6[5]));
+  shell.valueRanges = (box1f *)valueRanges;
+  size_t numMCs = shell.dims.x * size_t(shell.dims.y) * shell.dims.z;
+  for (size_t mcID = 0; mcID < numMCs; ++mcID) shell.valueRanges[mcID] = box1f(FLT_MAX, -FLT_MAX);
+  for (int cellID = 0; cellID < n; ++cellID) {
+    const ICONCell &cell = cells[cellID];
+    for (int i = 0; i < cell.numLayers; ++i) {
+      vec3i c1 = projectToSphericalGrid(vec3f(cell.height[i], cell.lat.x, cell.lon.x), shell.dims, shell.sphericalBounds);
+      vec3i c2 = projectToSphericalGrid(vec3f(cell.height[i], cell.lat.y, cell.lon.y), shell.dims, shell.sphericalBounds);
+      vec3i c3 = projectToSphericalGrid(vec3f(cell.height[i], cell.lat.z, cell.lon.z), shell.dims, shell.sphericalBounds);
+      vec3i c4 = projectToSphericalGrid(vec3f(cell.height[i + 1], cell.lat.x, cell.lon.x), shell.dims, shell.sphericalBounds);
+      vec3i c5 = projectToSphericalGrid(vec3f(cell.height[i + 1], cell.lat.y, cell.lon.y), shell.dims, shell.sphericalBounds);
+      vec3i c6 = projectToSphericalGrid(vec3f(cell.height[i + 1], cell.lat.z, cell.lon.z), shell.dims, shell.sphericalBounds);
+      vec3i loMC = min(c1, min(c2, c3));
+      vec3i upMC = max(c4, max(c5, c6));
+      box1f range(cell.getValue(cell.height[i]), cell.getValue(cell.height[i + 1]));
+      for (int mcz = loMC.z; mcz <= upMC.z; ++mcz)
+        for (int mcy = loMC.y; mcy <= upMC.y; ++mcy)
+          for (int mcx = loMC.x; mcx <= upMC.x; ++mcx) {
+            const size_t linearID = linearIndex(vec3i(mcx, mcy, mcz), shell.dims);
+            box1f &vrange = shell.valueRanges[linearID];
+            fmin_store(&vrange.lower, range.lower);
+            fmax_store(&vrange.upper, range.upper);
+          }
+    }
+  }
+}
+
+// ---- computeMaxOpacities(ShellAccel) (hostCode.cu:362-397), sequential
+void ref_max_opacities(const float *valueRangesf, long numMCs, const float *lutf, int size,
+                       float tfLo, float tfHi, float *maxOpacities) {
+  const box1f *valueRanges = (const box1f *)valueRangesf;
+  const vec4f *rgbaLUT = (const vec4f *)lutf;
+  box1f tf_valueRange(tfLo, tfHi);
+  for (long mcID = 0; mcID < numMCs; ++mcID) {
+    box1f valueRange = valueRanges[mcID];
+    if (valueRange.upper < valueRange.lower) {
+      maxOpacities[mcID] = 0.f;
+      continue;
+    }
+    valueRange.lower -= tf_valueRange.lower;
+    valueRange.lower /= tf_valueRange.upper - tf_valueRange.lower;
+    valueRange.upper -= tf_valueRange.lower;
+    valueRange.upper /= tf_valueRange.upper - tf_valueRange.lower;
+    int lo = clamp(int(valueRange.lower * (size - 1)), 0, size - 1);
+    int hi = clamp(int(valueRange.upper * (size - 1)) + 1, 0, size - 1);
+    float maxOpacity = 0.f;
+    for (int i = lo; i <= hi; ++i) maxOpacity = fmaxf(maxOpacity, rgbaLUT[i].w);
+    maxOpacities[mcID] = maxOpacity;
+  }
+}
+
+// ---- resampleLUT (dvr_course-common.h:44-70) exactly as the reference
+void ref_resample_lut(const float *src, int nsrc, float *dst, int ndst) {
+  std::vector<vec4f> s(nsrc), d(ndst);
+  memcpy(s.data(), src, sizeof(vec4f) * nsrc);
+  resampleLUT(d, s);
+  memcpy(dst, d.data(), sizeof(vec4f) * ndst);
+}
+
+// ---- Camera (camera.h) as hostCode.cu:819-821,939-945 + pipeline.cu:444-454 use it
+void ref_camera(int useViewAll, const float *box6, const float *vp_vi_vu9, float fovyDeg,
+                float *out12) {
+  Camera cam;
+  if (useViewAll) {
+    cam.viewAll(box3f(vec3f(box6[0], box6[1], box6[2]), vec3f(box6[3], box6[4], box6[5])));
+  } else {
+    float fovy = fovyDeg;
+    if (fovy < 1e-3f) fovy = 90.f;
+    fovy = fovy * M_PI / 180.f;
+    cam.setOrientation(vec3f(vp_vi_vu9[0], vp_vi_vu9[1], vp_vi_vu9[2]),
+                       vec3f(vp_vi_vu9[3], vp_vi_vu9[4], vp_vi_vu9[5]),
+                       vec3f(vp_vi_vu9[6], vp_vi_vu9[7], vp_vi_vu9[8]), fovy);
+  }
+  vec3f ll, h, v;
+  cam.getScreen(ll, h, v);
+  vec3f o = cam.getPosition();
+  const float r[12] = {o.x, o.y, o.z, ll.x, ll.y, ll.z, h.x, h.y, h.z, v.x, v.y, v.z};
+  memcpy(out12, r, sizeof(r));
+}
+
+// ---- single-function known answers from the reference's own code
+void ref_lcg(unsigned s0, unsigned s1, int n, float *out) {
+  Random r(s0, s1);
+  for (int i = 0; i < n; ++i) out[i] = r();
+}
+int ref_sample(const void *cell, const float *pos3, float *value) {
+  float v = 0.f;
+  bool ok = sample(*(const ICONCell *)cell, vec3f(pos3[0], pos3[1], pos3[2]), v);
+  if (ok) *value = v;
+  return ok;
+}
+int ref_find_height(const void *cell, float h) { return ((const ICONCell *)cell)->findHeight(h); }
+int ref_intersect_sphere(const float *org3, const float *dir3, float radius, float *tn, float *tf) {
+  Ray r(vec3f(org3[0], org3[1], org3[2]), vec3f(dir3[0], dir3[1], dir3[2]), 0.f, 1e10f);
+  return intersectSphere(r, radius, *tn, *tf);
+}
+int ref_box_test(const float *org3, const float *dir3, float tmin, float tmax, const float *box6,
+                 float *t0, float *t1) {
+  Ray r(vec3f(org3[0], org3[1], org3[2]), vec3f(dir3[0], dir3[1], dir3[2]), tmin, tmax);
+  return boxTest(r, box3f(vec3f(box6[0], box6[1], box6[2]), vec3f(box6[3], box6[4], box6[5])), *t0, *t1);
+}
+int ref_sdda_trace(const float *org3, const float *dir3, float tmin, float tmax, const int *dimsi,
+                   const float *sb6, int maxOut, int *leaf, float *t0, float *t1) {
+  Ray r(vec3f(org3[0], org3[1], org3[2]), vec3f(dir3[0], dir3[1], dir3[2]), tmin, tmax);
+  ShellAccel a;
+  a.dims = vec3i(dimsi[0], dimsi[1], dimsi[2]);
+  a.sphericalBounds = box3f(vec3f(sb6[0], sb6[1], sb6[2]), vec3f(sb6[3], sb6[4], sb6[5]));
+  int count = 0;
+  sdda(r, a, [&](const int l, float a0, float a1) {
+    if (count < maxOut) { leaf[count] = l; t0[count] = a0; t1[count] = a1; }
+    ++count;
+    return count < 100000;
+  });
+  return count;
+}
+float ref_linear_to_srgb(float x) { return linear_to_srgb(x); }
+unsigned ref_make_rgba(const float *c) { return make_rgba(vec4f(c[0], c[1], c[2], c[3])); }
+void ref_to_spherical(const float *c, float *out) {
+  vec3f s = toSpherical(vec3f(c[0], c[1], c[2]));
+  out[0] = s.x; out[1] = s.y; out[2] = s.z;
+}
+void ref_to_cartesian(const float *s, float *out) {
+  vec3f c = toCartesian(vec3f(s[0], s[1], s[2]));
+  out[0] = c.x; out[1] = c.y; out[2] = c.z;
+}
+void ref_get_bounds(const void *cell, float *out6) {
+  box3f b = ((const ICONCell *)cell)->getBounds();
+  const float r[6] = {b.lower.x, b.lower.y, b.lower.z, b.upper.x, b.upper.y, b.upper.z};
+  memcpy(out6, r, sizeof(r));
+}
+// The unsequenced generateRay expression on its own: returns the two LCG draws in
+// the order they were consumed (draw #1 multiplies dir_du iff out[2] == 0).
+void ref_generate_ray(const float *camera12, int x, int y, unsigned s0, unsigned s1, float *dir3) {
+  RefParams lp;
+  lp.org = vec3f(camera12[0], camera12[1], camera12[2]);
+  lp.dir_00 = vec3f(camera12[3], camera12[4], camera12[5]);
+  lp.dir_du = vec3f(camera12[6], camera12[7], camera12[8]);
+  lp.dir_dv = vec3f(camera12[9], camera12[10], camera12[11]);
+  Random rnd(s0, s1);
+  Ray r = generateRay(lp, vec2f(vec2i(x, y)) + vec2f(.5f), rnd);
+  dir3[0] = r.dir.x; dir3[1] = r.dir.y; dir3[2] = r.dir.z;
+}
+
+}  // extern "C"
