@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""bench.py -- Mray/s + ms/frame of the MI355X ICON renderer (BASELINE.json metric).
+
+One step = one frame of the hot path: the raygen woodcockTrackingWithAccel
+(icon_rt/deviceCode.cu:281-341) over every pixel of the launch, plus -- for N > 1 GPUs --
+the RCCL gather of the frame tiles to rank 0 and rank 0's unpack.  Inputs (cells, locator,
+shell accelerator, transfer function) are resident in HBM before the timed region.
+
+Default workload (configs[2] of BASELINE.json, C3): synthetic R2B07 ICON grid (1,310,720
+cells) x 90 levels (3,932,160 `.ic` records), 1024x1024, framing camera
+`--camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60`, the reference's default transfer function.
+N GPUs split the SAME frame into interleaved 64x64 tiles (strong scaling); each rank runs
+one process (torchrun), rank 0 gathers RGBA8 tiles over RCCL.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "icon-ray-tracing_amd", "python"))
+
+METRIC = "Mray/s + ms/frame at 1024², R2B07 ICON grid, 1/2/4/8 MI355X vs host CPU"
+HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
+BYTES_PER_SAMPLE = 92  # geometry 36 + findHeight 20 + value 4 + 2 LUT entries 32
+BYTES_PER_RAY = 44     # accum read 16 + write 16 + RGBA8 4 + 2 majorants 8
+
+CONFIGS = {
+    # name: (rootN, bisections, levels, W, H, description)
+    "c2": (2, 5, 47, 512, 512, "C2: R2B05 (81,920 cells) x 47 levels, 512x512"),
+    "c3": (2, 7, 90, 1024, 1024, "C3: R2B07 (1,310,720 cells) x 90 levels, 1024x1024"),
+    "c4": (2, 7, 90, 2048, 2048, "C4: R2B07 (1,310,720 cells) x 90 levels, 2048x2048"),
+}
+FRAMING = ((0.0, 0.0, 1.4e7), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(cells, setup, W, H, budget_s=15.0):
+    """The reference's CPU path (brute-force sampleVolume, deviceCode.cu:116-123) on the
+    host cores, on a bounded centre crop of the same frame."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    threads = max(1, min(16, os.cpu_count() or 1))
+    S = O.OracleScene(cells)
+    S.set_transfunc(setup.lut, setup.value_range, setup.opacity_scale)
+    lp = setup.lp
+    cam = (np.array(lp.org.tolist(), np.float32), np.array(lp.dir_00.tolist(), np.float32),
+           np.array(lp.dir_du.tolist(), np.float32), np.array(lp.dir_dv.tolist(), np.float32))
+    params = S.params(cam, accum_id=0, raygen=lp.raygen, unit_distance=lp.unitDistance)
+    # An unbiased bounded sample: a regular sub-grid of the frame's pixels, refined until
+    # the run takes about budget_s/4 .. budget_s of CPU time.
+    stride, elapsed, pix, st = 128, 0.0, 0, None
+    while True:
+        ys, xs = np.mgrid[stride // 2:H:stride, stride // 2:W:stride]
+        xy = np.stack([xs.ravel(), ys.ravel()], axis=1).astype(np.int32)
+        t = time.perf_counter()
+        _, _, st = S.render_pixels(params, W, H, xy, threads=threads, fast=False)
+        elapsed = time.perf_counter() - t
+        pix = xy.shape[0]
+        log(f"[cpu baseline] stride {stride}: {pix} rays in {elapsed:.2f} s")
+        if elapsed > budget_s / 4 or stride <= 8:
+            break
+        stride //= 2
+    mray = pix / elapsed / 1e6
+    sample = (f"every {stride}th pixel in x and y of the {W}x{H} frame ({pix} rays, "
+              f"{st.locate_calls} sampleVolume calls, {elapsed:.1f} s on {threads} threads): "
+              f"the reference's CPU raygen with its brute-force first-hit cell scan over "
+              f"{cells.size} records (deviceCode.cu:116-123), oracle restatement, literal "
+              f"sample() incl. toSpherical")
+    kind = "port"
+    return {"value": mray, "unit": "Mray/s", "cores": threads, "kind": kind, "sample": sample,
+            "ms_per_frame_extrapolated": W * H / (mray * 1e6) * 1e3}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    args = ap.parse_args()
+
+    import torch
+    import irt
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    device = local if world > 1 else 0
+    torch.cuda.set_device(device)
+    dev = torch.device(f"cuda:{device}")
+
+    rn, bis, L, W, H, desc = CONFIGS[args.config]
+    t0 = time.time()
+    cells = irt.synth_grid(rn, bis, L)
+    log(f"[rank {rank}] grid: {cells.size} records ({time.time() - t0:.1f} s)")
+    setup = irt.setup_frame(cells, W, H, camera=FRAMING)
+    t0 = time.time()
+    ctx = irt.Context(cells, device)
+    ctx.set_transfunc(setup.lut, setup.value_range, setup.opacity_scale)
+    log(f"[rank {rank}] context: {ctx.info.deviceBytes / 2**30:.2f} GiB HBM, locator G="
+        f"{ctx.info.locatorFaceRes} entries={ctx.info.locatorEntries} ({time.time() - t0:.1f} s)")
+
+    lp = setup.lp
+    ntiles = irt.num_tiles(W, H)
+    stream = torch.cuda.current_stream(device).cuda_stream
+    if world == 1:
+        fb = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        accum = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+        ctx.clear(fb.data_ptr(), accum.data_ptr(), W * H, stream)
+    else:
+        maxt = (ntiles + world - 1) // world
+        tiles_fb = torch.zeros(maxt * 4096, dtype=torch.int32, device=dev)
+        tiles_acc = torch.zeros(maxt * 4096 * 4, dtype=torch.float32, device=dev)
+        gathered = [torch.zeros_like(tiles_fb) for _ in range(world)] if rank == 0 else None
+        gbuf = torch.zeros(world * maxt * 4096, dtype=torch.int32, device=dev) if rank == 0 else None
+        fb = torch.zeros(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
+
+    kernel_ms, samples, in_box, launched = [], 0, 0, 0
+
+    def step(frame):
+        nonlocal samples, in_box, launched
+        lp.accumID = frame
+        if world == 1:
+            ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
+        else:
+            ctx.render_tiles(lp, W, H, rank, world, tiles_fb.data_ptr(), tiles_acc.data_ptr(), stream)
+            dist.gather(tiles_fb, gathered, dst=0)
+            if rank == 0:
+                torch.cat(gathered, out=gbuf)
+                ctx.unpack_tiles(gbuf.data_ptr(), world, maxt, W, H, fb.data_ptr(), stream)
+        st = ctx.stats()  # waits for this frame's kernel (like the reference's endTiming)
+        return st
+
+    for f in range(args.warmup):
+        st = step(f)
+        log(f"[rank {rank}] warmup frame {f}: kernel {st.kernelMs:.3f} ms, "
+            f"{st.samplesFound} samples, {st.candidatesTested} candidates")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        st = step(args.warmup + k)
+        kernel_ms.append(st.kernelMs)
+        samples += st.samplesFound
+        in_box += st.raysInBox
+        launched += st.raysLaunched
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    log(f"[rank {rank}] timed {args.steps} frames in {elapsed:.3f} s")
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        agg = torch.tensor([samples, in_box, launched], dtype=torch.float64, device=dev)
+        dist.all_reduce(agg)
+        samples_all, in_box_all, launched_all = (int(v) for v in agg.tolist())
+    else:
+        samples_all, in_box_all, launched_all = samples, in_box, launched
+
+    ms_per_step = elapsed / args.steps * 1e3
+    mray = W * H * args.steps / elapsed / 1e6
+    # roofline of the dominant kernel (k_render) on this rank: algorithmic bytes per launch
+    # over its HIP-event-timed average duration
+    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3 if kernel_ms else float("nan")
+    bytes_per_launch = (BYTES_PER_SAMPLE * samples + BYTES_PER_RAY * in_box) / max(args.steps, 1)
+    achieved = bytes_per_launch / avg_kernel_s
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(mray, 3),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": desc + ", framing camera --camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60, "
+                           "woodcockTrackingWithAccel, default TF, one frame per step",
+                "records": int(cells.size), "width": W, "height": H,
+                "parallelism": f"frame-tiles x{world} (64x64, interleaved), RCCL gather to rank 0"
+                if world > 1 else "single GPU",
+                "samples_per_frame": samples_all / args.steps,
+                "rays_in_box_per_frame": in_box_all / args.steps,
+                "kernel_ms_rank0": round(avg_kernel_s * 1e3, 4),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved / 1e9, 3),
+                "peak": HBM_PEAK / 1e9,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK,
+                "traffic": None,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cells, setup, W, H, args.cpu_budget)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

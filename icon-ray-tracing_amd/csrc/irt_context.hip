@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "irt_internal.h"
+#include "icon_rt_hip_debug.h"
 #include "irt_kernels.h"
 
 using namespace irt;
@@ -383,3 +384,42 @@ int irt_get_shell(const irt_context *c, float *valueRanges, float *maxOpacities)
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- debug (device math)
+namespace {
+__global__ void k_debug_math(const float *a, const float *y, const float *x, int n, float *oa,
+                             float *ot) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  oa[i] = glibc_asinf(a[i]);
+  ot[i] = glibc_atan2f(y[i], x[i]);
+}
+}  // namespace
+
+extern "C" int irt_debug_device_math(int device, const float *a, const float *y, const float *x,
+                                     int n, float *oa, float *ot) {
+  if (n <= 0 || !a || !y || !x || !oa || !ot) {
+    set_error("irt_debug_device_math: bad argument");
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(device));
+  float *d = nullptr;
+  IRT_HIP(hipMalloc((void **)&d, 5 * (size_t)n * sizeof(float)));
+  hipError_t e = hipSuccess;
+  e = e == hipSuccess ? hipMemcpy(d, a, n * sizeof(float), hipMemcpyHostToDevice) : e;
+  e = e == hipSuccess ? hipMemcpy(d + n, y, n * sizeof(float), hipMemcpyHostToDevice) : e;
+  e = e == hipSuccess ? hipMemcpy(d + 2 * (size_t)n, x, n * sizeof(float), hipMemcpyHostToDevice) : e;
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_debug_math, dim3((n + 255) / 256), dim3(256), 0, 0, d, d + n,
+                       d + 2 * (size_t)n, n, d + 3 * (size_t)n, d + 4 * (size_t)n);
+    e = hipGetLastError();
+  }
+  e = e == hipSuccess ? hipMemcpy(oa, d + 3 * (size_t)n, n * sizeof(float), hipMemcpyDeviceToHost) : e;
+  e = e == hipSuccess ? hipMemcpy(ot, d + 4 * (size_t)n, n * sizeof(float), hipMemcpyDeviceToHost) : e;
+  (void)hipFree(d);
+  if (e != hipSuccess) {
+    set_error("irt_debug_device_math: %s", hipGetErrorString(e));
+    return IRT_E_HIP;
+  }
+  return IRT_OK;
+}

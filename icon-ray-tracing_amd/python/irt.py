@@ -85,6 +85,14 @@ def lib() -> C.CDLL:
     """Load the in-tree product library (fails loudly if it was not built)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 (soname
+        # libamdhip64.so.7, like /opt/rocm's).  Loading torch first makes the dynamic
+        # linker bind our library to that same runtime, so torch tensors' device pointers,
+        # streams and RCCL are shared with the kernels.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise IrtError(f"{LIB_PATH} not built; run `make -C icon-ray-tracing_amd` "
                            "(or __graft_entry__.build())")

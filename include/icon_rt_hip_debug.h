@@ -38,6 +38,12 @@ int irt_debug_scene_candidates(const irt_debug_scene *s, irt_vec3f p, uint32_t *
 int irt_debug_scene_planes(const irt_debug_scene *s, uint32_t record, float *out12);
 void irt_debug_scene_free(irt_debug_scene *s);
 
+/* Evaluate the kernels' device versions of asinf(a[i]), atan2f(y[i], x[i]) and the
+ * LCG draw sequence on GPU `device` (host arrays in/out; n elements each).  Used to prove
+ * the device restatements round exactly like the host glibc. */
+int irt_debug_device_math(int device, const float *a, const float *y, const float *x, int n,
+                          float *out_asinf, float *out_atan2f);
+
 #ifdef __cplusplus
 }
 #endif

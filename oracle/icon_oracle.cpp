@@ -742,6 +742,46 @@ int oracle_render(const oc_cell *cells, size_t n, const oc_params *p, int W, int
   return 0;
 }
 
+int oracle_render_pixels(const oc_cell *cells, size_t n, const oc_params *p, int W, int H,
+                         const int32_t *xy, int numPixels, float *accum, uint32_t *fb,
+                         int nthreads, int fast, oc_stats *stats) {
+  if (!p || W <= 0 || H <= 0 || numPixels < 0) return -1;
+  for (int i = 0; i < numPixels; ++i)
+    if (xy[2 * i] < 0 || xy[2 * i] >= W || xy[2 * i + 1] < 0 || xy[2 * i + 1] >= H) return -1;
+  Scene S{cells, n, fast != 0, {}};
+  if (S.fast) {
+    S.planes.resize(n);
+    for (size_t i = 0; i < n; ++i) S.planes[i] = cellPlanes(cells[i]);
+  }
+  std::atomic<int> counter{0};
+  if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
+  if (nthreads <= 0) nthreads = 1;
+  std::vector<ThreadStats> tstats(nthreads);
+  auto worker = [&](int tid) {
+    for (;;) {
+      int i = counter.fetch_add(1);
+      if (i >= numPixels) break;
+      raygen(S, *p, xy[2 * i], xy[2 * i + 1], W, H, accum, fb, tstats[tid]);
+    }
+  };
+  std::vector<std::thread> threads;
+  for (int t = 1; t < nthreads; ++t) threads.emplace_back(worker, t);
+  worker(0);
+  for (auto &t : threads) t.join();
+  if (stats) {
+    memset(stats, 0, sizeof(*stats));
+    for (auto &ts : tstats) {
+      stats->rays_launched += ts.launched;
+      stats->rays_in_box += ts.inBox;
+      stats->locate_calls += ts.locate;
+      stats->samples_found += ts.found;
+      stats->rng_draws += ts.draws;
+      stats->leaves += ts.leaves;
+    }
+  }
+  return 0;
+}
+
 // ------------------------------------------------------------------ KATs
 void oracle_lcg(uint32_t seed0, uint32_t seed1, int n, float *out) {
   LCG r(seed0, seed1);

@@ -110,6 +110,13 @@ int oracle_render(const oc_cell *cells, size_t n, const oc_params *p, int W, int
                   int x0, int y0, int x1, int y1, float *accum, uint32_t *fb,
                   int nthreads, int fast, oc_stats *stats);
 
+/* The same raygen for an explicit list of pixels (xy pairs), scheduled one pixel at a
+   time over `nthreads` threads -- used to time a bounded, unbiased sample of a frame
+   (bench.py's cpu_baseline).  Writes accum/fb at the pixels' frame positions. */
+int oracle_render_pixels(const oc_cell *cells, size_t n, const oc_params *p, int W, int H,
+                         const int32_t *xy, int numPixels, float *accum, uint32_t *fb,
+                         int nthreads, int fast, oc_stats *stats);
+
 /* ---- known-answer helpers (single functions) ---- */
 void oracle_lcg(uint32_t seed0, uint32_t seed1, int n, float *out);            /* dvr_course-common-both.h:41-86 */
 int oracle_sample(const oc_cell *cell, oc_vec3 pos, float *value);              /* ICONGrid.h:181-208 */

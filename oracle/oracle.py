@@ -85,6 +85,9 @@ def olib() -> C.CDLL:
         L.oracle_render.argtypes = [P, S, C.POINTER(OParams), I, I, I, I, I, I, P, P, I, I,
                                     C.POINTER(OStats)]
         L.oracle_render.restype = I
+        L.oracle_render_pixels.argtypes = [P, S, C.POINTER(OParams), I, I, P, I, P, P, I, I,
+                                           C.POINTER(OStats)]
+        L.oracle_render_pixels.restype = I
         L.oracle_lcg.argtypes = [C.c_uint32, C.c_uint32, I, P]
         L.oracle_sample.argtypes = [P, OVec3, C.POINTER(C.c_float)]
         L.oracle_find_height.argtypes = [P, F]
@@ -227,6 +230,19 @@ class OracleScene:
         rc = olib().oracle_render(_p(self.cells), self.cells.size, C.byref(params), width, height,
                                   x0, y0, x1, y1, _p(accum), _p(fb), threads, 1 if fast else 0,
                                   C.byref(st))
+        assert rc == 0
+        return accum, fb, st
+
+    def render_pixels(self, params: OParams, width, height, xy: np.ndarray, threads=0,
+                      fast=False):
+        """Raygen over an explicit pixel list (n,2) int32; returns (accum, fb, stats)."""
+        xy = np.ascontiguousarray(xy, dtype=np.int32).reshape(-1, 2)
+        accum = np.zeros((height, width, 4), dtype=np.float32)
+        fb = np.zeros((height, width), dtype=np.uint32)
+        st = OStats()
+        rc = olib().oracle_render_pixels(_p(self.cells), self.cells.size, C.byref(params), width,
+                                         height, _p(xy), xy.shape[0], _p(accum), _p(fb), threads,
+                                         1 if fast else 0, C.byref(st))
         assert rc == 0
         return accum, fb, st
 

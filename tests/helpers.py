@@ -1,0 +1,71 @@
+"""Shared scene/frame helpers for the test-suite (oracle on the CPU, product on the GPU)."""
+import numpy as np
+
+import irt
+import oracle as O
+
+FRAMING = irt.FRAMING_CAMERA
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def oracle_frame(cells, W, H, camera=None, accum_ids=(0,), raygen=0, lut=None, value_range=None,
+                 opacity_scale=1.0, unit_distance=None, threads=0, rect=None):
+    """Oracle frames with the reference's main()-style setup; returns (accum, fb, stats, scene)."""
+    S = O.OracleScene(cells)
+    if lut is None:
+        lut, vr = S.default_lut()
+        value_range = vr if value_range is None else value_range
+    S.set_transfunc(lut, value_range, opacity_scale)
+    cam = S.camera(W, H, camera)
+    accum = np.zeros((H, W, 4), np.float32)
+    fb = np.zeros((H, W), np.uint32)
+    stats = []
+    for aid in accum_ids:
+        p = S.params(cam, accum_id=aid, raygen=raygen, unit_distance=unit_distance)
+        _, _, st = S.render(p, W, H, rect=rect, accum=accum, fb=fb, threads=threads)
+        stats.append(st)
+    return accum, fb, stats, S
+
+
+class GpuFrame:
+    """Device framebuffer (torch tensors as HBM allocations) for one context."""
+
+    def __init__(self, ctx, W, H):
+        import torch
+        self.torch = torch
+        self.ctx, self.W, self.H = ctx, W, H
+        self.fb = torch.zeros(W * H, dtype=torch.int32, device=f"cuda:{ctx.device}")
+        self.accum = torch.zeros(W * H * 4, dtype=torch.float32, device=f"cuda:{ctx.device}")
+
+    def render(self, lp):
+        s = self.torch.cuda.current_stream(self.ctx.device).cuda_stream
+        self.ctx.render(lp, self.W, self.H, self.fb.data_ptr(), self.accum.data_ptr(), s)
+        self.torch.cuda.synchronize(self.ctx.device)
+        return self.ctx.stats()
+
+    def host(self):
+        a = self.accum.cpu().numpy().reshape(self.H, self.W, 4)
+        f = self.fb.cpu().numpy().view(np.uint32).reshape(self.H, self.W)
+        return a, f
+
+
+def gpu_frame(cells, W, H, camera=None, accum_ids=(0,), raygen=0, lut=None, value_range=None,
+              opacity_scale=1.0, device=0, unit_distance=None):
+    setup = irt.setup_frame(cells, W, H, camera=camera, raygen=raygen)
+    if lut is None:
+        lut, value_range = setup.lut, setup.value_range
+    ctx = irt.Context(cells, device)
+    ctx.set_transfunc(lut, value_range, opacity_scale)
+    fr = GpuFrame(ctx, W, H)
+    stats = []
+    lp = setup.lp
+    if unit_distance is not None:
+        lp.unitDistance = unit_distance
+    for aid in accum_ids:
+        lp.accumID = aid
+        stats.append(fr.render(lp))
+    a, f = fr.host()
+    return a, f, stats, ctx
