@@ -46,7 +46,7 @@ def log(*a):
 
 def cpu_baseline(cells, setup, W, H, budget_s=15.0):
     """The reference's CPU path (brute-force sampleVolume, deviceCode.cu:116-123) on the
-    host cores, on a bounded centre crop of the same frame."""
+    host cores, on a bounded strided sample of the same frame's pixels."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     threads = max(1, min(16, os.cpu_count() or 1))
@@ -124,11 +124,12 @@ def main():
         accum = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
         ctx.clear(fb.data_ptr(), accum.data_ptr(), W * H, stream)
     else:
-        maxt = (ntiles + world - 1) // world
-        tiles_fb = torch.zeros(maxt * 4096, dtype=torch.int32, device=dev)
+        import irt_dist
+        split = irt_dist.TileSplit(W, H, rank, world)
+        assert split.num_tiles == ntiles
+        maxt = split.max_tiles
+        fg = irt_dist.FrameGather(split, dev)
         tiles_acc = torch.zeros(maxt * 4096 * 4, dtype=torch.float32, device=dev)
-        gathered = [torch.zeros_like(tiles_fb) for _ in range(world)] if rank == 0 else None
-        gbuf = torch.zeros(world * maxt * 4096, dtype=torch.int32, device=dev) if rank == 0 else None
         fb = torch.zeros(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
 
     kernel_ms, samples, in_box, launched = [], 0, 0, 0
@@ -139,11 +140,10 @@ def main():
         if world == 1:
             ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
         else:
-            ctx.render_tiles(lp, W, H, rank, world, tiles_fb.data_ptr(), tiles_acc.data_ptr(), stream)
-            dist.gather(tiles_fb, gathered, dst=0)
+            ctx.render_tiles(lp, W, H, rank, world, fg.tiles.data_ptr(), tiles_acc.data_ptr(), stream)
+            g = fg.gather()  # RCCL gather of the packed RGBA8 tiles to rank 0
             if rank == 0:
-                torch.cat(gathered, out=gbuf)
-                ctx.unpack_tiles(gbuf.data_ptr(), world, maxt, W, H, fb.data_ptr(), stream)
+                ctx.unpack_tiles(g.data_ptr(), world, maxt, W, H, fb.data_ptr(), stream)
         st = ctx.stats()  # waits for this frame's kernel (like the reference's endTiming)
         return st
 

@@ -1,0 +1,89 @@
+"""irt_dist -- multi-GPU frame splitting for the ICON renderer (one process per GPU).
+
+The reference is single-device; its CPU path already cuts a frame into 64x64 tiles pulled
+by a thread pool (common/for_each.h:70-85, common/thread_pool.h:146-161).  Here the same
+tiles are dealt round-robin to N ranks (tile t -> rank t mod N, which balances the globe in
+the middle of the frame), every rank renders its tiles into a packed buffer
+(irt_render_tiles), and rank 0 gathers the RGBA8 tiles over RCCL (torch.distributed,
+backend "nccl") and scatters them into the framebuffer (irt_unpack_tiles).  Pixel seeds
+depend only on (accumID, W, H, x, y) (deviceCode.cu:288-289), so the assembled frame is
+bit-identical to a single-GPU launch.  The accumulation buffer stays sharded: each rank
+keeps the accum of its own tiles across frames (progressive rendering needs no exchange).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+TILE = 64
+TILE_PIX = TILE * TILE
+
+
+@dataclass(frozen=True)
+class TileSplit:
+    width: int
+    height: int
+    rank: int
+    world: int
+
+    @property
+    def tiles_x(self) -> int:
+        return (self.width + TILE - 1) // TILE
+
+    @property
+    def num_tiles(self) -> int:
+        return self.tiles_x * ((self.height + TILE - 1) // TILE)
+
+    @property
+    def max_tiles(self) -> int:
+        return (self.num_tiles + self.world - 1) // self.world
+
+    def tiles(self, rank: int | None = None) -> list[int]:
+        r = self.rank if rank is None else rank
+        return list(range(r, self.num_tiles, self.world))
+
+    def tile_pixels(self, tile: int) -> np.ndarray:
+        """(x, y) of the in-frame pixels of a tile, in packed (ly*64 + lx) order, with -1
+        for pixels past the frame edge."""
+        tx, ty = tile % self.tiles_x, tile // self.tiles_x
+        ly, lx = np.mgrid[0:TILE, 0:TILE]
+        x, y = tx * TILE + lx.ravel(), ty * TILE + ly.ravel()
+        inside = (x < self.width) & (y < self.height)
+        return np.stack([np.where(inside, x, -1), np.where(inside, y, -1)], 1)
+
+
+def unpack_host(gathered: np.ndarray, split: TileSplit) -> np.ndarray:
+    """Host twin of irt_unpack_tiles: rank-major packed tiles -> (H, W) framebuffer."""
+    fb = np.zeros((split.height, split.width), dtype=gathered.dtype)
+    g = gathered.reshape(split.world, split.max_tiles, TILE_PIX)
+    for r in range(split.world):
+        for k, t in enumerate(split.tiles(r)):
+            xy = split.tile_pixels(t)
+            ok = xy[:, 0] >= 0
+            fb[xy[ok, 1], xy[ok, 0]] = g[r, k, ok]
+    return fb
+
+
+class FrameGather:
+    """Per-frame RCCL gather of packed RGBA8 tiles to rank 0 (torch.distributed)."""
+
+    def __init__(self, split: TileSplit, device):
+        import torch
+        import torch.distributed as dist
+        self.dist, self.torch, self.split = dist, torch, split
+        n = split.max_tiles * TILE_PIX
+        self.tiles = torch.zeros(n, dtype=torch.int32, device=device)
+        self.parts = ([torch.zeros_like(self.tiles) for _ in range(split.world)]
+                      if split.rank == 0 else None)
+        self.gathered = (torch.zeros(split.world * n, dtype=torch.int32, device=device)
+                         if split.rank == 0 else None)
+
+    def gather(self):
+        """Collective: every rank calls it after rendering into self.tiles.  On rank 0
+        returns the rank-major gathered tensor, elsewhere None."""
+        self.dist.gather(self.tiles, self.parts, dst=0)
+        if self.split.rank != 0:
+            return None
+        self.torch.cat(self.parts, out=self.gathered)
+        return self.gathered

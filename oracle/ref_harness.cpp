@@ -204,17 +204,25 @@ int ref_render(const void *cells, int numCells, const float *camera12, int accum
   lp.numCells = numCells;
 
   if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
-  thread_pool pool((unsigned)nthreads);
-  std::vector<Counters> perThread(nthreads);
   std::mutex mtx;
   Counters total;
-  parallel::for_each(pool, x0, x1, y0, y1, [&](int x, int y) {
+  auto pixel = [&](int x, int y) {
     Counters c;
     raygen(lp, x, y, W, H, (vec4f *)accum, fb, c);
     std::lock_guard<std::mutex> g(mtx);
     total.locate += c.locate;
     total.found += c.found;
-  });
+  };
+  if (nthreads == 1) {
+    // serial::for_each (common/for_each.h:18-37).  The reference's thread_pool publishes
+    // `start_threads` and notify_all()s without holding its mutex (thread_pool.h:88-107,
+    // 129-139), a lost-wakeup window that deadlocked golden generation here once; the
+    // schedule never changes a pixel, so fixtures are made serially.
+    serial::for_each(x0, x1, y0, y1, pixel);
+  } else {
+    thread_pool pool((unsigned)nthreads);
+    parallel::for_each(pool, x0, x1, y0, y1, pixel);
+  }
   if (counters2) {
     counters2[0] = total.locate;
     counters2[1] = total.found;

@@ -1,0 +1,169 @@
+"""Host logic of the product (no GPU): the setup of icon_rt's main() as the C ABI exposes
+it, the libm restatements and tables the kernels use, and the cell locator that replaces
+the reference's cell location -- each checked against the oracle / golden fixtures."""
+import ctypes as C
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+import irt
+import oracle as O
+from golden_util import FRAME_FIXTURES, load
+from helpers import FRAMING, bits
+
+
+@pytest.mark.parametrize("name", FRAME_FIXTURES)
+def test_volume_info_tf_camera_match_fixture(name):
+    d = load(name)
+    cells = d["cells"]
+    info = irt.volume_info(cells)
+    sb = [info.sphericalBounds.lower.x, info.sphericalBounds.lower.y, info.sphericalBounds.lower.z,
+          info.sphericalBounds.upper.x, info.sphericalBounds.upper.y, info.sphericalBounds.upper.z]
+    vb = [info.bounds.lower.x, info.bounds.lower.y, info.bounds.lower.z, info.bounds.upper.x,
+          info.bounds.upper.y, info.bounds.upper.z]
+    assert np.array_equal(bits(sb), bits(d["spherical_bounds"]))
+    assert np.array_equal(bits(vb), bits(d["volume_bounds"]))
+    assert np.array_equal(bits([info.dataRange.lower, info.dataRange.upper]), bits(d["data_range"]))
+    assert np.float32(info.unitDistance) == d["unit_distance"]
+    if float(d["opacity_scale"]) == 1.0:  # default-TF fixtures
+        lut, vr = irt.default_transfunc((info.dataRange.lower, info.dataRange.upper))
+        assert np.array_equal(bits(lut), bits(d["lut"]))
+        assert np.array_equal(bits(vr), bits(d["value_range"]))
+
+
+def test_cameras_match_reference_kats():
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "kats.npz"))
+    b6 = z["camera_box6"]
+    box = irt.Box3(irt.vec3(b6[:3]), irt.vec3(b6[3:]))
+    lp = irt.camera_view_all(box, 1, 1)
+    assert np.array_equal(bits(lp.camera12()), bits(z["cameras"][0]))
+    for spec, ref in zip(z["camera_specs"], z["cameras"][1:]):
+        lp = irt.camera_look_at(spec[0:3], spec[3:6], spec[6:9], float(spec[9]), 1, 1)
+        assert np.array_equal(bits(lp.camera12()), bits(ref))
+    src = z["lut_src"]
+    assert np.array_equal(bits(irt.resample_lut(src, 300)), bits(z["lut_300"]))
+
+
+def test_filter_and_ic_io_roundtrip():
+    cells = irt.synth_grid(2, 2, 35)
+    for lat, lon in [((-30, 60), (-90, 45)), ((0, 90), (-180, 180)), ((-5, 5), (10, 11))]:
+        a = irt.filter_cells(cells, lat, lon)
+        b = np.array(cells, copy=True)
+        n = O.olib().oracle_filter_cells(b.ctypes.data, b.size, lat[0], lat[1], lon[0], lon[1])
+        assert a.size == n and a.tobytes() == b[:n].tobytes()
+    with tempfile.TemporaryDirectory() as t:
+        p = os.path.join(t, "grid.ic")
+        irt.save_ic(p, cells)
+        assert os.path.getsize(p) == 284 * cells.size
+        back = irt.load_ic(p)
+        assert back.tobytes() == cells.tobytes()
+        assert irt.load_ic(p, 12).tobytes() == cells[:12].tobytes()  # --num-cells 12
+
+
+def test_synthetic_grid_shape():
+    for rn, bis, L in [(1, 0, 4), (2, 0, 90), (2, 3, 31), (2, 2, 32)]:
+        cells = irt.synth_grid(rn, bis, L)
+        per_col = (L + 30) // 31
+        assert cells.size == 20 * rn * rn * 4 ** bis * per_col
+        nl = cells["numLayers"].reshape(-1, per_col)
+        assert (nl.sum(1) == L).all() and (nl <= 31).all()
+        h = cells["height"].reshape(-1, per_col, 32)
+        for r in range(per_col - 1):  # consecutive records share the boundary height
+            assert (h[:, r, nl[0, r]] == h[:, r + 1, 0]).all()
+        assert cells["value"].max() <= 1.0 and cells["value"].min() >= 0.0
+
+
+def test_libm_restatements_match_glibc():
+    libm = C.CDLL("libm.so.6")
+    libm.asinf.restype = libm.atan2f.restype = libm.logf.restype = C.c_float
+    libm.asinf.argtypes = [C.c_float]
+    libm.atan2f.argtypes = [C.c_float, C.c_float]
+    libm.logf.argtypes = [C.c_float]
+    L = irt.lib()
+    rng = np.random.default_rng(1)
+    xs = np.concatenate([rng.uniform(-1, 1, 30000), [0.0, -0.0, 1.0, -1.0, 0.975, 0.5, 1e-30, -1e-9]]).astype(np.float32)
+    for x in xs:
+        assert np.float32(L.irt_debug_asinf(float(x))).view(np.uint32) == np.float32(libm.asinf(float(x))).view(np.uint32)
+    ys = (rng.normal(size=30000) * 7e6).astype(np.float32)
+    xs2 = (rng.normal(size=30000) * 7e6).astype(np.float32)
+    ys[:50] = 0
+    xs2[50:100] = 0
+    for y, x in zip(ys, xs2):
+        a, b = L.irt_debug_atan2f(float(y), float(x)), libm.atan2f(float(y), float(x))
+        assert np.float32(a).view(np.uint32) == np.float32(b).view(np.uint32)
+    for k in list(range(0, 1 << 24, 9973)) + [0, 1, 2, 12, (1 << 24) - 1]:
+        x = np.float32(1.0) - np.float32(k) / np.float32(1 << 24)
+        assert np.float32(L.irt_debug_logf_entry(k)).view(np.uint32) == np.float32(libm.logf(float(x))).view(np.uint32)
+    for f in [0.5, -0.5, 1e10, -1e10, 2147483520.0, 2147483648.0, -2147483648.0, float("nan"), float("inf")]:
+        v = L.irt_debug_f2i(f)
+        ref = int(f) if np.isfinite(f) and -2147483648.0 <= f < 2147483648.0 else -2147483648
+        assert v == ref, f
+
+
+def test_srgb_thresholds_reproduce_make_8bit():
+    """The kernels map accum -> RGBA8 by binary search in 255 host-built thresholds; that
+    must equal make_8bit(linear_to_srgb(x)) for every x (checked on a dense sweep and
+    around every threshold)."""
+    th = np.zeros(256, np.float32)
+    irt.lib().irt_debug_srgb_thresholds(th.ctypes.data)
+    assert np.all(np.diff(th[1:]) >= 0)
+    L = O.olib()
+
+    def ref_byte(x):  # deviceCode.cu:336-340: srgb on rgb, then make_rgba
+        c = np.array([L.oracle_linear_to_srgb(x), 0, 0, 0], np.float32)
+        return L.oracle_make_rgba(c.ctypes.data) & 0xFF
+
+    def byte(x):
+        return int(np.searchsorted(th[1:], np.float32(x), side="right"))
+    xs = np.concatenate([np.linspace(-0.1, 1.1, 20001, dtype=np.float32),
+                         np.float32([0.0, 0.0031308, 1.0, 2.0, -1.0])])
+    for x in xs:
+        assert byte(x) == ref_byte(float(x)), x
+    for b in range(1, 256):
+        t = th[b]
+        below = np.nextafter(t, np.float32(-1))
+        assert byte(t) == ref_byte(float(t)) and byte(below) == ref_byte(float(below))
+
+
+@pytest.mark.parametrize("rn,bis,L", [(1, 0, 4), (2, 2, 40), (2, 3, 90)])
+def test_locator_is_conservative_and_lowest_index(rn, bis, L):
+    """sampleVolume over the cube-map lists == the reference's first-hit linear scan, on
+    random points, points exactly on layer boundaries and points on shared triangle
+    edges (where neighbouring cells tie and the lower index must win)."""
+    cells = irt.synth_grid(rn, bis, L)
+    D = irt.DebugScene(cells)
+    Lb = O.olib()
+    rng = np.random.default_rng(rn * 100 + bis)
+    pts = []
+    sbl = float(cells["height"][:, 0].min())
+    sbu = float(np.max(cells["height"][np.arange(cells.size), cells["numLayers"]]))
+    d = rng.normal(size=(400, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    pts += list((d * rng.uniform(sbl - 50, sbu + 50, (400, 1))).astype(np.float32))
+    for i in rng.choice(cells.size, 60):
+        c = cells[i]
+        lat, lon = c["lat"].astype(np.float64), c["lon"].astype(np.float64)
+        cd = np.stack([np.cos(lat) * np.cos(lon), np.cos(lat) * np.sin(lon), np.sin(lat)], 1)
+        for j in (0, c["numLayers"] // 2, c["numLayers"]):
+            v = cd.mean(0)
+            pts.append((v / np.linalg.norm(v) * np.float64(c["height"][j])).astype(np.float32))
+        for a, b in ((0, 1), (1, 2), (2, 0)):  # edge midpoints and a corner
+            v = cd[a] + cd[b]
+            pts.append((v / np.linalg.norm(v) * np.float64(c["height"][1])).astype(np.float32))
+        pts.append((cd[0] * np.float64(c["height"][2])).astype(np.float32))
+    n_hit = 0
+    for p in pts:
+        hit, v, rec = D.locate(p)
+        val = C.c_float()
+        found = None
+        for i in range(cells.size):
+            if Lb.oracle_sample(cells[i:i + 1].ctypes.data, O.v3(p), C.byref(val)):
+                found = (i, np.float32(val.value))
+                break
+        assert (found is not None) == hit, p
+        if hit:
+            n_hit += 1
+            assert found[0] == rec and found[1] == np.float32(v), p
+    assert n_hit > len(pts) // 2

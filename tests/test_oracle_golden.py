@@ -1,0 +1,144 @@
+"""Pin the oracle: its restatement must reproduce the reference's own outputs
+(tests/golden, generated from /root/reference headers via oracle/_ref) bit for bit."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_util import FRAME_FIXTURES, load, oracle_scene, params
+from helpers import bits
+
+
+@pytest.mark.parametrize("name", FRAME_FIXTURES)
+def test_frame_fixture(name):
+    d = load(name)
+    S = oracle_scene(d)
+    # host setup: bounds, shell accelerator, majorants (hostCode.cu:792-808, 299-397)
+    assert np.array_equal(bits([S.sb.lower.x, S.sb.lower.y, S.sb.lower.z, S.sb.upper.x,
+                                S.sb.upper.y, S.sb.upper.z]), bits(d["spherical_bounds"]))
+    assert np.array_equal(bits([S.vb.lower.x, S.vb.lower.y, S.vb.lower.z, S.vb.upper.x,
+                                S.vb.upper.y, S.vb.upper.z]), bits(d["volume_bounds"]))
+    assert np.array_equal(S.value_ranges, d["value_ranges"])
+    assert np.array_equal(bits(S.max_op), bits(d["max_opacities"]))
+    assert np.float32(S.unit_distance) == d["unit_distance"]
+    W, H = int(d["width"]), int(d["height"])
+    accum = np.zeros((H, W, 4), np.float32)
+    fb = np.zeros((H, W), np.uint32)
+    for k, aid in enumerate(d["accum_ids"]):
+        _, _, st = S.render(params(S, d, aid), W, H, accum=accum, fb=fb, threads=4)
+        assert st.locate_calls == d["counts"][k][0] and st.samples_found == d["counts"][k][1]
+    assert np.array_equal(bits(accum), bits(d["accum"]))
+    assert np.array_equal(fb, d["fb"])
+
+
+@pytest.mark.parametrize("name", ["f2_r2b02_l90"])
+def test_literal_sample_mode_matches_fixture(name):
+    """The literal sample() (toSpherical incl. the dead asinf/atan2f, corners rebuilt per
+    call) gives the same frame as the fast mode the other tests use."""
+    d = load(name)
+    S = oracle_scene(d)
+    W, H = int(d["width"]), int(d["height"])
+    a, f, _ = S.render(params(S, d, 0), W, H, rect=(32, 32, 96, 96), threads=8, fast=False)
+    assert np.array_equal(bits(a[32:96, 32:96]), bits(d["accum"][32:96, 32:96]))
+    assert np.array_equal(f[32:96, 32:96], d["fb"][32:96, 32:96])
+
+
+@pytest.fixture(scope="module")
+def kats():
+    return load_kats()
+
+
+def load_kats():
+    z = np.load(O.os.path.join(O.os.path.dirname(O.HERE), "tests", "golden", "kats.npz"))
+    d = {k: z[k] for k in z.files}
+    d["cells"] = np.ascontiguousarray(d["cells"]).view(O.CELL_DTYPE).ravel()
+    return d
+
+
+def test_kat_lcg(kats):
+    L = O.olib()
+    for (a, b), ref in zip(kats["lcg_seeds"], kats["lcg"]):
+        out = np.zeros(16, np.float32)
+        L.oracle_lcg(int(a), int(b), 16, out.ctypes.data)
+        assert np.array_equal(bits(out), bits(ref))
+
+
+def test_kat_sample_and_find_height(kats):
+    L = O.olib()
+    cells = kats["cells"]
+    for p, i, hit, val in zip(kats["sample_points"], kats["sample_cell"], kats["sample_hit"],
+                              kats["sample_value"]):
+        v = C.c_float(0)
+        h = L.oracle_sample(cells[i:i + 1].ctypes.data, O.v3(p), C.byref(v))
+        assert h == hit and (not hit or np.float32(v.value) == val)
+    assert kats["sample_hit"].sum() > 100
+    for i, h, r in zip(kats["fh_cell"], kats["fh_h"], kats["fh_result"]):
+        assert L.oracle_find_height(cells[i:i + 1].ctypes.data, float(h)) == r
+    for i in range(cells.size):
+        b = O.OBox3()
+        L.oracle_get_bounds(cells[i:i + 1].ctypes.data, C.byref(b))
+        got = [b.lower.x, b.lower.y, b.lower.z, b.upper.x, b.upper.y, b.upper.z]
+        assert np.array_equal(bits(got), bits(kats["get_bounds"][i]))
+
+
+def test_kat_rays_and_sdda(kats):
+    L = O.olib()
+    dims = kats["sdda_dims"]
+    sb6 = kats["sdda_sb6"]
+    sb = O.b3(sb6[:3], sb6[3:])
+    box = O.b3(kats["box6"][:3], kats["box6"][3:])
+    for k, (o, dr) in enumerate(zip(kats["ray_org"], kats["ray_dir"])):
+        tn, tf = C.c_float(), C.c_float()
+        h = L.oracle_intersect_sphere(O.v3(o), O.v3(dr), 6.4e6, C.byref(tn), C.byref(tf))
+        ref = kats["sphere"][k]
+        assert h == ref[0] and (not h or (np.float32(tn.value) == ref[1] and np.float32(tf.value) == ref[2]))
+        t0, t1 = C.c_float(), C.c_float()
+        h = L.oracle_box_test(O.v3(o), O.v3(dr), 0.0, 1e10, box, C.byref(t0), C.byref(t1))
+        ref = kats["box_test"][k]
+        assert h == ref[0] and np.float32(t0.value) == ref[1] and np.float32(t1.value) == ref[2]
+        leaf = np.full(2048, -1, np.int32)
+        a0 = np.zeros(2048, np.float32)
+        a1 = np.zeros(2048, np.float32)
+        n = L.oracle_sdda_trace(O.v3(o), O.v3(dr), 0.0, 1e10, dims.ctypes.data, sb, 2048,
+                                leaf.ctypes.data, a0.ctypes.data, a1.ctypes.data)
+        assert n == kats["sdda_count"][k]
+        m = min(n, 2048)
+        assert np.array_equal(leaf[:m], kats["sdda_leaf"][k][:m])
+        assert np.array_equal(bits(a0[:m]), bits(kats["sdda_t0"][k][:m]))
+        assert np.array_equal(bits(a1[:m]), bits(kats["sdda_t1"][k][:m]))
+    assert (kats["sdda_count"] > 0).sum() > 50
+
+
+def test_kat_shading_and_spherical(kats):
+    L = O.olib()
+    srgb = np.array([L.oracle_linear_to_srgb(float(x)) for x in kats["srgb_x"]], np.float32)
+    assert np.array_equal(bits(srgb), bits(kats["srgb"]))
+    rgba = np.array([L.oracle_make_rgba(c.ctypes.data) for c in kats["rgba_in"]], np.uint32)
+    assert np.array_equal(rgba, kats["rgba"])
+    for c, ref in zip(kats["cart"], kats["to_spherical"]):
+        o = O.OVec3()
+        L.oracle_to_spherical(O.v3(c), C.byref(o))
+        assert np.array_equal(bits([o.x, o.y, o.z]), bits(ref))
+    for s, ref in zip(kats["sph"], kats["to_cartesian"]):
+        o = O.OVec3()
+        L.oracle_to_cartesian(O.v3(s), C.byref(o))
+        assert np.array_equal(bits([o.x, o.y, o.z]), bits(ref))
+
+
+def test_kat_lut_and_camera(kats):
+    L = O.olib()
+    src = kats["lut_src"]
+    dst = np.zeros((300, 4), np.float32)
+    L.oracle_resample_lut(src.ctypes.data, src.shape[0], dst.ctypes.data, 300)
+    assert np.array_equal(bits(dst), bits(kats["lut_300"]))
+    box = O.b3(kats["camera_box6"][:3], kats["camera_box6"][3:])
+    out = (O.OVec3 * 4)()
+    L.oracle_camera_view_all(box, 90.0, 1.0, C.cast(out, C.c_void_p))
+    got = [v for o in out for v in (o.x, o.y, o.z)]
+    assert np.array_equal(bits(got), bits(kats["cameras"][0]))
+    for spec, ref in zip(kats["camera_specs"], kats["cameras"][1:]):
+        L.oracle_camera_orient(O.v3(spec[0:3]), O.v3(spec[3:6]), O.v3(spec[6:9]), float(spec[9]),
+                               1.0, C.cast(out, C.c_void_p))
+        got = [v for o in out for v in (o.x, o.y, o.z)]
+        assert np.array_equal(bits(got), bits(ref))
