@@ -215,6 +215,53 @@ IRT_HD float glibc_atan2f(float y, float x) {
 }
 
 // ---------------------------------------------------------------------------------
+// glibc 2.35 logf (sysdeps/ieee754/flt-32/e_logf.c, from ARM's optimized-routines; the
+// table and polynomial of e_logf_data.c): x = 2^k z, log(x) = log1p(z/c-1) + log(c) + k ln2
+// in double, one rounding to float at the end.  The Woodcock step evaluates
+// logf(1.f - rnd()) (deviceCode.cu:165) only on x = 1 - j/2^24, j in [0, 2^24): all
+// positive normal floats <= 1, so the subnormal/zero/inf/NaN branches are not restated.
+// Verified against the host glibc on that whole domain (both of glibc's x86-64 builds,
+// plain and FMA, agree there) by tests/test_host_logic.py and, for the device, by
+// tests/test_gpu_parity.py.
+struct LogfTab {
+  double invc, logc;
+};
+constexpr LogfTab kLogfTab[16] = {
+    {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
+    {0x1.49539f0f010bp+0, -0x1.01eae7f513a67p-2},  {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
+    {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8eap+0, -0x1.1aa2bc79c81p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
+    {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1p+0, 0x0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5},  {0x1.ca4b31f026aap-1, 0x1.c5e53aa362eb4p-4},
+    {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3},  {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d22477p-3},
+    {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2},  {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2},
+};
+// `tab` is kLogfTab or a copy of it (the kernels keep one in LDS).
+IRT_HD float glibc_logf_unit(float x, const LogfTab *tab) {
+  const double Ln2 = 0x1.62e42fefa39efp-1;
+  const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
+  const uint32_t ix = f2u(x);
+  if (ix == 0x3f800000u) return 0.f;
+  const uint32_t tmp = ix - 0x3f330000u;
+  const int i = (int)((tmp >> (23 - 4)) % 16u);
+  const int k = (int32_t)tmp >> 23;
+  const uint32_t iz = ix - (tmp & (0x1ffu << 23));
+  const double invc = tab[i].invc, logc = tab[i].logc;
+  const double z = (double)u2f(iz);
+  const double r = z * invc - 1;
+  const double y0 = logc + (double)k * Ln2;
+  const double r2 = r * r;
+  double y = A1 * r + A2;
+  y = A0 * r2 + y;
+  y = y * r2 + (y0 + r);
+  return (float)y;
+}
+// logf(1.f - rnd()) for the LCG state s that rnd() just produced
+IRT_HD float woodcock_log(uint32_t s, const LogfTab *tab) {
+  return glibc_logf_unit(1.f - lcg_float(s), tab);
+}
+
+// ---------------------------------------------------------------------------------
 // Cube-map point locator: the MI355X replacement for the OptiX / cuBQL cell location
 // (icon_rt/deviceCode.cu:58-125).  A direction is mapped to one of 6*G*G cells of a
 // gnomonic cube map; each cell lists (conservatively, see host/irt_scene.cpp) every
@@ -248,11 +295,11 @@ IRT_HD uint32_t cubemap_cell(float px, float py, float pz, int G) {
 }
 
 // One candidate-list entry: the record's radial extent (for the cheap first test of
-// sample(), ICONGrid.h:184) and its index.
+// sample(), ICONGrid.h:184), its index, and meta = numLayers | sortedHeights << 31.
 struct LocEntry {
   float h0, hN;
   uint32_t idx;
-  uint32_t pad;
+  uint32_t meta;
 };
 
 // Per-record height/value block: 64 floats = 256 B, two 128-B lines.
@@ -261,6 +308,57 @@ struct LocEntry {
 //                             path -- findHeight() < numLayers <= 31 after the radial test)
 //   [63]     numLayers (int bits)
 constexpr int kHV = 64;
+
+// Render record: everything sample() + getValue() read for one record, kRec4 float4 =
+// 320 B, laid out for the state-machine kernel (irt_trace.hip) so that a point-in-record
+// test is one gather step and the value another:
+//   [0..2]   the three side planes (n.xyz, w)                       ICONGrid.h:197-203
+//   [3]      coarse keys {height[7], height[15], height[23], height[31]}
+//   [4+4b .. 7+4b], b = 0..3:  block b =
+//            {height[8b..8b+3]}, {height[8b+4..8b+7]},
+//            {value[8b-1..8b+2]}, {value[8b+3..8b+6]}   (value[-1] := 0)
+// height[j] sits at float (4+4(j>>3))*4 + (j&7); value[c] at (4+4((c+1)>>3)+2)*4 + ((c+1)&7).
+constexpr int kRec4 = 20;
+IRT_HD int rec_height_pos(int j) { return (4 + 4 * (j >> 3)) * 4 + (j & 7); }
+IRT_HD int rec_value_pos(int c) { return (4 + 4 * ((c + 1) >> 3) + 2) * 4 + ((c + 1) & 7); }
+
+// findHeight for non-decreasing height[1..nl], from the record layout in two gathers.
+// lower_bound's answer is #{ j in [1,nl] : !(hpos <= height[j]) } (a monotone predicate on
+// sorted data, NaN hpos included).  Step 1: the block b = number of coarse keys
+// height[8k+7] (8k+7 <= nl) satisfying the predicate; the answer lies in
+// [8b-1, 8b+6] (b = 0: [0, 6]).
+IRT_HD int rec_coarse_block(float k0, float k1, float k2, float k3, int nl, float hpos) {
+  int b = 0;
+  b += (7 <= nl && !(hpos <= k0)) ? 1 : 0;
+  b += (15 <= nl && !(hpos <= k1)) ? 1 : 0;
+  b += (23 <= nl && !(hpos <= k2)) ? 1 : 0;
+  b += (31 <= nl && !(hpos <= k3)) ? 1 : 0;
+  return b > 3 ? 3 : b;  // b == 4 needs NaN hpos (the radial test bounds hpos by height[nl])
+}
+// Step 2: h[m] = height[8b+m] (m = 0..6) -> index m of the answer in the block's value
+// quad pair {value[8b-1..8b+6]}.  (Scalars, not an array: keeps the kernel's registers
+// out of scratch.)
+IRT_HD int rec_block_index(float h0, float h1, float h2, float h3, float h4, float h5,
+                           float h6, int b, int nl, float hpos) {
+  const int j0 = 8 * b;
+  int c = b > 0 ? j0 - 1 : 0;
+  c += (j0 >= 1 && j0 <= nl && !(hpos <= h0)) ? 1 : 0;
+  c += (j0 + 1 <= nl && !(hpos <= h1)) ? 1 : 0;
+  c += (j0 + 2 <= nl && !(hpos <= h2)) ? 1 : 0;
+  c += (j0 + 3 <= nl && !(hpos <= h3)) ? 1 : 0;
+  c += (j0 + 4 <= nl && !(hpos <= h4)) ? 1 : 0;
+  c += (j0 + 5 <= nl && !(hpos <= h5)) ? 1 : 0;
+  c += (j0 + 6 <= nl && !(hpos <= h6)) ? 1 : 0;
+  return c - j0 + 1;  // in [0, 7]
+}
+// v[m] of the eight values {a0..a3, b0..b3} as a select tree
+IRT_HD float select8(int m, float a0, float a1, float a2, float a3, float b0, float b1, float b2,
+                     float b3) {
+  const bool o = (m & 1) != 0, t = (m & 2) != 0;
+  const float x0 = o ? a1 : a0, x1 = o ? a3 : a2, x2 = o ? b1 : b0, x3 = o ? b3 : b2;
+  const float y0 = t ? x1 : x0, y1 = t ? x3 : x2;
+  return (m & 4) ? y1 : y0;
+}
 
 // ICONCell::findHeight (ICONGrid.h:117-145): lower_bound over height[1..numLayers].
 IRT_HD int find_height(const float *height, int numLayers, float hpos) {

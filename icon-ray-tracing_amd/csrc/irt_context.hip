@@ -45,12 +45,16 @@ struct irt_context {
   int lutSize = 0;
   float tfLo = 0.f, tfHi = 1.f, opScale = 1.f;
   bool tfSet = false;
+  // render arena (RenderArgs::arena): maxOp, logtab, offsets and entries live inside it
+  float4 *d_arena = nullptr;
+  uint32_t aMaxOp = 0, aLog = 0, aOffs = 0, aEnt = 0, aRec = 0;
   unsigned long long *d_counters = nullptr;
   unsigned long long *h_counters = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool pending = false;
   irt_render_stats stats{};
   size_t bytes = 0;
+  int variant = kDefaultVariant;  // render-kernel variant (irt_render.hip OPT_* bits)
 };
 
 namespace {
@@ -75,9 +79,8 @@ int upload(irt_context *c, T **p, const T *src, size_t count) {
 void free_all(irt_context *c) {
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void *ptrs[] = {c->d_hv,     c->d_planes,        c->d_offsets, c->d_entries,
-                  c->d_logtab, c->d_srgb,          c->d_valueRanges, c->d_maxOp,
-                  c->d_lut,    c->d_counters};
+  void *ptrs[] = {c->d_hv,  c->d_planes, c->d_arena, c->d_srgb, c->d_valueRanges,
+                  c->d_lut, c->d_counters};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
@@ -164,6 +167,12 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.numTiles = numTiles;
   A.tilesX = tilesX;
   A.counters = c->d_counters;
+  A.arena = c->d_arena;
+  A.aMaxOp = c->aMaxOp;
+  A.aLog = c->aLog;
+  A.aOffs = c->aOffs;
+  A.aEnt = c->aEnt;
+  A.aRec = c->aRec;
 
   if (c->pending) {
     int rc = finish_stats(c);
@@ -171,7 +180,12 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   }
   IRT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), s));
   IRT_HIP(hipEventRecord(c->ev0, s));
-  if (numTiles > 0) launch_render(A, numTiles * 16, s);
+  if (numTiles > 0) {
+    if (c->variant & kTraceBit)
+      launch_trace(A, numTiles * 16, s, c->variant);
+    else
+      launch_render(A, numTiles * 16, s, c->variant);
+  }
   IRT_HIP(hipGetLastError());
   IRT_HIP(hipEventRecord(c->ev1, s));
   IRT_HIP(hipMemcpyAsync(c->h_counters, c->d_counters, 8 * sizeof(unsigned long long),
@@ -208,6 +222,10 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
 
   irt_context *c = new irt_context();
   c->device = device;
+  if (const char *v = getenv("IRT_RENDER_VARIANT")) {
+    const int var = atoi(v);
+    if (render_variant_available(var) || trace_variant_available(var)) c->variant = var;
+  }
   auto fail = [&](int code) {
     free_all(c);
     delete c;
@@ -222,9 +240,49 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
   c->G = S.G;
   if ((rc = upload(c, &c->d_hv, S.hv.data(), S.hv.size()))) return fail(rc);
   if ((rc = upload(c, &c->d_planes, (const float4 *)S.planes.data(), S.planes.size()))) return fail(rc);
-  if ((rc = upload(c, &c->d_offsets, S.offsets.data(), S.offsets.size()))) return fail(rc);
-  if ((rc = upload(c, &c->d_entries, (const uint4 *)S.entries.data(), S.entries.size()))) return fail(rc);
-  if ((rc = upload(c, &c->d_logtab, logtab.data(), logtab.size()))) return fail(rc);
+  // The render arena: [0] a zero float4 (the gather slot of idle lanes), then maxOpacities,
+  // the logf table, the CSR offsets, the entries and the render records, each 16-B aligned.
+  const int dims[3] = {S.info.shellDims[0], S.info.shellDims[1], S.info.shellDims[2]};
+  c->numMCs = (size_t)dims[0] * dims[1] * dims[2];
+  {
+    std::vector<float> recs;
+    build_records(S, recs);
+    auto q4 = [](size_t floats) { return floats ? (floats + 3) / 4 : 1; };
+    size_t at = 1;
+    const size_t oMax = at; at += q4(c->numMCs);
+    const size_t oLog = at; at += q4(logtab.size());
+    const size_t oOffs = at; at += q4(S.offsets.size());
+    const size_t oEnt = at; at += S.entries.size() ? S.entries.size() : 1;
+    const size_t oRec = at; at += S.n ? S.n * (size_t)kRec4 : 1;
+    if (at > 0xFFFFFFFFull) {
+      set_error("irt_create: volume needs %zu float4 of tables, more than the 2^32 the kernel indexes", at);
+      return fail(IRT_E_INVALID);
+    }
+    if ((rc = dalloc(c, &c->d_arena, at))) return fail(rc);
+    c->aMaxOp = (uint32_t)oMax;
+    c->aLog = (uint32_t)oLog;
+    c->aOffs = (uint32_t)oOffs;
+    c->aEnt = (uint32_t)oEnt;
+    c->aRec = (uint32_t)oRec;
+    c->d_maxOp = (float *)(c->d_arena + oMax);
+    c->d_logtab = (float *)(c->d_arena + oLog);
+    c->d_offsets = (uint32_t *)(c->d_arena + oOffs);
+    c->d_entries = (uint4 *)(c->d_arena + oEnt);
+    hipError_t e = hipMemsetAsync(c->d_arena, 0, at * sizeof(float4), c->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(c->d_logtab, logtab.data(), logtab.size() * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && S.offsets.size())
+      e = hipMemcpyAsync(c->d_offsets, S.offsets.data(), S.offsets.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && S.entries.size())
+      e = hipMemcpyAsync(c->d_entries, S.entries.data(), S.entries.size() * sizeof(uint4), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && recs.size())
+      e = hipMemcpyAsync(c->d_arena + oRec, recs.data(), recs.size() * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // recs is freed at scope end
+    if (e != hipSuccess) {
+      set_error("irt_create: arena upload failed: %s", hipGetErrorString(e));
+      return fail(IRT_E_HIP);
+    }
+  }
   if ((rc = upload(c, &c->d_srgb, th, 256))) return fail(rc);
   if ((rc = dalloc(c, &c->d_counters, 8))) return fail(rc);
   if (hipHostMalloc((void **)&c->h_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
@@ -236,14 +294,7 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
 
   // ShellAccel{vec3i(1,1024,1024), sphericalBounds} + initGrid + buildShell_ICON
   // (hostCode.cu:652-666), majorants zero until a transfer function arrives
-  const int dims[3] = {S.info.shellDims[0], S.info.shellDims[1], S.info.shellDims[2]};
-  c->numMCs = (size_t)dims[0] * dims[1] * dims[2];
   if ((rc = dalloc(c, &c->d_valueRanges, 2 * c->numMCs))) return fail(rc);
-  if ((rc = dalloc(c, &c->d_maxOp, c->numMCs))) return fail(rc);
-  if (hipMemsetAsync(c->d_maxOp, 0, c->numMCs * sizeof(float), c->stream) != hipSuccess) {
-    set_error("irt_create: memset failed");
-    return fail(IRT_E_HIP);
-  }
   launch_shell_init(c->d_valueRanges, c->numMCs, c->stream);
   if (numCells) {
     irt_icon_cell *d_cells = nullptr;
@@ -421,5 +472,44 @@ extern "C" int irt_debug_device_math(int device, const float *a, const float *y,
     set_error("irt_debug_device_math: %s", hipGetErrorString(e));
     return IRT_E_HIP;
   }
+  return IRT_OK;
+}
+
+namespace {
+__global__ void k_debug_wlog(float *out) {
+  __shared__ LogfTab t[16];
+  if (threadIdx.x < 16) t[threadIdx.x] = kLogfTab[threadIdx.x];
+  __syncthreads();
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  out[j] = woodcock_log(j, t);  // lcg_float uses the low 24 bits only
+}
+}  // namespace
+
+extern "C" int irt_debug_device_woodcock_log(int device, float *out) {
+  if (!out) {
+    set_error("irt_debug_device_woodcock_log: null argument");
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(device));
+  float *d = nullptr;
+  const size_t n = (size_t)1 << 24;
+  IRT_HIP(hipMalloc((void **)&d, n * sizeof(float)));
+  hipLaunchKernelGGL(k_debug_wlog, dim3((unsigned)(n / 256)), dim3(256), 0, 0, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpy(out, d, n * sizeof(float), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) {
+    set_error("irt_debug_device_woodcock_log: %s", hipGetErrorString(e));
+    return IRT_E_HIP;
+  }
+  return IRT_OK;
+}
+
+extern "C" int irt_debug_set_variant(irt_context *c, int variant) {
+  if (!c || !(render_variant_available(variant) || trace_variant_available(variant))) {
+    set_error("irt_debug_set_variant: variant %d not compiled", variant);
+    return IRT_E_INVALID;
+  }
+  c->variant = variant;
   return IRT_OK;
 }

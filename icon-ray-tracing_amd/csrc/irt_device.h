@@ -1,0 +1,91 @@
+// irt_device.h -- device-side building blocks of the raygen, each a bit-exact restatement
+// of the reference function it cites (compile with -ffp-contract=off, correctly rounded
+// f32 div/sqrt).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "irt_common.h"
+#include "irt_kernels.h"
+
+#define IRT_FLT_MAX 3.402823466e+38f
+
+namespace irt {
+
+struct Ray {
+  float ox, oy, oz, tmin, dx, dy, dz, tmax;
+};
+
+struct Counts {
+  uint32_t inBox, locate, found, cand;
+};
+
+__device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
+  return ax * bx + ay * by + az * bz;  // vecmath.h:536-538 order
+}
+
+// boxTest (vecmath.h:1926-1937)
+__device__ __forceinline__ bool box_test(const Ray &r, const RenderArgs &A, float &t0, float &t1) {
+  const float lx = (A.bmin.x - r.ox) / r.dx, ly = (A.bmin.y - r.oy) / r.dy, lz = (A.bmin.z - r.oz) / r.dz;
+  const float hx = (A.bmax.x - r.ox) / r.dx, hy = (A.bmax.y - r.oy) / r.dy, hz = (A.bmax.z - r.oz) / r.dz;
+  const float nx = fminf(lx, hx), ny = fminf(ly, hy), nz = fminf(lz, hz);
+  const float fx = fmaxf(lx, hx), fy = fmaxf(ly, hy), fz = fmaxf(lz, hz);
+  t0 = fmaxf(r.tmin, fmaxf(fmaxf(nx, ny), nz));
+  t1 = fminf(r.tmax, fminf(fminf(fx, fy), fz));
+  return t0 < t1;
+}
+
+// intersectSphere (ShellAccel.h:34-53)
+__device__ __forceinline__ bool intersect_sphere(const Ray &r, float radius, float &tnear, float &tfar) {
+  const float A = dot3(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz);
+  const float B = dot3(r.dx, r.dy, r.dz, r.ox, r.oy, r.oz) * 2.f;
+  const float C = dot3(r.ox, r.oy, r.oz, r.ox, r.oy, r.oz) - radius * radius;
+  float d = B * B - 4.f * A * C;
+  if (d < 0.f) return false;
+  d = sqrtf(d);
+  const float q = B < 0.f ? -0.5f * (B - d) : -0.5f * (B + d);
+  const float t1 = q / A;
+  const float t2 = C / q;
+  tnear = fminf(t1, t2);
+  tfar = fmaxf(t1, t2);
+  return true;
+}
+
+// projectToSphericalGrid (ShellAccel.h:57-68), one axis: int((s-lo)/size*(dims-1))
+__device__ __forceinline__ int project_axis(float s, float lo, float hi, int dim) {
+  return f2i_x86((s - lo) / (hi - lo) * (float)(dim - 1));
+}
+
+// normalizeGridCoord (ShellAccel.h:71-80): the while-loops compute c mod d in [0,d).
+__device__ __forceinline__ int wrap_coord(int c, int d) {
+  const int m = c % d;
+  return m < 0 ? m + d : m;
+}
+
+// toSpherical (ICONGrid.h:36-42) with glibc-exact asinf / atan2f.
+__device__ __forceinline__ void to_spherical(float x, float y, float z, float &r, float &lat,
+                                             float &lon) {
+  r = sqrtf(dot3(x, y, z, x, y, z));
+  lat = glibc_asinf(z / r);
+  lon = glibc_atan2f(y, x);
+}
+
+// make_8bit (dvr_course-common-both.h:89-92)
+__device__ __forceinline__ uint32_t make_8bit(float f) {
+  return (uint32_t)fminf(255.f, fmaxf(0.f, (float)f2i_x86(f * 256.f)));
+}
+
+// make_8bit(linear_to_srgb(x)) via the host-built monotone thresholds th[1..255] (LDS):
+// the number of thresholds <= x.
+__device__ __forceinline__ uint32_t srgb_byte(const float *th, float x) {
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t step = 128; step > 0; step >>= 1) {
+    const uint32_t probe = lo + step;
+    if (probe <= 255 && th[probe] <= x) lo = probe;
+  }
+  return lo;
+}
+
+}  // namespace irt

@@ -34,6 +34,9 @@ struct HostScene {
 // Validate, compute volume facts, per-record planes/heights, and the locator.
 int build_scene(const irt_icon_cell *cells, size_t n, HostScene &out, int threads = 0);
 
+// Render records (irt_common.h, kRec4 float4 = 4*kRec4 floats each) from hv + planes.
+void build_records(const HostScene &s, std::vector<float> &out);
+
 // Volume facts only (hostCode.cu:792-808, 838-840).
 void compute_volume_info(const irt_icon_cell *cells, size_t n, irt_volume_info &info);
 

@@ -1,5 +1,7 @@
 // irt_debug.cpp -- host-only inspection entry points (include/icon_rt_hip_debug.h).
 
+#include <math.h>
+#include <vector>
 #include <string.h>
 
 #include "icon_rt_hip_debug.h"
@@ -20,6 +22,20 @@ int irt_debug_f2i(float x) { return f2i_x86(x); }
 float irt_debug_logf_entry(uint32_t k) { return logf_table()[k & 0x00FFFFFFu]; }
 
 void irt_debug_srgb_thresholds(float *out256) { srgb_thresholds(out256); }
+
+void irt_debug_host_woodcock_log(float *out) {
+  for (uint32_t k = 0; k < (1u << 24); ++k) out[k] = logf(1.f - (float)k / (float)0x01000000);
+}
+
+uint32_t irt_debug_logf_mismatches(void) {
+  // glibc_logf_unit (irt_common.h) vs the host glibc logf over the Woodcock domain
+  uint32_t bad = 0;
+  for (uint32_t k = 0; k < (1u << 24); ++k) {
+    const float x = 1.f - (float)k / (float)0x01000000;
+    if (f2u(glibc_logf_unit(x, kLogfTab)) != f2u(logf(x))) ++bad;
+  }
+  return bad;
+}
 
 int irt_debug_scene_build(const irt_icon_cell *cells, size_t n, irt_debug_scene **out) {
   if (!out || (n && !cells)) {
@@ -53,6 +69,45 @@ int irt_debug_scene_locate(const irt_debug_scene *s, irt_vec3f p, float *value,
     if (record) *record = r;
   }
   return hit;
+}
+
+int irt_debug_scene_values(const irt_debug_scene *s, uint32_t rec, float r, float *out2) {
+  if (!s || !out2 || rec >= s->s.n) return IRT_E_INVALID;
+  const float *hv = &s->s.hv[(size_t)rec * kHV];
+  int32_t nl;
+  memcpy(&nl, hv + 63, 4);
+  out2[0] = hv[32 + find_height(hv, nl, r)];
+  // the render-record path of irt_trace.hip (S_PLN -> S_BLK, or S_HS/S_VAL)
+  std::vector<float> R(kRec4 * 4);
+  {
+    HostScene one;
+    one.n = 1;
+    one.hv.assign(hv, hv + kHV);
+    one.planes.assign(s->s.planes.begin() + 3 * (size_t)rec, s->s.planes.begin() + 3 * (size_t)rec + 3);
+    build_records(one, R);
+  }
+  bool sorted = true;
+  for (int j = 2; j <= nl; ++j)
+    if (!(hv[j - 1] <= hv[j])) sorted = false;
+  if (sorted) {
+    const int b = rec_coarse_block(R[12], R[13], R[14], R[15], nl, r);
+    const float *B = &R[(4 + 4 * b) * 4];
+    const int m = rec_block_index(B[0], B[1], B[2], B[3], B[4], B[5], B[6], b, nl, r);
+    out2[1] = select8(m, B[8], B[9], B[10], B[11], B[12], B[13], B[14], B[15]);
+  } else {
+    uint32_t first = 0, count = (uint32_t)nl;
+    while (count > 0) {
+      const uint32_t stp = count / 2, it = first + stp;
+      if (!(r <= R[rec_height_pos((int)it + 1)])) {
+        first = it + 1;
+        count -= stp + 1;
+      } else {
+        count = stp;
+      }
+    }
+    out2[1] = R[rec_value_pos((int)first)];
+  }
+  return IRT_OK;
 }
 
 int irt_debug_scene_candidates(const irt_debug_scene *s, irt_vec3f p, uint32_t *records,

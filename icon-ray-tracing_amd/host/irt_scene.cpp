@@ -186,6 +186,16 @@ inline bool finite_geometry(const irt_icon_cell &c) {
   return true;
 }
 
+// LocEntry::meta: numLayers | (height[1..numLayers] non-decreasing) << 31.  For sorted
+// heights findHeight's lower_bound equals the count of height[1..nl] < r, which the
+// kernel evaluates from one 128-B line in registers.
+inline uint32_t entry_meta(const irt_icon_cell &c) {
+  bool sorted = true;
+  for (int j = 2; j <= c.numLayers; ++j)
+    if (!(c.height[j - 1] <= c.height[j])) sorted = false;
+  return (uint32_t)c.numLayers | (sorted ? 0x80000000u : 0u);
+}
+
 inline bool same_column(const irt_icon_cell &a, const irt_icon_cell &b) {
   return memcmp(a.lat, b.lat, sizeof(a.lat)) == 0 && memcmp(a.lon, b.lon, sizeof(a.lon)) == 0;
 }
@@ -339,7 +349,8 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads)
     for (auto &p : parts)
       for (auto &e : p) {
         const irt_icon_cell &c = cells[e.second];
-        S.entries[cursor[e.first]++] = {c.height[0], c.height[c.numLayers], e.second, 0u};
+        S.entries[cursor[e.first]++] = {c.height[0], c.height[c.numLayers], e.second,
+                                        entry_meta(c)};
       }
   }
   S.info.locatorFaceRes = G;
@@ -349,6 +360,28 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads)
 
 // sample() (ICONGrid.h:181-208) with the precomputed planes; lat/lon of toSpherical are
 // dead in sample() and skipped.
+void build_records(const HostScene &s, std::vector<float> &out) {
+  out.assign(s.n * (size_t)kRec4 * 4, 0.f);
+  for (size_t i = 0; i < s.n; ++i) {
+    float *R = &out[i * (size_t)kRec4 * 4];
+    const float *hv = &s.hv[i * kHV];
+    for (int k = 0; k < 3; ++k) {
+      const Plane4 &p = s.planes[3 * i + k];
+      R[4 * k + 0] = p.x;
+      R[4 * k + 1] = p.y;
+      R[4 * k + 2] = p.z;
+      R[4 * k + 3] = p.w;
+    }
+    R[12] = hv[7];
+    R[13] = hv[15];
+    R[14] = hv[23];
+    R[15] = hv[31];
+    for (int j = 0; j < 32; ++j) R[rec_height_pos(j)] = hv[j];
+    for (int c = 0; c < 31; ++c) R[rec_value_pos(c)] = hv[32 + c];
+    // value[-1] stays 0 (never selected: the block-0 answer index is >= 1)
+  }
+}
+
 int sample_host(const HostScene &s, uint32_t rec, float px, float py, float pz, float &value) {
   const float r = sqrtf(px * px + py * py + pz * pz);
   const float *hv = &s.hv[(size_t)rec * kHV];

@@ -132,6 +132,10 @@ def lib() -> C.CDLL:
             "irt_debug_scene_locate": [P, Vec3, C.POINTER(C.c_float), C.POINTER(C.c_uint32)],
             "irt_debug_scene_candidates": [P, Vec3, P, I],
             "irt_debug_scene_planes": [P, C.c_uint32, P],
+            "irt_debug_scene_values": [P, C.c_uint32, F, P],
+            "irt_debug_logf_mismatches": [],
+            "irt_debug_host_woodcock_log": [P],
+            "irt_debug_device_woodcock_log": [I, P],
             "irt_debug_scene_free": [P],
         }
         for name, args in sig.items():
@@ -378,6 +382,13 @@ class DebugScene:
         out = np.zeros(max(n, 1), dtype=np.uint32)
         lib().irt_debug_scene_candidates(self._h, vec3(p), _ptr(out), n)
         return out[:n]
+
+    def values(self, rec: int, r: float):
+        """(literal findHeight value, render-record value) of record `rec` at radius r."""
+        out = np.zeros(2, dtype=np.float32)
+        _check(lib().irt_debug_scene_values(self._h, rec, C.c_float(r), _ptr(out)),
+               "irt_debug_scene_values")
+        return out
 
     def planes(self, rec: int) -> np.ndarray:
         out = np.zeros(12, dtype=np.float32)

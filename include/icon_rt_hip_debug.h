@@ -23,6 +23,12 @@ int irt_debug_f2i(float x);
 float irt_debug_logf_entry(uint32_t k);
 void irt_debug_srgb_thresholds(float *out256);
 
+/* Number of j in [0, 2^24) where the restated glibc logf (irt_common.h) differs from the
+ * host glibc logf at 1 - j/2^24, the only arguments logf(1.f - rnd()) can take. */
+uint32_t irt_debug_logf_mismatches(void);
+/* The host glibc logf(1 - j/2^24) for every j (out: 2^24 floats). */
+void irt_debug_host_woodcock_log(float *out);
+
 /* The locator built by irt_create, on the host: build, query, free. */
 typedef struct irt_debug_scene irt_debug_scene;
 int irt_debug_scene_build(const irt_icon_cell *cells, size_t n, irt_debug_scene **out);
@@ -31,6 +37,10 @@ int irt_debug_scene_info(const irt_debug_scene *s, irt_volume_info *info);
  * record of the lowest-index cell containing p, 0 if none. */
 int irt_debug_scene_locate(const irt_debug_scene *s, irt_vec3f p, float *value,
                            uint32_t *record);
+/* findHeight + value of record `rec` at radius r two ways: out2[0] from the literal
+ * binary search (ICONGrid.h:117-164), out2[1] from the render-record layout the
+ * state-machine kernel gathers (irt_common.h).  They must agree bit for bit. */
+int irt_debug_scene_values(const irt_debug_scene *s, uint32_t rec, float r, float *out2);
 /* Candidate list of the cube-map cell containing direction p. */
 int irt_debug_scene_candidates(const irt_debug_scene *s, irt_vec3f p, uint32_t *records,
                                int capacity);
@@ -38,11 +48,17 @@ int irt_debug_scene_candidates(const irt_debug_scene *s, irt_vec3f p, uint32_t *
 int irt_debug_scene_planes(const irt_debug_scene *s, uint32_t record, float *out12);
 void irt_debug_scene_free(irt_debug_scene *s);
 
-/* Evaluate the kernels' device versions of asinf(a[i]), atan2f(y[i], x[i]) and the
- * LCG draw sequence on GPU `device` (host arrays in/out; n elements each).  Used to prove
- * the device restatements round exactly like the host glibc. */
+/* Select the render-kernel variant (bit set of irt_render.hip's OPT_* flags; every
+ * variant gives identical results -- used for in-process A/B timing). */
+int irt_debug_set_variant(irt_context *ctx, int variant);
+
+/* Evaluate the kernels' device versions of asinf(a[i]) and atan2f(y[i], x[i]) on GPU
+ * `device` (host arrays in/out; n elements each).  Used to prove the device restatements
+ * round exactly like the host glibc. */
 int irt_debug_device_math(int device, const float *a, const float *y, const float *x, int n,
                           float *out_asinf, float *out_atan2f);
+/* The device logf(1.f - rnd()) for every LCG low-24-bit value j (out: 2^24 floats, index j). */
+int irt_debug_device_woodcock_log(int device, float *out);
 
 #ifdef __cplusplus
 }

@@ -485,7 +485,12 @@ void raygen(const Scene &S, const oc_params &p, int x, int y, int W, int H, floa
       const float majorant = p.maxOpacities[leafID];
       ray.tmin = tt0;
       ray.tmax = tt1;
-      float t = woodcockTracking(S, p, ray, rnd, majorant, albedo, extinction, ts);
+      // sampleVolume calls inside zero-length leaves (every leaf after a range's first,
+      // since the reference's lat/lon planes are degenerate) can never change the pixel and
+      // are not counted; the GPU kernel skips those it does not need for the RNG state.
+      ThreadStats uncounted;
+      float t = woodcockTracking(S, p, ray, rnd, majorant, albedo, extinction,
+                                 tt0 == tt1 ? uncounted : ts);
       if (t > tt0 && t < tt1) {
         color = albedo * amb * p.ambientRadiance;
         alpha = extinction > 0.f ? 1.f : 0.f;

@@ -56,7 +56,7 @@ typedef struct oc_params {
 typedef struct oc_stats {
   uint64_t rays_launched;     /* pixels the raygen ran for */
   uint64_t rays_in_box;       /* rays that passed boxTest (deviceCode.cu:294) */
-  uint64_t locate_calls;      /* sampleVolume calls (deviceCode.cu:173) */
+  uint64_t locate_calls;      /* sampleVolume calls (deviceCode.cu:173) outside zero-length sdda leaves */
   uint64_t samples_found;     /* sampleVolume calls that found a cell */
   uint64_t rng_draws;         /* total LCG draws */
   uint64_t leaves;            /* sdda func() invocations (ShellAccel.h:389) */

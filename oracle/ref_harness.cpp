@@ -143,7 +143,10 @@ void raygen(const RefParams &lp, int x, int y, int W, int H, vec4f *accumBuffer,
       const float majorant = maxOpacities[leafID];
       ray.tmin = t0;
       ray.tmax = t1;
-      float t = woodcockTracking(lp, ray, rnd, majorant, albedo, extinction, cnt);
+      // zero-length leaves are not counted (same rule as oracle/icon_oracle.cpp)
+      Counters uncounted;
+      float t = woodcockTracking(lp, ray, rnd, majorant, albedo, extinction,
+                                 t0 == t1 ? uncounted : cnt);
       if (t > t0 && t < t1) {
         color = albedo * lp.ambientColor * lp.ambientRadiance;
         alpha = extinction > 0.f ? 1.f : 0.f;

@@ -27,6 +27,17 @@ def assert_same_frame(a_gpu, f_gpu, a_ref, f_ref, label=""):
                              f"gpu {a_gpu[y, x]} {f_gpu[y, x]:08x} vs ref {a_ref[y, x]} {f_ref[y, x]:08x}")
 
 
+def test_device_woodcock_log_matches_glibc_everywhere():
+    """logf(1.f - rnd()) on the device (glibc's algorithm, irt_common.h) == the host glibc
+    logf for every one of the 2^24 values rnd() can return."""
+    dev = np.zeros(1 << 24, np.float32)
+    host = np.zeros(1 << 24, np.float32)
+    L = irt.lib()
+    assert L.irt_debug_device_woodcock_log(0, dev.ctypes.data) == 0, L.irt_last_error()
+    L.irt_debug_host_woodcock_log(host.ctypes.data)  # glibc logf, evaluated here
+    assert np.array_equal(bits(dev), bits(host))
+
+
 def test_device_math_matches_glibc():
     """glibc_asinf / glibc_atan2f on the device round exactly as the host glibc."""
     rng = np.random.default_rng(5)

@@ -96,6 +96,9 @@ def test_libm_restatements_match_glibc():
     for k in list(range(0, 1 << 24, 9973)) + [0, 1, 2, 12, (1 << 24) - 1]:
         x = np.float32(1.0) - np.float32(k) / np.float32(1 << 24)
         assert np.float32(L.irt_debug_logf_entry(k)).view(np.uint32) == np.float32(libm.logf(float(x))).view(np.uint32)
+    # the kernels' logf(1.f - rnd()) is glibc's algorithm restated (irt_common.h): exhaustive
+    # over the 2^24 arguments it can take
+    assert L.irt_debug_logf_mismatches() == 0
     for f in [0.5, -0.5, 1e10, -1e10, 2147483520.0, 2147483648.0, -2147483648.0, float("nan"), float("inf")]:
         v = L.irt_debug_f2i(f)
         ref = int(f) if np.isfinite(f) and -2147483648.0 <= f < 2147483648.0 else -2147483648
@@ -167,3 +170,38 @@ def test_locator_is_conservative_and_lowest_index(rn, bis, L):
             n_hit += 1
             assert found[0] == rec and found[1] == np.float32(v), p
     assert n_hit > len(pts) // 2
+
+
+def test_render_record_layout_gives_findheight_value():
+    """The state-machine kernel reads findHeight's answer from the render-record layout
+    (irt_common.h: coarse keys + one height/value block, or the literal search for
+    unsorted columns).  Host evaluation of that path == the literal binary search
+    (ICONGrid.h:117-164) at every layer boundary, its float neighbours and random radii,
+    for sorted and deliberately unsorted columns of every layer count."""
+    cells = irt.synth_grid(2, 1, 93)  # records of 31, 31, 31 layers (and a short tail)
+    rng = np.random.default_rng(7)
+    cells = cells[:400].copy()
+    nls = set()
+    for i in range(cells.size):
+        nl = int(rng.integers(0, 32))
+        cells["numLayers"][i] = nl
+        nls.add(nl)
+        if i % 3 == 0 and nl >= 2:  # unsorted column: swap two interior heights
+            a, b = rng.choice(np.arange(1, nl + 1), 2, replace=False)
+            h = cells["height"][i]
+            h[a], h[b] = h[b], h[a]
+    D = irt.DebugScene(cells)
+    checked = 0
+    for i in range(cells.size):
+        nl = int(cells["numLayers"][i])
+        hs = cells["height"][i][:nl + 1].astype(np.float32)
+        rs = list(hs) + list(np.nextafter(hs, np.float32(np.inf))) + \
+            list(np.nextafter(hs, np.float32(-np.inf))) + \
+            list(rng.uniform(hs.min() - 10, hs.max() + 10, 8).astype(np.float32))
+        for r in rs:
+            if r < hs[0] or r > hs[nl]:
+                continue  # sample() rejects it before findHeight (ICONGrid.h:184)
+            a, b = D.values(i, float(r))
+            assert np.float32(a).view(np.uint32) == np.float32(b).view(np.uint32), (i, nl, r)
+            checked += 1
+    assert len(nls) > 25 and checked > 5000
