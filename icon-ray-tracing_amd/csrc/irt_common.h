@@ -322,6 +322,43 @@ constexpr int kRec4 = 20;
 IRT_HD int rec_height_pos(int j) { return (4 + 4 * (j >> 3)) * 4 + (j & 7); }
 IRT_HD int rec_value_pos(int c) { return (4 + 4 * ((c + 1) >> 3) + 2) * 4 + ((c + 1) & 7); }
 
+// ---------------------------------------------------------------------------------
+// Radially binned candidate lists (the product locator).  Each cube-map cell splits the
+// radius axis at up to kMaxEdges edges e0 < e1 < e2 (unused edges = +inf) into open bins
+//   bin k = (e_{k-1}, e_k)   (e_{-1} = -inf, e_E = +inf)
+// and lists, per bin and in record-index order, every record of the cell whose radial
+// extent can contain such an r:  h0 < e_k && hN > e_{k-1}  (plus zero-thickness records
+// h0 == hN == e_k, assigned to the bin below their edge).  A radius strictly inside bin k
+// therefore scans only bin k; a radius exactly on edge e_k scans bins k and k+1 and keeps
+// the lower first hit.  Either way the first record passing sample() is the reference's
+// lowest-index answer (deviceCode.cu:119-122).
+constexpr int kMaxEdges = 3;
+constexpr int kBinHdrWords = 8;  // {e0, e1, e2, base} {end0, end1, end2, end3}: 32 B per cell
+IRT_HD int bin_of(float r, float e0, float e1, float e2) {
+  return (e0 < r ? 1 : 0) + (e1 < r ? 1 : 0) + (e2 < r ? 1 : 0);
+}
+
+// Zero-thickness records are spheres (host/irt_scene.cpp); a 2^16-bit hash bitmap of
+// their radii says "certainly not a sphere radius" for almost every sample.
+constexpr int kSphBitWords = 2048;
+IRT_HD uint32_t sph_hash(float r) {
+  uint32_t h = f2u(r) * 0x9E3779B1u;
+  return h >> 16;
+}
+
+// Fat entry: everything one candidate test of sample() reads, kFat4 float4 = 80 B:
+//   [0..2]  the record's three side planes (n.xyz, w)              ICONGrid.h:197-203
+//   [3]     {height[0], height[numLayers], record index, meta}     ICONGrid.h:184
+//           meta = numLayers | (height[1..numLayers] non-decreasing) << 31
+//   [4]     coarse keys {height[7], height[15], height[23], height[31]}
+constexpr int kFat4 = 5;
+// Per-record height/value blocks (the render record without its planes/keys), kBlk4
+// float4 = 256 B: block b (4 float4) = {height[8b..8b+3]}, {height[8b+4..8b+7]},
+// {value[8b-1..8b+2]}, {value[8b+3..8b+6]} (value[-1] := 0).
+constexpr int kBlk4 = 16;
+IRT_HD int blk_height_pos(int j) { return 16 * (j >> 3) + (j & 7); }
+IRT_HD int blk_value_pos(int c) { return 16 * ((c + 1) >> 3) + 8 + ((c + 1) & 7); }
+
 // findHeight for non-decreasing height[1..nl], from the record layout in two gathers.
 // lower_bound's answer is #{ j in [1,nl] : !(hpos <= height[j]) } (a monotone predicate on
 // sorted data, NaN hpos included).  Step 1: the block b = number of coarse keys

@@ -31,11 +31,18 @@ struct irt_context {
   uint32_t n = 0;
   int G = 0;
   // HBM
-  float *d_hv = nullptr;
-  float4 *d_planes = nullptr;
-  uint32_t *d_offsets = nullptr;
-  uint4 *d_entries = nullptr;
-  float *d_logtab = nullptr;
+  uint4 *d_binHdr = nullptr;   // binned locator (irt_common.h)
+  float4 *d_fat = nullptr;
+  float4 *d_blocks = nullptr;
+  uint32_t numSph = 0;         // zero-thickness records (spheres)
+  float *d_sphR = nullptr;
+  uint32_t *d_sphOff = nullptr;
+  uint2 *d_sphRec = nullptr;
+  uint32_t *d_sphBits = nullptr;
+  uint4 *d_queue = nullptr;      // march queue and continuation list (irt_render.hip),
+  uint32_t *d_contList = nullptr;  // sized for the largest launch so far
+  uint32_t *d_segCount = nullptr;
+  size_t queueCap = 0;
   float *d_srgb = nullptr;
   float *d_valueRanges = nullptr;
   float *d_maxOp = nullptr;
@@ -45,9 +52,6 @@ struct irt_context {
   int lutSize = 0;
   float tfLo = 0.f, tfHi = 1.f, opScale = 1.f;
   bool tfSet = false;
-  // render arena (RenderArgs::arena): maxOp, logtab, offsets and entries live inside it
-  float4 *d_arena = nullptr;
-  uint32_t aMaxOp = 0, aLog = 0, aOffs = 0, aEnt = 0, aRec = 0;
   unsigned long long *d_counters = nullptr;
   unsigned long long *h_counters = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -79,7 +83,8 @@ int upload(irt_context *c, T **p, const T *src, size_t count) {
 void free_all(irt_context *c) {
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void *ptrs[] = {c->d_hv,  c->d_planes, c->d_arena, c->d_srgb, c->d_valueRanges,
+  void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
+                  c->d_sphBits, c->d_queue, c->d_contList, c->d_segCount, c->d_maxOp, c->d_srgb, c->d_valueRanges,
                   c->d_lut, c->d_counters};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -151,11 +156,6 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.lutSize = c->lutSize;
   A.numCells = c->n;
   A.G = c->G;
-  A.offsets = c->d_offsets;
-  A.entries = c->d_entries;
-  A.planes = c->d_planes;
-  A.hv = c->d_hv;
-  A.logtab = c->d_logtab;
   A.srgbTh = c->d_srgb;
   A.W = W;
   A.H = H;
@@ -167,28 +167,48 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.numTiles = numTiles;
   A.tilesX = tilesX;
   A.counters = c->d_counters;
-  A.arena = c->d_arena;
-  A.aMaxOp = c->aMaxOp;
-  A.aLog = c->aLog;
-  A.aOffs = c->aOffs;
-  A.aEnt = c->aEnt;
-  A.aRec = c->aRec;
+  A.binHdr = c->d_binHdr;
+  A.fat = c->d_fat;
+  A.blocks = c->d_blocks;
+  A.numSph = c->numSph;
+  A.sphR = c->d_sphR;
+  A.sphOff = c->d_sphOff;
+  A.sphRec = c->d_sphRec;
+  A.sphBits = c->d_sphBits;
 
   if (c->pending) {
     int rc = finish_stats(c);
     if (rc) return rc;
   }
-  IRT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), s));
+  const size_t lanes = (size_t)numTiles * 4096;
+  if (lanes > c->queueCap) {
+    IRT_HIP(hipStreamSynchronize(s));
+    if (c->d_queue) IRT_HIP(hipFree(c->d_queue));
+    if (c->d_contList) IRT_HIP(hipFree(c->d_contList));
+    if (c->d_segCount) IRT_HIP(hipFree(c->d_segCount));
+    c->d_queue = nullptr;
+    c->d_contList = nullptr;
+    c->d_segCount = nullptr;
+    c->bytes -= c->queueCap * (sizeof(uint4) + sizeof(uint32_t)) + c->queueCap / 256 * sizeof(uint32_t);
+    c->queueCap = 0;
+    int rc = dalloc(c, &c->d_queue, lanes);
+    if (rc == IRT_OK) rc = dalloc(c, &c->d_contList, lanes);
+    if (rc == IRT_OK) rc = dalloc(c, &c->d_segCount, lanes / 256);
+    if (rc) return rc;
+    c->queueCap = lanes;
+    c->info.deviceBytes = c->bytes;
+  }
+  A.queue = c->d_queue;
+  A.contList = c->d_contList;
+  A.segCount = c->d_segCount;
+  IRT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), s));
   IRT_HIP(hipEventRecord(c->ev0, s));
   if (numTiles > 0) {
-    if (c->variant & kTraceBit)
-      launch_trace(A, numTiles * 16, s, c->variant);
-    else
-      launch_render(A, numTiles * 16, s, c->variant);
+    launch_render(A, numTiles * 16, s, c->variant);
   }
   IRT_HIP(hipGetLastError());
   IRT_HIP(hipEventRecord(c->ev1, s));
-  IRT_HIP(hipMemcpyAsync(c->h_counters, c->d_counters, 8 * sizeof(unsigned long long),
+  IRT_HIP(hipMemcpyAsync(c->h_counters, c->d_counters, 16 * sizeof(unsigned long long),
                          hipMemcpyDeviceToHost, s));
   c->pending = true;
   return IRT_OK;
@@ -216,7 +236,6 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
   HostScene S;
   int rc = build_scene(cells, numCells, S);
   if (rc) return rc;
-  const std::vector<float> &logtab = logf_table();
   float th[256];
   srgb_thresholds(th);
 
@@ -224,7 +243,7 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
   c->device = device;
   if (const char *v = getenv("IRT_RENDER_VARIANT")) {
     const int var = atoi(v);
-    if (render_variant_available(var) || trace_variant_available(var)) c->variant = var;
+    if (render_variant_available(var)) c->variant = var;
   }
   auto fail = [&](int code) {
     free_all(c);
@@ -238,59 +257,34 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
   c->info = S.info;
   c->n = (uint32_t)S.n;
   c->G = S.G;
-  if ((rc = upload(c, &c->d_hv, S.hv.data(), S.hv.size()))) return fail(rc);
-  if ((rc = upload(c, &c->d_planes, (const float4 *)S.planes.data(), S.planes.size()))) return fail(rc);
-  // The render arena: [0] a zero float4 (the gather slot of idle lanes), then maxOpacities,
-  // the logf table, the CSR offsets, the entries and the render records, each 16-B aligned.
+  if ((rc = upload(c, &c->d_binHdr, (const uint4 *)S.binHdr.data(), S.binHdr.size() / 4))) return fail(rc);
+  if ((rc = upload(c, &c->d_fat, (const float4 *)S.fat.data(), S.fat.size() / 4))) return fail(rc);
+  if ((rc = upload(c, &c->d_blocks, (const float4 *)S.blocks.data(), S.blocks.size() / 4))) return fail(rc);
+  {
+    std::vector<uint2> sr(S.sphRec.size());
+    for (size_t k = 0; k < sr.size(); ++k) {
+      const uint32_t rec = S.sphRec[k];
+      sr[k] = make_uint2(rec, (uint32_t)cells[rec].numLayers);
+    }
+    c->numSph = (uint32_t)S.sphR.size();
+    if ((rc = upload(c, &c->d_sphR, S.sphR.data(), S.sphR.size()))) return fail(rc);
+    if ((rc = upload(c, &c->d_sphOff, S.sphOff.data(), S.sphOff.size()))) return fail(rc);
+    if ((rc = upload(c, &c->d_sphRec, sr.data(), sr.size()))) return fail(rc);
+    if ((rc = upload(c, &c->d_sphBits, S.sphBits.data(), S.sphBits.size()))) return fail(rc);
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(IRT_E_HIP);  // sr
+  }
   const int dims[3] = {S.info.shellDims[0], S.info.shellDims[1], S.info.shellDims[2]};
   c->numMCs = (size_t)dims[0] * dims[1] * dims[2];
-  {
-    std::vector<float> recs;
-    build_records(S, recs);
-    auto q4 = [](size_t floats) { return floats ? (floats + 3) / 4 : 1; };
-    size_t at = 1;
-    const size_t oMax = at; at += q4(c->numMCs);
-    const size_t oLog = at; at += q4(logtab.size());
-    const size_t oOffs = at; at += q4(S.offsets.size());
-    const size_t oEnt = at; at += S.entries.size() ? S.entries.size() : 1;
-    const size_t oRec = at; at += S.n ? S.n * (size_t)kRec4 : 1;
-    if (at > 0xFFFFFFFFull) {
-      set_error("irt_create: volume needs %zu float4 of tables, more than the 2^32 the kernel indexes", at);
-      return fail(IRT_E_INVALID);
-    }
-    if ((rc = dalloc(c, &c->d_arena, at))) return fail(rc);
-    c->aMaxOp = (uint32_t)oMax;
-    c->aLog = (uint32_t)oLog;
-    c->aOffs = (uint32_t)oOffs;
-    c->aEnt = (uint32_t)oEnt;
-    c->aRec = (uint32_t)oRec;
-    c->d_maxOp = (float *)(c->d_arena + oMax);
-    c->d_logtab = (float *)(c->d_arena + oLog);
-    c->d_offsets = (uint32_t *)(c->d_arena + oOffs);
-    c->d_entries = (uint4 *)(c->d_arena + oEnt);
-    hipError_t e = hipMemsetAsync(c->d_arena, 0, at * sizeof(float4), c->stream);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(c->d_logtab, logtab.data(), logtab.size() * sizeof(float), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess && S.offsets.size())
-      e = hipMemcpyAsync(c->d_offsets, S.offsets.data(), S.offsets.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess && S.entries.size())
-      e = hipMemcpyAsync(c->d_entries, S.entries.data(), S.entries.size() * sizeof(uint4), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess && recs.size())
-      e = hipMemcpyAsync(c->d_arena + oRec, recs.data(), recs.size() * sizeof(float), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // recs is freed at scope end
-    if (e != hipSuccess) {
-      set_error("irt_create: arena upload failed: %s", hipGetErrorString(e));
-      return fail(IRT_E_HIP);
-    }
-  }
+  if ((rc = dalloc(c, &c->d_maxOp, c->numMCs))) return fail(rc);
+  if (hipMemsetAsync(c->d_maxOp, 0, c->numMCs * sizeof(float), c->stream) != hipSuccess) return fail(IRT_E_HIP);
   if ((rc = upload(c, &c->d_srgb, th, 256))) return fail(rc);
-  if ((rc = dalloc(c, &c->d_counters, 8))) return fail(rc);
-  if (hipHostMalloc((void **)&c->h_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
+  if ((rc = dalloc(c, &c->d_counters, 16))) return fail(rc);
+  if (hipHostMalloc((void **)&c->h_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
     set_error("irt_create: event/pinned allocation failed");
     return fail(IRT_E_HIP);
   }
-  memset(c->h_counters, 0, 8 * sizeof(unsigned long long));
+  memset(c->h_counters, 0, 16 * sizeof(unsigned long long));
 
   // ShellAccel{vec3i(1,1024,1024), sphericalBounds} + initGrid + buildShell_ICON
   // (hostCode.cu:652-666), majorants zero until a transfer function arrives
@@ -505,8 +499,19 @@ extern "C" int irt_debug_device_woodcock_log(int device, float *out) {
   return IRT_OK;
 }
 
+extern "C" int irt_debug_counters(irt_context *c, unsigned long long *out16) {
+  if (!c || !out16) {
+    set_error("irt_debug_counters: null argument");
+    return IRT_E_INVALID;
+  }
+  int rc = finish_stats(c);
+  if (rc) return rc;
+  memcpy(out16, c->h_counters, 16 * sizeof(unsigned long long));
+  return IRT_OK;
+}
+
 extern "C" int irt_debug_set_variant(irt_context *c, int variant) {
-  if (!c || !(render_variant_available(variant) || trace_variant_available(variant))) {
+  if (!c || !render_variant_available(variant)) {
     set_error("irt_debug_set_variant: variant %d not compiled", variant);
     return IRT_E_INVALID;
   }

@@ -29,7 +29,22 @@ struct HostScene {
   int G = 0;                      // cube-map cells per face edge
   std::vector<uint32_t> offsets;  // 6*G*G + 1 CSR offsets
   std::vector<LocEntry> entries;  // candidate lists, each sorted by record index
+  // the product locator (irt_common.h "radially binned candidate lists")
+  std::vector<uint32_t> binHdr;   // 6*G*G * kBinHdrWords
+  std::vector<float> fat;         // binEntries * kFat4 * 4
+  std::vector<float> blocks;      // n * kBlk4 * 4
+  size_t binEntries = 0;
+  // zero-thickness records (spheres): distinct radii, CSR into record indices (ascending),
+  // and a hash bitmap of the radii (irt_common.h sph_hash) the kernel keeps in LDS
+  std::vector<float> sphR;
+  std::vector<uint32_t> sphOff, sphRec, sphBits;
 };
+
+// Build the binned locator (binHdr, fat, blocks) from the CSR lists; build_scene calls it.
+int build_bins(HostScene &S, int threads);
+// Point location over the binned locator, as the kernel does it (host restatement).
+int locate_bins_host(const HostScene &s, float px, float py, float pz, float &value,
+                     uint32_t *record, uint32_t *tested);
 
 // Validate, compute volume facts, per-record planes/heights, and the locator.
 int build_scene(const irt_icon_cell *cells, size_t n, HostScene &out, int threads = 0);

@@ -27,16 +27,11 @@ struct RenderArgs {
   float tfLo, tfHi, opacityScale;
   const float4 *lut;
   int lutSize;
-  // locator + records
+  // locator
   uint32_t numCells;
   int G;
-  const uint32_t *offsets;
-  const uint4 *entries;
-  const float4 *planes;
-  const float *hv;
-  // libm tables
-  const float *logtab;   // 2^24 entries
-  const float *srgbTh;   // 256 entries
+  // sRGB byte thresholds (256 entries, host/irt_host.cpp)
+  const float *srgbTh;
   // output
   int W, H;
   uint32_t *fb;
@@ -44,24 +39,29 @@ struct RenderArgs {
   int packed;            // 0: linear x + W*y; 1: packed 64x64 tiles
   int tileBegin, tileStride, numTiles, tilesX;
   unsigned long long *counters;  // [0] launched [1] inBox [2] locate [3] found [4] candidates
-  // The render arena (irt_trace.hip): one allocation holding every table the raygen
-  // gathers from, addressed by 32-bit float4 indices so a gather step is 4 loads off one
-  // base.  Offsets (in float4) of the sub-tables:
-  const float4 *arena;
-  uint32_t aMaxOp;       // ShellAccel::maxOpacities, numMCs floats
-  uint32_t aLog;         // logf table, 2^24 floats
-  uint32_t aOffs;        // cube-map CSR offsets, 6G^2+1 uint32
-  uint32_t aEnt;         // LocEntry, one float4 each
-  uint32_t aRec;         // render records, kRec4 float4 each (irt_common.h)
+  // The binned locator (irt_common.h): per cube-map cell a 32-B header, fat entries,
+  // per-record height/value blocks.
+  const uint4 *binHdr;
+  const float4 *fat;
+  const float4 *blocks;
+  // zero-thickness records (spheres, host/irt_scene.cpp): sorted distinct radii, CSR into
+  // (record, numLayers) pairs, and the radius hash bitmap (kSphBitWords words)
+  uint32_t numSph;
+  const float *sphR;
+  const uint32_t *sphOff;
+  const uint2 *sphRec;
+  const uint32_t *sphBits;
+  // the setup -> march -> continuation pipeline (irt_render.hip): the march queue
+  // ({gid | flags, t0, t1, majorant} per ray, one compacted segment per setup workgroup)
+  // and the continuation list (gids, count in counters[11])
+  uint4 *queue;
+  uint32_t *segCount;    // rays per 256-slot queue segment (one per setup workgroup)
+  uint32_t *contList;
 };
 
-// Render-kernel variants.  Bit 12 selects the state-machine raygen (irt_trace.hip,
-// bits 8-11 = minimum waves per SIMD); otherwise the bit set of irt_render.hip's OPT_*
-// flags.  All give identical results.
-constexpr int kTraceBit = 4096;
-constexpr int kDefaultVariant = 9728;  // k_render<OPT_REC, 6 waves/SIMD>: fastest measured (profiles/)
-bool trace_variant_available(int variant);
-void launch_trace(const RenderArgs &A, int numBlocks, hipStream_t s, int variant);
+// Render-kernel variants: the bit set of irt_render.hip's OPT_* flags (bits 8-11: minimum
+// waves per SIMD).  All give identical results.
+constexpr int kDefaultVariant = 5120;  // one kernel per frame, 4 waves/SIMD: fastest measured (profiles/)
 bool render_variant_available(int variant);
 void launch_render(const RenderArgs &A, int numBlocks, hipStream_t s, int variant);
 void launch_shell_init(float *valueRanges, size_t numMCs, hipStream_t s);

@@ -1,18 +1,22 @@
-// irt_render.hip -- the hot path: the raygen woodcockTrackingWithAccel /
-// woodcockTrackingAE (icon_rt/deviceCode.cu:239-341) as a gfx950 kernel.
+// irt_render.hip -- the hot path: the raygens woodcockTrackingWithAccel and
+// woodcockTrackingAE (icon_rt/deviceCode.cu:239-341) as one gfx950 kernel.
 //
-// One lane per pixel, one wave64 per 8x8 pixel packet (neighbouring rays walk the same
-// cube-map cells and records), a 256-thread workgroup per 16x16 block, 16 workgroups per
-// 64x64 frame tile -- the unit the reference's CPU parallel_for hands out
-// (common/for_each.h:70-85) and the unit of the multi-GPU frame split.
+// Mapping: one lane per pixel, one wave64 per 8x8 pixel packet (neighbouring rays visit
+// the same cube-map cells, fat entries and majorants), a 256-thread workgroup per 16x16
+// block, 16 workgroups per 64x64 frame tile -- the unit the reference's CPU parallel_for
+// hands out (common/for_each.h:70-85) and the unit of the multi-GPU frame split.
 //
-// The kernel is a chain of dependent gathers (logf table -> cube-map cell -> candidate
-// entries -> side planes -> heights -> value -> LUT), so its speed is the number of
-// dependent memory round trips per sample.  The OPT bits below remove round trips without
-// changing a single result; each combination is a separate instantiation so variants can
-// be A/B-timed in one process (irt_debug_set_variant) and checked for parity.
+// Where the time goes (profiles/): the kernel is a chain of dependent gathers per
+// Woodcock sample -- cube-map cell header -> fat candidate entry -> height/value block --
+// plus the VALU of the ray setup.  Design choices that follow from that:
+//   * the binned locator (irt_common.h): a sample costs ~3 round trips instead of ~10;
+//   * one Woodcock call site (the locate code is inlined once), counters aggregated per
+//     wave in LDS, coarse height keys fetched only after the plane tests pass: fewer live
+//     VGPRs, so more waves per SIMD hide the gathers;
+//   * the sdda exit-point toSpherical (two glibc-exact asinf/atan2f) is evaluated only
+//     when a later range can still read the RNG state it drives (see below).
 //
-// Bit-exactness: see irt_common.h / irt_device.h and DESIGN.md section 3.
+// Bit-exactness: irt_common.h / irt_device.h and DESIGN.md section 3.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,157 +26,237 @@
 namespace irt {
 
 enum : int {
-  OPT_BATCH = 1,    // load candidate entries 4 at a time (one round trip per 4)
-  OPT_PLANES = 2,   // issue the 3 side-plane loads together
-  OPT_HVEC = 4,     // sorted columns: findHeight from one 128-B line held in registers
-  OPT_SPEC = 8,     // issue that line together with the planes (speculative)
-  OPT_LUTLDS = 32,  // transfer-function LUT in LDS
-  OPT_ACCPF = 64,   // read the old accum value at ray start
-  OPT_REC = 8192    // render-record layout (irt_common.h): planes + coarse keys in one
-                    // gather, findHeight's block + value in a second
+  OPT_BATCH = 1,      // two fat entries per round trip
+  OPT_PF = 2,         // next sample's cell header prefetched (woodcock_pf)
+  OPT_ACCPF = 64,     // read the old accum value at ray start
+  OPT_STATS = 32768,  // per-wave statistics into counters[5..9] (measurement only)
+  // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
-constexpr int kLutLds = 1024;
+// cube-map cell of a sample point.  The lists are rasterised with 1e-5 padding in face
+// coordinates (host/irt_scene.cpp), so the hardware reciprocal (1 ulp) is exact enough:
+// any cell it picks lists every record that can contain the point.
+__device__ __forceinline__ uint32_t cubemap_cell_fast(float px, float py, float pz, int G) {
+  const float ax = __builtin_fabsf(px), ay = __builtin_fabsf(py), az = __builtin_fabsf(pz);
+  uint32_t face;
+  float num0, num1, den;
+  if (ax >= ay && ax >= az) {
+    face = px >= 0.f ? 0u : 1u;
+    num0 = py;
+    num1 = pz;
+    den = ax;
+  } else if (ay >= az) {
+    face = py >= 0.f ? 2u : 3u;
+    num0 = px;
+    num1 = pz;
+    den = ay;
+  } else {
+    face = pz >= 0.f ? 4u : 5u;
+    num0 = px;
+    num1 = py;
+    den = az;
+  }
+  const float inv = __builtin_amdgcn_rcpf(den);
+  const float fg = 0.5f * (float)G;
+  int i = (int)((num0 * inv + 1.f) * fg);
+  int j = (int)((num1 * inv + 1.f) * fg);
+  i = i < 0 ? 0 : (i >= G ? G - 1 : i);
+  j = j < 0 ? 0 : (j >= G ? G - 1 : j);
+  return face * (uint32_t)G * (uint32_t)G + (uint32_t)j * (uint32_t)G + (uint32_t)i;
+}
+
+constexpr int kLutAlphaLds = 1024;
 
 template <int OPT>
 struct Tracer {
   const RenderArgs &A;
-  const float4 *s_lut;
-  bool lutLds;
   const LogfTab *s_logf;
-  Counts &cnt;
+  const uint32_t *s_sph;
+  uint32_t *s_cnt;  // [0] launched [1] inBox [2] locate [3] found [4] candidates
+  Counts cnt;       // per-lane statistics (OPT_STATS)
+  const float *s_lutA = nullptr;  // LUT alpha column in LDS (march kernel)
 
-  __device__ Tracer(const RenderArgs &a, const float4 *sl, bool ll, const LogfTab *lt, Counts &c)
-      : A(a), s_lut(sl), lutLds(ll), s_logf(lt), cnt(c) {}
-
-  // logf(1.f - rnd()) for the draw that produced state s (deviceCode.cu:165): glibc's
-  // algorithm in registers (irt_common.h), no table gather
-  __device__ __forceinline__ float log_at(uint32_t s) { return woodcock_log(s, s_logf); }
-
-  // getValue (ICONGrid.h:147-164) of record E.z at radius r
-  __device__ __forceinline__ float get_value(const uint4 &E, float r, const float4 *h, bool haveH) {
-    const uint32_t idx = E.z, nl = E.w & 0x7fffffffu;
-    const float *hv = A.hv + (size_t)idx * kHV;
-    if constexpr ((OPT & OPT_HVEC) != 0) {
-      if (E.w >> 31) {
-        float4 hh[8];
-        const float4 *H = reinterpret_cast<const float4 *>(hv);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) hh[q] = haveH ? h[q] : H[q];
-        // sorted height[1..nl]: lower_bound == #{ j in [1,nl] : height[j] < r }
-        uint32_t c = 0;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float hq[4] = {hh[q].x, hh[q].y, hh[q].z, hh[q].w};
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const uint32_t j = 4 * q + s;
-            if (j >= 1) c += (j <= nl && hq[s] < r) ? 1u : 0u;
-          }
-        }
-        return hv[32 + c];
-      }
-    }
-    return hv[32 + find_height(hv, (int)nl, r)];
+  // one wave-aggregated LDS add per event site
+  __device__ __forceinline__ void count(int k) {
+    const unsigned long long m = __ballot(1);
+    if (__lane_id() == (unsigned)(__ffsll((long long)m) - 1)) atomicAdd(&s_cnt[k], (uint32_t)__popcll(m));
   }
 
-  // sample(cell, pos, value) (ICONGrid.h:181-208) for one candidate that passed the radial
-  // test: the three ccw side planes, then getValue.
-  __device__ __forceinline__ bool test_record(const uint4 &E, float px, float py, float pz,
-                                              float r, float &value) {
-    const float4 *P = A.planes + 3 * (size_t)E.z;
-    float4 h[8];
-    bool haveH = false;
-    if constexpr ((OPT & OPT_SPEC) != 0 && (OPT & OPT_HVEC) != 0) {
-      if (E.w >> 31) {
-        const float4 *H = reinterpret_cast<const float4 *>(A.hv + (size_t)E.z * kHV);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) h[q] = H[q];
-        haveH = true;
+  // findHeight (ICONGrid.h:117-145) literally, over a record's blocks; getValue (147-164)
+  __device__ __forceinline__ float find_value_literal(const float4 *B, int nl, float r) {
+    const float *Bf = reinterpret_cast<const float *>(B);
+    int first = 0, count = nl;
+    while (count > 0) {
+      const int stp = count / 2, it = first + stp;
+      if (!(r <= Bf[blk_height_pos(it + 1)])) {
+        first = it + 1;
+        count -= stp + 1;
+      } else {
+        count = stp;
       }
     }
-    if constexpr ((OPT & OPT_PLANES) != 0) {
-      const float4 p0 = P[0], p1 = P[1], p2 = P[2];
-      if (dot3(px, py, pz, p0.x, p0.y, p0.z) - p0.w > 0.f) return false;  // ICONGrid.h:201
-      if (dot3(px, py, pz, p1.x, p1.y, p1.z) - p1.w > 0.f) return false;  // 202
-      if (dot3(px, py, pz, p2.x, p2.y, p2.z) - p2.w > 0.f) return false;  // 203
-    } else {
-      const float4 p0 = P[0];
-      if (dot3(px, py, pz, p0.x, p0.y, p0.z) - p0.w > 0.f) return false;
-      const float4 p1 = P[1];
-      if (dot3(px, py, pz, p1.x, p1.y, p1.z) - p1.w > 0.f) return false;
-      const float4 p2 = P[2];
-      if (dot3(px, py, pz, p2.x, p2.y, p2.z) - p2.w > 0.f) return false;
-    }
-    value = get_value(E, r, h, haveH);
-    return true;
+    return Bf[blk_value_pos(first)];
   }
 
-  // sample() on the render record (OPT_REC): two gathers for a hit
-  __device__ __forceinline__ bool test_rec(const uint4 &E, float px, float py, float pz, float r,
-                                           float &value) {
-    const float4 *R = A.arena + A.aRec + (size_t)E.z * kRec4;
-    const float4 p0 = R[0], p1 = R[1], p2 = R[2], ck = R[3];
+  // sample()'s point test (ICONGrid.h:184, 197-203) on one fat entry {p0, p1, p2, m, ck}:
+  // the radial range and the three ccw side planes
+  __device__ __forceinline__ bool pass_fat(const float4 &p0, const float4 &p1, const float4 &p2,
+                                           const float4 &m, float px, float py, float pz, float r) {
+    count(4);
+    if (r < m.x || r > m.y) return false;                                 // ICONGrid.h:184
     if (dot3(px, py, pz, p0.x, p0.y, p0.z) - p0.w > 0.f) return false;  // ICONGrid.h:201
     if (dot3(px, py, pz, p1.x, p1.y, p1.z) - p1.w > 0.f) return false;  // 202
     if (dot3(px, py, pz, p2.x, p2.y, p2.z) - p2.w > 0.f) return false;  // 203
-    const int nl = (int)(E.w & 0x7fffffffu);
-    if (E.w >> 31) {
-      const int b = rec_coarse_block(ck.x, ck.y, ck.z, ck.w, nl, r);
-      const float4 *B = R + 4 + 4 * b;
-      const float4 h0 = B[0], h1 = B[1], v0 = B[2], v1 = B[3];
-      const int m = rec_block_index(h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, b, nl, r);
-      value = select8(m, v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w);
-    } else {
-      const float *Rf = reinterpret_cast<const float *>(R);
-      int first = 0, count = nl;  // findHeight, literally (ICONGrid.h:117-145)
-      while (count > 0) {
-        const int stp = count / 2, it = first + stp;
-        if (!(r <= Rf[rec_height_pos(it + 1)])) {
-          first = it + 1;
-          count -= stp + 1;
-        } else {
-          count = stp;
-        }
-      }
-      value = Rf[rec_value_pos(first)];
-    }
     return true;
   }
 
-  __device__ __forceinline__ bool try_entry(const uint4 &E, float px, float py, float pz, float r,
-                                            float &value) {
-    ++cnt.cand;
-    if (r < __uint_as_float(E.x) || r > __uint_as_float(E.y)) return false;  // ICONGrid.h:184
-    if constexpr ((OPT & OPT_REC) != 0) return test_rec(E, px, py, pz, r, value);
-    return test_record(E, px, py, pz, r, value);
+  // The record a point test found: index, meta (numLayers | sorted << 31), coarse keys.
+  struct Found {
+    uint32_t rec, meta;
+    float4 ck;
+  };
+
+  // First entry of fat entries [q, qe) whose point test passes, among records < limit.
+  // Only the point test runs in the (lane-divergent) loop; getValue's gathers come after.
+  __device__ __forceinline__ bool scan_fat(uint32_t q, uint32_t qe, uint32_t limit, float px,
+                                           float py, float pz, float r, Found &f) {
+    if constexpr ((OPT & OPT_BATCH) != 0) {
+      for (; q < qe; q += 2) {
+        const float4 *F = A.fat + (size_t)q * kFat4;
+        const float4 *F1 = A.fat + (size_t)min(q + 1, qe - 1) * kFat4;
+        const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3], ak = F[4];
+        const float4 b0 = F1[0], b1 = F1[1], b2 = F1[2], bm = F1[3], bk = F1[4];
+        if (__float_as_uint(am.z) >= limit) return false;
+        if (pass_fat(a0, a1, a2, am, px, py, pz, r)) {
+          f = {__float_as_uint(am.z), __float_as_uint(am.w), ak};
+          return true;
+        }
+        if (q + 1 < qe) {
+          if (__float_as_uint(bm.z) >= limit) return false;
+          if (pass_fat(b0, b1, b2, bm, px, py, pz, r)) {
+            f = {__float_as_uint(bm.z), __float_as_uint(bm.w), bk};
+            return true;
+          }
+        }
+      }
+    } else {
+      for (; q < qe; ++q) {
+        const float4 *F = A.fat + (size_t)q * kFat4;
+        const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3], ak = F[4];
+        if (__float_as_uint(am.z) >= limit) return false;
+        if (pass_fat(a0, a1, a2, am, px, py, pz, r)) {
+          f = {__float_as_uint(am.z), __float_as_uint(am.w), ak};
+          return true;
+        }
+      }
+    }
+    return false;
   }
 
-  // sampleVolume (deviceCode.cu:58-125) over the cube-map candidate lists: lists are
-  // sorted by record index, so the first entry passing sample() is the reference's
-  // lowest-index answer (116-123).
+  // getValue (ICONGrid.h:147-164) of the found record at radius r: sorted heights take the
+  // coarse key's 64-B height/value block (one gather), others the literal binary search
+  __device__ __forceinline__ float record_value(const Found &f, float r) {
+    const int nl = (int)(f.meta & 0x7fffffffu);
+    const float4 *B = A.blocks + (size_t)f.rec * kBlk4;
+    if (f.meta >> 31) {
+      const int b = rec_coarse_block(f.ck.x, f.ck.y, f.ck.z, f.ck.w, nl, r);
+      const float4 *Q = B + 4 * b;
+      const float4 h0 = Q[0], h1 = Q[1], v0 = Q[2], v1 = Q[3];
+      const int k = rec_block_index(h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, b, nl, r);
+      return select8(k, v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w);
+    }
+    return find_value_literal(B, nl, r);
+  }
+
+  // A zero-thickness record at exactly radius r (a sphere, host/irt_scene.cpp), if any:
+  // the lowest such record and its getValue.
+  __device__ __forceinline__ bool sphere_at(float r, float &value, uint32_t &rec) {
+    uint32_t lo = 0, hi = A.numSph;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (A.sphR[mid] < r) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo >= A.numSph || !(A.sphR[lo] == r)) return false;
+    const uint2 q = A.sphRec[A.sphOff[lo]];
+    value = find_value_literal(A.blocks + (size_t)q.x * kBlk4, (int)q.y, r);
+    rec = q.x;
+    return true;
+  }
+
+  // sampleVolume (deviceCode.cu:58-125) over the binned lists (irt_common.h): the first
+  // record in index order passing sample() -- the reference's linear scan's answer
+  // (116-123).
   __device__ __forceinline__ bool locate(float px, float py, float pz, float &value) {
     if (A.numCells == 0) return false;
     const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
-    const uint32_t cell = cubemap_cell(px, py, pz, A.G);
-    const uint32_t beg = A.offsets[cell], end = A.offsets[cell + 1];
-    if constexpr ((OPT & OPT_BATCH) != 0) {
-      for (uint32_t e = beg; e < end; e += 4) {
-        const uint32_t last = end - 1;
-        const uint4 E0 = A.entries[e];
-        const uint4 E1 = A.entries[min(e + 1, last)];
-        const uint4 E2 = A.entries[min(e + 2, last)];
-        const uint4 E3 = A.entries[min(e + 3, last)];
-        if (try_entry(E0, px, py, pz, r, value)) return true;
-        if (e + 1 < end && try_entry(E1, px, py, pz, r, value)) return true;
-        if (e + 2 < end && try_entry(E2, px, py, pz, r, value)) return true;
-        if (e + 3 < end && try_entry(E3, px, py, pz, r, value)) return true;
+    const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G);
+    const uint4 H0 = A.binHdr[2 * (size_t)cell], H1 = A.binHdr[2 * (size_t)cell + 1];
+    return locate_hdr(px, py, pz, r, H0, H1, value);
+  }
+
+  // the cell header of a sample point (one gather), for locate_hdr
+  __device__ __forceinline__ void fetch_hdr(float px, float py, float pz, uint4 &H0, uint4 &H1) {
+    const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G);
+    H0 = A.binHdr[2 * (size_t)cell];
+    H1 = A.binHdr[2 * (size_t)cell + 1];
+  }
+
+  __device__ __forceinline__ bool locate_hdr(float px, float py, float pz, float r, const uint4 &H0,
+                                             const uint4 &H1, float &value) {
+    const float e0 = __uint_as_float(H0.x), e1 = __uint_as_float(H0.y), e2 = __uint_as_float(H0.z);
+    const int b = bin_of(r, e0, e1, e2);
+    // bin b's [beg, end) from the cumulative ends, and its upper edge, selected with masks
+    // (a select chain on b becomes a scratch lookup table otherwise)
+    const uint32_t m1 = b > 0 ? ~0u : 0u, m2 = b > 1 ? ~0u : 0u, m3 = b > 2 ? ~0u : 0u;
+    const uint32_t beg = (m1 & H1.x) + (m2 & (H1.y - H1.x)) + (m3 & (H1.z - H1.y));
+    const uint32_t end = H1.x + (m1 & (H1.y - H1.x)) + (m2 & (H1.z - H1.y)) + (m3 & (H1.w - H1.z));
+    const uint32_t end2 = H1.y + (m1 & (H1.z - H1.y)) + (m2 & (H1.w - H1.z));
+    // r exactly on the bin's upper edge: records starting at that edge sit in the next
+    // bin, so a second pass scans it for a lower record (one scan site, two passes)
+    const float eb = __uint_as_float(H0.x ^ (m1 & (H0.x ^ H0.y)) ^ (m2 & (H0.y ^ H0.z)));
+    const bool onEdge = b < kMaxEdges && r == eb;
+    uint32_t qb = H0.w + beg, qe = H0.w + end;
+    Found f = {0xFFFFFFFFu, 0u, make_float4(0.f, 0.f, 0.f, 0.f)};
+    bool hit = false;
+    for (int pass = 0; pass < 2; ++pass) {
+      Found g;
+      if (scan_fat(qb, qe, f.rec, px, py, pz, r, g)) {
+        f = g;
+        hit = true;
       }
-    } else {
-      for (uint32_t e = beg; e < end; ++e)
-        if (try_entry(A.entries[e], px, py, pz, r, value)) return true;
+      if (!onEdge) break;
+      qb = qe;
+      qe = H0.w + end2;
     }
-    return false;
+    if (A.numSph) {
+      const uint32_t h = sph_hash(r);
+      if ((s_sph[h >> 5] >> (h & 31)) & 1u) {
+        float v2;
+        uint32_t rec2;
+        if (sphere_at(r, v2, rec2) && (!hit || rec2 < f.rec)) {
+          value = v2;
+          return true;
+        }
+      }
+    }
+    if (hit) value = record_value(f, r);
+    return hit;
+  }
+
+  // postClassify's alpha only (the acceptance test needs nothing else), from the LUT's
+  // alpha column in LDS when it fits; the colour comes from post_classify on acceptance
+  __device__ __forceinline__ float classify_alpha(float v) {
+    v = (v - A.tfLo) / (A.tfHi - A.tfLo);
+    const int size = A.lutSize;
+    const int idx = f2i_x86(v * (float)size);
+    const float frac = (v * (float)size) - (float)idx;
+    const int i1 = idx < 0 ? 0 : (idx > size - 1 ? size - 1 : idx);
+    const int idx2 = (int)((uint32_t)idx + 1u);
+    const int i2 = idx2 < 0 ? 0 : (idx2 > size - 1 ? size - 1 : idx2);
+    const bool lds = s_lutA && size <= kLutAlphaLds;
+    const float a = lds ? s_lutA[i1] : A.lut[i1].w, b = lds ? s_lutA[i2] : A.lut[i2].w;
+    return a * frac + b * (1.f - frac) * A.opacityScale;
   }
 
   // postClassify (deviceCode.cu:127-135): weights reversed, opacityScale on 2nd term only
@@ -184,14 +268,7 @@ struct Tracer {
     const int i1 = idx < 0 ? 0 : (idx > size - 1 ? size - 1 : idx);
     const int idx2 = (int)((uint32_t)idx + 1u);
     const int i2 = idx2 < 0 ? 0 : (idx2 > size - 1 ? size - 1 : idx2);
-    float4 a, b;
-    if ((OPT & OPT_LUTLDS) != 0 && lutLds) {
-      a = s_lut[i1];
-      b = s_lut[i2];
-    } else {
-      a = A.lut[i1];
-      b = A.lut[i2];
-    }
+    const float4 a = A.lut[i1], b = A.lut[i2];
     const float om = 1.f - frac;
     float4 o;
     o.x = a.x * frac + b.x * om * 1.f;
@@ -201,233 +278,543 @@ struct Tracer {
     return o;
   }
 
-  // woodcockTracking (deviceCode.cu:149-186).  `count` is false inside zero-length sdda
-  // leaves, whose sampleVolume calls are not counted (see the sdda loop below).
-  __device__ __forceinline__ float woodcock(const Ray &ray, uint32_t &st, float majorant,
-                                            float4 &sampleOut, bool count = true) {
-    float t = ray.tmin;
+  // woodcockTracking with the next sample's cell header in flight while the current
+  // sample is located: the next position depends only on the RNG state after this
+  // sample's acceptance draw, which exists whenever the sample lands in a cell (all but
+  // ~0.1% of samples).  Same draws, same samples, same result; one gather less per step.
+  __device__ __forceinline__ float woodcock_pf(float dx, float dy, float dz, float t, float tmax,
+                                               uint32_t &st, float majorant, float q,
+                                               float4 &sampleOut, bool counted) {
+    uint32_t sN = lcg_next(st);                        // this step's xi
+    float tN = t - (woodcock_log(sN, s_logf) / q);     // deviceCode.cu:165
+    uint4 H0 = make_uint4(0u, 0u, 0u, 0u), H1 = H0;
+    if (tN <= tmax) fetch_hdr(A.org.x + dx * tN, A.org.y + dy * tN, A.org.z + dz * tN, H0, H1);
     while (true) {
-      if (majorant <= 0.f) break;
-      st = lcg_next(st);
-      const float lg = log_at(st);
-      t -= (lg / (majorant / A.unitDistance));
-      if (t > ray.tmax) break;
-      const float px = ray.ox + ray.dx * t, py = ray.oy + ray.dy * t, pz = ray.oz + ray.dz * t;
+      if constexpr ((OPT & OPT_STATS) != 0) ++cnt.steps;
+      st = sN;
+      t = tN;
+      if (t > tmax) break;                             // 167-168
+      const float px = A.org.x + dx * t, py = A.org.y + dy * t, pz = A.org.z + dz * t;
+      // speculate: this sample is found, so the acceptance draw sU precedes the next xi
+      const uint32_t sU = lcg_next(st), sN2 = lcg_next(sU);
+      const float tN2 = t - (woodcock_log(sN2, s_logf) / q);
+      uint4 G0 = make_uint4(0u, 0u, 0u, 0u), G1 = G0;
+      if (tN2 <= tmax) fetch_hdr(A.org.x + dx * tN2, A.org.y + dy * tN2, A.org.z + dz * tN2, G0, G1);
+      if (counted) count(2);
       float value = 0.f;
-      if (count) ++cnt.locate;
+      const float r = sqrtf(dot3(px, py, pz, px, py, pz));
+      if (!locate_hdr(px, py, pz, r, H0, H1, value)) {
+        // not in any cell: no acceptance draw (172-173), the next xi follows directly
+        sN = lcg_next(st);
+        tN = t - (woodcock_log(sN, s_logf) / q);
+        if (tN <= tmax) fetch_hdr(A.org.x + dx * tN, A.org.y + dy * tN, A.org.z + dz * tN, H0, H1);
+        continue;
+      }
+      if (counted) count(3);
+      const float sw = classify_alpha(value);  // postClassify(value).w (175)
+      st = sU;
+      const float u = lcg_float(st);           // 176
+      if (sw >= u * majorant) {                // 177-181
+        sampleOut = post_classify(value);
+        break;
+      }
+      sN = sN2;
+      tN = tN2;
+      H0 = G0;
+      H1 = G1;
+    }
+    return fminf(t, tmax);
+  }
+
+  // woodcockTracking (deviceCode.cu:149-186) over [tmin, tmax].  `counted` is false in
+  // zero-length sdda leaves, whose sampleVolume calls the statistics leave out.
+  __device__ __forceinline__ float woodcock(float dx, float dy, float dz, float tmin, float tmax,
+                                            uint32_t &st, float majorant, float4 &sampleOut,
+                                            bool counted) {
+    float t = tmin;
+    if (majorant <= 0.f) return fminf(t, tmax);
+    const float q = majorant / A.unitDistance;  // the same value every iteration (165)
+    if constexpr ((OPT & OPT_PF) != 0) {
+      if (A.numCells != 0) return woodcock_pf(dx, dy, dz, t, tmax, st, majorant, q, sampleOut, counted);
+    }
+    while (true) {
+      if constexpr ((OPT & OPT_STATS) != 0) ++cnt.steps;
+      st = lcg_next(st);
+      t -= (woodcock_log(st, s_logf) / q);
+      if (t > tmax) break;
+      const float px = A.org.x + dx * t, py = A.org.y + dy * t, pz = A.org.z + dz * t;
+      float value = 0.f;
+      if (counted) count(2);
       if (!locate(px, py, pz, value)) continue;
-      if (count) ++cnt.found;
-      const float4 s = post_classify(value);
+      if (counted) count(3);
+      const float sw = classify_alpha(value);  // postClassify(value).w
       st = lcg_next(st);
       const float u = lcg_float(st);
-      if (s.w >= u * majorant) {
-        sampleOut = s;
+      if (sw >= u * majorant) {
+        sampleOut = post_classify(value);
         break;
       }
     }
-    return fminf(t, ray.tmax);
+    return fminf(t, tmax);
   }
 };
 
-// Variant bits 8-11: minimum waves per SIMD asked of the register allocator (0: none).
-template <int OPT>
-__global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1) k_render(RenderArgs A) {
-  __shared__ float s_th[256];
-  __shared__ uint32_t s_cnt[4];
-  __shared__ float4 s_lut[(OPT & OPT_LUTLDS) != 0 ? kLutLds : 1];
-  __shared__ LogfTab s_logf[16];
-  const int tid = threadIdx.x;
-  s_th[tid] = A.srgbTh[tid];
-  if (tid < 16) s_logf[tid] = kLogfTab[tid];
-  if (tid < 4) s_cnt[tid] = 0;
-  const bool lutLds = (OPT & OPT_LUTLDS) != 0 && A.lutSize <= kLutLds;
-  if ((OPT & OPT_LUTLDS) != 0 && lutLds)
-    for (int i = tid; i < A.lutSize; i += 256) s_lut[i] = A.lut[i];
-  __syncthreads();
-
-  // block -> (tile k of this launch, 16x16 sub-block); wave -> 8x8 packet; lane -> pixel
-  const int k = blockIdx.x >> 4, sub = blockIdx.x & 15;
+// ------------------------------------------------------------------ per-pixel pieces
+// The frame grid: 256-thread workgroup b, thread t -> gid = 256 b + t.  Workgroup b covers
+// 16x16 pixels of tile k = b / 16 of this launch (frame tile tileBegin + k*tileStride),
+// wave w an 8x8 packet, lane l one pixel.
+struct Pixel {
+  int x, y;
+  size_t outIdx;
+  bool active;
+};
+__device__ __forceinline__ Pixel pixel_of(const RenderArgs &A, uint32_t gid) {
+  const int blk = (int)(gid >> 8), tid = (int)(gid & 255);
+  const int k = blk >> 4, sub = blk & 15;
   const int wave = tid >> 6, lane = tid & 63;
   const int lx = ((sub & 3) << 4) | ((wave & 1) << 3) | (lane & 7);
   const int ly = ((sub >> 2) << 4) | ((wave >> 1) << 3) | (lane >> 3);
   const int tileId = A.tileBegin + k * A.tileStride;
   const int tx = tileId % A.tilesX, ty = tileId / A.tilesX;
-  const int x = tx * 64 + lx, y = ty * 64 + ly;
-  Counts cnt = {0, 0, 0, 0};
-  Tracer<OPT> T(A, s_lut, lutLds, s_logf, cnt);
-  const bool active = k < A.numTiles && x < A.W && y < A.H;
-  if (active) {
-    const size_t outIdx = A.packed ? (size_t)k * 4096 + ly * 64 + lx : (size_t)x + (size_t)A.W * y;
-    float4 old = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr ((OPT & OPT_ACCPF) != 0) old = A.accum[outIdx];
-    // Random rnd(accumID*W*H + x, y) (deviceCode.cu:288-289)
-    uint32_t st = lcg_seed((uint32_t)A.accumID * (uint32_t)A.W * (uint32_t)A.H + (uint32_t)x, (uint32_t)y);
-    // generateRay (deviceCode.cu:36-49): g++ draws the dir_dv jitter first
-    st = lcg_next(st);
-    const float jv = lcg_float(st);
-    st = lcg_next(st);
-    const float ju = lcg_float(st);
-    const float su = (float)x + .5f, sv = (float)y + .5f;
-    const float a = su + ju, b = sv + jv;
-    float dx = (A.dir00.x + a * A.du.x) + b * A.dv.x;
-    float dy = (A.dir00.y + a * A.du.y) + b * A.dv.y;
-    float dz = (A.dir00.z + a * A.du.z) + b * A.dv.z;
-    const float len = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
-    dx = dx / len;
-    dy = dy / len;
-    dz = dz / len;
-    if (fabsf(dx) < 1e-5f) dx = 1e-5f;
-    if (fabsf(dy) < 1e-5f) dy = 1e-5f;
-    if (fabsf(dz) < 1e-5f) dz = 1e-5f;
-    Ray ray = {A.org.x, A.org.y, A.org.z, 0.f, dx, dy, dz, 1e10f};
+  Pixel p;
+  p.x = tx * 64 + lx;
+  p.y = ty * 64 + ly;
+  p.active = k < A.numTiles && p.x < A.W && p.y < A.H;
+  p.outIdx = A.packed ? (size_t)k * 4096 + ly * 64 + lx : (size_t)p.x + (size_t)A.W * p.y;
+  return p;
+}
+
+// Random rnd(accumID*W*H + x, y) (deviceCode.cu:288-289) and generateRay (36-49); g++
+// draws the dir_dv jitter first.
+__device__ __forceinline__ void gen_ray(const RenderArgs &A, int x, int y, uint32_t &st, float &dx,
+                                        float &dy, float &dz) {
+  st = lcg_seed((uint32_t)A.accumID * (uint32_t)A.W * (uint32_t)A.H + (uint32_t)x, (uint32_t)y);
+  st = lcg_next(st);
+  const float jv = lcg_float(st);
+  st = lcg_next(st);
+  const float ju = lcg_float(st);
+  const float su = (float)x + .5f, sv = (float)y + .5f;
+  const float a = su + ju, b = sv + jv;
+  dx = (A.dir00.x + a * A.du.x) + b * A.dv.x;
+  dy = (A.dir00.y + a * A.du.y) + b * A.dv.y;
+  dz = (A.dir00.z + a * A.du.z) + b * A.dv.z;
+  const float len = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
+  dx = dx / len;
+  dy = dy / len;
+  dz = dz / len;
+  if (fabsf(dx) < 1e-5f) dx = 1e-5f;
+  if (fabsf(dy) < 1e-5f) dy = 1e-5f;
+  if (fabsf(dz) < 1e-5f) dz = 1e-5f;
+}
+
+// accumulate lerp(vec4f(color,alpha), old, 1/(accumID+1)) and write linear_to_srgb +
+// make_rgba (deviceCode.cu:333-340)
+__device__ __forceinline__ void write_pixel(const RenderArgs &A, size_t outIdx, float cr, float cg,
+                                            float cb, float alpha, const float *s_th) {
+  const float4 old = A.accum[outIdx];
+  const float w = 1.f / (float)(A.accumID + 1);
+  float4 nv;
+  nv.x = w * cr + (1.f - w) * old.x;
+  nv.y = w * cg + (1.f - w) * old.y;
+  nv.z = w * cb + (1.f - w) * old.z;
+  nv.w = w * alpha + (1.f - w) * old.w;
+  A.accum[outIdx] = nv;
+  A.fb[outIdx] = srgb_byte(s_th, nv.x) + (srgb_byte(s_th, nv.y) << 8) +
+                 (srgb_byte(s_th, nv.z) << 16) + (make_8bit(nv.w) << 24);
+}
+
+// Wave-aggregated append: lanes with `want` get consecutive slots of queue counter *ctr
+// (one atomic per wave).  Call with the whole wave converged.
+__device__ __forceinline__ uint32_t wave_append(unsigned long long *ctr, bool want) {
+  const unsigned long long m = __ballot(want);
+  if (!m) return 0;
+  const int leader = __ffsll((long long)m) - 1;
+  uint32_t base = 0;
+  if ((int)__lane_id() == leader) base = (uint32_t)atomicAdd(ctr, (unsigned long long)__popcll(m));
+  base = __shfl(base, leader, 64);
+  const unsigned long long below = m & ((1ull << __lane_id()) - 1ull);
+  return base + (uint32_t)__popcll(below);
+}
+
+__device__ __forceinline__ void flush_counters(const RenderArgs &A, uint32_t *s_cnt, int tid) {
+  __syncthreads();
+  if (tid < 5 && s_cnt[tid]) atomicAdd(&A.counters[tid], (unsigned long long)s_cnt[tid]);
+}
+
+// march-queue record: {gid | flags, t0, t1, majorant} -- the first leaf of a ray's first
+// range, where (for the default data and cameras) nearly every ray ends
+constexpr uint32_t kRecLast = 0x80000000u;  // nothing after this leaf can change the pixel
+constexpr uint32_t kRecAE = 0x40000000u;    // woodcockTrackingAE semantics
+constexpr uint32_t kRecGid = 0x3FFFFFFFu;
+// continuation-list counter (in RenderArgs::counters)
+constexpr int kCtrCont = 11;
+
+// ------------------------------------------------------------------ kernel 1: setup
+// Per pixel: the ray, boxTest, the shell ranges (ShellAccel.h:94-111) and the first leaf
+// of the first range (121-124, 163-170).  Pixels the raygen leaves without a Woodcock step
+// are written here; rays with a first leaf to march are appended to the march queue
+// (compacted: only in-shell rays occupy lanes of the march kernel); rays whose first leaf
+// cannot decide them go to the continuation list.
+template <int OPT>
+__global__ void __launch_bounds__(256) k_setup(RenderArgs A) {
+  __shared__ float s_th[256];
+  __shared__ uint32_t s_cnt[8];
+  __shared__ uint32_t s_wcnt[4];
+  const int tid = threadIdx.x;
+  s_th[tid] = A.srgbTh[tid];
+  if (tid < 8) s_cnt[tid] = 0;
+  __syncthreads();
+  const uint32_t gid = blockIdx.x * 256u + (uint32_t)tid;
+  const Pixel px = pixel_of(A, gid);
+  int action = 0;  // 0 nothing, 1 write a zero sample, 2 march queue, 3 continuation
+  uint4 rec = make_uint4(0u, 0u, 0u, 0u);
+  if (px.active) {
+    uint32_t st;
+    float dx, dy, dz;
+    gen_ray(A, px.x, px.y, st, dx, dy, dz);
+    const Ray ray = {A.org.x, A.org.y, A.org.z, 0.f, dx, dy, dz, 1e10f};
     float t0, t1;
     if (box_test(ray, A, t0, t1)) {
-      ++cnt.inBox;
-      ray.tmin = t0;
-      ray.tmax = t1;
+      {
+        const unsigned long long m = __ballot(1);
+        if (__lane_id() == (unsigned)(__ffsll((long long)m) - 1)) atomicAdd(&s_cnt[1], (uint32_t)__popcll(m));
+      }
+      if (A.raygen == 1) {  // woodcockTrackingAE: one leaf, the box interval, majorant 1
+        action = 2;
+        rec = make_uint4(gid | kRecAE | kRecLast, __float_as_uint(t0), __float_as_uint(t1), __float_as_uint(1.f));
+      } else {
+        float st1 = 0.f, st2 = 0.f, st3 = 0.f, st4 = 0.f;
+        const bool s1 = intersect_sphere(ray, A.sbHi.x, st1, st4);
+        const bool s2 = intersect_sphere(ray, A.sbLo.x, st2, st3);
+        float lower = 0.f, upper = -1.f;
+        bool twoRanges = false;
+        if ((s1 || s2) && !(st4 < t0)) {
+          if (s1 && !s2) {
+            lower = st1; upper = st4;
+          } else if (t0 < st2) {
+            lower = st1; upper = st2;
+            twoRanges = !(st4 <= st3);  // range 1 not box1f::empty (lastRange's test)
+          } else {
+            lower = st3; upper = st4;
+          }
+        }
+        if (upper <= lower) {
+          action = 1;  // no range: the pixel accumulates a zero sample
+        } else {
+          const float e1 = lower + A.sbLo.x * 1e-6f;
+          float r1, la1, lo1;
+          to_spherical(ray.ox + ray.dx * e1, ray.oy + ray.dy * e1, ray.oz + ray.dz * e1, r1, la1, lo1);
+          const int cx = project_axis(r1, A.sbLo.x, A.sbHi.x, A.dims.x);
+          const int cy = project_axis(la1, A.sbLo.y, A.sbHi.y, A.dims.y);
+          const int cz = project_axis(lo1, A.sbLo.z, A.sbHi.z, A.dims.z);
+          // first leaf: tt1 = the least of tnext = {upper, 0, 0} that is >= lower
+          float tt1 = IRT_FLT_MAX;
+          if (upper < tt1 && upper >= lower) tt1 = upper;
+          if (0.f < tt1 && 0.f >= lower) tt1 = 0.f;
+          const uint32_t leaf = (uint32_t)wrap_coord(cz, A.dims.z) * (uint32_t)A.dims.x * (uint32_t)A.dims.y +
+                                (uint32_t)wrap_coord(cy, A.dims.y) * (uint32_t)A.dims.x +
+                                (uint32_t)wrap_coord(cx, A.dims.x);
+          const float maj = A.maxOp[leaf];
+          if (tt1 == lower || !(maj > 0.f)) {
+            // a zero-length first leaf or a zero majorant: no sample can hit here
+            action = twoRanges ? 3 : 1;
+          } else {
+            action = 2;
+            rec = make_uint4(gid | (twoRanges ? 0u : kRecLast), __float_as_uint(lower),
+                             __float_as_uint(tt1), __float_as_uint(maj));
+          }
+        }
+      }
+    }
+  }
+  // march queue: this workgroup's rays, compacted to the front of its own 256-slot
+  // segment (an LDS prefix over the waves, no global atomics); the count per segment
+  // tells the march kernel how many of its lanes have work
+  {
+    const unsigned long long m = __ballot(action == 2);
+    const int w = tid >> 6;
+    if ((tid & 63) == 0) s_wcnt[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t off = 0;
+    for (int k = 0; k < w; ++k) off += s_wcnt[k];
+    const uint32_t pos = off + (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
+    if (action == 2) A.queue[blockIdx.x * 256u + pos] = rec;
+    if (tid == 0) A.segCount[blockIdx.x] = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+  }
+  const uint32_t ci = wave_append(&A.counters[kCtrCont], action == 3);
+  if (action == 3) A.contList[ci] = gid;
+  if (action == 1) write_pixel(A, px.outIdx, 0.f, 0.f, 0.f, 0.f, s_th);
+  if (A.counters) {
+    if (px.active) atomicAdd(&s_cnt[0], 1u);
+    flush_counters(A, s_cnt, tid);
+  }
+}
+
+// ------------------------------------------------------------------ kernel 2: march
+// One lane per queued ray: woodcockTracking over the first leaf (deviceCode.cu:149-186
+// via the woodcockFunc lambda, 304-323, or the AE raygen, 239-275) with the binned
+// locator; writes the pixel, or hands an undecided ray with a later range on.
+template <int OPT>
+__global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1) k_march(RenderArgs A) {
+  const uint32_t count = A.segCount[blockIdx.x];  // rays of setup workgroup blockIdx.x
+  if (count == 0) return;                         // whole workgroup: nothing to march
+  __shared__ float s_th[256];
+  __shared__ uint32_t s_cnt[8];
+  __shared__ LogfTab s_logf[16];
+  __shared__ uint32_t s_sph[kSphBitWords];
+  __shared__ float s_lutA[kLutAlphaLds];
+  const int tid = threadIdx.x;
+  if (A.numSph)
+    for (int i = tid; i < kSphBitWords; i += 256) s_sph[i] = A.sphBits[i];
+  if (A.lutSize <= kLutAlphaLds)
+    for (int i = tid; i < A.lutSize; i += 256) s_lutA[i] = A.lut[i].w;
+  s_th[tid] = A.srgbTh[tid];
+  if (tid < 16) s_logf[tid] = kLogfTab[tid];
+  if (tid < 8) s_cnt[tid] = 0;
+  __syncthreads();
+  Tracer<OPT> T{A, s_logf, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}, s_lutA};
+  const uint32_t j = (uint32_t)tid;
+  bool cont = false;
+  uint32_t gid = 0;
+  if (j < count) {
+    const uint4 rec = A.queue[blockIdx.x * 256u + j];
+    gid = rec.x & kRecGid;
+    const Pixel px = pixel_of(A, gid);
+    uint32_t st;
+    float dx, dy, dz;
+    gen_ray(A, px.x, px.y, st, dx, dy, dz);
+    const float t0 = __uint_as_float(rec.y), t1 = __uint_as_float(rec.z);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float tw = T.woodcock(dx, dy, dz, t0, t1, st, __uint_as_float(rec.w), s, true);
+    const bool hit = (rec.x & kRecAE) || (tw > t0 && tw < t1);
+    if (hit || (rec.x & kRecLast)) {
       float cr = 0.f, cg = 0.f, cb = 0.f, alpha = 0.f;
-      if (A.raygen == 1) {
-        // woodcockTrackingAE (deviceCode.cu:239-275): majorant 1 over the box interval,
-        // color/alpha from the last accepted sample (zero if none)
-        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        T.woodcock(ray, st, 1.f, s);
+      if (hit) {
         cr = s.x * A.amb.x * A.ambRad;
         cg = s.y * A.amb.y * A.ambRad;
         cb = s.z * A.amb.z * A.ambRad;
         alpha = s.w > 0.f ? 1.f : 0.f;
-      } else {
-        // sdda (ShellAccel.h:82-229) driving the woodcockFunc lambda (deviceCode.cu:304-323)
-        const float sceneEPS = A.sbLo.x * 1e-6f;
-        float st1 = 0.f, st2 = 0.f, st3 = 0.f, st4 = 0.f;
-        const bool s1 = intersect_sphere(ray, A.sbHi.x, st1, st4);
-        const bool s2 = intersect_sphere(ray, A.sbLo.x, st2, st3);
-        if ((s1 || s2) && !(st4 < ray.tmin)) {
-          float rlo[2] = {__builtin_inff(), __builtin_inff()};
-          float rhi[2] = {-__builtin_inff(), -__builtin_inff()};
-          if (s1 && !s2) {
-            rlo[0] = st1; rhi[0] = st4;
-          } else if (ray.tmin < st2) {
-            rlo[0] = st1; rhi[0] = st2;
-            rlo[1] = st3; rhi[1] = st4;
-          } else {
-            rlo[0] = st3; rhi[0] = st4;
-          }
-          bool done = false;
-          for (int i = 0; i < 2 && !done; ++i) {
-            const float lower = rlo[i], upper = rhi[i];
-            if (upper <= lower) break;  // box1f::empty (vecmath.h:981)
-            const float e1 = lower + sceneEPS, e2 = upper - sceneEPS;
-            float r1, la1, lo1, r2, la2, lo2;
-            to_spherical(ray.ox + ray.dx * e1, ray.oy + ray.dy * e1, ray.oz + ray.dz * e1, r1, la1, lo1);
-            to_spherical(ray.ox + ray.dx * e2, ray.oy + ray.dy * e2, ray.oz + ray.dz * e2, r2, la2, lo2);
-            // cellID / step / stop (ShellAccel.h:121-132)
-            int cx = project_axis(r1, A.sbLo.x, A.sbHi.x, A.dims.x);
-            int cy = project_axis(la1, A.sbLo.y, A.sbHi.y, A.dims.y);
-            int cz = project_axis(lo1, A.sbLo.z, A.sbHi.z, A.dims.z);
-            const int sx = r1 < r2 ? 1 : -1, sy = la1 < la2 ? 1 : -1, sz = lo1 < lo2 ? 1 : -1;
-            const int ex = (int)((uint32_t)project_axis(r2, A.sbLo.x, A.sbHi.x, A.dims.x) + (uint32_t)sx);
-            const int ey = (int)((uint32_t)project_axis(la2, A.sbLo.y, A.sbHi.y, A.dims.y) + (uint32_t)sy);
-            const int ez = (int)((uint32_t)project_axis(lo2, A.sbLo.z, A.sbHi.z, A.dims.z) + (uint32_t)sz);
-            // The lat/lon "planes" (ShellAccel.h:147-160, 183-200) are built from
-            // toCartesian(vec3f(0.f, ...)) -- radius 0 -- so N = 0, w = 0 and every
-            // evalPlane(...) is exactly +-0: tnext = {upper, 0, 0} throughout, and the sign
-            // of those zeros never changes a comparison.  (radius/sphereT1, 136-146, is dead.)
-            const float tnx = upper, tny = 0.f, tnz = 0.f;
-            // Since tnext never changes, every leaf after the first sees the same interval
-            // [t_closest, t_closest] (t_closest = min(upper, 0)): a zero-length leaf, where
-            // woodcockTracking can only draw (its tw <= tmax == tmin never passes
-            // deviceCode.cu:316).  Such leaves matter only through the RNG state they
-            // advance, i.e. only when another range follows.
-            const bool lastRange = i == 1 || rhi[1] <= rlo[1];
-            float t = lower;
-            for (int iter = 0; iter < (1 << 22); ++iter) {
-              float tt1 = IRT_FLT_MAX;
-              if (tnx < tt1 && tnx >= t) tt1 = tnx;
-              if (tny < tt1 && tny >= t) tt1 = tny;
-              if (tnz < tt1 && tnz >= t) tt1 = tnz;
-              const uint32_t leaf = (uint32_t)wrap_coord(cz, A.dims.z) * (uint32_t)A.dims.x * (uint32_t)A.dims.y +
-                                    (uint32_t)wrap_coord(cy, A.dims.y) * (uint32_t)A.dims.x +
-                                    (uint32_t)wrap_coord(cx, A.dims.x);
-              if (tt1 == t) {
-                // zero-length leaf: nothing later reads the RNG state in the last range
-                if (lastRange) break;
-                const float maj = A.maxOp[leaf];
-                const float q = maj / A.unitDistance;
-                const uint32_t nx = lcg_next(st);
-                if (maj > 0.f && q > 0.f && q <= 1e30f && (nx & 0x00FFFFFFu) != 0u) {
-                  // one draw: logf(1-xi) < 0 puts t past tmax (deviceCode.cu:165-166)
-                  st = nx;
-                } else {
-                  Ray wr = ray;
-                  wr.tmin = t;
-                  wr.tmax = tt1;
-                  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-                  T.woodcock(wr, st, maj, s, false);
-                }
-              } else {  // woodcockFunc(leafID, t, tt1)
-                Ray wr = ray;
-                wr.tmin = t;
-                wr.tmax = tt1;
-                float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-                const float tw = T.woodcock(wr, st, A.maxOp[leaf], s);
-                if (tw > t && tw < tt1) {
-                  cr = s.x * A.amb.x * A.ambRad;
-                  cg = s.y * A.amb.y * A.ambRad;
-                  cb = s.z * A.amb.z * A.ambRad;
-                  alpha = s.w > 0.f ? 1.f : 0.f;
-                  done = true;
-                  break;
-                }
-              }
-              const float t_closest = fminf(fminf(tnx, tny), tnz);
-              if (tnx == t_closest) {
-                cx += sx;
-                if (cx == ex) break;
-              }
-              if (tny == t_closest) {
-                cy += sy;
-                if (cy == ey) break;
-              }
-              if (tnz == t_closest) {
-                cz += sz;
-                if (cz == ez) break;
-              }
-              t = t_closest;
-            }
-          }
-        }
       }
-      // accumulate: lerp(vec4f(color,alpha), old, 1/(accumID+1)) (deviceCode.cu:333-334)
-      if constexpr ((OPT & OPT_ACCPF) == 0) old = A.accum[outIdx];
-      const float w = 1.f / (float)(A.accumID + 1);
-      float4 nv;
-      nv.x = w * cr + (1.f - w) * old.x;
-      nv.y = w * cg + (1.f - w) * old.y;
-      nv.z = w * cb + (1.f - w) * old.z;
-      nv.w = w * alpha + (1.f - w) * old.w;
-      A.accum[outIdx] = nv;
-      // linear_to_srgb + make_rgba (deviceCode.cu:336-340)
-      A.fb[outIdx] = srgb_byte(s_th, nv.x) + (srgb_byte(s_th, nv.y) << 8) +
-                     (srgb_byte(s_th, nv.z) << 16) + (make_8bit(nv.w) << 24);
+      write_pixel(A, px.outIdx, cr, cg, cb, alpha, s_th);
+    } else {
+      cont = true;
     }
   }
-  if (A.counters) {
-    // per-workgroup reduction, one 64-bit atomic per counter per workgroup
-    atomicAdd(&s_cnt[0], active ? 1u : 0u);
-    if (cnt.inBox) atomicAdd(&s_cnt[1], cnt.inBox);
-    if (cnt.locate) atomicAdd(&s_cnt[2], cnt.locate);
-    if (cnt.found) atomicAdd(&s_cnt[3], cnt.found);
-    __syncthreads();
-    if (tid < 4) atomicAdd(&A.counters[tid], (unsigned long long)s_cnt[tid]);
-    uint32_t c = cnt.cand;  // candidate-list entries examined (wave-reduced)
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
-    if (lane == 0 && c) atomicAdd(&A.counters[4], (unsigned long long)c);
+  const uint32_t ci = wave_append(&A.counters[kCtrCont], cont);
+  if (cont) A.contList[ci] = gid;
+  if (A.counters) flush_counters(A, s_cnt, tid);
+  if constexpr ((OPT & OPT_STATS) != 0) {
+    uint32_t ss = T.cnt.steps, sm = T.cnt.steps;
+    for (int off = 32; off > 0; off >>= 1) {
+      ss += __shfl_down(ss, off, 64);
+      sm = max(sm, (uint32_t)__shfl_down(sm, off, 64));
+    }
+    if ((tid & 63) == 0) {
+      atomicAdd(&A.counters[5], (unsigned long long)ss);
+      atomicAdd(&A.counters[6], (unsigned long long)sm);
+      atomicMax(&A.counters[9], (unsigned long long)sm);  // longest ray (draws)
+    }
+    if (j < count) {  // draws histogram: <= 2, 3-5, 6-10, > 10
+      const int bkt = T.cnt.steps <= 2 ? 12 : (T.cnt.steps <= 5 ? 13 : (T.cnt.steps <= 10 ? 14 : 15));
+      atomicAdd(&A.counters[bkt], 1ull);
+    }
   }
 }
 
+// ------------------------------------------------------------------ the full raygen
+// One pixel of woodcockTrackingWithAccel / woodcockTrackingAE, every range and leaf.  Used
+// alone (variant bit OPT_MONO) or as the continuation pass for the rays the march kernel
+// could not decide (skipFirst: the first leaf's sampleVolume calls were counted there).
+template <int OPT>
+__device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
+                                             const float *s_th, int4 *s_dda, float4 *s_entry,
+                                             int tid, bool skipFirst) {
+  uint32_t st;
+  float dx, dy, dz;
+  gen_ray(A, px.x, px.y, st, dx, dy, dz);
+  const Ray ray = {A.org.x, A.org.y, A.org.z, 0.f, dx, dy, dz, 1e10f};
+  float t0, t1;
+  if (!box_test(ray, A, t0, t1)) return;  // deviceCode.cu:294-295: pixel untouched
+  if (!skipFirst) T.count(1);
+  float cr = 0.f, cg = 0.f, cb = 0.f, alpha = 0.f;
+  const bool ae = A.raygen == 1;
+  // The ranges the raygen tracks.  woodcockTrackingAE (deviceCode.cu:239-275): the box
+  // interval, majorant 1, one leaf.  woodcockTrackingWithAccel: sdda (ShellAccel.h:82-229)
+  // over the shell's (at most two) sphere ranges (94-111), each a sequence of macrocell
+  // leaves handed to the woodcockFunc lambda (deviceCode.cu:304-323).
+  float rlo0 = t0, rhi0 = t1, rlo1 = __builtin_inff(), rhi1 = -__builtin_inff();
+  int numRanges = 1;
+  if (!ae) {
+    float st1 = 0.f, st2 = 0.f, st3 = 0.f, st4 = 0.f;
+    const bool s1 = intersect_sphere(ray, A.sbHi.x, st1, st4);
+    const bool s2 = intersect_sphere(ray, A.sbLo.x, st2, st3);
+    numRanges = 0;
+    if ((s1 || s2) && !(st4 < t0)) {  // ray.tmin == t0 here
+      numRanges = 2;
+      if (s1 && !s2) {
+        rlo0 = st1; rhi0 = st4;
+      } else if (t0 < st2) {
+        rlo0 = st1; rhi0 = st2;
+        rlo1 = st3; rhi1 = st4;
+      } else {
+        rlo0 = st3; rhi0 = st4;
+      }
+    }
+  }
+  const float sceneEPS = A.sbLo.x * 1e-6f;
+  for (int i = 0; i < numRanges; ++i) {
+    const float lower = i ? rlo1 : rlo0, upper = i ? rhi1 : rhi0;
+    if (upper <= lower) break;  // box1f::empty (vecmath.h:981)
+    const bool lastRange = ae || i == 1 || rhi1 <= rlo1;
+    // cellID of the entry point (ShellAccel.h:121-124)
+    int cx = 0, cy = 0, cz = 0;
+    if (!ae) {
+      const float e1 = lower + sceneEPS;
+      float r1, la1, lo1;
+      to_spherical(ray.ox + ray.dx * e1, ray.oy + ray.dy * e1, ray.oz + ray.dz * e1, r1, la1, lo1);
+      cx = project_axis(r1, A.sbLo.x, A.sbHi.x, A.dims.x);
+      cy = project_axis(la1, A.sbLo.y, A.sbHi.y, A.dims.y);
+      cz = project_axis(lo1, A.sbLo.z, A.sbHi.z, A.dims.z);
+      if (!lastRange) s_entry[tid] = make_float4(r1, la1, lo1, 0.f);  // for step (125-127)
+    }
+    // The lat/lon "planes" (ShellAccel.h:147-160, 183-200) are built from
+    // toCartesian(vec3f(0.f, ...)) -- radius 0 -- so N = 0, w = 0 and every evalPlane(...)
+    // is exactly +-0: tnext = {upper, 0, 0} throughout, and the sign of those zeros never
+    // changes a comparison.  (radius/sphereT1, 136-146, is dead.)  So only a range's FIRST
+    // leaf can have positive length: every later one is [t_c, t_c] with t_c = min(upper, 0),
+    // where woodcockTracking can only consume draws (its tw <= tmax == tmin never passes
+    // deviceCode.cu:316).  Those leaves matter only through the RNG state, i.e. only when
+    // another range follows -- and only then are the exit point, step and stop needed.
+    const float tnx = upper, tny = 0.f, tnz = 0.f;
+    float t = lower;
+    for (int iter = 0; iter < (1 << 22); ++iter) {
+      float tt1 = IRT_FLT_MAX;
+      if (ae) {
+        tt1 = upper;
+      } else {
+        if (tnx < tt1 && tnx >= t) tt1 = tnx;
+        if (tny < tt1 && tny >= t) tt1 = tny;
+        if (tnz < tt1 && tnz >= t) tt1 = tnz;
+      }
+      const bool zeroLen = tt1 == t;
+      if (zeroLen && lastRange) break;
+      float maj = 1.f;
+      if (!ae) {
+        const uint32_t leaf = (uint32_t)wrap_coord(cz, A.dims.z) * (uint32_t)A.dims.x * (uint32_t)A.dims.y +
+                              (uint32_t)wrap_coord(cy, A.dims.y) * (uint32_t)A.dims.x +
+                              (uint32_t)wrap_coord(cx, A.dims.x);
+        maj = A.maxOp[leaf];
+      }
+      bool fast = false;
+      if (zeroLen) {
+        const float q = maj / A.unitDistance;
+        const uint32_t nx = lcg_next(st);
+        if (!(maj > 0.f)) {
+          fast = true;  // woodcockTracking returns at once (deviceCode.cu:161-162)
+        } else if (q > 0.f && q <= 1e30f && (nx & 0x00FFFFFFu) != 0u) {
+          st = nx;  // one draw: logf(1-xi) < 0 puts t past tmax (165-166)
+          fast = true;
+        }
+      }
+      if (!fast) {  // woodcockFunc(leafID, t, tt1)
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool counted = !zeroLen && !(skipFirst && i == 0 && iter == 0);
+        const float tw = T.woodcock(ray.dx, ray.dy, ray.dz, t, tt1, st, maj, s, counted);
+        if (!zeroLen && (ae || (tw > t && tw < tt1))) {
+          // AE: colour/alpha from the last accepted sample, zero if none (239-275)
+          cr = s.x * A.amb.x * A.ambRad;
+          cg = s.y * A.amb.y * A.ambRad;
+          cb = s.z * A.amb.z * A.ambRad;
+          alpha = s.w > 0.f ? 1.f : 0.f;
+          i = 2;  // done: no further ranges
+          break;
+        }
+      }
+      if (lastRange) break;  // every later leaf of the last range is zero-length
+      int4 dd;               // {packed steps, ex, ey, ez}
+      if (iter == 0) {
+        // exit point, step and stop (ShellAccel.h:125-132), first needed now
+        const float e2 = upper - sceneEPS;
+        float r2, la2, lo2;
+        to_spherical(ray.ox + ray.dx * e2, ray.oy + ray.dy * e2, ray.oz + ray.dz * e2, r2, la2, lo2);
+        const float4 en = s_entry[tid];
+        const float r1 = en.x, la1 = en.y, lo1 = en.z;
+        const int sx = r1 < r2 ? 1 : -1, sy = la1 < la2 ? 1 : -1, sz = lo1 < lo2 ? 1 : -1;
+        dd.x = (sx > 0 ? 1 : 0) | (sy > 0 ? 2 : 0) | (sz > 0 ? 4 : 0);
+        dd.y = (int)((uint32_t)project_axis(r2, A.sbLo.x, A.sbHi.x, A.dims.x) + (uint32_t)sx);
+        dd.z = (int)((uint32_t)project_axis(la2, A.sbLo.y, A.sbHi.y, A.dims.y) + (uint32_t)sy);
+        dd.w = (int)((uint32_t)project_axis(lo2, A.sbLo.z, A.sbHi.z, A.dims.z) + (uint32_t)sz);
+        s_dda[tid] = dd;
+      } else {
+        dd = s_dda[tid];
+      }
+      const float t_closest = fminf(fminf(tnx, tny), tnz);
+      if (tnx == t_closest) {
+        cx += (dd.x & 1) ? 1 : -1;
+        if (cx == dd.y) break;
+      }
+      if (tny == t_closest) {
+        cy += (dd.x & 2) ? 1 : -1;
+        if (cy == dd.z) break;
+      }
+      if (tnz == t_closest) {
+        cz += (dd.x & 4) ? 1 : -1;
+        if (cz == dd.w) break;
+      }
+      t = t_closest;
+    }
+  }
+  write_pixel(A, px.outIdx, cr, cg, cb, alpha, s_th);
+}
+
+// The full raygen per pixel: alone over the frame grid (OPT_MONO), or as the continuation
+// pass over A.contList (a workgroup-stride loop over the list).
+template <int OPT>
+__global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1) k_render(RenderArgs A, int listMode) {
+  uint32_t n = 0;
+  if (listMode) {
+    n = (uint32_t)A.counters[kCtrCont];
+    if (blockIdx.x * 256u >= n) return;  // whole workgroup: nothing to continue
+  }
+  __shared__ float s_th[256];
+  __shared__ uint32_t s_cnt[8];
+  __shared__ LogfTab s_logf[16];
+  __shared__ uint32_t s_sph[kSphBitWords];
+  __shared__ int4 s_dda[256];       // sdda state needed only after a range's first leaf
+  __shared__ float4 s_entry[256];
+  const int tid = threadIdx.x;
+  if (A.numSph)
+    for (int i = tid; i < kSphBitWords; i += 256) s_sph[i] = A.sphBits[i];
+  s_th[tid] = A.srgbTh[tid];
+  if (tid < 16) s_logf[tid] = kLogfTab[tid];
+  if (tid < 8) s_cnt[tid] = 0;
+  __syncthreads();
+  Tracer<OPT> T{A, s_logf, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
+  if (listMode) {
+    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
+      const uint32_t j = base + (uint32_t)tid;
+      if (j < n) {
+        const Pixel px = pixel_of(A, A.contList[j]);
+        render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, true);
+      }
+    }
+  } else {
+    const Pixel px = pixel_of(A, blockIdx.x * 256u + (uint32_t)tid);
+    if (px.active) render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, false);
+    if (A.counters && px.active) atomicAdd(&s_cnt[0], 1u);
+  }
+  if (A.counters) flush_counters(A, s_cnt, tid);
+}
+
 // ------------------------------------------------------------------ variants / launcher
+// Variant bits: irt_render.hip OPT_* (bits 8-11: minimum waves per SIMD of the march
+// kernel).  OPT_MONO = 4096 runs the full raygen per pixel in one kernel instead of the
+// setup -> march -> continuation pipeline.  All variants give identical results.
+constexpr int OPT_MONO = 4096;
+constexpr int kContBlocks = 128;
+
 #define IRT_VARIANTS(X) \
-  X(0) X(1536) X(8192) X(8224) X(9728) X(9760) X(10240) X(10272) X(9729) X(9731)
+  X(0) X(1) X(2) X(1536) X(2048) X(32768) X(4096) X(4097) X(4098) X(5120) X(5376) X(5632) X(6144) X(36864)
 
 bool render_variant_available(int v) {
 #define IRT_CASE(N) if (v == N) return true;
@@ -436,16 +823,28 @@ bool render_variant_available(int v) {
   return false;
 }
 
+template <int N>
+void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
+  constexpr int K = N & ~OPT_MONO;
+  if constexpr ((N & OPT_MONO) != 0) {
+    hipLaunchKernelGGL(k_render<K>, dim3(numBlocks), dim3(256), 0, s, A, 0);
+  } else {
+    hipLaunchKernelGGL(k_setup<K>, dim3(numBlocks), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_march<K>, dim3(numBlocks), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_render<K & ~0xF00>, dim3(kContBlocks), dim3(256), 0, s, A, 1);
+  }
+}
+
 void launch_render(const RenderArgs &A, int numBlocks, hipStream_t s, int variant) {
   switch (variant) {
 #define IRT_CASE(N) \
   case N:           \
-    hipLaunchKernelGGL(k_render<N>, dim3(numBlocks), dim3(256), 0, s, A); \
+    launch_variant<N>(A, numBlocks, s); \
     return;
     IRT_VARIANTS(IRT_CASE)
 #undef IRT_CASE
     default:
-      hipLaunchKernelGGL(k_render<0>, dim3(numBlocks), dim3(256), 0, s, A);
+      launch_variant<0>(A, numBlocks, s);
   }
 }
 

@@ -71,6 +71,19 @@ int irt_debug_scene_locate(const irt_debug_scene *s, irt_vec3f p, float *value,
   return hit;
 }
 
+int irt_debug_scene_locate_binned(const irt_debug_scene *s, irt_vec3f p, float *value,
+                                  uint32_t *record, uint32_t *tested) {
+  if (!s || !value) return IRT_E_INVALID;
+  float v = 0.f;
+  uint32_t r = 0;
+  int hit = locate_bins_host(s->s, p.x, p.y, p.z, v, &r, tested);
+  if (hit) {
+    *value = v;
+    if (record) *record = r;
+  }
+  return hit;
+}
+
 int irt_debug_scene_values(const irt_debug_scene *s, uint32_t rec, float r, float *out2) {
   if (!s || !out2 || rec >= s->s.n) return IRT_E_INVALID;
   const float *hv = &s->s.hv[(size_t)rec * kHV];

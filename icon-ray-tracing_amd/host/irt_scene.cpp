@@ -299,6 +299,9 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads)
           int mode = 2;  // 0 normal, 1 antipodal, 2 degenerate
           for (size_t i = i0; i < i1 && mode == 2; ++i) {
             const irt_icon_cell &ci = cells[i];
+            // only records with a positive radial extent carve out a cone (inverted ones
+            // never pass the radial test; zero-thickness ones are spheres, see below)
+            if (!(ci.height[0] < ci.height[ci.numLayers])) continue;
             const double rm = 0.5 * ((double)ci.height[0] + (double)ci.height[ci.numLayers]);
             for (int sgn = 0; sgn < 2 && mode == 2; ++sgn) {
               const double s = sgn ? -rm : rm;
@@ -322,13 +325,43 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads)
           gc.erase(std::unique(gc.begin(), gc.end()), gc.end());
           for (size_t i = i0; i < i1; ++i) {
             const irt_icon_cell &ci = cells[i];
-            if (ci.height[0] > ci.height[ci.numLayers]) continue;  // radial test never passes
+            // inverted: the radial test never passes; zero thickness: the sphere table
+            if (!(ci.height[0] < ci.height[ci.numLayers])) continue;
             for (uint32_t g : gc) out.emplace_back(g, (uint32_t)i);
           }
         }
       });
     }
     for (auto &t : ts) t.join();
+  }
+
+  // --- zero-thickness records (height[0] == height[numLayers], e.g. the numLayers == 0
+  //     records convert_icon writes for numLayers % 32 == 1, convert_icon.cpp:363-365):
+  //     their bottom and top corners coincide, so every side plane has N == 0 and
+  //     sample() accepts ANY direction at r == height[0] exactly -- a sphere.  They are
+  //     kept out of the cell lists, in a table sorted by (radius, record).
+  {
+    std::vector<std::pair<float, uint32_t>> sph;
+    for (size_t i = 0; i < n; ++i)
+      if (cells[i].height[0] == cells[i].height[cells[i].numLayers])
+        sph.emplace_back(cells[i].height[0], (uint32_t)i);
+    std::sort(sph.begin(), sph.end());
+    S.sphR.clear();
+    S.sphOff.assign(1, 0u);
+    S.sphRec.clear();
+    for (size_t k = 0; k < sph.size(); ++k) {
+      if (k == 0 || sph[k].first != sph[k - 1].first) {
+        if (k) S.sphOff.push_back((uint32_t)S.sphRec.size());
+        S.sphR.push_back(sph[k].first);
+      }
+      S.sphRec.push_back(sph[k].second);
+    }
+    if (!sph.empty()) S.sphOff.push_back((uint32_t)S.sphRec.size());
+    S.sphBits.assign(kSphBitWords, 0u);
+    for (float r : S.sphR) {
+      const uint32_t h = sph_hash(r);
+      S.sphBits[h >> 5] |= 1u << (h & 31);
+    }
   }
 
   // --- stable counting sort by grid cell -> CSR
@@ -355,7 +388,254 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads)
   }
   S.info.locatorFaceRes = G;
   S.info.locatorEntries = total;
+  return build_bins(S, threads);
+}
+
+// ---------------------------------------------------------------- radially binned lists
+namespace {
+
+// Open bin (lo, hi) membership of a record with radial extent [h0, hN] (irt_common.h).
+inline bool in_bin(float h0, float hN, float lo, float hi) {
+  return (h0 < hi && hN > lo) || (h0 == hN && h0 == hi);
+}
+
+// Expected number of list entries a radius drawn uniformly from the cell's radial extent
+// meets, for the given edges: sum over bins of (bin length within [rmin, rmax]) * count.
+double bin_cost(const std::vector<LocEntry> &E, const float *edges, int ne, double rmin,
+                double rmax) {
+  double cost = 0;
+  for (int k = 0; k <= ne; ++k) {
+    const float lo = k ? edges[k - 1] : -INFINITY, hi = k < ne ? edges[k] : INFINITY;
+    const double a = std::max(rmin, (double)lo), b = std::min(rmax, (double)hi);
+    if (!(b > a)) continue;
+    size_t cnt = 0;
+    for (const LocEntry &e : E) cnt += in_bin(e.h0, e.hN, lo, hi) ? 1 : 0;
+    cost += (b - a) * (double)cnt;
+  }
+  return cost;
+}
+
+// Up to kMaxEdges edges for one cell, greedily, among the records' bottom heights.
+int choose_edges(const std::vector<LocEntry> &E, float *edges) {
+  if (E.size() <= 2) return 0;
+  double rmin = INFINITY, rmax = -INFINITY;
+  std::vector<float> cand;
+  for (const LocEntry &e : E) {
+    rmin = std::min(rmin, (double)e.h0);
+    rmax = std::max(rmax, (double)e.hN);
+    cand.push_back(e.h0);
+  }
+  std::sort(cand.begin(), cand.end());
+  cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+  std::vector<float> c2;
+  for (float v : cand)
+    if (v > rmin && v < rmax) c2.push_back(v);
+  if (c2.size() > 48) {  // bound the search: 48 quantiles
+    std::vector<float> q;
+    for (int k = 0; k < 48; ++k) q.push_back(c2[(size_t)k * c2.size() / 48]);
+    q.erase(std::unique(q.begin(), q.end()), q.end());
+    c2.swap(q);
+  }
+  int ne = 0;
+  double best = bin_cost(E, edges, 0, rmin, rmax);
+  while (ne < kMaxEdges) {
+    int bi = -1;
+    double bc = best;
+    for (size_t i = 0; i < c2.size(); ++i) {
+      float tr[kMaxEdges];
+      int m = 0;
+      bool dup = false;
+      for (int k = 0; k < ne; ++k) {
+        if (edges[k] == c2[i]) dup = true;
+        tr[m++] = edges[k];
+      }
+      if (dup) continue;
+      tr[m++] = c2[i];
+      std::sort(tr, tr + m);
+      const double c = bin_cost(E, tr, m, rmin, rmax);
+      if (c < bc * 0.98) {
+        bc = c;
+        bi = (int)i;
+      }
+    }
+    if (bi < 0) break;
+    edges[ne++] = c2[bi];
+    std::sort(edges, edges + ne);
+    best = bc;
+  }
+  return ne;
+}
+
+}  // namespace
+
+int build_bins(HostScene &S, int threads) {
+  const uint32_t numGridCells = 6u * S.G * S.G;
+  // per-record height/value blocks
+  S.blocks.assign(S.n * (size_t)kBlk4 * 4, 0.f);
+  for (size_t i = 0; i < S.n; ++i) {
+    float *B = &S.blocks[i * (size_t)kBlk4 * 4];
+    const float *hv = &S.hv[i * kHV];
+    for (int j = 0; j < 32; ++j) B[blk_height_pos(j)] = hv[j];
+    for (int c = 0; c < 31; ++c) B[blk_value_pos(c)] = hv[32 + c];
+  }
+  // pass 1: edges and per-bin counts per cell
+  S.binHdr.assign((size_t)numGridCells * kBinHdrWords, 0u);
+  std::vector<uint64_t> cellCount(numGridCells + 1, 0);
+  auto parallel = [&](auto &&fn) {
+    std::vector<std::thread> ts;
+    const uint32_t chunk = (numGridCells + threads - 1) / std::max(threads, 1);
+    for (int t = 0; t < threads; ++t) {
+      const uint32_t b = t * chunk, e = std::min(numGridCells, b + chunk);
+      if (b >= e) break;
+      ts.emplace_back([&, b, e] { fn(b, e); });
+    }
+    for (auto &t : ts) t.join();
+  };
+  parallel([&](uint32_t b, uint32_t e) {
+    std::vector<LocEntry> E;
+    for (uint32_t cell = b; cell < e; ++cell) {
+      E.assign(S.entries.begin() + S.offsets[cell], S.entries.begin() + S.offsets[cell + 1]);
+      float edges[kMaxEdges];
+      const int ne = choose_edges(E, edges);
+      uint32_t *H = &S.binHdr[(size_t)cell * kBinHdrWords];
+      uint32_t cum = 0;
+      for (int k = 0; k < kMaxEdges; ++k) H[k] = f2u(k < ne ? edges[k] : INFINITY);
+      for (int k = 0; k <= kMaxEdges; ++k) {
+        if (k <= ne) {
+          const float lo = k ? edges[k - 1] : -INFINITY, hi = k < ne ? edges[k] : INFINITY;
+          for (const LocEntry &x : E) cum += in_bin(x.h0, x.hN, lo, hi) ? 1u : 0u;
+        }
+        H[4 + k] = cum;
+      }
+      cellCount[cell + 1] = cum;
+    }
+  });
+  for (uint32_t k = 0; k < numGridCells; ++k) cellCount[k + 1] += cellCount[k];
+  const uint64_t total = cellCount[numGridCells];
+  if (total > 0xFFFFFFF0ull) {
+    set_error("binned locator too large (%llu entries)", (unsigned long long)total);
+    return IRT_E_INVALID;
+  }
+  S.binEntries = total;
+  S.fat.assign(total * kFat4 * 4, 0.f);
+  // pass 2: fill the fat entries
+  parallel([&](uint32_t b, uint32_t e) {
+    for (uint32_t cell = b; cell < e; ++cell) {
+      uint32_t *H = &S.binHdr[(size_t)cell * kBinHdrWords];
+      H[3] = (uint32_t)cellCount[cell];
+      size_t at = cellCount[cell];
+      const float edges[kMaxEdges] = {u2f(H[0]), u2f(H[1]), u2f(H[2])};
+      int ne = 0;
+      while (ne < kMaxEdges && edges[ne] != INFINITY) ++ne;
+      for (int k = 0; k <= ne; ++k) {
+        const float lo = k ? edges[k - 1] : -INFINITY, hi = k < ne ? edges[k] : INFINITY;
+        for (uint32_t q = S.offsets[cell]; q < S.offsets[cell + 1]; ++q) {
+          const LocEntry &x = S.entries[q];
+          if (!in_bin(x.h0, x.hN, lo, hi)) continue;
+          float *F = &S.fat[at++ * kFat4 * 4];
+          memcpy(F, &S.planes[3 * (size_t)x.idx], 12 * sizeof(float));
+          F[12] = x.h0;
+          F[13] = x.hN;
+          F[14] = u2f(x.idx);
+          F[15] = u2f(x.meta);
+          const float *hv = &S.hv[(size_t)x.idx * kHV];
+          F[16] = hv[7];
+          F[17] = hv[15];
+          F[18] = hv[23];
+          F[19] = hv[31];
+        }
+      }
+    }
+  });
   return IRT_OK;
+}
+
+namespace {
+// sample() of one fat entry (ICONGrid.h:181-208), value from the record's blocks
+bool test_fat(const HostScene &s, const float *F, float px, float py, float pz, float r,
+              float &value) {
+  if (r < F[12] || r > F[13]) return false;  // ICONGrid.h:184
+  for (int k = 0; k < 3; ++k) {
+    const Plane4 p = {F[4 * k], F[4 * k + 1], F[4 * k + 2], F[4 * k + 3]};
+    if (evalPlane(p, px, py, pz) > 0.f) return false;  // ICONGrid.h:201-203
+  }
+  const uint32_t rec = f2u(F[14]), meta = f2u(F[15]);
+  const int nl = (int)(meta & 0x7fffffffu);
+  const float *B = &s.blocks[(size_t)rec * kBlk4 * 4];
+  if (meta >> 31) {
+    const int b = rec_coarse_block(F[16], F[17], F[18], F[19], nl, r);
+    const float *Q = B + 16 * b;
+    const int m = rec_block_index(Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], Q[6], b, nl, r);
+    value = select8(m, Q[8], Q[9], Q[10], Q[11], Q[12], Q[13], Q[14], Q[15]);
+  } else {
+    int first = 0, count = nl;  // findHeight, literally (ICONGrid.h:117-145)
+    while (count > 0) {
+      const int stp = count / 2, it = first + stp;
+      if (!(r <= B[blk_height_pos(it + 1)])) {
+        first = it + 1;
+        count -= stp + 1;
+      } else {
+        count = stp;
+      }
+    }
+    value = B[blk_value_pos(first)];
+  }
+  return true;
+}
+// getValue (ICONGrid.h:147-164) of a zero-thickness record: literal findHeight
+float sphere_value(const HostScene &s, uint32_t rec, float r) {
+  const float *hv = &s.hv[(size_t)rec * kHV];
+  int32_t nl;
+  memcpy(&nl, hv + 63, 4);
+  return hv[32 + find_height(hv, nl, r)];
+}
+}  // namespace
+
+int locate_bins_host(const HostScene &s, float px, float py, float pz, float &value,
+                     uint32_t *record, uint32_t *tested) {
+  if (tested) *tested = 0;
+  if (s.n == 0 || s.G == 0) return 0;
+  const float r = sqrtf(px * px + py * py + pz * pz);
+  const uint32_t cell = cubemap_cell(px, py, pz, s.G);
+  const uint32_t *H = &s.binHdr[(size_t)cell * kBinHdrWords];
+  const float e[3] = {u2f(H[0]), u2f(H[1]), u2f(H[2])};
+  const int b = bin_of(r, e[0], e[1], e[2]);
+  int hit = 0;
+  uint32_t best = 0;
+  float bestV = 0.f;
+  const int last = (b < kMaxEdges && r == e[b]) ? b + 1 : b;  // exactly on an edge
+  for (int k = b; k <= last; ++k) {
+    const uint32_t beg = H[3] + (k ? H[4 + k - 1] : 0), end = H[3] + H[4 + k];
+    for (uint32_t q = beg; q < end; ++q) {
+      const float *F = &s.fat[(size_t)q * kFat4 * 4];
+      if (hit && f2u(F[14]) >= best) break;
+      if (tested) ++*tested;
+      float v;
+      if (test_fat(s, F, px, py, pz, r, v)) {
+        hit = 1;
+        best = f2u(F[14]);
+        bestV = v;
+        break;
+      }
+    }
+  }
+  // sphere records at exactly this radius (see build_scene)
+  if (!s.sphR.empty()) {
+    const auto it = std::lower_bound(s.sphR.begin(), s.sphR.end(), r);
+    if (it != s.sphR.end() && *it == r) {
+      const uint32_t rec = s.sphRec[s.sphOff[it - s.sphR.begin()]];  // lowest index
+      if (!hit || rec < best) {
+        hit = 1;
+        best = rec;
+        bestV = sphere_value(s, rec, r);
+      }
+    }
+  }
+  if (hit) {
+    value = bestV;
+    if (record) *record = best;
+  }
+  return hit;
 }
 
 // sample() (ICONGrid.h:181-208) with the precomputed planes; lat/lon of toSpherical are

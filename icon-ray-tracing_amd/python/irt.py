@@ -26,6 +26,9 @@ assert CELL_DTYPE.itemsize == 284
 
 RAYGEN_WITH_ACCEL = 0  # woodcockTrackingWithAccel (deviceCode.cu:281-341)
 RAYGEN_AE = 1          # woodcockTrackingAE (deviceCode.cu:239-275)
+# compiled variants of the raygen (irt_render.hip OPT_* bits; 4096 = one monolithic
+# kernel instead of the setup -> march -> continuation pipeline); all bit-identical
+BIN_VARIANTS = (0, 1, 2, 1536, 2048, 32768, 4096, 4097, 4098, 5120, 5376, 5632, 6144, 36864)
 
 
 class IrtError(RuntimeError):
@@ -130,6 +133,8 @@ def lib() -> C.CDLL:
             "irt_debug_scene_build": [P, S, C.POINTER(P)],
             "irt_debug_scene_info": [P, C.POINTER(VolumeInfo)],
             "irt_debug_scene_locate": [P, Vec3, C.POINTER(C.c_float), C.POINTER(C.c_uint32)],
+            "irt_debug_scene_locate_binned": [P, Vec3, C.POINTER(C.c_float),
+                                              C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)],
             "irt_debug_scene_candidates": [P, Vec3, P, I],
             "irt_debug_scene_planes": [P, C.c_uint32, P],
             "irt_debug_scene_values": [P, C.c_uint32, F, P],
@@ -376,6 +381,16 @@ class DebugScene:
         r = C.c_uint32()
         hit = lib().irt_debug_scene_locate(self._h, vec3(p), C.byref(v), C.byref(r))
         return (True, v.value, r.value) if hit == 1 else (False, 0.0, None)
+
+    def locate_binned(self, p):
+        """locate() through the binned locator of the render kernel; also returns the
+        number of candidate entries examined."""
+        v = C.c_float()
+        r = C.c_uint32()
+        t = C.c_uint32()
+        hit = lib().irt_debug_scene_locate_binned(self._h, vec3(p), C.byref(v), C.byref(r),
+                                                  C.byref(t))
+        return (True, v.value, r.value, t.value) if hit == 1 else (False, 0.0, None, t.value)
 
     def candidates(self, p):
         n = lib().irt_debug_scene_candidates(self._h, vec3(p), None, 0)

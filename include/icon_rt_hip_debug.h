@@ -37,6 +37,10 @@ int irt_debug_scene_info(const irt_debug_scene *s, irt_volume_info *info);
  * record of the lowest-index cell containing p, 0 if none. */
 int irt_debug_scene_locate(const irt_debug_scene *s, irt_vec3f p, float *value,
                            uint32_t *record);
+/* The same query through the binned locator the render kernel uses (radial bins of fat
+ * entries, irt_common.h); *tested = candidate entries examined. */
+int irt_debug_scene_locate_binned(const irt_debug_scene *s, irt_vec3f p, float *value,
+                                  uint32_t *record, uint32_t *tested);
 /* findHeight + value of record `rec` at radius r two ways: out2[0] from the literal
  * binary search (ICONGrid.h:117-164), out2[1] from the render-record layout the
  * state-machine kernel gathers (irt_common.h).  They must agree bit for bit. */
@@ -51,6 +55,11 @@ void irt_debug_scene_free(irt_debug_scene *s);
 /* Select the render-kernel variant (bit set of irt_render.hip's OPT_* flags; every
  * variant gives identical results -- used for in-process A/B timing). */
 int irt_debug_set_variant(irt_context *ctx, int variant);
+/* The raw per-frame counters of the last render (waits for it): [0] launched [1] in box
+ * [2] sampleVolume calls [3] found [4] candidates; with the statistics variant bit also
+ * [5] Woodcock draws [6] sum over waves of the per-wave max draws [7] zero-length leaves
+ * [8] sum over waves of the per-wave max zero-length leaves [9] rays reaching range 1. */
+int irt_debug_counters(irt_context *ctx, unsigned long long *out16);
 
 /* Evaluate the kernels' device versions of asinf(a[i]) and atan2f(y[i], x[i]) on GPU
  * `device` (host arrays in/out; n elements each).  Used to prove the device restatements

@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=10)
-    ap.add_argument("--variants", default="1536,4096,5376,5632,6144")
+    ap.add_argument("--variants", default="0,1,1536,2048,4096")
     ap.add_argument("--camera", default="framing", choices=["framing", "viewall"])
     ap.add_argument("--no-check", action="store_true",
                     help="report but do not stop on differences (counter-collection passes may "

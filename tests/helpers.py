@@ -69,3 +69,33 @@ def gpu_frame(cells, W, H, camera=None, accum_ids=(0,), raygen=0, lut=None, valu
         stats.append(fr.render(lp))
     a, f = fr.host()
     return a, f, stats, ctx
+
+
+def terrain_cells(seed=11, bisections=1, levels=70):
+    """A synthetic scene with terrain-following record boundaries (per-column offsets, like
+    ICON's HHL), a few unsorted-height records, zero-thickness records (numLayers 0, as
+    convert_icon writes for numLayers % 32 == 1) and inverted records."""
+    cells = irt.synth_grid(2, bisections, levels)
+    rng = np.random.default_rng(seed)
+    ncol = cells.size // 3
+    for c in range(ncol):  # per-column terrain offset, shrinking with height
+        off = np.float32(rng.uniform(0, 3000))
+        for k in range(3):
+            i = 3 * c + k
+            nl = int(cells["numLayers"][i])
+            h = cells["height"][i].astype(np.float64)
+            h[:nl + 1] += off * (1.0 - (h[:nl + 1] - 6.371229e6) / 75e3)
+            cells["height"][i][:nl + 1] = h[:nl + 1].astype(np.float32)
+        for k in (1, 2):  # keep the stack contiguous (record k starts where k-1 ends)
+            i = 3 * c + k
+            cells["height"][i][0] = cells["height"][i - 1][cells["numLayers"][i - 1]]
+    for i in rng.choice(cells.size, 40, replace=False):
+        nl = int(cells["numLayers"][i])
+        if i % 4 == 0 and nl >= 3:
+            h = cells["height"][i]
+            h[1], h[2] = h[2], h[1]
+        elif i % 4 == 1:
+            cells["numLayers"][i] = 0  # zero-thickness record
+        elif i % 4 == 2:
+            cells["height"][i][nl] = cells["height"][i][0] - 1.0  # inverted: never hit
+    return cells

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import irt
-from helpers import FRAMING, bits, gpu_frame, oracle_frame
+from helpers import FRAMING, bits, gpu_frame, oracle_frame, terrain_cells
 
 pytestmark = pytest.mark.gpu
 
@@ -208,4 +208,44 @@ def test_gpu_matches_reference_golden(name):
         assert (st.locateCalls, st.samplesFound) == tuple(int(v) for v in d["counts"][k])
     a, f = fr.host()
     assert_same_frame(a, f, d["accum"], d["fb"], name)
+    ctx.close()
+
+
+def test_terrain_and_degenerate_records_bit_exact():
+    """Terrain-following record boundaries (per-cell radial bin edges differ), unsorted
+    heights, zero-thickness records (spheres) and inverted records."""
+    cells = terrain_cells(11)
+    for cam in (FRAMING, None):
+        a_ref, f_ref, st_ref, _ = oracle_frame(cells, 80, 80, camera=cam)
+        a_gpu, f_gpu, st_gpu, _ = gpu_frame(cells, 80, 80, camera=cam)
+        assert_same_frame(a_gpu, f_gpu, a_ref, f_ref, "terrain")
+        assert st_gpu[0].locateCalls == st_ref[0].locate_calls
+        assert st_gpu[0].samplesFound == st_ref[0].samples_found
+
+
+def test_all_render_variants_identical():
+    """Every compiled variant of the binned raygen (batching, occupancy bounds, LUT in LDS)
+    renders the same frame and counts as the default."""
+    L = irt.lib()
+    L.irt_debug_set_variant.argtypes = [C.c_void_p, C.c_int]
+    cells = irt.synth_grid(2, 3, 90)
+    W = 128
+    setup = irt.setup_frame(cells, W, W, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    import torch
+    fb = torch.zeros(W * W, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(W * W * 4, dtype=torch.float32, device="cuda")
+    ref = None
+    for v in irt.BIN_VARIANTS:
+        assert L.irt_debug_set_variant(ctx._h, v) == 0
+        acc.zero_()
+        ctx.render(setup.lp, W, W, fb.data_ptr(), acc.data_ptr())
+        st = ctx.stats()
+        out = (fb.cpu().numpy().copy(), bits(acc.cpu().numpy()), st.locateCalls, st.samplesFound)
+        if ref is None:
+            ref = out
+            continue
+        assert np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1]), v
+        assert out[2:] == ref[2:], v
     ctx.close()

@@ -11,7 +11,7 @@ import pytest
 import irt
 import oracle as O
 from golden_util import FRAME_FIXTURES, load
-from helpers import FRAMING, bits
+from helpers import FRAMING, bits, terrain_cells
 
 
 @pytest.mark.parametrize("name", FRAME_FIXTURES)
@@ -159,6 +159,8 @@ def test_locator_is_conservative_and_lowest_index(rn, bis, L):
     n_hit = 0
     for p in pts:
         hit, v, rec = D.locate(p)
+        hb, vb, recb, _ = D.locate_binned(p)  # the render kernel's binned lists
+        assert (hb, recb, np.float32(vb)) == (hit, rec, np.float32(v)), p
         val = C.c_float()
         found = None
         for i in range(cells.size):
@@ -205,3 +207,73 @@ def test_render_record_layout_gives_findheight_value():
             assert np.float32(a).view(np.uint32) == np.float32(b).view(np.uint32), (i, nl, r)
             checked += 1
     assert len(nls) > 25 and checked > 5000
+
+
+def _norm32(p):
+    p = p.astype(np.float32)
+    return np.sqrt(np.float32(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]))
+
+
+def _on_radius(v, r):
+    """A float32 point in direction v whose float32 |p| (sqrtf(x*x+y*y+z*z), as
+    toSpherical computes it) equals r exactly, when one is found nearby."""
+    v = np.asarray(v, np.float64)
+    v = v / np.linalg.norm(v)
+    r = np.float32(r)
+    s = np.float64(r)
+    p = (v * s).astype(np.float32)
+    for _ in range(64):
+        q = _norm32(p)
+        if q == r:
+            break
+        s *= 1 + (float(r) - float(q)) / float(r) * 0.999 + (1e-8 if q < r else -1e-8)
+        p = (v * s).astype(np.float32)
+    return p
+
+
+def test_binned_locator_on_terrain_following_columns():
+    """The binned lists (per-cell radial edges, fat entries) against the brute-force first
+    hit on columns whose record boundaries differ from column to column (terrain-following
+    levels, like ICON's HHL), records with unsorted heights, zero-thickness records and
+    inverted records -- at random radii, exactly on every record boundary and its float
+    neighbours."""
+    cells = terrain_cells(11)
+    rng = np.random.default_rng(12)
+    D = irt.DebugScene(cells)
+    Lb = O.olib()
+    pts = []
+    d = rng.normal(size=(300, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    sbl = float(cells["height"][:, 0].min())
+    sbu = float(cells["height"].max())
+    pts += list((d * rng.uniform(sbl - 50, sbu + 50, (300, 1))).astype(np.float32))
+    for i in rng.choice(cells.size, 80):
+        c = cells[i]
+        lat, lon = c["lat"].astype(np.float64), c["lon"].astype(np.float64)
+        cd = np.stack([np.cos(lat) * np.cos(lon), np.cos(lat) * np.sin(lon), np.sin(lat)], 1)
+        v = cd.mean(0)
+        v /= np.linalg.norm(v)
+        for hh in (c["height"][0], c["height"][c["numLayers"]]):
+            for rr in (hh, np.nextafter(hh, np.float32(np.inf)), np.nextafter(hh, np.float32(0))):
+                pts.append(_on_radius(v, rr))
+    # a direction far from any column of a zero-thickness record, on its radius exactly
+    zt = [i for i in range(cells.size) if cells["height"][i][0] == cells["height"][i][cells["numLayers"][i]]]
+    assert zt
+    for i in zt[:10]:
+        pts.append(_on_radius(rng.normal(size=3), cells["height"][i][0]))
+    n_hit = n_sph = 0
+    zt = set(zt)
+    for p in pts:
+        hb, vb, recb, _ = D.locate_binned(p)
+        val = C.c_float()
+        found = None
+        for i in range(cells.size):
+            if Lb.oracle_sample(cells[i:i + 1].ctypes.data, O.v3(p), C.byref(val)):
+                found = (i, np.float32(val.value))
+                break
+        assert (found is not None) == hb, p
+        if hb:
+            n_hit += 1
+            assert found[0] == recb and found[1] == np.float32(vb), (p, found, recb)
+            n_sph += found[0] in zt
+    assert n_hit > len(pts) // 3 and n_sph >= 3
