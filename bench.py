@@ -1,16 +1,25 @@
 #!/usr/bin/env python3
 """bench.py -- Mray/s + ms/frame of the MI355X ICON renderer (BASELINE.json metric).
 
-One step = one frame of the hot path: the raygen woodcockTrackingWithAccel
-(icon_rt/deviceCode.cu:281-341) over every pixel of the launch, plus -- for N > 1 GPUs --
-the RCCL gather of the frame tiles to rank 0 and rank 0's unpack.  Inputs (cells, locator,
-shell accelerator, transfer function) are resident in HBM before the timed region.
+The hot path is the raygen woodcockTrackingWithAccel (icon_rt/deviceCode.cu:281-341) over
+every pixel of a 1024x1024 frame.  Inputs (cells, locator, shell accelerator, transfer
+function) are resident in HBM before the timed region.
 
 Default workload (configs[2] of BASELINE.json, C3): synthetic R2B07 ICON grid (1,310,720
 cells) x 90 levels (3,932,160 `.ic` records), 1024x1024, framing camera
 `--camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60`, the reference's default transfer function.
-N GPUs split the SAME frame into interleaved 64x64 tiles (strong scaling); each rank runs
-one process (torchrun), rank 0 gathers RGBA8 tiles over RCCL.
+
+One step:
+  * 1 GPU: one frame (one launch of the raygen over the 1024x1024 frame);
+  * N GPUs (weak scaling, one process per GPU under torchrun): N consecutive frames of the
+    reference's progressive accumulation (--sample-limit, accumID = step*N + k), tile-split:
+    every rank renders its interleaved 64x64 tiles of all N frames in ONE launch
+    (irt_render_tiles_accumulate), and rank 0 gathers the final RGBA8 tiles over RCCL
+    (torch.distributed "nccl") and unpacks the framebuffer.  The gather of step s runs on
+    the collective's stream while step s+1 renders (double-buffered tiles).  Per-GPU work
+    is one frame's rays per step at every N; `value` counts all ranks' rays.
+Frames are enqueued back to back: per-launch statistics come back through a ring, never
+stalling the host between launches.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -89,6 +98,9 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the multi-rank path with host-staged collectives "
+                         "(ranks may share a GPU); nccl (RCCL) is the measured path")
     args = ap.parse_args()
 
     import torch
@@ -97,11 +109,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = local % max(torch.cuda.device_count(), 1) if world > 1 else 0
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    device = local if world > 1 else 0
+        torch.cuda.set_device(device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{device}"))
+        else:
+            dist.init_process_group("gloo")
     torch.cuda.set_device(device)
     dev = torch.device(f"cuda:{device}")
 
@@ -119,6 +134,10 @@ def main():
     lp = setup.lp
     ntiles = irt.num_tiles(W, H)
     stream = torch.cuda.current_stream(device).cuda_stream
+    # frames per step: 1 on one GPU; N on N GPUs (weak scaling: N frames of the
+    # progressive accumulation per step, each rank rendering its interleaved 64x64 tiles of
+    # all N frames in one launch, rank 0 gathering the final RGBA8 tiles over RCCL)
+    frames = world
     if world == 1:
         fb = torch.zeros(W * H, dtype=torch.int32, device=dev)
         accum = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
@@ -128,63 +147,74 @@ def main():
         split = irt_dist.TileSplit(W, H, rank, world)
         assert split.num_tiles == ntiles
         maxt = split.max_tiles
-        fg = irt_dist.FrameGather(split, dev)
+        fg = irt_dist.FrameGather(split, dev, buffers=2, stage_cpu=args.dist_backend == "gloo")
         tiles_acc = torch.zeros(maxt * 4096 * 4, dtype=torch.float32, device=dev)
         fb = torch.zeros(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
+    inflight = {}
 
-    kernel_ms, samples, in_box, launched = [], 0, 0, 0
-
-    def step(frame):
-        nonlocal samples, in_box, launched
-        lp.accumID = frame
+    def step(s):
+        lp.accumID = s * frames
         if world == 1:
             ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
-        else:
-            ctx.render_tiles(lp, W, H, rank, world, fg.tiles.data_ptr(), tiles_acc.data_ptr(), stream)
-            g = fg.gather()  # RCCL gather of the packed RGBA8 tiles to rank 0
-            if rank == 0:
-                ctx.unpack_tiles(g.data_ptr(), world, maxt, W, H, fb.data_ptr(), stream)
-        st = ctx.stats()  # waits for this frame's kernel (like the reference's endTiming)
-        return st
+            return
+        b = s % 2
+        if b in inflight:  # the gather that last read this buffer must be done
+            finish(inflight.pop(b), b)
+        ctx.render_tiles_accumulate(lp, W, H, rank, world, frames, fg.bufs[b].data_ptr(),
+                                    tiles_acc.data_ptr(), stream)
+        inflight[b] = fg.gather_async(b)  # RCCL gather of this step's frame, overlapped
+
+    def finish(work, b):
+        g = fg.finish(work, b)
+        if rank == 0:
+            ctx.unpack_tiles(g.data_ptr(), world, maxt, W, H, fb.data_ptr(), stream)
+
+    def drain():
+        for b in sorted(inflight):
+            finish(inflight.pop(b), b)
 
     for f in range(args.warmup):
-        st = step(f)
-        log(f"[rank {rank}] warmup frame {f}: kernel {st.kernelMs:.3f} ms, "
-            f"{st.samplesFound} samples, {st.candidatesTested} candidates")
+        step(f)
+    drain()
+    st = ctx.stats()
+    log(f"[rank {rank}] warmup: last launch kernel {st.kernelMs:.3f} ms, {st.samplesFound} "
+        f"samples, {st.candidatesTested} candidates")
+    ctx.reset_stats_total()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
-        st = step(args.warmup + k)
-        kernel_ms.append(st.kernelMs)
-        samples += st.samplesFound
-        in_box += st.raysInBox
-        launched += st.raysLaunched
+        step(args.warmup + k)
+    if world > 1:
+        drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
-    log(f"[rank {rank}] timed {args.steps} frames in {elapsed:.3f} s")
+    tot, launches = ctx.stats_total()
+    log(f"[rank {rank}] timed {args.steps} steps ({launches} launches) in {elapsed:.3f} s")
+    samples, in_box = tot.samplesFound, tot.raysInBox
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        rdev = dev if args.dist_backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        agg = torch.tensor([samples, in_box, launched], dtype=torch.float64, device=dev)
+        agg = torch.tensor([samples, in_box, tot.raysLaunched], dtype=torch.float64, device=rdev)
         dist.all_reduce(agg)
         samples_all, in_box_all, launched_all = (int(v) for v in agg.tolist())
     else:
-        samples_all, in_box_all, launched_all = samples, in_box, launched
+        samples_all, in_box_all, launched_all = samples, in_box, tot.raysLaunched
 
     ms_per_step = elapsed / args.steps * 1e3
-    mray = W * H * args.steps / elapsed / 1e6
-    # roofline of the dominant kernel (k_render) on this rank: algorithmic bytes per launch
-    # over its HIP-event-timed average duration
-    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3 if kernel_ms else float("nan")
-    bytes_per_launch = (BYTES_PER_SAMPLE * samples + BYTES_PER_RAY * in_box) / max(args.steps, 1)
-    achieved = bytes_per_launch / avg_kernel_s
+    mray = W * H * frames * args.steps / elapsed / 1e6  # all ranks' rays
+    # roofline of the dominant kernel on this rank: algorithmic bytes per launch over its
+    # HIP-event-timed average duration (events on the stream the kernel runs on)
+    avg_kernel_s = tot.kernelMs / 1e3 / max(launches, 1)
+    bytes_per_launch = (BYTES_PER_SAMPLE * samples + BYTES_PER_RAY * in_box) / max(launches, 1)
+    achieved = bytes_per_launch / avg_kernel_s if avg_kernel_s > 0 else float("nan")
 
     if rank == 0:
         out = {
@@ -196,7 +226,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
@@ -204,11 +234,16 @@ def main():
                 "workload": desc + ", framing camera --camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60, "
                            "woodcockTrackingWithAccel, default TF, one frame per step",
                 "records": int(cells.size), "width": W, "height": H,
-                "parallelism": f"frame-tiles x{world} (64x64, interleaved), RCCL gather to rank 0"
+                "parallelism": (f"{world} GPUs x 64x64 interleaved frame tiles, {frames} progressive "
+                                f"frames per step in one launch per rank, RCCL gather of the "
+                                f"final RGBA8 tiles to rank 0 overlapped with the next step")
                 if world > 1 else "single GPU",
-                "samples_per_frame": samples_all / args.steps,
-                "rays_in_box_per_frame": in_box_all / args.steps,
+                "frames_per_step": frames,
+                "ms_per_frame": round(elapsed / (args.steps * frames) * 1e3, 4),
+                "samples_per_frame": samples_all / args.steps / frames,
+                "rays_in_box_per_frame": in_box_all / args.steps / frames,
                 "kernel_ms_rank0": round(avg_kernel_s * 1e3, 4),
+                "bytes_per_launch_rank0": bytes_per_launch,
             },
             "roofline": {
                 "bound": "hbm",

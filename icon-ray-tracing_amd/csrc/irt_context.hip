@@ -42,6 +42,8 @@ struct irt_context {
   uint4 *d_queue = nullptr;      // march queue and continuation list (irt_render.hip),
   uint32_t *d_contList = nullptr;  // sized for the largest launch so far
   uint32_t *d_segCount = nullptr;
+  float4 *d_samples = nullptr;   // per-frame colours of a progressive batch
+  size_t sampleCap = 0;
   size_t queueCap = 0;
   float *d_srgb = nullptr;
   float *d_valueRanges = nullptr;
@@ -52,11 +54,21 @@ struct irt_context {
   int lutSize = 0;
   float tfLo = 0.f, tfHi = 1.f, opScale = 1.f;
   bool tfSet = false;
-  unsigned long long *d_counters = nullptr;
-  unsigned long long *h_counters = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool pending = false;
+  // Per-launch statistics, read back without stalling the host: a ring of kSlots
+  // counter blocks and event pairs; a slot is finished (synchronised) only when it is
+  // reused or its statistics are asked for.  The last finished launch is `stats`; every
+  // finished launch also adds into `total`.
+  static constexpr int kSlots = 32;
+  unsigned long long *d_counters = nullptr;  // kSlots x 16
+  unsigned long long *h_counters = nullptr;  // pinned, kSlots x 16
+  hipEvent_t ev0[kSlots] = {}, ev1[kSlots] = {};  // kernel timing
+  hipEvent_t evDone[kSlots] = {};                  // counters landed in h_counters
+  bool pending[kSlots] = {};
+  long long launches = 0;     // slot of launch i: i % kSlots
   irt_render_stats stats{};
+  unsigned long long h_last[16] = {};
+  irt_render_stats total{};
+  long long totalLaunches = 0;
   size_t bytes = 0;
   int variant = kDefaultVariant;  // render-kernel variant (irt_render.hip OPT_* bits)
 };
@@ -84,35 +96,60 @@ void free_all(irt_context *c) {
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
-                  c->d_sphBits, c->d_queue, c->d_contList, c->d_segCount, c->d_maxOp, c->d_srgb, c->d_valueRanges,
+                  c->d_sphBits, c->d_queue, c->d_contList, c->d_segCount, c->d_samples, c->d_maxOp, c->d_srgb, c->d_valueRanges,
                   c->d_lut, c->d_counters};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (int i = 0; i < irt_context::kSlots; ++i) {
+    if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
+    if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
+    if (c->evDone[i]) (void)hipEventDestroy(c->evDone[i]);
+  }
   if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
-int finish_stats(irt_context *c) {
-  if (!c->pending) return IRT_OK;
-  IRT_HIP(hipEventSynchronize(c->ev1));
+int finish_slot(irt_context *c, int i) {
+  if (!c->pending[i]) return IRT_OK;
+  IRT_HIP(hipEventSynchronize(c->evDone[i]));
   float ms = 0.f;
-  IRT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-  c->stats.raysLaunched = c->h_counters[0];
-  c->stats.raysInBox = c->h_counters[1];
-  c->stats.locateCalls = c->h_counters[2];
-  c->stats.samplesFound = c->h_counters[3];
-  c->stats.candidatesTested = c->h_counters[4];
-  c->stats.kernelMs = ms;
-  c->pending = false;
+  IRT_HIP(hipEventElapsedTime(&ms, c->ev0[i], c->ev1[i]));
+  const unsigned long long *h = c->h_counters + 16 * i;
+  irt_render_stats st;
+  st.raysLaunched = h[0];
+  st.raysInBox = h[1];
+  st.locateCalls = h[2];
+  st.samplesFound = h[3];
+  st.candidatesTested = h[4];
+  st.kernelMs = ms;
+  c->stats = st;
+  memcpy(c->h_last, h, sizeof(c->h_last));
+  c->total.raysLaunched += st.raysLaunched;
+  c->total.raysInBox += st.raysInBox;
+  c->total.locateCalls += st.locateCalls;
+  c->total.samplesFound += st.samplesFound;
+  c->total.candidatesTested += st.candidatesTested;
+  c->total.kernelMs += ms;
+  ++c->totalLaunches;
+  c->pending[i] = false;
+  return IRT_OK;
+}
+
+// finish every pending launch, oldest first (the last one ends up in c->stats)
+int finish_stats(irt_context *c) {
+  for (long long j = c->launches - irt_context::kSlots; j < c->launches; ++j) {
+    if (j < 0) continue;
+    int rc = finish_slot(c, (int)(j % irt_context::kSlots));
+    if (rc) return rc;
+  }
   return IRT_OK;
 }
 
 int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int packed,
                 int tileBegin, int tileStride, uint32_t *fb, irt_vec4f *accum, int *numTilesOut,
-                void *stream) {
-  if (!c || !lp || W <= 0 || H <= 0 || !fb || !accum || tileStride <= 0 || tileBegin < 0) {
+                void *stream, int numFrames = 1) {
+  if (!c || !lp || W <= 0 || H <= 0 || !fb || !accum || tileStride <= 0 || tileBegin < 0 ||
+      numFrames < 1 || numFrames > 65535) {
     set_error("irt_render: bad argument");
     return IRT_E_INVALID;
   }
@@ -166,7 +203,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.tileStride = tileStride;
   A.numTiles = numTiles;
   A.tilesX = tilesX;
-  A.counters = c->d_counters;
+  A.counters = c->d_counters + 16 * (c->launches % irt_context::kSlots);
   A.binHdr = c->d_binHdr;
   A.fat = c->d_fat;
   A.blocks = c->d_blocks;
@@ -176,8 +213,9 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.sphRec = c->d_sphRec;
   A.sphBits = c->d_sphBits;
 
-  if (c->pending) {
-    int rc = finish_stats(c);
+  const int slot = (int)(c->launches % irt_context::kSlots);
+  if (c->pending[slot]) {  // the ring is full: retire that launch (long done by now)
+    int rc = finish_slot(c, slot);
     if (rc) return rc;
   }
   const size_t lanes = (size_t)numTiles * 4096;
@@ -201,16 +239,34 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.queue = c->d_queue;
   A.contList = c->d_contList;
   A.segCount = c->d_segCount;
-  IRT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), s));
-  IRT_HIP(hipEventRecord(c->ev0, s));
+  A.numSamples = numFrames;
+  if (numFrames > 1) {
+    const size_t need = lanes * (size_t)numFrames;
+    if (need > c->sampleCap) {
+      IRT_HIP(hipStreamSynchronize(s));
+      if (c->d_samples) IRT_HIP(hipFree(c->d_samples));
+      c->d_samples = nullptr;
+      c->bytes -= c->sampleCap * sizeof(float4);
+      c->sampleCap = 0;
+      int rc = dalloc(c, &c->d_samples, need);
+      if (rc) return rc;
+      c->sampleCap = need;
+      c->info.deviceBytes = c->bytes;
+    }
+  }
+  A.sampleBuf = c->d_samples;
+  IRT_HIP(hipMemsetAsync(A.counters, 0, 16 * sizeof(unsigned long long), s));
+  IRT_HIP(hipEventRecord(c->ev0[slot], s));
   if (numTiles > 0) {
     launch_render(A, numTiles * 16, s, c->variant);
   }
   IRT_HIP(hipGetLastError());
-  IRT_HIP(hipEventRecord(c->ev1, s));
-  IRT_HIP(hipMemcpyAsync(c->h_counters, c->d_counters, 16 * sizeof(unsigned long long),
+  IRT_HIP(hipEventRecord(c->ev1[slot], s));
+  IRT_HIP(hipMemcpyAsync(c->h_counters + 16 * slot, A.counters, 16 * sizeof(unsigned long long),
                          hipMemcpyDeviceToHost, s));
-  c->pending = true;
+  IRT_HIP(hipEventRecord(c->evDone[slot], s));
+  c->pending[slot] = true;
+  ++c->launches;
   return IRT_OK;
 }
 
@@ -278,13 +334,18 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
   if ((rc = dalloc(c, &c->d_maxOp, c->numMCs))) return fail(rc);
   if (hipMemsetAsync(c->d_maxOp, 0, c->numMCs * sizeof(float), c->stream) != hipSuccess) return fail(IRT_E_HIP);
   if ((rc = upload(c, &c->d_srgb, th, 256))) return fail(rc);
-  if ((rc = dalloc(c, &c->d_counters, 16))) return fail(rc);
-  if (hipHostMalloc((void **)&c->h_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
-    set_error("irt_create: event/pinned allocation failed");
+  if ((rc = dalloc(c, &c->d_counters, 16 * irt_context::kSlots))) return fail(rc);
+  if (hipHostMalloc((void **)&c->h_counters, 16 * irt_context::kSlots * sizeof(unsigned long long)) != hipSuccess) {
+    set_error("irt_create: pinned allocation failed");
     return fail(IRT_E_HIP);
   }
-  memset(c->h_counters, 0, 16 * sizeof(unsigned long long));
+  for (int i = 0; i < irt_context::kSlots; ++i)
+    if (hipEventCreate(&c->ev0[i]) != hipSuccess || hipEventCreate(&c->ev1[i]) != hipSuccess ||
+        hipEventCreate(&c->evDone[i]) != hipSuccess) {
+      set_error("irt_create: event creation failed");
+      return fail(IRT_E_HIP);
+    }
+  memset(c->h_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long));
 
   // ShellAccel{vec3i(1,1024,1024), sphericalBounds} + initGrid + buildShell_ICON
   // (hostCode.cu:652-666), majorants zero until a transfer function arrives
@@ -390,6 +451,17 @@ int irt_render_tiles(irt_context *c, const irt_launch_params *lp, int W, int H, 
   return render_impl(c, lp, W, H, 1, tileBegin, tileStride, fb, accum, numTiles, stream);
 }
 
+int irt_render_accumulate(irt_context *c, const irt_launch_params *lp, int W, int H,
+                          int numFrames, uint32_t *fb, irt_vec4f *accum, void *stream) {
+  return render_impl(c, lp, W, H, 0, 0, 1, fb, accum, nullptr, stream, numFrames);
+}
+
+int irt_render_tiles_accumulate(irt_context *c, const irt_launch_params *lp, int W, int H,
+                                int tileBegin, int tileStride, int numFrames, uint32_t *fb,
+                                irt_vec4f *accum, int *numTiles, void *stream) {
+  return render_impl(c, lp, W, H, 1, tileBegin, tileStride, fb, accum, numTiles, stream, numFrames);
+}
+
 int irt_unpack_tiles(irt_context *c, const uint32_t *g, int numRanks, int maxTiles, int W, int H,
                      uint32_t *fb, void *stream) {
   if (!c || !g || !fb || numRanks <= 0 || maxTiles < 0 || W <= 0 || H <= 0) {
@@ -411,6 +483,31 @@ int irt_get_render_stats(const irt_context *cc, irt_render_stats *st) {
   int rc = finish_stats(c);
   if (rc) return rc;
   *st = c->stats;
+  return IRT_OK;
+}
+
+int irt_get_render_stats_total(const irt_context *cc, irt_render_stats *total, long long *launches) {
+  irt_context *c = const_cast<irt_context *>(cc);
+  if (!c || !total) {
+    set_error("irt_get_render_stats_total: null argument");
+    return IRT_E_INVALID;
+  }
+  int rc = finish_stats(c);
+  if (rc) return rc;
+  *total = c->total;
+  if (launches) *launches = c->totalLaunches;
+  return IRT_OK;
+}
+
+int irt_reset_render_stats_total(irt_context *c) {
+  if (!c) {
+    set_error("irt_reset_render_stats_total: null context");
+    return IRT_E_INVALID;
+  }
+  int rc = finish_stats(c);
+  if (rc) return rc;
+  c->total = irt_render_stats{};
+  c->totalLaunches = 0;
   return IRT_OK;
 }
 
@@ -506,7 +603,7 @@ extern "C" int irt_debug_counters(irt_context *c, unsigned long long *out16) {
   }
   int rc = finish_stats(c);
   if (rc) return rc;
-  memcpy(out16, c->h_counters, 16 * sizeof(unsigned long long));
+  memcpy(out16, c->h_last, 16 * sizeof(unsigned long long));
   return IRT_OK;
 }
 

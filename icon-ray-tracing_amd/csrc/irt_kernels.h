@@ -55,7 +55,11 @@ struct RenderArgs {
   // ({gid | flags, t0, t1, majorant} per ray, one compacted segment per setup workgroup)
   // and the continuation list (gids, count in counters[11])
   uint4 *queue;
-  uint32_t *segCount;    // rays per 256-slot queue segment (one per setup workgroup)
+  uint32_t *segCount;
+  // progressive batch (irt_render_accumulate): frames accumID .. accumID+numSamples-1;
+  // for numSamples > 1 each frame's colour goes to sampleBuf[frame][lane] first
+  int numSamples;
+  float4 *sampleBuf;    // rays per 256-slot queue segment (one per setup workgroup)
   uint32_t *contList;
 };
 

@@ -386,9 +386,9 @@ __device__ __forceinline__ Pixel pixel_of(const RenderArgs &A, uint32_t gid) {
 
 // Random rnd(accumID*W*H + x, y) (deviceCode.cu:288-289) and generateRay (36-49); g++
 // draws the dir_dv jitter first.
-__device__ __forceinline__ void gen_ray(const RenderArgs &A, int x, int y, uint32_t &st, float &dx,
-                                        float &dy, float &dz) {
-  st = lcg_seed((uint32_t)A.accumID * (uint32_t)A.W * (uint32_t)A.H + (uint32_t)x, (uint32_t)y);
+__device__ __forceinline__ void gen_ray(const RenderArgs &A, int accumID, int x, int y, uint32_t &st,
+                                        float &dx, float &dy, float &dz) {
+  st = lcg_seed((uint32_t)accumID * (uint32_t)A.W * (uint32_t)A.H + (uint32_t)x, (uint32_t)y);
   st = lcg_next(st);
   const float jv = lcg_float(st);
   st = lcg_next(st);
@@ -446,6 +446,8 @@ __device__ __forceinline__ void flush_counters(const RenderArgs &A, uint32_t *s_
 constexpr uint32_t kRecLast = 0x80000000u;  // nothing after this leaf can change the pixel
 constexpr uint32_t kRecAE = 0x40000000u;    // woodcockTrackingAE semantics
 constexpr uint32_t kRecGid = 0x3FFFFFFFu;
+// sample-buffer marker of a frame whose ray missed the box (alpha is 0 or 1 otherwise)
+constexpr float kNoSample = -1.f;
 // continuation-list counter (in RenderArgs::counters)
 constexpr int kCtrCont = 11;
 
@@ -471,7 +473,7 @@ __global__ void __launch_bounds__(256) k_setup(RenderArgs A) {
   if (px.active) {
     uint32_t st;
     float dx, dy, dz;
-    gen_ray(A, px.x, px.y, st, dx, dy, dz);
+    gen_ray(A, A.accumID, px.x, px.y, st, dx, dy, dz);
     const Ray ray = {A.org.x, A.org.y, A.org.z, 0.f, dx, dy, dz, 1e10f};
     float t0, t1;
     if (box_test(ray, A, t0, t1)) {
@@ -582,7 +584,7 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
     const Pixel px = pixel_of(A, gid);
     uint32_t st;
     float dx, dy, dz;
-    gen_ray(A, px.x, px.y, st, dx, dy, dz);
+    gen_ray(A, A.accumID, px.x, px.y, st, dx, dy, dz);
     const float t0 = __uint_as_float(rec.y), t1 = __uint_as_float(rec.z);
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     const float tw = T.woodcock(dx, dy, dz, t0, t1, st, __uint_as_float(rec.w), s, true);
@@ -628,13 +630,17 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
 template <int OPT>
 __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
                                              const float *s_th, int4 *s_dda, float4 *s_entry,
-                                             int tid, bool skipFirst) {
+                                             int tid, bool skipFirst, int accumID,
+                                             float4 *sampleOut) {
   uint32_t st;
   float dx, dy, dz;
-  gen_ray(A, px.x, px.y, st, dx, dy, dz);
+  gen_ray(A, accumID, px.x, px.y, st, dx, dy, dz);
   const Ray ray = {A.org.x, A.org.y, A.org.z, 0.f, dx, dy, dz, 1e10f};
   float t0, t1;
-  if (!box_test(ray, A, t0, t1)) return;  // deviceCode.cu:294-295: pixel untouched
+  if (!box_test(ray, A, t0, t1)) {  // deviceCode.cu:294-295: pixel untouched
+    if (sampleOut) *sampleOut = make_float4(0.f, 0.f, 0.f, kNoSample);
+    return;
+  }
   if (!skipFirst) T.count(1);
   float cr = 0.f, cg = 0.f, cb = 0.f, alpha = 0.f;
   const bool ae = A.raygen == 1;
@@ -764,7 +770,10 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
       t = t_closest;
     }
   }
-  write_pixel(A, px.outIdx, cr, cg, cb, alpha, s_th);
+  if (sampleOut)
+    *sampleOut = make_float4(cr, cg, cb, alpha);
+  else
+    write_pixel(A, px.outIdx, cr, cg, cb, alpha, s_th);
 }
 
 // The full raygen per pixel: alone over the frame grid (OPT_MONO), or as the continuation
@@ -795,15 +804,51 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
       const uint32_t j = base + (uint32_t)tid;
       if (j < n) {
         const Pixel px = pixel_of(A, A.contList[j]);
-        render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, true);
+        render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, true, A.accumID, nullptr);
       }
     }
   } else {
-    const Pixel px = pixel_of(A, blockIdx.x * 256u + (uint32_t)tid);
-    if (px.active) render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, false);
+    // grid.y = frame k of a progressive batch (accumID + k), whose colour goes to the
+    // sample buffer for k_accumulate; a single frame writes accum/fb directly
+    const uint32_t gid = blockIdx.x * 256u + (uint32_t)tid;
+    const Pixel px = pixel_of(A, gid);
+    float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + gid : nullptr;
+    if (px.active)
+      render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, false, A.accumID + (int)blockIdx.y, slot);
     if (A.counters && px.active) atomicAdd(&s_cnt[0], 1u);
   }
   if (A.counters) flush_counters(A, s_cnt, tid);
+}
+
+// ------------------------------------------------------------------ progressive batch
+// The lerp chain of K consecutive frames (deviceCode.cu:333-334, accumID..accumID+K-1) over
+// the per-frame samples k_render stored, in frame order: bit-identical to K launches.
+// Frames whose ray missed the box leave the pixel untouched (kNoSample), as the
+// reference's raygen returns before writing (294-295); fb is written after the last frame.
+__global__ void __launch_bounds__(256) k_accumulate(RenderArgs A) {
+  __shared__ float s_th[256];
+  s_th[threadIdx.x] = A.srgbTh[threadIdx.x];
+  __syncthreads();
+  const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
+  const Pixel px = pixel_of(A, gid);
+  if (!px.active) return;
+  const size_t lanes = (size_t)gridDim.x * 256u;
+  float4 a = A.accum[px.outIdx];
+  bool wrote = false;
+  for (int k = 0; k < A.numSamples; ++k) {
+    const float4 c = A.sampleBuf[(size_t)k * lanes + gid];
+    if (c.w == kNoSample) continue;
+    const float w = 1.f / (float)(A.accumID + k + 1);
+    a.x = w * c.x + (1.f - w) * a.x;
+    a.y = w * c.y + (1.f - w) * a.y;
+    a.z = w * c.z + (1.f - w) * a.z;
+    a.w = w * c.w + (1.f - w) * a.w;
+    wrote = true;
+  }
+  if (!wrote) return;
+  A.accum[px.outIdx] = a;
+  A.fb[px.outIdx] = srgb_byte(s_th, a.x) + (srgb_byte(s_th, a.y) << 8) +
+                    (srgb_byte(s_th, a.z) << 16) + (make_8bit(a.w) << 24);
 }
 
 // ------------------------------------------------------------------ variants / launcher
@@ -812,6 +857,7 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
 // setup -> march -> continuation pipeline.  All variants give identical results.
 constexpr int OPT_MONO = 4096;
 constexpr int kContBlocks = 128;
+static_assert((kDefaultVariant & OPT_MONO) != 0, "progressive batches use the default kernel");
 
 #define IRT_VARIANTS(X) \
   X(0) X(1) X(2) X(1536) X(2048) X(32768) X(4096) X(4097) X(4098) X(5120) X(5376) X(5632) X(6144) X(36864)
@@ -826,6 +872,12 @@ bool render_variant_available(int v) {
 template <int N>
 void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
   constexpr int K = N & ~OPT_MONO;
+  if (A.numSamples > 1) {  // progressive batch: one frame per grid row, then the lerp chain
+    constexpr int M = (N & OPT_MONO) != 0 ? K : (kDefaultVariant & ~OPT_MONO);
+    hipLaunchKernelGGL(k_render<M>, dim3(numBlocks, A.numSamples), dim3(256), 0, s, A, 0);
+    hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);
+    return;
+  }
   if constexpr ((N & OPT_MONO) != 0) {
     hipLaunchKernelGGL(k_render<K>, dim3(numBlocks), dim3(256), 0, s, A, 0);
   } else {

@@ -111,8 +111,13 @@ def lib() -> C.CDLL:
             "irt_render": [P, C.POINTER(LaunchParams), I, I, P, P, P],
             "irt_render_tiles": [P, C.POINTER(LaunchParams), I, I, I, I, P, P,
                                  C.POINTER(C.c_int), P],
+            "irt_render_accumulate": [P, C.POINTER(LaunchParams), I, I, I, P, P, P],
+            "irt_render_tiles_accumulate": [P, C.POINTER(LaunchParams), I, I, I, I, I, P, P,
+                                            C.POINTER(C.c_int), P],
             "irt_unpack_tiles": [P, P, I, I, I, I, P, P],
             "irt_get_render_stats": [P, C.POINTER(RenderStats)],
+            "irt_get_render_stats_total": [P, C.POINTER(RenderStats), C.POINTER(C.c_longlong)],
+            "irt_reset_render_stats_total": [P],
             "irt_get_shell": [P, P, P],
             "irt_num_tiles": [I, I],
             "irt_load_ic": [C.c_char_p, C.c_long, P, S, C.POINTER(S)],
@@ -345,6 +350,24 @@ class Context:
                                       C.byref(n), C.c_void_p(stream)), "irt_render_tiles")
         return n.value
 
+    def render_accumulate(self, lp: LaunchParams, width: int, height: int, num_frames: int,
+                          fb_ptr: int, accum_ptr: int, stream: int = 0):
+        """Frames lp.accumID .. lp.accumID+num_frames-1 of the progressive accumulation in
+        one launch (irt_render_accumulate)."""
+        _check(lib().irt_render_accumulate(self._h, C.byref(lp), width, height, num_frames,
+                                           C.c_void_p(fb_ptr), C.c_void_p(accum_ptr),
+                                           C.c_void_p(stream)), "irt_render_accumulate")
+
+    def render_tiles_accumulate(self, lp: LaunchParams, width: int, height: int, tile_begin: int,
+                                tile_stride: int, num_frames: int, fb_ptr: int, accum_ptr: int,
+                                stream: int = 0) -> int:
+        n = C.c_int()
+        _check(lib().irt_render_tiles_accumulate(self._h, C.byref(lp), width, height, tile_begin,
+                                                 tile_stride, num_frames, C.c_void_p(fb_ptr),
+                                                 C.c_void_p(accum_ptr), C.byref(n),
+                                                 C.c_void_p(stream)), "irt_render_tiles_accumulate")
+        return n.value
+
     def unpack_tiles(self, gathered_ptr: int, num_ranks: int, max_tiles: int, width: int,
                      height: int, fb_ptr: int, stream: int = 0):
         _check(lib().irt_unpack_tiles(self._h, C.c_void_p(gathered_ptr), num_ranks, max_tiles,
@@ -355,6 +378,17 @@ class Context:
         st = RenderStats()
         _check(lib().irt_get_render_stats(self._h, C.byref(st)), "irt_get_render_stats")
         return st
+
+    def stats_total(self) -> tuple[RenderStats, int]:
+        """Sums of the statistics of every launch since reset_stats_total()."""
+        st = RenderStats()
+        n = C.c_longlong()
+        _check(lib().irt_get_render_stats_total(self._h, C.byref(st), C.byref(n)),
+               "irt_get_render_stats_total")
+        return st, n.value
+
+    def reset_stats_total(self):
+        _check(lib().irt_reset_render_stats_total(self._h), "irt_reset_render_stats_total")
 
     def shell(self) -> tuple[np.ndarray, np.ndarray]:
         n = int(np.prod(list(self.info.shellDims)))

@@ -66,24 +66,43 @@ def unpack_host(gathered: np.ndarray, split: TileSplit) -> np.ndarray:
 
 
 class FrameGather:
-    """Per-frame RCCL gather of packed RGBA8 tiles to rank 0 (torch.distributed)."""
+    """Per-frame RCCL gather of packed RGBA8 tiles to rank 0 (torch.distributed).
 
-    def __init__(self, split: TileSplit, device):
+    `buffers` > 1 double-buffers the packed tiles so that the gather of frame s can run
+    (async_op, on the collective's own stream) while frame s+1 renders into the other
+    buffer: gather_async() returns a pending handle, finish() waits for it (making the
+    current stream wait, not the host) and on rank 0 returns the rank-major frame."""
+
+    def __init__(self, split: TileSplit, device, buffers: int = 1, stage_cpu: bool = False):
         import torch
         import torch.distributed as dist
         self.dist, self.torch, self.split = dist, torch, split
+        self.stage_cpu = stage_cpu  # gloo rehearsal of the GPU path: collectives on host copies
         n = split.max_tiles * TILE_PIX
-        self.tiles = torch.zeros(n, dtype=torch.int32, device=device)
-        self.parts = ([torch.zeros_like(self.tiles) for _ in range(split.world)]
-                      if split.rank == 0 else None)
+        cdev = "cpu" if stage_cpu else device
+        self.bufs = [torch.zeros(n, dtype=torch.int32, device=device) for _ in range(buffers)]
+        self.parts = ([[torch.zeros(n, dtype=torch.int32, device=cdev) for _ in range(split.world)]
+                       for _ in range(buffers)] if split.rank == 0 else None)
         self.gathered = (torch.zeros(split.world * n, dtype=torch.int32, device=device)
                          if split.rank == 0 else None)
+        self.tiles = self.bufs[0]
+
+    def gather_async(self, b: int = 0):
+        src = self.bufs[b].cpu() if self.stage_cpu else self.bufs[b]
+        return self.dist.gather(src, self.parts[b] if self.parts else None, dst=0,
+                                async_op=True)
+
+    def finish(self, work, b: int = 0):
+        work.wait()
+        if self.split.rank != 0:
+            return None
+        if self.stage_cpu:
+            self.gathered.copy_(self.torch.cat(self.parts[b]))
+        else:
+            self.torch.cat(self.parts[b], out=self.gathered)
+        return self.gathered
 
     def gather(self):
         """Collective: every rank calls it after rendering into self.tiles.  On rank 0
         returns the rank-major gathered tensor, elsewhere None."""
-        self.dist.gather(self.tiles, self.parts, dst=0)
-        if self.split.rank != 0:
-            return None
-        self.torch.cat(self.parts, out=self.gathered)
-        return self.gathered
+        return self.finish(self.gather_async(0), 0)

@@ -135,12 +135,33 @@ int irt_render_tiles(irt_context *ctx, const irt_launch_params *lp, int width, i
                      int tileBegin, int tileStride, uint32_t *d_fb_tiles,
                      irt_vec4f *d_accum_tiles, int *numTiles, void *stream);
 
+/* The reference's progressive accumulation (`--sample-limit N`: Pipeline::isRunning /
+ * launch, pipeline.cu:991-1075, with accumID = frameID, hostCode.cu:947-958) batched:
+ * numFrames consecutive frames accumID = lp->accumID .. lp->accumID+numFrames-1 in one
+ * launch, bit-identical to numFrames irt_render calls with accumID incremented (each
+ * frame's lerp(new, old, 1/(accumID+1)), deviceCode.cu:333-334, applied in order; fb holds
+ * the last frame's make_rgba(linear_to_srgb(accum))).  The _tiles form packs like
+ * irt_render_tiles and is what each rank runs in the multi-GPU weak-scaling split. */
+int irt_render_accumulate(irt_context *ctx, const irt_launch_params *lp, int width, int height,
+                          int numFrames, uint32_t *d_fb, irt_vec4f *d_accum, void *stream);
+int irt_render_tiles_accumulate(irt_context *ctx, const irt_launch_params *lp, int width,
+                                int height, int tileBegin, int tileStride, int numFrames,
+                                uint32_t *d_fb_tiles, irt_vec4f *d_accum_tiles, int *numTiles,
+                                void *stream);
+
 /* Scatter packed tiles (as produced by irt_render_tiles on `numRanks` ranks and gathered
  * rank-major into d_gathered[rank][maxTilesPerRank][4096]) into a linear framebuffer. */
 int irt_unpack_tiles(irt_context *ctx, const uint32_t *d_gathered, int numRanks,
                      int maxTilesPerRank, int width, int height, uint32_t *d_fb, void *stream);
 
+/* Statistics of the most recent launch (waits for it).  Launches never wait for earlier
+ * ones' statistics: counters are read back through a ring, so frames queue back to back
+ * like the reference's GPU path (owlLaunch2D is asynchronous, pipeline.cu:1064). */
 int irt_get_render_stats(const irt_context *ctx, irt_render_stats *stats);
+/* Sums over every launch since the last reset (kernelMs summed too); *launches = count. */
+int irt_get_render_stats_total(const irt_context *ctx, irt_render_stats *total,
+                               long long *launches);
+int irt_reset_render_stats_total(irt_context *ctx);
 
 /* Download the shell accelerator (for checking): valueRanges as 2 floats per
  * macrocell, maxOpacities as 1 float per macrocell; either may be NULL. */

@@ -1,7 +1,7 @@
 """The N>1 frame split on CPU: world_size-2 gloo processes render their interleaved tiles
-with the oracle, gather the packed RGBA8 tiles to rank 0 through torch.distributed
-(the code path bench.py runs over RCCL), and rank 0's assembled frame must equal the
-single-process frame bit for bit."""
+with the oracle, gather the packed RGBA8 tiles to rank 0 through torch.distributed with
+two frames in flight (irt_dist.FrameGather, the code path bench.py runs over RCCL), and
+rank 0's assembled frames must equal the single-process frames bit for bit."""
 import os
 import socket
 import sys
@@ -37,21 +37,28 @@ def _worker(rank, world, port, W, H, out_path):
     S = O.OracleScene(cells)
     lut, vr = S.default_lut()
     S.set_transfunc(lut, vr)
-    p = S.params(S.camera(W, H, FRAMING))
+    cam = S.camera(W, H, FRAMING)
     split = irt_dist.TileSplit(W, H, rank, world)
-    fg = irt_dist.FrameGather(split, "cpu")
-    # render this rank's tiles (oracle stands in for irt_render_tiles) into the packed buffer
-    packed = np.zeros((split.max_tiles, irt_dist.TILE_PIX), np.uint32)
-    for k, t in enumerate(split.tiles()):
-        xy = split.tile_pixels(t)
-        ok = xy[:, 0] >= 0
-        _, fb, _ = S.render_pixels(p, W, H, xy[ok].astype(np.int32), threads=2)
-        packed[k, ok] = fb[xy[ok, 1], xy[ok, 0]]
-    fg.tiles.copy_(torch.from_numpy(packed.view(np.int32).ravel()))
-    g = fg.gather()
-    if rank == 0:
-        frame = irt_dist.unpack_host(g.numpy().view(np.uint32), split)
-        np.save(out_path, frame)
+    # two frames in flight, as bench.py runs them: render frame s into buffer s % 2, start
+    # its gather asynchronously, finish it only when the buffer is needed again
+    fg = irt_dist.FrameGather(split, "cpu", buffers=2)
+    works = []
+    for s in (0, 1):
+        p = S.params(cam, accum_id=s)
+        # this rank's tiles (the oracle stands in for irt_render_tiles) into the packed buffer
+        packed = np.zeros((split.max_tiles, irt_dist.TILE_PIX), np.uint32)
+        for k, t in enumerate(split.tiles()):
+            xy = split.tile_pixels(t)
+            ok = xy[:, 0] >= 0
+            _, fb, _ = S.render_pixels(p, W, H, xy[ok].astype(np.int32), threads=2)
+            packed[k, ok] = fb[xy[ok, 1], xy[ok, 0]]
+        fg.bufs[s].copy_(torch.from_numpy(packed.view(np.int32).ravel()))
+        works.append(fg.gather_async(s))
+    for s in (0, 1):
+        g = fg.finish(works[s], s)
+        if rank == 0:
+            frame = irt_dist.unpack_host(g.numpy().view(np.uint32), split)
+            np.save(out_path.replace(".npy", f"{s}.npy"), frame)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -67,10 +74,12 @@ def test_two_rank_gloo_frame_split(tmp_path, world):
     out = str(tmp_path / "frame.npy")
     mp.start_processes(_worker, args=(world, _free_port(), W, H, out), nprocs=world,
                        join=True, start_method="spawn")
-    frame = np.load(out)
-    _, fb_ref, _, _ = oracle_frame(irt.synth_grid(2, 1, 31), W, H, camera=FRAMING)
-    assert np.array_equal(frame, fb_ref)
-    assert (fb_ref != 0).mean() > 0.3
+    cells = irt.synth_grid(2, 1, 31)
+    for s in (0, 1):
+        frame = np.load(out.replace(".npy", f"{s}.npy"))
+        _, fb_ref, _, _ = oracle_frame(cells, W, H, camera=FRAMING, accum_ids=(s,))
+        assert np.array_equal(frame, fb_ref), s
+        assert (fb_ref != 0).mean() > 0.3
 
 
 def test_tile_split_covers_every_pixel_once():

@@ -249,3 +249,70 @@ def test_all_render_variants_identical():
         assert np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1]), v
         assert out[2:] == ref[2:], v
     ctx.close()
+
+
+def _batch_frame(cells, W, camera, first, k, prior=()):
+    """GPU frames: `prior` single-frame launches, then one progressive batch of k frames
+    starting at accumID `first` (irt_render_accumulate)."""
+    import torch
+    setup = irt.setup_frame(cells, W, W, camera=camera)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    fb = torch.zeros(W * W, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(W * W * 4, dtype=torch.float32, device="cuda")
+    lp = setup.lp
+    for aid in prior:
+        lp.accumID = aid
+        ctx.render(lp, W, W, fb.data_ptr(), acc.data_ptr())
+    lp.accumID = first
+    ctx.render_accumulate(lp, W, W, k, fb.data_ptr(), acc.data_ptr())
+    torch.cuda.synchronize()
+    st = ctx.stats()
+    a = acc.cpu().numpy().reshape(W, W, 4)
+    f = fb.cpu().numpy().view(np.uint32).reshape(W, W)
+    ctx.close()
+    return a, f, st
+
+
+@pytest.mark.parametrize("cam", [FRAMING, None])
+def test_progressive_batch_equals_sequential_frames(cam):
+    """irt_render_accumulate (k frames in one launch) == k reference frames in sequence,
+    including pixels whose jittered ray hits the box in some frames only (viewAll)."""
+    cells = irt.synth_grid(2, 1, 31)
+    W = 72
+    a_ref, f_ref, st_ref, _ = oracle_frame(cells, W, W, camera=cam, accum_ids=(0, 1, 2, 3, 4))
+    a_gpu, f_gpu, st = _batch_frame(cells, W, cam, 0, 5)
+    assert_same_frame(a_gpu, f_gpu, a_ref, f_ref, "batch of 5")
+    assert st.locateCalls == sum(s.locate_calls for s in st_ref)
+    assert st.raysLaunched == 5 * W * W
+    # a batch continuing an accumulation (frames 0,1 single, then 2..6 batched)
+    a_ref, f_ref, _, _ = oracle_frame(cells, W, W, camera=cam, accum_ids=tuple(range(7)))
+    a_gpu, f_gpu, _ = _batch_frame(cells, W, cam, 2, 5, prior=(0, 1))
+    assert_same_frame(a_gpu, f_gpu, a_ref, f_ref, "frames 0,1 + batch 2..6")
+
+
+def test_tiles_accumulate_match_full_batch():
+    """The weak-scaling split: every rank renders its interleaved tiles for k frames;
+    unpacked, the ranks' tiles equal the full-frame batch."""
+    import torch
+    cells = irt.synth_grid(2, 2, 47)
+    W, H, k, ranks = 200, 136, 3, 3
+    setup = irt.setup_frame(cells, W, H, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    lp = setup.lp
+    fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    ctx.render_accumulate(lp, W, H, k, fb.data_ptr(), acc.data_ptr())
+    ntiles = irt.num_tiles(W, H)
+    maxt = (ntiles + ranks - 1) // ranks
+    g = torch.zeros(ranks * maxt * 4096, dtype=torch.int32, device="cuda")
+    for r in range(ranks):
+        tacc = torch.zeros(maxt * 4096 * 4, dtype=torch.float32, device="cuda")
+        ctx.render_tiles_accumulate(lp, W, H, r, ranks, k, g[r * maxt * 4096:].data_ptr(),
+                                    tacc.data_ptr())
+    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    ctx.unpack_tiles(g.data_ptr(), ranks, maxt, W, H, out.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), fb.cpu().numpy())
+    ctx.close()
