@@ -25,6 +25,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4]
        torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -88,6 +89,26 @@ def cpu_baseline(cells, setup, W, H, budget_s=15.0):
     kind = "port"
     return {"value": mray, "unit": "Mray/s", "cores": threads, "kind": kind, "sample": sample,
             "ms_per_frame_extrapolated": W * H / (mray * 1e6) * 1e3}
+
+
+def profiled_traffic(kernel, records, width):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 summary of the
+    same workload (profiles/*/summary.json: FETCH_SIZE x 2 + WRITE_SIZE, per the gfx950
+    correction of MI355X_MICROARCH.md), or None."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json"))):
+        try:
+            s = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        b = s.get("bench") or {}
+        if not any(k.endswith(kernel) for k in s.get("kernels", {})):
+            continue
+        if s.get("records") not in (None, records) or s.get("width") not in (None, width):
+            continue
+        if "traffic_bytes_per_launch_fetch_x2" in s and b:
+            best = (s["traffic_bytes_per_launch_fetch_x2"], os.path.relpath(p, ROOT))
+    return best
 
 
 def main():
@@ -254,6 +275,12 @@ def main():
                 "traffic": None,
             },
         }
+        prof = profiled_traffic(f"k_render<{irt.default_kernel_id()}>", int(cells.size), W)
+        if prof and world == 1:
+            out["roofline"]["traffic"] = prof[0]
+            out["roofline"]["traffic_source"] = (
+                f"{prof[1]}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE per launch "
+                f"of the same kernel and workload")
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cells, setup, W, H, args.cpu_budget)
         print(json.dumps(out), flush=True)

@@ -607,6 +607,8 @@ extern "C" int irt_debug_counters(irt_context *c, unsigned long long *out16) {
   return IRT_OK;
 }
 
+extern "C" int irt_debug_default_variant(void) { return kDefaultVariant; }
+
 extern "C" int irt_debug_set_variant(irt_context *c, int variant) {
   if (!c || !render_variant_available(variant)) {
     set_error("irt_debug_set_variant: variant %d not compiled", variant);

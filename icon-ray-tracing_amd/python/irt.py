@@ -182,6 +182,12 @@ def box1(lo, hi) -> Box1:
 
 
 # ----------------------------------------------------------------------- host helpers
+def default_kernel_id() -> int:
+    """Template id of the raygen kernel the default variant launches (k_render<id>), as
+    rocprofv3 names it."""
+    return int(lib().irt_debug_default_variant()) & ~4096  # OPT_MONO: one kernel per frame
+
+
 def synth_grid(root_n: int, bisections: int, levels: int, top_height: float = 75e3,
                noise: float = 0.0, seed: int = 1234) -> np.ndarray:
     """Synthetic RnBk ICON grid as `.ic` records (host/irt_synth.cpp)."""

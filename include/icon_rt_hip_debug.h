@@ -55,6 +55,8 @@ void irt_debug_scene_free(irt_debug_scene *s);
 /* Select the render-kernel variant (bit set of irt_render.hip's OPT_* flags; every
  * variant gives identical results -- used for in-process A/B timing). */
 int irt_debug_set_variant(irt_context *ctx, int variant);
+/* The variant a new context launches (IRT_RENDER_VARIANT overrides it per context). */
+int irt_debug_default_variant(void);
 /* The raw per-frame counters of the last render (waits for it): [0] launched [1] in box
  * [2] sampleVolume calls [3] found [4] candidates; with the statistics variant bit also
  * [5] Woodcock draws [6] sum over waves of the per-wave max draws [7] zero-length leaves
