@@ -397,6 +397,25 @@ IRT_HD float select8(int m, float a0, float a1, float a2, float a3, float b0, fl
   return (m & 4) ? y1 : y0;
 }
 
+// ---------------------------------------------------------------------------------
+// GRID_ACCEL_MODE (Params.h:34): the 256^3 Cartesian macrocell grid over the volume
+// bounds (hostCode.cu:668-682) and its traversal dda3 (DDA.h:35-136).
+constexpr int kGridDim = 256;  // Grid{nullptr, vec3i(256), volbounds} (hostCode.cu:670)
+
+// projectOnGrid (DDA.h:23-31), one axis: clamp(int((V-lo)/(hi-lo)*dims), 0, dims-1)
+IRT_HD int project_on_grid(float v, float lo, float hi, int dim) {
+  const int c = f2i_x86(((v - lo) / (hi - lo)) * (float)dim);
+  return c < 0 ? 0 : (c > dim - 1 ? dim - 1 : c);  // vecmath clamp(int) = max(a, min(x, b))
+}
+
+// `min(reduce_min(tnext), ray.tmax)` (DDA.h:96): vecmath.h has no float min, so the
+// reference's g++ (CPU) build resolves it to `int min(int, int)` (vecmath.h:46-49) --
+// both operands truncated (cvttss2si), the int converted back to float.
+IRT_HD float dda3_min_quirk(float a, float b) {
+  const int x = f2i_x86(a), y = f2i_x86(b);
+  return (float)(x < y ? x : y);
+}
+
 // ICONCell::findHeight (ICONGrid.h:117-145): lower_bound over height[1..numLayers].
 IRT_HD int find_height(const float *height, int numLayers, float hpos) {
   int first = 0, count = numLayers;

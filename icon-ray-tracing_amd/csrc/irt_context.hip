@@ -48,6 +48,8 @@ struct irt_context {
   float *d_srgb = nullptr;
   float *d_valueRanges = nullptr;
   float *d_maxOp = nullptr;
+  float *d_gridVR = nullptr;     // GRID_ACCEL_MODE: Grid::valueRanges, kGridDim^3 box1f
+  float *d_gridMaxOp = nullptr;  // Grid::maxOpacities
   size_t numMCs = 0;
   float4 *d_lut = nullptr;
   int lutCap = 0;
@@ -96,7 +98,7 @@ void free_all(irt_context *c) {
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
-                  c->d_sphBits, c->d_queue, c->d_contList, c->d_segCount, c->d_samples, c->d_maxOp, c->d_srgb, c->d_valueRanges,
+                  c->d_sphBits, c->d_queue, c->d_contList, c->d_segCount, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_srgb, c->d_valueRanges,
                   c->d_lut, c->d_counters};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -161,6 +163,10 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     set_error("irt_render: unknown raygen %d", lp->raygen);
     return IRT_E_INVALID;
   }
+  if (lp->accelMode != IRT_ACCEL_SPHERE && lp->accelMode != IRT_ACCEL_GRID) {
+    set_error("irt_render: unknown accelMode %d", lp->accelMode);
+    return IRT_E_INVALID;
+  }
   IRT_HIP(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const int tilesX = (W + 63) / 64, tilesY = (H + 63) / 64;
@@ -186,6 +192,8 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.sbLo = make_float3(I.sphericalBounds.lower.x, I.sphericalBounds.lower.y, I.sphericalBounds.lower.z);
   A.sbHi = make_float3(I.sphericalBounds.upper.x, I.sphericalBounds.upper.y, I.sphericalBounds.upper.z);
   A.maxOp = c->d_maxOp;
+  A.accelMode = lp->accelMode;
+  A.gridMaxOp = c->d_gridMaxOp;
   A.tfLo = c->tfLo;
   A.tfHi = c->tfHi;
   A.opacityScale = c->opScale;
@@ -351,6 +359,11 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
   // (hostCode.cu:652-666), majorants zero until a transfer function arrives
   if ((rc = dalloc(c, &c->d_valueRanges, 2 * c->numMCs))) return fail(rc);
   launch_shell_init(c->d_valueRanges, c->numMCs, c->stream);
+  const size_t gridMCs = (size_t)kGridDim * kGridDim * kGridDim;
+  if ((rc = dalloc(c, &c->d_gridVR, 2 * gridMCs))) return fail(rc);
+  if ((rc = dalloc(c, &c->d_gridMaxOp, gridMCs))) return fail(rc);
+  launch_shell_init(c->d_gridVR, gridMCs, c->stream);  // initGrid(Grid) (hostCode.cu:205-214)
+  if (hipMemsetAsync(c->d_gridMaxOp, 0, gridMCs * sizeof(float), c->stream) != hipSuccess) return fail(IRT_E_HIP);
   if (numCells) {
     irt_icon_cell *d_cells = nullptr;
     if (hipMalloc((void **)&d_cells, numCells * sizeof(irt_icon_cell)) != hipSuccess ||
@@ -364,7 +377,19 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
     launch_shell_build(d_cells, numCells, make_int3(dims[0], dims[1], dims[2]),
                        make_float3(sb.lower.x, sb.lower.y, sb.lower.z),
                        make_float3(sb.upper.x, sb.upper.y, sb.upper.z), c->d_valueRanges, c->stream);
-    hipError_t e = hipStreamSynchronize(c->stream);
+    // buildICONGrid (hostCode.cu:668-682): initGrid + buildGrid_ICON over volbounds
+    float4 *d_trig = nullptr;
+    hipError_t e = hipMalloc((void **)&d_trig, numCells * 3 * sizeof(float4));
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(d_trig, S.trig.data(), numCells * 3 * sizeof(float4), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+      const irt_box3f &vb = S.info.bounds;
+      launch_grid_build(d_cells, d_trig, numCells, make_float3(vb.lower.x, vb.lower.y, vb.lower.z),
+                        make_float3(vb.upper.x, vb.upper.y, vb.upper.z), c->d_gridVR, c->stream);
+      e = hipStreamSynchronize(c->stream);
+    }
+    if (d_trig) (void)hipFree(d_trig);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(d_cells);
     if (e != hipSuccess || hipGetLastError() != hipSuccess) {
       set_error("irt_create: shell build failed: %s", hipGetErrorString(e));
@@ -422,6 +447,8 @@ int irt_set_transfunc(irt_context *c, const irt_vec4f *lut, int size, irt_box1f 
   // ignore opacityScale exactly like the reference kernel (hostCode.cu:362-397)
   launch_max_opacities(c->d_valueRanges, c->numMCs, c->d_lut, size, valueRange.lower,
                        valueRange.upper, c->d_maxOp, c->stream);
+  launch_max_opacities(c->d_gridVR, (size_t)kGridDim * kGridDim * kGridDim, c->d_lut, size,
+                       valueRange.lower, valueRange.upper, c->d_gridMaxOp, c->stream);
   IRT_HIP(hipGetLastError());
   IRT_HIP(hipStreamSynchronize(c->stream));
   c->tfSet = true;
@@ -508,6 +535,21 @@ int irt_reset_render_stats_total(irt_context *c) {
   if (rc) return rc;
   c->total = irt_render_stats{};
   c->totalLaunches = 0;
+  return IRT_OK;
+}
+
+int irt_get_grid(const irt_context *c, float *valueRanges, float *maxOpacities) {
+  if (!c) {
+    set_error("irt_get_grid: null context");
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(c->device));
+  IRT_HIP(hipStreamSynchronize(c->stream));
+  const size_t n = (size_t)kGridDim * kGridDim * kGridDim;
+  if (valueRanges)
+    IRT_HIP(hipMemcpy(valueRanges, c->d_gridVR, 2 * n * sizeof(float), hipMemcpyDeviceToHost));
+  if (maxOpacities)
+    IRT_HIP(hipMemcpy(maxOpacities, c->d_gridMaxOp, n * sizeof(float), hipMemcpyDeviceToHost));
   return IRT_OK;
 }
 

@@ -26,6 +26,8 @@ struct HostScene {
   irt_volume_info info{};
   std::vector<float> hv;          // n * kHV floats (see irt_common.h)
   std::vector<Plane4> planes;     // n * 3 side planes of sample() (ICONGrid.h:197-199)
+  std::vector<float> trig;        // n * 12: per corner {cosf lat, sinf lat, cosf lon, sinf lon}
+                                  // (glibc, for toCartesian in the grid build)
   int G = 0;                      // cube-map cells per face edge
   std::vector<uint32_t> offsets;  // 6*G*G + 1 CSR offsets
   std::vector<LocEntry> entries;  // candidate lists, each sorted by record index

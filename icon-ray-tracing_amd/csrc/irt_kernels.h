@@ -23,6 +23,8 @@ struct RenderArgs {
   int3 dims;             // ShellAccel::dims
   float3 sbLo, sbHi;     // ShellAccel::sphericalBounds
   const float *maxOp;    // ShellAccel::maxOpacities
+  int accelMode;         // Volume::accelMode (Params.h:33-34): 0 sphere (sdda), 1 grid (dda3)
+  const float *gridMaxOp;  // Grid::maxOpacities, kGridDim^3 over bmin..bmax (Params.h:44-49)
   // transfer function (Params.h:77-82)
   float tfLo, tfHi, opacityScale;
   const float4 *lut;
@@ -71,6 +73,8 @@ void launch_render(const RenderArgs &A, int numBlocks, hipStream_t s, int varian
 void launch_shell_init(float *valueRanges, size_t numMCs, hipStream_t s);
 void launch_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, float3 lo, float3 hi,
                         float *valueRanges, hipStream_t s);
+void launch_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n, float3 lo,
+                       float3 hi, float *valueRanges, hipStream_t s);
 void launch_max_opacities(const float *valueRanges, size_t numMCs, const float4 *lut, int size,
                           float lo, float hi, float *maxOp, hipStream_t s);
 void launch_clear(uint32_t *fb, float4 *accum, size_t n, hipStream_t s);

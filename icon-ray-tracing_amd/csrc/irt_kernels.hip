@@ -83,6 +83,80 @@ __global__ void k_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, f
   }
 }
 
+// buildGrid_ICON + rasterizeBox (hostCode.cu:227-297): per cell and layer the Cartesian
+// box of the layer's wedge (top corners pushed out by (R-|bary|)/R, ICONGrid-style),
+// rasterised into the 256^3 grid with the layer's value range.  toCartesian's glibc
+// cosf/sinf come precomputed from the host (trig = {cos lat, sin lat, cos lon, sin lon}
+// per corner, host/irt_scene.cpp), the rest is the same float expressions.  Consecutive
+// layers covering the same macrocell box are merged before the CAS-loop min/max (the
+// same min/max).  One lane per cell.
+__device__ __forceinline__ float3 to_cartesian_trig(float r, const float4 &t) {
+  return make_float3((r * t.x) * t.z, (r * t.x) * t.w, r * t.y);  // ICONGrid.h:44-54
+}
+
+__global__ void k_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n, int dim,
+                             float3 lo, float3 hi, float *valueRanges) {
+  const size_t ci = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (ci >= n) return;
+  const irt_icon_cell &c = cells[ci];
+  const float4 t0 = trig[3 * ci], t1 = trig[3 * ci + 1], t2 = trig[3 * ci + 2];
+  int3 pLo = make_int3(0, 0, 0), pHi = make_int3(-1, -1, -1);
+  float rLo = 0.f, rHi = 0.f;
+  bool have = false;
+  auto flush = [&]() {
+    for (int mz = pLo.z; mz <= pHi.z; ++mz)
+      for (int my = pLo.y; my <= pHi.y; ++my)
+        for (int mx = pLo.x; mx <= pHi.x; ++mx) {
+          float *vr = valueRanges + 2 * ((size_t)mz * dim * dim + (size_t)my * dim + mx);
+          atomic_min_f(vr, rLo);
+          atomic_max_f(vr + 1, rHi);
+        }
+  };
+  for (int i = 0; i < c.numLayers; ++i) {
+    const float hb = c.height[i], ht = c.height[i + 1];
+    const float3 b1 = to_cartesian_trig(hb, t0), b2 = to_cartesian_trig(hb, t1), b3 = to_cartesian_trig(hb, t2);
+    float3 v1 = to_cartesian_trig(ht, t0), v2 = to_cartesian_trig(ht, t1), v3 = to_cartesian_trig(ht, t2);
+    float3 bl = make_float3(__builtin_inff(), __builtin_inff(), __builtin_inff());
+    float3 bu = make_float3(-__builtin_inff(), -__builtin_inff(), -__builtin_inff());
+    auto ext = [&](const float3 &v) {  // box3f::extend (vecmath.h:1096-1100): fminf/fmaxf
+      bl = make_float3(fminf(bl.x, v.x), fminf(bl.y, v.y), fminf(bl.z, v.z));
+      bu = make_float3(fmaxf(bu.x, v.x), fmaxf(bu.y, v.y), fmaxf(bu.z, v.z));
+    };
+    ext(b1); ext(b2); ext(b3);
+    const float3 bary = make_float3(((v1.x + v2.x) + v3.x) / 3.f, ((v1.y + v2.y) + v3.y) / 3.f,
+                                    ((v1.z + v2.z) + v3.z) / 3.f);
+    const float R = ht;
+    const float D = R - sqrtf(bary.x * bary.x + bary.y * bary.y + bary.z * bary.z);
+    const float off = D / R;
+    v1 = make_float3(v1.x + v1.x * off, v1.y + v1.y * off, v1.z + v1.z * off);
+    v2 = make_float3(v2.x + v2.x * off, v2.y + v2.y * off, v2.z + v2.z * off);
+    v3 = make_float3(v3.x + v3.x * off, v3.y + v3.y * off, v3.z + v3.z * off);
+    ext(v1); ext(v2); ext(v3);
+    // box1f valueRange(INFINITY,-INFINITY).extend(getValue(h[i])).extend(getValue(h[i+1]))
+    const float g0 = c.value[find_height(c.height, c.numLayers, hb)];
+    const float g1 = c.value[find_height(c.height, c.numLayers, ht)];
+    const float vlo = fminf(fminf(__builtin_inff(), g0), g1);
+    const float vhi = fmaxf(fmaxf(-__builtin_inff(), g0), g1);
+    const int3 a = make_int3(project_on_grid(bl.x, lo.x, hi.x, dim), project_on_grid(bl.y, lo.y, hi.y, dim),
+                             project_on_grid(bl.z, lo.z, hi.z, dim));
+    const int3 b = make_int3(project_on_grid(bu.x, lo.x, hi.x, dim), project_on_grid(bu.y, lo.y, hi.y, dim),
+                             project_on_grid(bu.z, lo.z, hi.z, dim));
+    if (have && a.x == pLo.x && a.y == pLo.y && a.z == pLo.z && b.x == pHi.x && b.y == pHi.y &&
+        b.z == pHi.z) {
+      rLo = (vlo < rLo) ? vlo : rLo;  // the atomics' "store only if strictly smaller/larger"
+      rHi = (vhi > rHi) ? vhi : rHi;
+      continue;
+    }
+    if (have) flush();
+    pLo = a;
+    pHi = b;
+    rLo = vlo;
+    rHi = vhi;
+    have = true;
+  }
+  if (have) flush();
+}
+
 // computeMaxOpacities(ShellAccel) (hostCode.cu:362-397)
 __global__ void k_max_opacities(const float2 *valueRanges, size_t numMCs, const float4 *lut,
                                 int size, float tfLo, float tfHi, float *maxOp) {
@@ -137,6 +211,12 @@ void launch_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, float3 
                         float *vr, hipStream_t s) {
   if (n == 0) return;
   hipLaunchKernelGGL(k_shell_build, dim3((unsigned)n), dim3(64), 0, s, cells, n, dims, lo, hi, vr);
+}
+void launch_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n, float3 lo,
+                       float3 hi, float *vr, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_grid_build, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, cells, trig,
+                     n, kGridDim, lo, hi, vr);
 }
 void launch_max_opacities(const float *vr, size_t numMCs, const float4 *lut, int size, float lo,
                           float hi, float *maxOp, hipStream_t s) {

@@ -623,6 +623,71 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   }
 }
 
+// The woodcockTrackingWithAccel raygen in GRID_ACCEL_MODE (deviceCode.cu:326-328): dda3
+// (DDA.h:35-136) over the 256^3 Cartesian grid, each cell handed to the woodcockFunc
+// lambda (304-323) with the grid's majorant.  Written exactly as the reference's g++ CPU
+// build evaluates it, including `min(reduce_min(tnext), ray.tmax)` going through
+// `int min(int, int)` (dda3_min_quirk, irt_common.h).
+template <int OPT>
+__device__ __forceinline__ void render_grid(const RenderArgs &A, Tracer<OPT> &T, const Ray &ray,
+                                            float rtmin, float rtmax, uint32_t &st, float &cr,
+                                            float &cg, float &cb, float &alpha) {
+  const int D = kGridDim;
+  // move ray so tmin becomes 0 (DDA.h:42-46)
+  const float ox = ray.ox + rtmin * ray.dx, oy = ray.oy + rtmin * ray.dy, oz = ray.oz + rtmin * ray.dz;
+  const float tmax = rtmax - rtmin;
+  const float rx = 1.f / ray.dx, ry = 1.f / ray.dy, rz = 1.f / ray.dz;
+  const float lx = (A.bmin.x - ox) * rx, ly = (A.bmin.y - oy) * ry, lz = (A.bmin.z - oz) * rz;
+  const float hx = (A.bmax.x - ox) * rx, hy = (A.bmax.y - oy) * ry, hz = (A.bmax.z - oz) * rz;
+  float nx = fminf(lx, hx), ny = fminf(ly, hy), nz = fminf(lz, hz);
+  const float fx = fmaxf(lx, hx), fy = fmaxf(ly, hy), fz = fmaxf(lz, hz);
+  if (ray.dx == 0.f) nx = IRT_FLT_MAX;
+  if (ray.dy == 0.f) ny = IRT_FLT_MAX;
+  if (ray.dz == 0.f) nz = IRT_FLT_MAX;
+  int cx = project_on_grid(ox, A.bmin.x, A.bmax.x, D);
+  int cy = project_on_grid(oy, A.bmin.y, A.bmax.y, D);
+  int cz = project_on_grid(oz, A.bmin.z, A.bmax.z, D);
+  const float dx = fmaxf(0.f, (fx - nx) / (float)D), dy = fmaxf(0.f, (fy - ny) / (float)D),
+              dz = fmaxf(0.f, (fz - nz) / (float)D);
+  const int sx = ray.dx > 0.f ? 1 : -1, sy = ray.dy > 0.f ? 1 : -1, sz = ray.dz > 0.f ? 1 : -1;
+  const int ex = ray.dx > 0.f ? D : -1, ey = ray.dy > 0.f ? D : -1, ez = ray.dz > 0.f ? D : -1;
+  float tnx = ray.dx > 0.f ? nx + (float)(cx + 1) * dx : nx + (float)(D - cx) * dx;
+  float tny = ray.dy > 0.f ? ny + (float)(cy + 1) * dy : ny + (float)(D - cy) * dy;
+  float tnz = ray.dz > 0.f ? nz + (float)(cz + 1) * dz : nz + (float)(D - cz) * dz;
+  float tc0 = 0.f;
+  for (int iter = 0; iter < 4 * D + 16; ++iter) {  // a cell per step, <= 3*D steps
+    const float tmn = fminf(fminf(tnx, tny), tnz);  // reduce_min (vecmath.h:512-514)
+    const float tc1 = dda3_min_quirk(tmn, tmax);
+    const float w0 = rtmin + tc0, w1 = rtmin + tc1;  // func(leaf, ray_tmin+t0, ray_tmin+t1)
+    const float maj = A.gridMaxOp[(size_t)cz * D * D + (size_t)cy * D + cx];
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float tw = T.woodcock(ray.dx, ray.dy, ray.dz, w0, w1, st, maj, s, !(w0 == w1));
+    if (tw > w0 && tw < w1) {
+      cr = s.x * A.amb.x * A.ambRad;
+      cg = s.y * A.amb.y * A.ambRad;
+      cb = s.z * A.amb.z * A.ambRad;
+      alpha = s.w > 0.f ? 1.f : 0.f;
+      return;
+    }
+    if (tnx == tmn) {
+      tnx += dx;
+      cx += sx;
+      if (cx == ex) return;
+    }
+    if (tny == tmn) {
+      tny += dy;
+      cy += sy;
+      if (cy == ey) return;
+    }
+    if (tnz == tmn) {
+      tnz += dz;
+      cz += sz;
+      if (cz == ez) return;
+    }
+    tc0 = tc1;
+  }
+}
+
 // ------------------------------------------------------------------ the full raygen
 // One pixel of woodcockTrackingWithAccel / woodcockTrackingAE, every range and leaf.  Used
 // alone (variant bit OPT_MONO) or as the continuation pass for the rays the march kernel
@@ -666,6 +731,10 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
         rlo0 = st3; rhi0 = st4;
       }
     }
+  }
+  if (!ae && A.accelMode == IRT_ACCEL_GRID) {
+    render_grid(A, T, ray, t0, t1, st, cr, cg, cb, alpha);
+    numRanges = 0;
   }
   const float sceneEPS = A.sbLo.x * 1e-6f;
   for (int i = 0; i < numRanges; ++i) {
@@ -872,10 +941,12 @@ bool render_variant_available(int v) {
 template <int N>
 void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
   constexpr int K = N & ~OPT_MONO;
-  if (A.numSamples > 1) {  // progressive batch: one frame per grid row, then the lerp chain
+  if (A.numSamples > 1 || A.accelMode != IRT_ACCEL_SPHERE) {
+    // progressive batch (one frame per grid row, then the lerp chain) or the grid accel:
+    // the one-kernel raygen
     constexpr int M = (N & OPT_MONO) != 0 ? K : (kDefaultVariant & ~OPT_MONO);
     hipLaunchKernelGGL(k_render<M>, dim3(numBlocks, A.numSamples), dim3(256), 0, s, A, 0);
-    hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);
+    if (A.numSamples > 1) hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);
     return;
   }
   if constexpr ((N & OPT_MONO) != 0) {

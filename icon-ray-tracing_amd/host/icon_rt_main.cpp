@@ -8,6 +8,8 @@
 //           [--bench K]                         (render K extra frames, print timing)
 //           [--true-size]                       (dir_du/dir_dv over the real W/H instead
 //                                                of the reference's hard-coded 512)
+//           [--accel sphere|grid]               (the "Accel mode" UI option,
+//                                                hostCode.cu:853-857, 170-199)
 
 #include <math.h>
 #include <stdio.h>
@@ -33,6 +35,7 @@ struct AppState {  // hostCode.cu:65-92 (the parts this backend uses)
   int synth[3] = {0, 0, 0};
   int benchFrames = 0;
   bool trueSize = false;
+  int accelMode = IRT_ACCEL_SPHERE;  // g_appState.accelMode (hostCode.cu:75)
 } g;
 
 bool endsWith(const std::string &s, const std::string &suffix) {
@@ -63,6 +66,8 @@ void parseCommandLine(int argc, char *argv[]) {  // hostCode.cu:106-129
       g.benchFrames = atoi(argv[++i]);
     else if (arg == "--true-size")
       g.trueSize = true;
+    else if (arg == "--accel" && i + 1 < argc)
+      g.accelMode = std::string(argv[++i]) == "grid" ? IRT_ACCEL_GRID : IRT_ACCEL_SPHERE;
   }
 }
 
@@ -148,6 +153,7 @@ int main(int argc, char *argv[]) {
   lp.ambientRadiance = 1.f;
   lp.unitDistance = info.unitDistance;
   lp.raygen = IRT_RAYGEN_WITH_ACCEL;  // setRayGen(woodcockTrackingWithAccel) (863)
+  lp.accelMode = g.accelMode;         // toggleAccelMode (hostCode.cu:170-199)
 
   pl.clearFramebuffer = [&] {
     if (irt_clear_frame(ctx, fb.fbPointer, fb.accumBuffer, (size_t)fb.width * fb.height, nullptr))

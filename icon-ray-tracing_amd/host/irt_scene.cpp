@@ -226,6 +226,7 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads)
   // --- per-record planes and height/value blocks
   S.hv.assign(n * kHV, 0.f);
   S.planes.resize(n * 3);
+  S.trig.resize(n * 12);
   {
     std::vector<std::thread> ts;
     const size_t chunk = (n + threads - 1) / std::max(threads, 1);
@@ -244,6 +245,13 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads)
           S.planes[3 * i + 0] = makePlane(bv[0], bv[1], tv[1]);
           S.planes[3 * i + 1] = makePlane(bv[1], bv[2], tv[2]);
           S.planes[3 * i + 2] = makePlane(bv[2], bv[0], tv[0]);
+          for (int k = 0; k < 3; ++k) {
+            float *t = &S.trig[12 * i + 4 * k];
+            t[0] = cosf(c.lat[k]);
+            t[1] = sinf(c.lat[k]);
+            t[2] = cosf(c.lon[k]);
+            t[3] = sinf(c.lon[k]);
+          }
           float *hv = &S.hv[i * kHV];
           memcpy(hv, c.height, 32 * sizeof(float));
           memcpy(hv + 32, c.value, 31 * sizeof(float));

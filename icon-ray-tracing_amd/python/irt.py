@@ -26,6 +26,8 @@ assert CELL_DTYPE.itemsize == 284
 
 RAYGEN_WITH_ACCEL = 0  # woodcockTrackingWithAccel (deviceCode.cu:281-341)
 RAYGEN_AE = 1          # woodcockTrackingAE (deviceCode.cu:239-275)
+ACCEL_SPHERE = 0       # SPHERE_ACCEL_MODE (Params.h:33): sdda over the shell grid
+ACCEL_GRID = 1         # GRID_ACCEL_MODE (Params.h:34): dda3 over the 256^3 grid
 # compiled variants of the raygen (irt_render.hip OPT_* bits; 4096 = one monolithic
 # kernel instead of the setup -> march -> continuation pipeline); all bit-identical
 BIN_VARIANTS = (0, 1, 2, 1536, 2048, 32768, 4096, 4097, 4098, 5120, 5376, 5632, 6144, 36864)
@@ -58,7 +60,7 @@ class LaunchParams(C.Structure):
     """Per-frame part of icon_rt::LaunchParams (icon_rt/Params.h:92-119)."""
     _fields_ = [("org", Vec3), ("dir_00", Vec3), ("dir_du", Vec3), ("dir_dv", Vec3),
                 ("accumID", C.c_int32), ("ambientColor", Vec3), ("ambientRadiance", C.c_float),
-                ("unitDistance", C.c_float), ("raygen", C.c_int32)]
+                ("unitDistance", C.c_float), ("raygen", C.c_int32), ("accelMode", C.c_int32)]
 
     def camera12(self) -> np.ndarray:
         return np.array(self.org.tolist() + self.dir_00.tolist() + self.dir_du.tolist()
@@ -119,6 +121,7 @@ def lib() -> C.CDLL:
             "irt_get_render_stats_total": [P, C.POINTER(RenderStats), C.POINTER(C.c_longlong)],
             "irt_reset_render_stats_total": [P],
             "irt_get_shell": [P, P, P],
+            "irt_get_grid": [P, P, P],
             "irt_num_tiles": [I, I],
             "irt_load_ic": [C.c_char_p, C.c_long, P, S, C.POINTER(S)],
             "irt_save_ic": [C.c_char_p, P, S],
@@ -395,6 +398,14 @@ class Context:
 
     def reset_stats_total(self):
         _check(lib().irt_reset_render_stats_total(self._h), "irt_reset_render_stats_total")
+
+    def grid(self) -> tuple[np.ndarray, np.ndarray]:
+        """GRID_ACCEL_MODE grid: (valueRanges (256^3, 2), maxOpacities (256^3,))."""
+        n = 256 ** 3
+        vr = np.zeros((n, 2), np.float32)
+        mo = np.zeros(n, np.float32)
+        _check(lib().irt_get_grid(self._h, _ptr(vr), _ptr(mo)), "irt_get_grid")
+        return vr, mo
 
     def shell(self) -> tuple[np.ndarray, np.ndarray]:
         n = int(np.prod(list(self.info.shellDims)))

@@ -54,6 +54,8 @@ typedef struct irt_box3f { irt_vec3f lower, upper; } irt_box3f;
 /* Raygen selector == Pipeline::setRayGen(...) choice (hostCode.cu:138-149, 863). */
 #define IRT_RAYGEN_WITH_ACCEL 0 /* woodcockTrackingWithAccel, deviceCode.cu:281-341 */
 #define IRT_RAYGEN_AE 1         /* woodcockTrackingAE, deviceCode.cu:239-275 */
+#define IRT_ACCEL_SPHERE 0      /* SPHERE_ACCEL_MODE (Params.h:33): sdda, ShellAccel.h:82-229 */
+#define IRT_ACCEL_GRID 1        /* GRID_ACCEL_MODE (Params.h:34): dda3, DDA.h:35-136 */
 
 /* Per-frame part of icon_rt::LaunchParams (icon_rt/Params.h:92-119).  The volume,
  * accelerator and transfer-function members live in the context (set by irt_create /
@@ -68,6 +70,10 @@ typedef struct irt_launch_params {
   float ambientRadiance;    /* Params.h:115; hostCode.cu:926 */
   float unitDistance;       /* Params.h:118; hostCode.cu:956 */
   int32_t raygen;           /* IRT_RAYGEN_* */
+  int32_t accelMode;        /* volume.accelMode (Params.h:33-34; hostCode.cu:170-200, the
+                               "Accel mode" UI option 853-857): IRT_ACCEL_SPHERE (sdda over
+                               the shell grid, the default) or IRT_ACCEL_GRID (dda3 over the
+                               256^3 Cartesian grid) */
 } irt_launch_params;
 
 /* Scene facts computed at irt_create exactly as hostCode.cu:792-808, 838-840. */
@@ -162,6 +168,10 @@ int irt_get_render_stats(const irt_context *ctx, irt_render_stats *stats);
 int irt_get_render_stats_total(const irt_context *ctx, irt_render_stats *total,
                                long long *launches);
 int irt_reset_render_stats_total(irt_context *ctx);
+
+/* Download the GRID_ACCEL_MODE grid (256^3 macrocells over the volume bounds,
+ * hostCode.cu:668-682; index x + 256*(y + 256*z)), same conventions as irt_get_shell. */
+int irt_get_grid(const irt_context *ctx, float *valueRanges, float *maxOpacities);
 
 /* Download the shell accelerator (for checking): valueRanges as 2 floats per
  * macrocell, maxOpacities as 1 float per macrocell; either may be NULL. */

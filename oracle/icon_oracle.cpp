@@ -344,6 +344,66 @@ inline void sdda(Ray ray, const int dims[3], const B3 &sb, const Func &func) {
   }
 }
 
+// projectOnGrid (DDA.h:23-31)
+inline I3 projectOnGrid(V3 V, const int dims[3], const B3 &wb) {
+  const V3 V01 = (V - wb.lower) / (wb.upper - wb.lower);
+  const V3 Vs = V01 * V3{(float)dims[0], (float)dims[1], (float)dims[2]};
+  return {iclamp(f2i(Vs.x), 0, dims[0] - 1), iclamp(f2i(Vs.y), 0, dims[1] - 1),
+          iclamp(f2i(Vs.z), 0, dims[2] - 1)};
+}
+
+// dda3 (DDA.h:35-136) as the reference's g++ CPU build compiles it: vecmath.h declares no
+// float min, so `min(reduce_min(tnext), ray.tmax)` (96) resolves to int min(int, int)
+// (vecmath.h:46-49): both operands truncated, the result converted back to float.
+template <typename Func>
+inline void dda3(Ray ray, const int dims[3], const B3 &modelBounds, const Func &func) {
+  const float ray_tmin = ray.tmin;
+  ray.org = ray.org + v3(ray.tmin) * ray.dir;
+  ray.tmin = 0.f;
+  ray.tmax -= ray_tmin;
+  const V3 rcp_dir = v3(1.f) / ray.dir;
+  const V3 lo = (modelBounds.lower - ray.org) * rcp_dir;
+  const V3 hi = (modelBounds.upper - ray.org) * rcp_dir;
+  V3 tnear = vmin(lo, hi);
+  const V3 tfar = vmax(lo, hi);
+  if (ray.dir.x == 0.f) tnear.x = FLT_MAX;
+  if (ray.dir.y == 0.f) tnear.y = FLT_MAX;
+  if (ray.dir.z == 0.f) tnear.z = FLT_MAX;
+  I3 cellID = projectOnGrid(ray.org, dims, modelBounds);
+  const V3 dist = vmax(v3(0.f), (tfar - tnear) / V3{(float)dims[0], (float)dims[1], (float)dims[2]});
+  const I3 step = {ray.dir.x > 0.f ? 1 : -1, ray.dir.y > 0.f ? 1 : -1, ray.dir.z > 0.f ? 1 : -1};
+  const I3 stop = {ray.dir.x > 0.f ? dims[0] : -1, ray.dir.y > 0.f ? dims[1] : -1,
+                   ray.dir.z > 0.f ? dims[2] : -1};
+  V3 tnext = {ray.dir.x > 0.f ? tnear.x + float(cellID.x + 1) * dist.x
+                              : tnear.x + float(dims[0] - cellID.x) * dist.x,
+              ray.dir.y > 0.f ? tnear.y + float(cellID.y + 1) * dist.y
+                              : tnear.y + float(dims[1] - cellID.y) * dist.y,
+              ray.dir.z > 0.f ? tnear.z + float(cellID.z + 1) * dist.z
+                              : tnear.z + float(dims[2] - cellID.z) * dist.z};
+  float t0 = 0.f;
+  while (1) {
+    const float t1 = (float)imin(f2i(reduce_min(tnext)), f2i(ray.tmax));
+    if (!func((int)linearIndex(cellID, dims), ray_tmin + t0, ray_tmin + t1)) return;
+    const float t_closest = reduce_min(tnext);
+    if (tnext.x == t_closest) {
+      tnext.x += dist.x;
+      cellID.x += step.x;
+      if (cellID.x == stop.x) break;
+    }
+    if (tnext.y == t_closest) {
+      tnext.y += dist.y;
+      cellID.y += step.y;
+      if (cellID.y == stop.y) break;
+    }
+    if (tnext.z == t_closest) {
+      tnext.z += dist.z;
+      cellID.z += step.z;
+      if (cellID.z == stop.z) break;
+    }
+    t0 = t1;
+  }
+}
+
 // ---------------------------------------------------------------- shading
 // dvr_course-common-both.h:30-35
 inline float linear_to_srgb(float x) {
@@ -498,7 +558,29 @@ void raygen(const Scene &S, const oc_params &p, int x, int y, int W, int H, floa
       }
       return true;
     };
-    sdda(ray, p.dims, sb, woodcockFunc);
+    if (p.accelMode == 1) {  // GRID_ACCEL_MODE (deviceCode.cu:326-328)
+      const float *gridMaxOp = p.gridMaxOpacities;
+      auto gridFunc = [&](const int leafID, float tt0, float tt1) {
+        ++ts.leaves;
+        V3 albedo = v3(0.f);
+        float extinction = 0.f;
+        const float majorant = gridMaxOp[leafID];
+        ray.tmin = tt0;
+        ray.tmax = tt1;
+        ThreadStats uncounted;
+        float t = woodcockTracking(S, p, ray, rnd, majorant, albedo, extinction,
+                                   tt0 == tt1 ? uncounted : ts);
+        if (t > tt0 && t < tt1) {
+          color = albedo * amb * p.ambientRadiance;
+          alpha = extinction > 0.f ? 1.f : 0.f;
+          return false;
+        }
+        return true;
+      };
+      dda3(ray, p.gridDims, toB3(p.gridBounds), gridFunc);
+    } else {
+      sdda(ray, p.dims, sb, woodcockFunc);
+    }
   }
   accumulate(p, color, alpha, accum + 4 * (size_t)pixelID, fb + pixelID);
   ts.draws += rnd.draws;
@@ -670,6 +752,56 @@ void oracle_build_shell(const oc_cell *cells, size_t n, const int32_t dims[3],
   }
 }
 
+void oracle_build_grid(const oc_cell *cells, size_t n, const int32_t dims[3], oc_box3 worldBounds,
+                       float *valueRanges) {
+  const int d[3] = {dims[0], dims[1], dims[2]};
+  const size_t numMCs = (size_t)d[0] * d[1] * d[2];
+  for (size_t i = 0; i < numMCs; ++i) {  // initGrid(Grid) (hostCode.cu:205-214)
+    valueRanges[2 * i] = FLT_MAX;
+    valueRanges[2 * i + 1] = -FLT_MAX;
+  }
+  const B3 wb = toB3(worldBounds);
+  for (size_t ci = 0; ci < n; ++ci) {  // buildGrid_ICON (hostCode.cu:245-297)
+    const oc_cell &cell = cells[ci];
+    for (int i = 0; i < cell.numLayers; ++i) {
+      B3 bounds{v3(INFINITY), v3(-INFINITY)};
+      V3 bv[3], tv[3];
+      for (int k = 0; k < 3; ++k) {
+        bv[k] = toCartesian({cell.height[i], cell.lat[k], cell.lon[k]});
+        tv[k] = toCartesian({cell.height[i + 1], cell.lat[k], cell.lon[k]});
+      }
+      for (int k = 0; k < 3; ++k) {
+        bounds.lower = vmin(bounds.lower, bv[k]);
+        bounds.upper = vmax(bounds.upper, bv[k]);
+      }
+      const V3 bary = (tv[0] + tv[1] + tv[2]) / 3.f;
+      const float R = cell.height[i + 1];
+      const float D = R - length(bary);
+      const float off = D / R;
+      for (int k = 0; k < 3; ++k) {
+        tv[k] = tv[k] + tv[k] * off;
+        bounds.lower = vmin(bounds.lower, tv[k]);
+        bounds.upper = vmax(bounds.upper, tv[k]);
+      }
+      B1 range{INFINITY, -INFINITY};  // box1f::extend (vecmath.h:1001-1004)
+      const float g0 = getValue(cell, cell.height[i]), g1 = getValue(cell, cell.height[i + 1]);
+      range.lower = fminf(range.lower, g0);
+      range.upper = fmaxf(range.upper, g0);
+      range.lower = fminf(range.lower, g1);
+      range.upper = fmaxf(range.upper, g1);
+      // rasterizeBox (hostCode.cu:227-243)
+      const I3 lo = projectOnGrid(bounds.lower, d, wb), up = projectOnGrid(bounds.upper, d, wb);
+      for (int mcz = lo.z; mcz <= up.z; ++mcz)
+        for (int mcy = lo.y; mcy <= up.y; ++mcy)
+          for (int mcx = lo.x; mcx <= up.x; ++mcx) {
+            float *vr = valueRanges + 2 * linearIndex({mcx, mcy, mcz}, d);
+            if (range.lower < vr[0]) vr[0] = range.lower;
+            if (range.upper > vr[1]) vr[1] = range.upper;
+          }
+    }
+  }
+}
+
 void oracle_max_opacities(const float *valueRanges, size_t numMCs, const float *lut, int size,
                           float tfLo, float tfHi, float *maxOpacities) {
   for (size_t mc = 0; mc < numMCs; ++mc) {
@@ -819,6 +951,23 @@ int oracle_sdda_trace(oc_vec3 org, oc_vec3 dir, float tmin, float tmax, const in
   const int d[3] = {dims[0], dims[1], dims[2]};
   int count = 0;
   sdda(r, d, toB3(sphericalBounds), [&](int l, float a, float b) {
+    if (count < maxOut) {
+      leaf[count] = l;
+      t0[count] = a;
+      t1[count] = b;
+    }
+    ++count;
+    return count < 100000;
+  });
+  return count;
+}
+
+int oracle_dda3_trace(oc_vec3 org, oc_vec3 dir, float tmin, float tmax, const int32_t dims[3],
+                      oc_box3 worldBounds, int maxOut, int32_t *leaf, float *t0, float *t1) {
+  Ray r{toV3(org), tmin, toV3(dir), tmax};
+  const int d[3] = {dims[0], dims[1], dims[2]};
+  int count = 0;
+  dda3(r, d, toB3(worldBounds), [&](int l, float a, float b) {
     if (count < maxOut) {
       leaf[count] = l;
       t0[count] = a;

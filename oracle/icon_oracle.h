@@ -51,6 +51,12 @@ typedef struct oc_params {
   float tf_lower, tf_upper, opacityScale;
   const float *lut;               /* vec4f[lut_size] as 4*lut_size floats */
   int32_t lut_size;
+  /* GRID_ACCEL_MODE (Params.h:34, 44-49): accelMode 1 traverses gridMaxOpacities with
+     dda3 (DDA.h:35-136) instead of the shell accelerator with sdda */
+  int32_t accelMode;
+  int32_t gridDims[3];
+  oc_box3 gridBounds;
+  const float *gridMaxOpacities;
 } oc_params;
 
 typedef struct oc_stats {
@@ -94,6 +100,10 @@ void oracle_build_shell(const oc_cell *cells, size_t n, const int32_t dims[3],
                         oc_box3 sphericalBounds, float *valueRanges);
 
 /* computeMaxOpacities(ShellAccel) (hostCode.cu:362-397). */
+/* initGrid(Grid) + buildGrid_ICON + rasterizeBox (hostCode.cu:205-214, 227-297):
+   valueRanges = 2*dims^3 floats over worldBounds (the volume bounds). */
+void oracle_build_grid(const oc_cell *cells, size_t n, const int32_t dims[3], oc_box3 worldBounds,
+                       float *valueRanges);
 void oracle_max_opacities(const float *valueRanges, size_t numMCs, const float *lut,
                           int size, float tfLo, float tfHi, float *maxOpacities);
 
@@ -128,6 +138,9 @@ int oracle_box_test(oc_vec3 org, oc_vec3 dir, float tmin, float tmax, oc_box3 bo
    writes up to maxOut (leaf, t0, t1) triples, returns the number of leaves visited. */
 int oracle_sdda_trace(oc_vec3 org, oc_vec3 dir, float tmin, float tmax, const int32_t dims[3],
                       oc_box3 sphericalBounds, int maxOut, int32_t *leaf, float *t0, float *t1);
+/* dda3 (DDA.h:35-136) leaf sequence over a dims grid of worldBounds. */
+int oracle_dda3_trace(oc_vec3 org, oc_vec3 dir, float tmin, float tmax, const int32_t dims[3],
+                      oc_box3 worldBounds, int maxOut, int32_t *leaf, float *t0, float *t1);
 float oracle_linear_to_srgb(float x);                                          /* dvr_course-common-both.h:30-35 */
 uint32_t oracle_make_rgba(const float *rgba4);                                 /* dvr_course-common-both.h:103-110 */
 void oracle_to_spherical(oc_vec3 c, oc_vec3 *out);                             /* ICONGrid.h:36-42 */

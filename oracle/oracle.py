@@ -35,7 +35,9 @@ class OParams(C.Structure):
                 ("unitDistance", C.c_float), ("raygen", C.c_int32), ("bounds", OBox3),
                 ("dims", C.c_int32 * 3), ("sphericalBounds", OBox3),
                 ("maxOpacities", C.c_void_p), ("tf_lower", C.c_float), ("tf_upper", C.c_float),
-                ("opacityScale", C.c_float), ("lut", C.c_void_p), ("lut_size", C.c_int32)]
+                ("opacityScale", C.c_float), ("lut", C.c_void_p), ("lut_size", C.c_int32),
+                ("accelMode", C.c_int32), ("gridDims", C.c_int32 * 3), ("gridBounds", OBox3),
+                ("gridMaxOpacities", C.c_void_p)]
 
 
 class OStats(C.Structure):
@@ -94,6 +96,8 @@ def olib() -> C.CDLL:
         L.oracle_intersect_sphere.argtypes = [OVec3, OVec3, F, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.oracle_box_test.argtypes = [OVec3, OVec3, F, F, OBox3, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.oracle_sdda_trace.argtypes = [OVec3, OVec3, F, F, P, OBox3, I, P, P, P]
+        L.oracle_dda3_trace.argtypes = [OVec3, OVec3, F, F, P, OBox3, I, P, P, P]
+        L.oracle_build_grid.argtypes = [P, S, P, OBox3, P]
         L.oracle_linear_to_srgb.argtypes = [F]
         L.oracle_linear_to_srgb.restype = F
         L.oracle_make_rgba.argtypes = [P]
@@ -128,6 +132,9 @@ def rlib() -> C.CDLL:
         L.ref_intersect_sphere.argtypes = [P, P, F, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.ref_box_test.argtypes = [P, P, F, F, P, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.ref_sdda_trace.argtypes = [P, P, F, F, P, P, I, P, P, P]
+        L.ref_dda3_trace.argtypes = [P, P, F, F, P, P, I, P, P, P]
+        L.ref_build_grid.argtypes = [P, I, P, P, P]
+        L.ref_set_accel.argtypes = [I, P, P, P]
         L.ref_linear_to_srgb.argtypes = [F]
         L.ref_linear_to_srgb.restype = F
         L.ref_make_rgba.argtypes = [P]
@@ -165,6 +172,28 @@ class OracleScene:
                              _p(self.value_ranges))
         self.max_op = np.zeros(self.num_mcs, dtype=np.float32)
         self.lut = None
+        self.grid_vr = None  # GRID_ACCEL_MODE grid, built on demand (build_grid)
+        self.grid_max_op = None
+
+    GRID_DIMS = (256, 256, 256)  # Grid{nullptr, vec3i(256), volbounds} (hostCode.cu:670)
+
+    def build_grid(self):
+        """buildICONGrid (hostCode.cu:668-682) over the volume bounds; majorants follow the TF."""
+        if self.grid_vr is None:
+            n = int(np.prod(self.GRID_DIMS))
+            self.grid_dims = np.array(self.GRID_DIMS, dtype=np.int32)
+            self.grid_vr = np.zeros((n, 2), dtype=np.float32)
+            olib().oracle_build_grid(_p(self.cells), self.cells.size, _p(self.grid_dims), self.vb,
+                                     _p(self.grid_vr))
+            self.grid_max_op = np.zeros(n, dtype=np.float32)
+            if self.lut is not None:
+                self._grid_max_opacities()
+        return self.grid_vr
+
+    def _grid_max_opacities(self):
+        olib().oracle_max_opacities(_p(self.grid_vr), self.grid_vr.shape[0], _p(self.lut),
+                                    self.lut.shape[0], self.value_range[0], self.value_range[1],
+                                    _p(self.grid_max_op))
 
     def default_lut(self):
         L = olib()
@@ -182,6 +211,8 @@ class OracleScene:
         olib().oracle_max_opacities(_p(self.value_ranges), self.num_mcs, _p(self.lut),
                                     self.lut.shape[0], self.value_range[0], self.value_range[1],
                                     _p(self.max_op))
+        if self.grid_vr is not None:
+            self._grid_max_opacities()
 
     def camera(self, width, height, camera=None, camera_div=None):
         """(org, dir_00, dir_du, dir_dv) as hostCode.cu:939-945."""
@@ -198,7 +229,7 @@ class OracleScene:
         v = np.array([out[3].x, out[3].y, out[3].z], dtype=np.float32) / np.float32(dh)
         return (np.array(org, np.float32), np.array(ll, np.float32), h, v)
 
-    def params(self, cam, accum_id=0, raygen=0, unit_distance=None) -> OParams:
+    def params(self, cam, accum_id=0, raygen=0, unit_distance=None, accel_mode=0) -> OParams:
         org, ll, du, dv = cam
         p = OParams()
         p.org, p.dir_00, p.dir_du, p.dir_dv = v3(org), v3(ll), v3(du), v3(dv)
@@ -216,6 +247,13 @@ class OracleScene:
         p.opacityScale = self.opacity_scale
         p.lut = self.lut.ctypes.data
         p.lut_size = self.lut.shape[0]
+        p.accelMode = accel_mode
+        if accel_mode == 1:
+            self.build_grid()
+            for i in range(3):
+                p.gridDims[i] = int(self.grid_dims[i])
+            p.gridBounds = self.vb
+            p.gridMaxOpacities = self.grid_max_op.ctypes.data
         return p
 
     def render(self, params: OParams, width, height, rect=None, accum=None, fb=None,
@@ -266,6 +304,14 @@ def ref_render(scene: OracleScene, params: OParams, width, height, rect=None, ac
                     scene.sb.upper.y, scene.sb.upper.z], dtype=np.float32)
     tf3 = np.array([params.tf_lower, params.tf_upper, params.opacityScale], dtype=np.float32)
     counters = np.zeros(2, dtype=np.uint64)
+    if params.accelMode == 1:
+        gd = np.array(list(params.gridDims), dtype=np.int32)
+        wb6 = np.array([params.gridBounds.lower.x, params.gridBounds.lower.y,
+                        params.gridBounds.lower.z, params.gridBounds.upper.x,
+                        params.gridBounds.upper.y, params.gridBounds.upper.z], dtype=np.float32)
+        R.ref_set_accel(1, _p(gd), _p(wb6), C.c_void_p(params.gridMaxOpacities))
+    else:
+        R.ref_set_accel(0, None, None, None)
     R.ref_render(_p(scene.cells), scene.cells.size, _p(cam), params.accumID, _p(amb),
                  params.unitDistance, params.raygen, _p(bounds6), _p(scene.dims), _p(sb6),
                  _p(scene.max_op), _p(tf3), _p(scene.lut), scene.lut.shape[0], width, height,

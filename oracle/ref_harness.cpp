@@ -6,7 +6,8 @@
 // common/dvr_course-common.h (resampleLUT), common/camera.h (Camera),
 // common/thread_pool.h + common/for_each.h (the CPU parallel_for),
 // icon_rt/ICONGrid.h (ICONCell, sample, toSpherical/toCartesian),
-// icon_rt/ShellAccel.h (intersectSphere, sdda), icon_rt/DDA.h (linearIndex).
+// icon_rt/ShellAccel.h (intersectSphere, sdda), icon_rt/DDA.h (linearIndex, projectOnGrid,
+// dda3).
 //
 // icon_rt/deviceCode.cu itself cannot be compiled here: it includes Params.h,
 // which includes cuBQL/traversal/fixedBoxQuery.h from the un-vendored cuBQL
@@ -61,6 +62,14 @@ struct RefParams {
 struct Counters {
   unsigned long long locate = 0, found = 0;
 };
+
+// volume.gridAccel + volume.accelMode (Params.h:44-49, 74), set by ref_set_accel
+struct GridAccel {
+  int accelMode = 0;  // SPHERE_ACCEL_MODE
+  vec3i dims;
+  box3f worldBounds;
+  const float *maxOpacities = nullptr;
+} g_grid;
 
 // deviceCode.cu:36-49 (expression kept as in the reference)
 inline Ray generateRay(const RefParams &lp, const vec2f screen, Random &rnd) {
@@ -136,7 +145,7 @@ void raygen(const RefParams &lp, int x, int y, int W, int H, vec4f *accumBuffer,
     color = albedo * lp.ambientColor * lp.ambientRadiance;
     alpha = extinction > 0.f ? 1.f : 0.f;
   } else {
-    const float *maxOpacities = lp.accel.maxOpacities;
+    const float *maxOpacities = lp.accel.maxOpacities;  // deviceCode.cu:302, 326
     auto woodcockFunc = [&](const int leafID, float t0, float t1) {
       vec3f albedo = 0.f;
       float extinction = 0.f;
@@ -154,7 +163,12 @@ void raygen(const RefParams &lp, int x, int y, int W, int H, vec4f *accumBuffer,
       }
       return true;
     };
-    sdda(ray, lp.accel, woodcockFunc, false);
+    if (g_grid.accelMode == 0) {  // deviceCode.cu:325-331
+      sdda(ray, lp.accel, woodcockFunc, false);
+    } else {
+      maxOpacities = g_grid.maxOpacities;
+      dda3(ray, g_grid.dims, g_grid.worldBounds, woodcockFunc);
+    }
   }
   float accum = 1.f / (lp.accumID + 1);
   accumBuffer[pixelID] = lerp(vec4f(color, alpha), accumBuffer[pixelID], accum);
@@ -298,6 +312,63 @@ void ref_build_shell(const void *cellsv, int n, const int *dimsi, const float *s
   }
 }
 
+// ---- GRID_ACCEL_MODE selection for ref_render (toggleAccelMode, hostCode.cu:170-199)
+void ref_set_accel(int accelMode, const int *dimsi, const float *wb6, const float *maxOpacities) {
+  g_grid.accelMode = accelMode;
+  if (dimsi) g_grid.dims = vec3i(dimsi[0], dimsi[1], dimsi[2]);
+  if (wb6) g_grid.worldBounds = box3f(vec3f(wb6[0], wb6[1], wb6[2]), vec3f(wb6[3], wb6[4], wb6[5]));
+  g_grid.maxOpacities = maxOpacities;
+}
+
+// ---- initGrid(Grid) + buildGrid_ICON + rasterizeBox (hostCode.cu:205-214, 227-297),
+// sequential, with projectOnGrid/linearIndex from the reference's DDA.h
+void ref_build_grid(const void *cellsv, int n, const int *dimsi, const float *wb6,
+                    float *valueRanges) {
+  const ICONCell *cells = (const ICONCell *)cellsv;
+  const vec3i dims(dimsi[0], dimsi[1], dimsi[2]);
+  const box3f worldBounds(vec3f(wb6[0], wb6[1], wb6[2]), vec3f(wb6[3], wb6[4], wb6[5]));
+  box1f *vr = (box1f *)valueRanges;
+  const size_t numMCs = dims.x * size_t(dims.y) * dims.z;
+  for (size_t mcID = 0; mcID < numMCs; ++mcID) vr[mcID] = box1f(FLT_MAX, -FLT_MAX);
+  for (int cellID = 0; cellID < n; ++cellID) {
+    const ICONCell &cell = cells[cellID];
+    for (int i = 0; i < cell.numLayers; ++i) {
+      box3f bounds({INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY});
+      vec3f bv1 = toCartesian({cell.height[i], cell.lat.x, cell.lon.x});
+      vec3f bv2 = toCartesian({cell.height[i], cell.lat.y, cell.lon.y});
+      vec3f bv3 = toCartesian({cell.height[i], cell.lat.z, cell.lon.z});
+      bounds.extend(bv1);
+      bounds.extend(bv2);
+      bounds.extend(bv3);
+      vec3f tv1 = toCartesian({cell.height[i + 1], cell.lat.x, cell.lon.x});
+      vec3f tv2 = toCartesian({cell.height[i + 1], cell.lat.y, cell.lon.y});
+      vec3f tv3 = toCartesian({cell.height[i + 1], cell.lat.z, cell.lon.z});
+      vec3f bary = (tv1 + tv2 + tv3) / 3.f;
+      float R = cell.height[i + 1];
+      float D = R - length(bary);
+      float off = D / R;
+      tv1 += tv1 * off;
+      tv2 += tv2 * off;
+      tv3 += tv3 * off;
+      bounds.extend(tv1);
+      bounds.extend(tv2);
+      bounds.extend(tv3);
+      box1f valueRange(INFINITY, -INFINITY);
+      valueRange.extend(cell.getValue(cell.height[i]));
+      valueRange.extend(cell.getValue(cell.height[i + 1]));
+      const vec3i loMC = projectOnGrid(bounds.lower, dims, worldBounds);
+      const vec3i upMC = projectOnGrid(bounds.upper, dims, worldBounds);
+      for (int mcz = loMC.z; mcz <= upMC.z; ++mcz)
+        for (int mcy = loMC.y; mcy <= upMC.y; ++mcy)
+          for (int mcx = loMC.x; mcx <= upMC.x; ++mcx) {
+            box1f &vrange = vr[linearIndex(vec3i(mcx, mcy, mcz), dims)];
+            fmin_store(&vrange.lower, valueRange.lower);
+            fmax_store(&vrange.upper, valueRange.upper);
+          }
+    }
+  }
+}
+
 // ---- computeMaxOpacities(ShellAccel) (hostCode.cu:362-397), sequential
 void ref_max_opacities(const float *valueRangesf, long numMCs, const float *lutf, int size,
                        float tfLo, float tfHi, float *maxOpacities) {
@@ -384,6 +455,20 @@ int ref_sdda_trace(const float *org3, const float *dir3, float tmin, float tmax,
     ++count;
     return count < 100000;
   });
+  return count;
+}
+// dda3 (DDA.h:35-136) itself, compiled from the reference header
+int ref_dda3_trace(const float *org3, const float *dir3, float tmin, float tmax, const int *dimsi,
+                   const float *wb6, int maxOut, int *leaf, float *t0, float *t1) {
+  Ray r(vec3f(org3[0], org3[1], org3[2]), vec3f(dir3[0], dir3[1], dir3[2]), tmin, tmax);
+  int count = 0;
+  dda3(r, vec3i(dimsi[0], dimsi[1], dimsi[2]),
+       box3f(vec3f(wb6[0], wb6[1], wb6[2]), vec3f(wb6[3], wb6[4], wb6[5])),
+       [&](const int l, float a0, float a1) {
+         if (count < maxOut) { leaf[count] = l; t0[count] = a0; t1[count] = a1; }
+         ++count;
+         return count < 100000;
+       });
   return count;
 }
 float ref_linear_to_srgb(float x) { return linear_to_srgb(x); }

@@ -9,7 +9,8 @@ Each frame fixture holds its inputs (the `.ic` records, the LUT/value range, the
 LaunchParams, accumIDs) and the reference outputs (accumBuffer float32 RGBA, fbPointer
 RGBA8, sampleVolume call counts).  kats.npz holds single-function known answers from the
 reference functions (LCG, sample, findHeight, intersectSphere, boxTest, sdda,
-linear_to_srgb/make_rgba, toSpherical/toCartesian, getBounds, resampleLUT, Camera).
+linear_to_srgb/make_rgba, toSpherical/toCartesian, getBounds, resampleLUT, Camera);
+kats_grid.npz + f6_*_grid.npz the GRID_ACCEL_MODE path (dda3, buildGrid_ICON, a frame).
 The `.ic` inputs are synthetic grids from icon-ray-tracing_amd's generator (real DWD data
 is not available offline); they are stored verbatim, so the fixtures do not depend on it.
 """
@@ -231,9 +232,110 @@ def make_kats():
     print("kats:", {k: v.shape for k, v in out.items()})
 
 
+def make_grid_fixtures(frame=True):
+    """GRID_ACCEL_MODE (Params.h:34): dda3 known answers from DDA.h itself, the 256^3
+    buildGrid_ICON value ranges (hostCode.cu:205-297) as a digest plus sampled entries, and
+    one frame of woodcockTrackingWithAccel with accelMode = GRID_ACCEL_MODE."""
+    import hashlib
+    R = O.rlib()
+    rng = np.random.default_rng(20261016)
+    out = {}
+    n = 400
+    org = (rng.normal(size=(n, 3)) * 1.4e7).astype(np.float32)
+    org[:30] = (rng.normal(size=(30, 3)) * 2e6).astype(np.float32)  # starting inside the grid
+    tgt = (rng.normal(size=(n, 3)) * 3e6).astype(np.float32)
+    dirs = tgt - org
+    dirs = (dirs / np.linalg.norm(dirs, axis=1, keepdims=True)).astype(np.float32)
+    dirs[:10, 0] = np.float32(1e-5)  # generateRay's clamped components
+    tmin = rng.uniform(0, 1e7, n).astype(np.float32)
+    tmin[:100] = 0.0
+    tmax = (tmin + rng.uniform(1e3, 3e7, n)).astype(np.float32)
+    dims_all = np.zeros((n, 3), np.int32)
+    dims_all[:] = (256, 256, 256)
+    dims_all[300:] = rng.integers(1, 40, (n - 300, 3))  # ragged grids
+    wb6 = np.array([-6.45e6, -6.44e6, -6.43e6, 6.45e6, 6.44e6, 6.43e6], np.float32)
+    maxo = 2048
+    leaves = np.full((n, maxo), -1, np.int32)
+    lt0 = np.zeros((n, maxo), np.float32)
+    lt1 = np.zeros((n, maxo), np.float32)
+    cnt = np.zeros(n, np.int32)
+    for k in range(n):
+        cnt[k] = R.ref_dda3_trace(org[k].ctypes.data, dirs[k].ctypes.data, float(tmin[k]),
+                                  float(tmax[k]), dims_all[k].ctypes.data, wb6.ctypes.data, maxo,
+                                  leaves[k].ctypes.data, lt0[k].ctypes.data, lt1[k].ctypes.data)
+    out.update(dda3_org=org, dda3_dir=dirs, dda3_tmin=tmin, dda3_tmax=tmax, dda3_dims=dims_all,
+               dda3_wb6=wb6, dda3_count=cnt, dda3_leaf=leaves, dda3_t0=lt0, dda3_t1=lt1)
+    # buildGrid_ICON over a synthetic R2B02 x 60 scene
+    cells = irt.synth_grid(2, 2, 60, noise=0.2)
+    sb6, vb6, dr = np.zeros(6, np.float32), np.zeros(6, np.float32), np.zeros(2, np.float32)
+    R.ref_compute_bounds(cells.ctypes.data, cells.size, sb6.ctypes.data, vb6.ctypes.data,
+                         dr.ctypes.data)
+    gdims = np.array([256, 256, 256], np.int32)
+    gvr = np.zeros((256 ** 3, 2), np.float32)
+    R.ref_build_grid(cells.ctypes.data, cells.size, gdims.ctypes.data, vb6.ctypes.data,
+                     gvr.ctypes.data)
+    pick = np.sort(np.concatenate([rng.choice(256 ** 3, 20000, replace=False),
+                                   rng.choice(np.flatnonzero(gvr[:, 1] >= gvr[:, 0]), 20000,
+                                              replace=False)]))
+    out.update(grid_cells=cells.view(np.uint8).reshape(cells.size, 284), grid_vb6=vb6,
+               grid_sha256=np.frombuffer(hashlib.sha256(gvr.tobytes()).digest(), np.uint8),
+               grid_nonempty=np.int64((gvr[:, 1] >= gvr[:, 0]).sum()), grid_pick=pick,
+               grid_pick_vr=gvr[pick])
+    lut5 = np.array([[0.149, 0.015, 0.705, 1.0], [0.486, 0.603, 0.956, 0.75],
+                     [0.866, 0.866, 0.866, 0.5], [0.996, 0.690, 0.552, 0.25],
+                     [0.752, 0.298, 0.231, 0.0]], np.float32)
+    lut = np.zeros((300, 4), np.float32)
+    R.ref_resample_lut(lut5.ctypes.data, 5, lut.ctypes.data, 300)
+    gmo = np.zeros(256 ** 3, np.float32)
+    R.ref_max_opacities(gvr.ctypes.data, 256 ** 3, lut.ctypes.data, 300, float(dr[0]),
+                        float(dr[1]), gmo.ctypes.data)
+    out.update(grid_lut=lut, grid_value_range=dr.copy(),
+               grid_maxop_sha256=np.frombuffer(hashlib.sha256(gmo.tobytes()).digest(), np.uint8),
+               grid_pick_maxop=gmo[pick])
+    np.savez_compressed(os.path.join(HERE, "kats_grid.npz"), **out)
+    print("kats_grid:", cnt.sum(), "dda3 leaves;", int(out["grid_nonempty"]), "non-empty MCs")
+    if not frame:
+        return
+    # one GRID_ACCEL_MODE frame (the sphere-mode machinery of make_frame, accelMode 1)
+    W = H = 80
+    S = O.OracleScene(cells)
+    vr_ref = np.zeros((S.num_mcs, 2), np.float32)
+    R.ref_build_shell(cells.ctypes.data, cells.size, S.dims.ctypes.data, sb6.ctypes.data,
+                      vr_ref.ctypes.data)
+    S.value_ranges[:] = vr_ref
+    S.set_transfunc(lut, (float(dr[0]), float(dr[1])), 1.0)
+    S.build_grid()
+    S.grid_vr[:] = gvr
+    S.grid_max_op[:] = gmo
+    cam12 = np.zeros(12, np.float32)
+    vp9 = np.array(list(FRAMING[0]) + list(FRAMING[1]) + list(FRAMING[2]), np.float32)
+    R.ref_camera(0, vb6.ctypes.data, vp9.ctypes.data, FRAMING[3], cam12.ctypes.data)
+    cam12[6:9] = cam12[6:9] / np.float32(W)
+    cam12[9:12] = cam12[9:12] / np.float32(H)
+    unit_c = C.c_float(O.olib().oracle_unit_distance(float(sb6[0]))).value
+    p = S.params((cam12[0:3], cam12[3:6], cam12[6:9], cam12[9:12]), raygen=0,
+                 unit_distance=unit_c, accel_mode=1)
+    accum = np.zeros((H, W, 4), np.float32)
+    fb = np.zeros((H, W), np.uint32)
+    _, _, c = O.ref_render(S, p, W, H, accum=accum, fb=fb, threads=1)
+    np.savez_compressed(
+        os.path.join(HERE, "f6_r2b02_l60_grid.npz"),
+        cells=cells.view(np.uint8).reshape(cells.size, 284), width=W, height=H, camera12=cam12,
+        accum_ids=np.array([0], np.int32), raygen=0, accel_mode=1, lut=lut,
+        value_range=dr.copy(), opacity_scale=np.float32(1.0), unit_distance=np.float32(unit_c),
+        spherical_bounds=sb6, volume_bounds=vb6, data_range=dr, accum=accum, fb=fb,
+        counts=np.array([c.copy()], np.uint64))
+    print(f"f6_r2b02_l60_grid: {cells.size} records {W}x{H}, "
+          f"hit {(accum[..., 3] > 0).mean():.3f}, samples {c}")
+
+
 if __name__ == "__main__":
     if not O.have_ref():
         sys.exit("oracle/_ref/libiconref.so missing: make -C oracle ref (needs /root/reference)")
+    if len(sys.argv) > 1 and sys.argv[1] == "grid":
+        make_grid_fixtures()
+        sys.exit(0)
     for name, spec in FRAMES.items():
         make_frame(name, spec)
     make_kats()
+    make_grid_fixtures()

@@ -27,4 +27,5 @@ def oracle_scene(d):
 def params(S, d, accum_id):
     c = d["camera12"]
     return S.params((c[0:3], c[3:6], c[6:9], c[9:12]), accum_id=int(accum_id),
-                    raygen=int(d["raygen"]), unit_distance=float(d["unit_distance"]))
+                    raygen=int(d["raygen"]), unit_distance=float(d["unit_distance"]),
+                    accel_mode=int(d.get("accel_mode", 0)))
