@@ -125,6 +125,7 @@ def lib() -> C.CDLL:
             "irt_num_tiles": [I, I],
             "irt_load_ic": [C.c_char_p, C.c_long, P, S, C.POINTER(S)],
             "irt_save_ic": [C.c_char_p, P, S],
+            "irt_convert_icon": [C.POINTER(ConvertOpts), P, S, C.POINTER(S)],
             "irt_filter_cells": [P, S, Box1, Box1, C.POINTER(S)],
             "irt_compute_volume_info": [P, S, C.POINTER(VolumeInfo)],
             "irt_default_transfunc": [Box1, P, C.POINTER(Box1)],
@@ -209,6 +210,29 @@ def load_ic(path: str, max_num_cells: int = -1) -> np.ndarray:
     cells = np.zeros(n.value, dtype=CELL_DTYPE)
     _check(lib().irt_load_ic(path.encode(), max_num_cells, _ptr(cells), n.value, C.byref(n)),
            "irt_load_ic")
+    return cells
+
+
+class ConvertOpts(C.Structure):
+    """irt_convert_opts: convert_icon's command line (convert_icon.cpp:121-161)."""
+    _fields_ = [("hgridFile", C.c_char_p), ("hsurfFile", C.c_char_p),
+                ("hhlFiles", C.POINTER(C.c_char_p)), ("numHhlFiles", C.c_int),
+                ("dataFiles", C.POINTER(C.c_char_p)), ("numDataFiles", C.c_int),
+                ("varName", C.c_char_p), ("maxLayers", C.c_int)]
+
+
+def convert_icon(hgrid: str, hsurf: str, hhl: list, data: list, var: str = "pres",
+                 max_layers: int = 5) -> np.ndarray:
+    """tools/convert_icon (convert_icon.cpp:168-391): DWD ICON netCDF files -> .ic records."""
+    hp = (C.c_char_p * max(len(hhl), 1))(*[f.encode() for f in hhl])
+    dp = (C.c_char_p * max(len(data), 1))(*[f.encode() for f in data])
+    o = ConvertOpts(hgrid.encode(), hsurf.encode(), hp, len(hhl), dp, len(data), var.encode(),
+                    max_layers)
+    n = C.c_size_t()
+    _check(lib().irt_convert_icon(C.byref(o), None, 0, C.byref(n)), "irt_convert_icon")
+    cells = np.zeros(n.value, dtype=CELL_DTYPE)
+    _check(lib().irt_convert_icon(C.byref(o), _ptr(cells), n.value, C.byref(n)),
+           "irt_convert_icon")
     return cells
 
 

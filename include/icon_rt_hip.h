@@ -192,6 +192,30 @@ int irt_load_ic(const char *path, long maxNumCells, irt_icon_cell *out, size_t c
                 size_t *count);
 int irt_save_ic(const char *path, const irt_icon_cell *cells, size_t count);
 
+/* convert_icon (tools/convert_icon/convert_icon.cpp:168-391): DWD ICON netCDF inputs ->
+ * `.ic` records, the convertToIC branch (353-391) evaluated exactly, including its
+ * quirks: at most maxLayers data levels (24, 345-349), the last record of a column gets
+ * `numLayers % 32 - 1` layers (365), heights R + HHL - HSURF with float/double mixing as
+ * written (361, 371), values min/max-normalised in double (317-328), HHL and data files
+ * sorted by their `height` level index, descending (274, 337).  Inputs are netCDF
+ * classic files (CDF-1/2/5; the netCDF library is replaced by host/irt_netcdf.cpp);
+ * netCDF-4/HDF5 inputs fail with IRT_E_IO.  Where the reference reads out of bounds
+ * (too few HHL/data files for the layers, a data file with fewer than `cell` values)
+ * this returns IRT_E_DATA.  Slots the reference leaves uninitialised are zero.
+ * Two-call pattern: out == NULL returns the record count in *count. */
+typedef struct irt_convert_opts {
+  const char *hgridFile;          /* -hgrid: clon_vertices/clat_vertices (200-203) */
+  const char *hsurfFile;          /* -hsurf: HSURF (225) */
+  const char *const *hhlFiles;    /* -hhl: height + HHL per file (239-272) */
+  int numHhlFiles;
+  const char *const *dataFiles;   /* -data: ncells, height + the variable (282-335) */
+  int numDataFiles;
+  const char *varName;            /* NULL = "pres" (308) */
+  int maxLayers;                  /* <= 0: 5 (24) */
+} irt_convert_opts;
+int irt_convert_icon(const irt_convert_opts *opts, irt_icon_cell *out, size_t capacity,
+                     size_t *count);
+
 /* Lat/lon filter in degrees (hostCode.cu:736-758); stable, in place; returns the kept
  * count in *count. */
 int irt_filter_cells(irt_icon_cell *cells, size_t n, irt_box1f latRangeDeg,

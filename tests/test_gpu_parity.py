@@ -319,3 +319,18 @@ def test_tiles_accumulate_match_full_batch():
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), fb.cpu().numpy())
     ctx.close()
+
+
+def test_converted_icon_files_render_bit_exact(tmp_path):
+    """convert_icon output (netCDF -> .ic, with the reference's HSURF/HHL mixing and its
+    numLayers % 32 - 1 record quirk) through irt_load_ic and the raygen, vs the oracle."""
+    from icon_nc import write_icon_set
+    hg, hs, hhl, data = write_icon_set(str(tmp_path), bisections=2, levels=40)
+    irt.save_ic(str(tmp_path / "c.ic"), irt.convert_icon(hg, hs, hhl, data, max_layers=40))
+    cells = irt.load_ic(str(tmp_path / "c.ic"))
+    for accel in (0, 1):
+        a_ref, f_ref, st_ref, _ = oracle_frame(cells, 64, 64, camera=FRAMING, accel_mode=accel)
+        a_gpu, f_gpu, st_gpu, ctx = gpu_frame(cells, 64, 64, camera=FRAMING, accel_mode=accel)
+        assert_same_frame(a_gpu, f_gpu, a_ref, f_ref, f"converted accel={accel}")
+        assert st_gpu[0].locateCalls == st_ref[0].locate_calls
+        ctx.close()
