@@ -433,3 +433,103 @@ IRT_HD int find_height(const float *height, int numLayers, float hpos) {
 }
 
 }  // namespace irt
+
+// ---------------------------------------------------------------------------------
+// CUBQL_MODE wedges: intersectWedgeEXT (UElems.h:176-311, adapted from OpenVKL) on the
+// wedges buildCuBQLAccel makes (hostCode.cu:557-600), shared by the kernel and the host
+// checks.  A wedge is 6 vertices (x, y, z, scalar): bottom triangle, then top.
+namespace irt {
+struct WV4 {
+  float x, y, z, w;
+};
+
+// determinant(mat3f) (vecmath.h:733-748) of the matrix with columns c0, c1, c2
+// (make_LinearSpace3f, UElems.h:20-28)
+IRT_HD float wedge_det3(const float *c0, const float *c1, const float *c2) {
+  const float a00 = c1[1] * c2[2] - c1[2] * c2[1];
+  const float a01 = c0[1] * c2[2] - c0[2] * c2[1];
+  const float a02 = c0[1] * c1[2] - c0[2] * c1[1];
+  return c0[0] * a00 - c1[0] * a01 + c2[0] * a02;
+}
+
+IRT_HD float wmin(float a, float b) { return b < a ? b : a; }  // fminf on finite input
+IRT_HD float wmax(float a, float b) { return b > a ? b : a; }
+IRT_HD float wabs(float a) { return u2f(f2u(a) & 0x7fffffffu); }
+
+// WEDGE_CONVERGED (1e-4, a double) compared against a float |d|: |d| < 1e-4 <=> |d| <= c
+// for c = (float)1e-4, which rounds below 1e-4 (the next float is above it).
+constexpr float kWedgeConverged = (float)1e-4;
+static_assert((double)kWedgeConverged < 1e-4, "float(1e-4) rounds down");
+// lowerlimit / upperlimit: `0.f - 1e-6` and `1.f + 1e-6` folded in double, then to float
+constexpr float kWedgeLo = (float)(0.0 - 1e-6), kWedgeHi = (float)(1.0 + 1e-6);
+
+IRT_HD bool intersect_wedge(float &value, float px, float py, float pz, const WV4 *V) {
+  // bbox (233-236) and the determinant tolerance: norm2(vec3f) binds to norm2(vec2f)
+  // (vecmath.h:317, 386-389), x and y only
+  float lx = 1e31f, ly = 1e31f, hx = -1e31f, hy = -1e31f;
+  for (int i = 0; i < 6; ++i) {
+    lx = wmin(lx, V[i].x);
+    ly = wmin(ly, V[i].y);
+    hx = wmax(hx, V[i].x);
+    hy = wmax(hy, V[i].y);
+  }
+  const float sx = hx - lx, sy = hy - ly;
+  const float tol = (sx * sx + sy * sy) * 1e-6f;
+  float p0 = .5f, p1 = .5f, p2 = .5f;
+  float w[6];
+  bool converged = false;
+  for (int it = 0; !converged && it < 10; ++it) {
+    const float q = 1.f - p0 - p1, m2 = 1.f - p2;
+    w[0] = q * m2;  // wedgeInterpolationFunctions (176-184)
+    w[1] = p0 * m2;
+    w[2] = p1 * m2;
+    w[3] = q * p2;
+    w[4] = p0 * p2;
+    w[5] = p1 * p2;
+    // wedgeInterpolationDerivs (187-212): r, s, t rows
+    const float dr[6] = {-1.f + p2, 1.f - p2, 0.f, -p2, p2, 0.f};
+    const float ds[6] = {-1.f + p2, 0.f, 1.f - p2, -p2, 0.f, p2};
+    const float dt[6] = {-1.f + p0 + p1, -p0, -p1, 1.f - p0 - p1, p0, p1};
+    float f[3] = {0.f, 0.f, 0.f}, r[3] = {0.f, 0.f, 0.f}, s[3] = {0.f, 0.f, 0.f},
+          t[3] = {0.f, 0.f, 0.f};
+    for (int i = 0; i < 6; ++i) {  // the Newton columns (253-260), in order
+      f[0] = f[0] + V[i].x * w[i];
+      f[1] = f[1] + V[i].y * w[i];
+      f[2] = f[2] + V[i].z * w[i];
+      r[0] = r[0] + V[i].x * dr[i];
+      r[1] = r[1] + V[i].y * dr[i];
+      r[2] = r[2] + V[i].z * dr[i];
+      s[0] = s[0] + V[i].x * ds[i];
+      s[1] = s[1] + V[i].y * ds[i];
+      s[2] = s[2] + V[i].z * ds[i];
+      t[0] = t[0] + V[i].x * dt[i];
+      t[1] = t[1] + V[i].y * dt[i];
+      t[2] = t[2] + V[i].z * dt[i];
+    }
+    f[0] = f[0] - px;
+    f[1] = f[1] - py;
+    f[2] = f[2] - pz;
+    const float d = wedge_det3(r, s, t);
+    if (wabs(d) < tol) return false;
+    const float d0 = wedge_det3(f, s, t) / d;
+    const float d1 = wedge_det3(r, f, t) / d;
+    const float d2 = wedge_det3(r, s, f) / d;
+    p0 = p0 - d0;
+    p1 = p1 - d1;
+    p2 = p2 - d2;
+    if (wabs(d0) <= kWedgeConverged && wabs(d1) <= kWedgeConverged && wabs(d2) <= kWedgeConverged)
+      converged = true;
+    else if (wabs(p0) > 1e6f || wabs(p1) > 1e6f || wabs(p2) > 1e6f)
+      return false;
+  }
+  if (!converged) return false;
+  if (p0 >= kWedgeLo && p0 <= kWedgeHi && p1 >= kWedgeLo && p1 <= kWedgeHi && p2 >= kWedgeLo &&
+      p2 <= kWedgeHi && p0 + p1 <= kWedgeHi) {
+    float val = 0.f;  // 301-305, with the weights of the last iteration
+    for (int i = 0; i < 6; ++i) val += w[i] * V[i].w;
+    value = val;
+    return true;
+  }
+  return false;
+}
+}  // namespace irt

@@ -50,6 +50,10 @@ struct irt_context {
   float *d_maxOp = nullptr;
   float *d_gridVR = nullptr;     // GRID_ACCEL_MODE: Grid::valueRanges, kGridDim^3 box1f
   float *d_gridMaxOp = nullptr;  // Grid::maxOpacities
+  // CUBQL_MODE wedge locator (irt_build_wedge_accel; irt_internal.h WedgeScene)
+  int wG = 0;
+  uint32_t *d_wOff = nullptr, *d_wRec = nullptr;
+  float4 *d_wBox = nullptr, *d_wTrig = nullptr;
   size_t numMCs = 0;
   float4 *d_lut = nullptr;
   int lutCap = 0;
@@ -98,7 +102,7 @@ void free_all(irt_context *c) {
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
-                  c->d_sphBits, c->d_queue, c->d_contList, c->d_segCount, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_srgb, c->d_valueRanges,
+                  c->d_sphBits, c->d_queue, c->d_contList, c->d_segCount, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_srgb, c->d_valueRanges,
                   c->d_lut, c->d_counters};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -167,6 +171,16 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     set_error("irt_render: unknown accelMode %d", lp->accelMode);
     return IRT_E_INVALID;
   }
+  if (lp->mode != IRT_MODE_USER_GEOM && lp->mode != IRT_MODE_CUBQL) {
+    set_error("irt_render: sampler mode %d not supported (IRT_MODE_USER_GEOM or IRT_MODE_CUBQL)",
+              lp->mode);
+    return IRT_E_INVALID;
+  }
+  if (lp->mode == IRT_MODE_CUBQL && c->wG == 0 && c->n != 0) {
+    set_error("irt_render: IRT_MODE_CUBQL needs irt_build_wedge_accel first (buildCuBQLAccel, "
+              "hostCode.cu:557-649)");
+    return IRT_E_INVALID;
+  }
   IRT_HIP(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const int tilesX = (W + 63) / 64, tilesY = (H + 63) / 64;
@@ -194,6 +208,12 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.maxOp = c->d_maxOp;
   A.accelMode = lp->accelMode;
   A.gridMaxOp = c->d_gridMaxOp;
+  A.sampler = lp->mode;
+  A.wG = c->wG;
+  A.wOff = c->d_wOff;
+  A.wRec = c->d_wRec;
+  A.wBox = c->d_wBox;
+  A.wTrig = c->d_wTrig;
   A.tfLo = c->tfLo;
   A.tfHi = c->tfHi;
   A.opacityScale = c->opScale;
@@ -535,6 +555,30 @@ int irt_reset_render_stats_total(irt_context *c) {
   if (rc) return rc;
   c->total = irt_render_stats{};
   c->totalLaunches = 0;
+  return IRT_OK;
+}
+
+int irt_build_wedge_accel(irt_context *c, const irt_icon_cell *cells, size_t n) {
+  if (!c || (n && !cells)) {
+    set_error("irt_build_wedge_accel: null argument");
+    return IRT_E_INVALID;
+  }
+  if (n != c->n) {
+    set_error("irt_build_wedge_accel: %zu cells, the context has %u", n, c->n);
+    return IRT_E_INVALID;
+  }
+  if (c->wG) return IRT_OK;  // built once per context, like buildCuBQLAccel
+  WedgeScene W;
+  int rc = build_wedges(cells, n, W);
+  if (rc) return rc;
+  IRT_HIP(hipSetDevice(c->device));
+  if ((rc = upload(c, &c->d_wOff, W.offsets.data(), W.offsets.size())) ||
+      (rc = upload(c, &c->d_wRec, W.recs.data(), W.recs.size())) ||
+      (rc = upload(c, &c->d_wBox, (const float4 *)W.box.data(), W.box.size() / 4)) ||
+      (rc = upload(c, &c->d_wTrig, (const float4 *)W.trig.data(), W.trig.size() / 4)))
+    return rc;
+  IRT_HIP(hipStreamSynchronize(c->stream));
+  c->wG = W.G;
   return IRT_OK;
 }
 

@@ -71,6 +71,22 @@ int sample_host(const HostScene &s, uint32_t rec, float px, float py, float pz, 
 int locate_host(const HostScene &s, float px, float py, float pz, float &value,
                 uint32_t *record);
 
+// CUBQL_MODE (Params.h:31; deviceCode.cu:90-115) wedge locator, the replacement of
+// buildCuBQLAccel's cuBQL BVH (hostCode.cu:557-649): per record the glibc corner trig and
+// the union of its wedges' primBounds, and a gnomonic cube map listing, per cell, every
+// record with a wedge whose box can contain a point of that direction (sorted by index).
+struct WedgeScene {
+  int G = 0;
+  std::vector<float> trig;       // n * 12: per corner {cosf lat, sinf lat, cosf lon, sinf lon}
+  std::vector<float> box;        // n * 8: lo.xyz, numLayers (int bits), hi.xyz, 0
+  std::vector<uint32_t> offsets; // 6*G*G + 1
+  std::vector<uint32_t> recs;    // record indices
+};
+int build_wedges(const irt_icon_cell *cells, size_t n, WedgeScene &W, int threads = 0);
+// CUBQL_MODE sampleVolume over the wedge locator, as the kernel does it (host check).
+bool wedge_locate_host(const WedgeScene &W, const irt_icon_cell *cells, float px, float py,
+                       float pz, float &value);
+
 int default_threads();
 
 }  // namespace irt

@@ -25,6 +25,11 @@ struct RenderArgs {
   const float *maxOp;    // ShellAccel::maxOpacities
   int accelMode;         // Volume::accelMode (Params.h:33-34): 0 sphere (sdda), 1 grid (dda3)
   const float *gridMaxOp;  // Grid::maxOpacities, kGridDim^3 over bmin..bmax (Params.h:44-49)
+  int sampler;           // Volume::mode (Params.h:60): 0 cell sample() scan, 2 CUBQL wedges
+  int wG;                // CUBQL_MODE wedge locator (host/irt_scene.cpp build_wedges)
+  const uint32_t *wOff, *wRec;
+  const float4 *wBox;    // per record: {lo.xyz, numLayers bits}, {hi.xyz, 0}
+  const float4 *wTrig;   // per record: 3 corners {cosf lat, sinf lat, cosf lon, sinf lon}
   // transfer function (Params.h:77-82)
   float tfLo, tfHi, opacityScale;
   const float4 *lut;

@@ -29,6 +29,7 @@ enum : int {
   OPT_BATCH = 1,      // two fat entries per round trip
   OPT_PF = 2,         // next sample's cell header prefetched (woodcock_pf)
   OPT_ACCPF = 64,     // read the old accum value at ray start
+  OPT_WEDGE = 16384,  // CUBQL_MODE sampler (locate_wedge); kept out of the default kernels
   OPT_STATS = 32768,  // per-wave statistics into counters[5..9] (measurement only)
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
@@ -187,8 +188,60 @@ struct Tracer {
   // sampleVolume (deviceCode.cu:58-125) over the binned lists (irt_common.h): the first
   // record in index order passing sample() -- the reference's linear scan's answer
   // (116-123).
+  // CUBQL_MODE sampleVolume (deviceCode.cu:90-115) over the wedge locator: the first wedge
+  // in (record, layer) order whose primBounds (hostCode.cu:534-552) contain the point and
+  // whose intersectWedgeEXT (UElems.h:214-311) accepts it.  Wedges are rebuilt in
+  // registers from the record's corner trig and heights exactly as buildCuBQLAccel makes
+  // them (hostCode.cu:557-590); a record's union box rejects it first.
+  __device__ __forceinline__ bool locate_wedge(float px, float py, float pz, float &value) {
+    const uint32_t cell = cubemap_cell_fast(px, py, pz, A.wG);
+    const uint32_t qe = A.wOff[cell + 1];
+    for (uint32_t q = A.wOff[cell]; q < qe; ++q) {
+      const uint32_t rec = A.wRec[q];
+      const float4 lo = A.wBox[2 * (size_t)rec], hi = A.wBox[2 * (size_t)rec + 1];
+      if (!(lo.x <= px && px <= hi.x && lo.y <= py && py <= hi.y && lo.z <= pz && pz <= hi.z))
+        continue;
+      const int nl = (int)__float_as_uint(lo.w);
+      const float4 t0 = A.wTrig[3 * (size_t)rec], t1 = A.wTrig[3 * (size_t)rec + 1],
+                   t2 = A.wTrig[3 * (size_t)rec + 2];
+      const float4 *B = A.blocks + (size_t)rec * kBlk4;
+      const float *Bf = reinterpret_cast<const float *>(B);
+      for (int h = 0; h < nl; ++h) {
+        const float hb = Bf[blk_height_pos(h)], ht = Bf[blk_height_pos(h + 1)];
+        WV4 V[6];
+        V[0] = {(hb * t0.x) * t0.z, (hb * t0.x) * t0.w, hb * t0.y, 0.f};
+        V[1] = {(hb * t1.x) * t1.z, (hb * t1.x) * t1.w, hb * t1.y, 0.f};
+        V[2] = {(hb * t2.x) * t2.z, (hb * t2.x) * t2.w, hb * t2.y, 0.f};
+        V[3] = {(ht * t0.x) * t0.z, (ht * t0.x) * t0.w, ht * t0.y, 0.f};
+        V[4] = {(ht * t1.x) * t1.z, (ht * t1.x) * t1.w, ht * t1.y, 0.f};
+        V[5] = {(ht * t2.x) * t2.z, (ht * t2.x) * t2.w, ht * t2.y, 0.f};
+        float bl[3] = {1e31f, 1e31f, 1e31f}, bu[3] = {-1e31f, -1e31f, -1e31f};
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          bl[0] = fminf(bl[0], V[k].x);
+          bl[1] = fminf(bl[1], V[k].y);
+          bl[2] = fminf(bl[2], V[k].z);
+          bu[0] = fmaxf(bu[0], V[k].x);
+          bu[1] = fmaxf(bu[1], V[k].y);
+          bu[2] = fmaxf(bu[2], V[k].z);
+        }
+        if (!(bl[0] <= px && px <= bu[0] && bl[1] <= py && py <= bu[1] && bl[2] <= pz && pz <= bu[2]))
+          continue;
+        // the per-layer scalar (hostCode.cu:571-572) on all six vertices (`#if 1`, 574-577)
+        const float bv = h == 0 ? find_value_literal(B, nl, hb)
+                                : (find_value_literal(B, nl, Bf[blk_height_pos(h - 1)]) +
+                                   find_value_literal(B, nl, hb)) * 0.5f;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) V[k].w = bv;
+        if (intersect_wedge(value, px, py, pz, V)) return true;
+      }
+    }
+    return false;
+  }
+
   __device__ __forceinline__ bool locate(float px, float py, float pz, float &value) {
     if (A.numCells == 0) return false;
+    if constexpr ((OPT & OPT_WEDGE) != 0) return locate_wedge(px, py, pz, value);
     const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
     const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G);
     const uint4 H0 = A.binHdr[2 * (size_t)cell], H1 = A.binHdr[2 * (size_t)cell + 1];
@@ -335,7 +388,8 @@ struct Tracer {
     if (majorant <= 0.f) return fminf(t, tmax);
     const float q = majorant / A.unitDistance;  // the same value every iteration (165)
     if constexpr ((OPT & OPT_PF) != 0) {
-      if (A.numCells != 0) return woodcock_pf(dx, dy, dz, t, tmax, st, majorant, q, sampleOut, counted);
+      if constexpr ((OPT & OPT_WEDGE) == 0)
+        if (A.numCells != 0) return woodcock_pf(dx, dy, dz, t, tmax, st, majorant, q, sampleOut, counted);
     }
     while (true) {
       if constexpr ((OPT & OPT_STATS) != 0) ++cnt.steps;
@@ -941,11 +995,15 @@ bool render_variant_available(int v) {
 template <int N>
 void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
   constexpr int K = N & ~OPT_MONO;
-  if (A.numSamples > 1 || A.accelMode != IRT_ACCEL_SPHERE) {
-    // progressive batch (one frame per grid row, then the lerp chain) or the grid accel:
-    // the one-kernel raygen
+  if (A.numSamples > 1 || A.accelMode != IRT_ACCEL_SPHERE || A.sampler != IRT_MODE_USER_GEOM) {
+    // progressive batch (one frame per grid row, then the lerp chain), the grid accel or
+    // the wedge sampler: the one-kernel raygen
     constexpr int M = (N & OPT_MONO) != 0 ? K : (kDefaultVariant & ~OPT_MONO);
-    hipLaunchKernelGGL(k_render<M>, dim3(numBlocks, A.numSamples), dim3(256), 0, s, A, 0);
+    if (A.sampler == IRT_MODE_CUBQL)
+      hipLaunchKernelGGL(k_render<(kDefaultVariant & ~OPT_MONO) | OPT_WEDGE>,
+                         dim3(numBlocks, A.numSamples), dim3(256), 0, s, A, 0);
+    else
+      hipLaunchKernelGGL(k_render<M>, dim3(numBlocks, A.numSamples), dim3(256), 0, s, A, 0);
     if (A.numSamples > 1) hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);
     return;
   }

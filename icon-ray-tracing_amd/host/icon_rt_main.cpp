@@ -2,7 +2,8 @@
 // icon_rt/hostCode.cu main() (703-968) step by step, with the launch going through the C
 // ABI of include/icon_rt_hip.h.
 //
-//   icon_rt <file.ic> [--num-cells N] [--lat-range a:b] [--lon-range a:b] [-mode M]
+//   icon_rt <file.ic> [--num-cells N] [--lat-range a:b] [--lon-range a:b]
+//           [-mode 0|2]                         (0 cell sample(), 2 cuBQL wedges)
 //           [Pipeline flags: --size W H, --camera ..., -fovy f, --xf f, --sample-limit N]
 //           [--synth rootN bisections levels]   (no .ic file: synthetic ICON grid)
 //           [--bench K]                         (render K extra frames, print timing)
@@ -36,6 +37,7 @@ struct AppState {  // hostCode.cu:65-92 (the parts this backend uses)
   int benchFrames = 0;
   bool trueSize = false;
   int accelMode = IRT_ACCEL_SPHERE;  // g_appState.accelMode (hostCode.cu:75)
+  int mode = IRT_MODE_USER_GEOM;     // g_appState.mode: the sampler (Params.h:29-31)
 } g;
 
 bool endsWith(const std::string &s, const std::string &suffix) {
@@ -59,7 +61,7 @@ void parseCommandLine(int argc, char *argv[]) {  // hostCode.cu:106-129
     else if (arg == "--lon-range" && i + 1 < argc)
       parseRange(argv[++i], g.lonRange);
     else if (arg == "-mode" && i + 1 < argc)
-      ++i;  // OptiX/cuBQL sampler selection: one HIP locator serves all modes
+      g.mode = atoi(argv[++i]);  // hostCode.cu:125-127
     else if (arg == "--synth" && i + 3 < argc) {
       for (int k = 0; k < 3; ++k) g.synth[k] = atoi(argv[++i]);
     } else if (arg == "--bench" && i + 1 < argc)
@@ -154,6 +156,13 @@ int main(int argc, char *argv[]) {
   lp.unitDistance = info.unitDistance;
   lp.raygen = IRT_RAYGEN_WITH_ACCEL;  // setRayGen(woodcockTrackingWithAccel) (863)
   lp.accelMode = g.accelMode;         // toggleAccelMode (hostCode.cu:170-199)
+  if (g.mode == IRT_MODE_CUBQL) {     // toggleMode (hostCode.cu:152-168) + buildCuBQLAccel
+    if (irt_build_wedge_accel(ctx, cells.data(), cells.size())) die("irt_build_wedge_accel");
+    lp.mode = IRT_MODE_CUBQL;
+  } else if (g.mode != IRT_MODE_USER_GEOM) {
+    fprintf(stderr, "icon_rt: -mode %d (OptiX triangles) is not available; using the cell "
+                    "sampler (-mode 0)\n", g.mode);
+  }
 
   pl.clearFramebuffer = [&] {
     if (irt_clear_frame(ctx, fb.fbPointer, fb.accumBuffer, (size_t)fb.width * fb.height, nullptr))

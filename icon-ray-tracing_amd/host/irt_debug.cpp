@@ -11,6 +11,8 @@ using namespace irt;
 
 struct irt_debug_scene {
   HostScene s;
+  std::vector<irt_icon_cell> cells;  // kept for the CUBQL_MODE wedge queries
+  WedgeScene w;
 };
 
 extern "C" {
@@ -141,5 +143,32 @@ int irt_debug_scene_planes(const irt_debug_scene *s, uint32_t record, float *out
 }
 
 void irt_debug_scene_free(irt_debug_scene *s) { delete s; }
+
+int irt_debug_scene_locate_wedge(irt_debug_scene *s, irt_vec3f p, float *value) {
+  if (!s || !value) return IRT_E_INVALID;
+  if (s->w.G == 0) {
+    set_error("irt_debug_scene_locate_wedge: call irt_debug_scene_build_wedges first");
+    return IRT_E_INVALID;
+  }
+  return wedge_locate_host(s->w, s->cells.data(), p.x, p.y, p.z, *value) ? 1 : 0;
+}
+
+int irt_debug_scene_build_wedges(irt_debug_scene *s, const irt_icon_cell *cells, size_t n) {
+  if (!s || (n && !cells) || n != s->s.n) {
+    set_error("irt_debug_scene_build_wedges: cells do not match the scene");
+    return IRT_E_INVALID;
+  }
+  s->cells.assign(cells, cells + n);
+  return build_wedges(cells, n, s->w);
+}
+
+int irt_debug_intersect_wedge(const float *v24, irt_vec3f p, float *value) {
+  WV4 V[6];
+  memcpy(V, v24, sizeof(V));
+  float v = 0.f;
+  const bool hit = intersect_wedge(v, p.x, p.y, p.z, V);
+  if (hit) *value = v;
+  return hit ? 1 : 0;
+}
 
 }  // extern "C"

@@ -698,4 +698,182 @@ int locate_host(const HostScene &s, float px, float py, float pz, float &value,
   return 0;
 }
 
+// ---------------------------------------------------------------- CUBQL_MODE wedges
+namespace {
+
+// toCartesian (ICONGrid.h:44-54) from the corner's glibc trig, the same float expression
+inline V3 wedge_vertex(float r, const float *t) { return {(r * t[0]) * t[2], (r * t[0]) * t[3], r * t[1]}; }
+
+// getValue (ICONGrid.h:147-164)
+inline float cell_value(const irt_icon_cell &c, float h) {
+  return c.value[find_height(c.height, c.numLayers, h)];
+}
+
+// The wedge of layer h of record c (hostCode.cu:562-590) and its primBounds (534-552).
+inline void make_wedge(const irt_icon_cell &c, const float *trig, int h, WV4 V[6], float lo[3],
+                       float hi[3]) {
+  const float bv = h == 0 ? cell_value(c, c.height[h])
+                          : (cell_value(c, c.height[h - 1]) + cell_value(c, c.height[h])) * 0.5f;
+  for (int k = 0; k < 3; ++k) {
+    const V3 b = wedge_vertex(c.height[h], trig + 4 * k), t = wedge_vertex(c.height[h + 1], trig + 4 * k);
+    V[k] = {b.x, b.y, b.z, bv};
+    V[k + 3] = {t.x, t.y, t.z, bv};
+  }
+  lo[0] = lo[1] = lo[2] = 1e31f;
+  hi[0] = hi[1] = hi[2] = -1e31f;
+  for (int k = 0; k < 6; ++k) {
+    lo[0] = fminf(lo[0], V[k].x);
+    lo[1] = fminf(lo[1], V[k].y);
+    lo[2] = fminf(lo[2], V[k].z);
+    hi[0] = fmaxf(hi[0], V[k].x);
+    hi[1] = fmaxf(hi[1], V[k].y);
+    hi[2] = fmaxf(hi[2], V[k].z);
+  }
+}
+
+// Grid cells of the cube map that can hold the direction of a point of box [lo, hi]:
+// per face, the gnomonic projection of the box (all corners in front of the face) is the
+// convex hull of its projected corners; a box straddling a face's plane takes the whole
+// face; a box holding the origin takes every cell.
+void rasterize_box(const double lo[3], const double hi[3], int G, std::vector<uint32_t> &out) {
+  if (lo[0] <= 0 && hi[0] >= 0 && lo[1] <= 0 && hi[1] >= 0 && lo[2] <= 0 && hi[2] >= 0) {
+    for (uint32_t k = 0; k < 6u * G * G; ++k) out.push_back(k);
+    return;
+  }
+  const double padG = kPadUV * 0.5 * G;
+  for (int f = 0; f < 6; ++f) {
+    int ax, ua, va;
+    double sgn;
+    face_axes(f, ax, ua, va, sgn);
+    int front = 0, behind = 0;
+    double mnu = 1e300, mxu = -1e300, mnv = 1e300, mxv = -1e300;
+    for (int c = 0; c < 8; ++c) {
+      const double p[3] = {(c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2]};
+      const double w = sgn * p[ax];
+      if (w > 0) {
+        ++front;
+        const double u = p[ua] / w, v = p[va] / w;
+        mnu = std::min(mnu, u);
+        mxu = std::max(mxu, u);
+        mnv = std::min(mnv, v);
+        mxv = std::max(mxv, v);
+      } else {
+        ++behind;
+      }
+    }
+    if (front == 0) continue;
+    int i0 = 0, i1 = G - 1, j0 = 0, j1 = G - 1;
+    if (behind == 0) {
+      i0 = std::max(0, (int)floor((mnu + 1.0) * 0.5 * G - padG));
+      i1 = std::min(G - 1, (int)floor((mxu + 1.0) * 0.5 * G + padG));
+      j0 = std::max(0, (int)floor((mnv + 1.0) * 0.5 * G - padG));
+      j1 = std::min(G - 1, (int)floor((mxv + 1.0) * 0.5 * G + padG));
+    }
+    for (int j = j0; j <= j1; ++j)
+      for (int i = i0; i <= i1; ++i) out.push_back((uint32_t)f * G * G + (uint32_t)j * G + (uint32_t)i);
+  }
+}
+
+}  // namespace
+
+int build_wedges(const irt_icon_cell *cells, size_t n, WedgeScene &W, int threads) {
+  if (threads <= 0) threads = default_threads();
+  W = WedgeScene();
+  W.trig.resize(n * 12);
+  W.box.assign(n * 8, 0.f);
+  size_t numRuns = 0;
+  for (size_t i = 0; i < n; ++i)
+    if (i == 0 || !same_column(cells[i], cells[i - 1])) ++numRuns;
+  int G = (int)llround(sqrt((double)std::max<size_t>(numRuns, 1) / 6.0) * 1.5);
+  G = std::max(4, std::min(G, 2048));
+  W.G = G;
+  const uint32_t numGridCells = 6u * G * G;
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> parts(threads);
+  std::vector<std::thread> ts;
+  const size_t chunk = (n + threads - 1) / std::max(threads, 1);
+  for (int t = 0; t < threads; ++t) {
+    const size_t b = t * chunk, e = std::min(n, b + chunk);
+    if (b >= e) break;
+    ts.emplace_back([&, t, b, e] {
+      std::vector<uint32_t> gc;
+      for (size_t i = b; i < e; ++i) {
+        const irt_icon_cell &c = cells[i];
+        float *tr = &W.trig[12 * i];
+        for (int k = 0; k < 3; ++k) {
+          tr[4 * k + 0] = cosf(c.lat[k]);
+          tr[4 * k + 1] = sinf(c.lat[k]);
+          tr[4 * k + 2] = cosf(c.lon[k]);
+          tr[4 * k + 3] = sinf(c.lon[k]);
+        }
+        float lo[3] = {1e31f, 1e31f, 1e31f}, hi[3] = {-1e31f, -1e31f, -1e31f};
+        for (int h = 0; h < c.numLayers; ++h) {
+          WV4 V[6];
+          float wl[3], wh[3];
+          make_wedge(c, tr, h, V, wl, wh);
+          for (int a = 0; a < 3; ++a) {
+            lo[a] = fminf(lo[a], wl[a]);
+            hi[a] = fmaxf(hi[a], wh[a]);
+          }
+        }
+        float *bx = &W.box[8 * i];
+        int32_t nl = c.numLayers;
+        bx[0] = lo[0], bx[1] = lo[1], bx[2] = lo[2];
+        memcpy(bx + 3, &nl, 4);
+        bx[4] = hi[0], bx[5] = hi[1], bx[6] = hi[2];
+        if (c.numLayers == 0) continue;  // no wedges
+        // pad the union box by a relative 1e-6 against the double evaluation
+        double dl[3], dh[3];
+        for (int a = 0; a < 3; ++a) {
+          const double m = 1e-6 * std::max(fabs((double)lo[a]), fabs((double)hi[a])) + 1e-3;
+          dl[a] = (double)lo[a] - m;
+          dh[a] = (double)hi[a] + m;
+        }
+        gc.clear();
+        rasterize_box(dl, dh, G, gc);
+        for (uint32_t g : gc) parts[t].emplace_back(g, (uint32_t)i);
+      }
+    });
+  }
+  for (auto &th : ts) th.join();
+  W.offsets.assign(numGridCells + 1, 0);
+  size_t total = 0;
+  for (auto &p : parts) {
+    total += p.size();
+    for (auto &e : p) W.offsets[e.first + 1]++;
+  }
+  if (total > 0xFFFFFFF0ull) {
+    set_error("wedge locator too large (%zu entries)", total);
+    return IRT_E_INVALID;
+  }
+  for (uint32_t k = 0; k < numGridCells; ++k) W.offsets[k + 1] += W.offsets[k];
+  W.recs.resize(total);
+  std::vector<uint32_t> cursor(W.offsets.begin(), W.offsets.end() - 1);
+  for (auto &p : parts)
+    for (auto &e : p) W.recs[cursor[e.first]++] = e.second;
+  return IRT_OK;
+}
+
+bool wedge_locate_host(const WedgeScene &W, const irt_icon_cell *cells, float px, float py,
+                       float pz, float &value) {
+  if (W.G == 0) return false;
+  const uint32_t cell = cubemap_cell(px, py, pz, W.G);
+  for (uint32_t q = W.offsets[cell]; q < W.offsets[cell + 1]; ++q) {
+    const uint32_t rec = W.recs[q];
+    const float *bx = &W.box[8 * (size_t)rec];
+    if (!(bx[0] <= px && px <= bx[4] && bx[1] <= py && py <= bx[5] && bx[2] <= pz && pz <= bx[6]))
+      continue;
+    const irt_icon_cell &c = cells[rec];
+    for (int h = 0; h < c.numLayers; ++h) {
+      WV4 V[6];
+      float lo[3], hi[3];
+      make_wedge(c, &W.trig[12 * (size_t)rec], h, V, lo, hi);
+      // box3f::contains (vecmath.h:1088-1092) of the wedge's primBounds
+      if (!(lo[0] <= px && px <= hi[0] && lo[1] <= py && py <= hi[1] && lo[2] <= pz && pz <= hi[2]))
+        continue;
+      if (intersect_wedge(value, px, py, pz, V)) return true;
+    }
+  }
+  return false;
+}
+
 }  // namespace irt

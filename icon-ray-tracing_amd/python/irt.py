@@ -28,6 +28,8 @@ RAYGEN_WITH_ACCEL = 0  # woodcockTrackingWithAccel (deviceCode.cu:281-341)
 RAYGEN_AE = 1          # woodcockTrackingAE (deviceCode.cu:239-275)
 ACCEL_SPHERE = 0       # SPHERE_ACCEL_MODE (Params.h:33): sdda over the shell grid
 ACCEL_GRID = 1         # GRID_ACCEL_MODE (Params.h:34): dda3 over the 256^3 grid
+MODE_USER_GEOM = 0     # Volume::mode (Params.h:29-31): sample() on the cells (default)
+MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
 # compiled variants of the raygen (irt_render.hip OPT_* bits; 4096 = one monolithic
 # kernel instead of the setup -> march -> continuation pipeline); all bit-identical
 BIN_VARIANTS = (0, 1, 2, 1536, 2048, 32768, 4096, 4097, 4098, 5120, 5376, 5632, 6144, 36864)
@@ -60,7 +62,8 @@ class LaunchParams(C.Structure):
     """Per-frame part of icon_rt::LaunchParams (icon_rt/Params.h:92-119)."""
     _fields_ = [("org", Vec3), ("dir_00", Vec3), ("dir_du", Vec3), ("dir_dv", Vec3),
                 ("accumID", C.c_int32), ("ambientColor", Vec3), ("ambientRadiance", C.c_float),
-                ("unitDistance", C.c_float), ("raygen", C.c_int32), ("accelMode", C.c_int32)]
+                ("unitDistance", C.c_float), ("raygen", C.c_int32), ("accelMode", C.c_int32),
+                ("mode", C.c_int32)]
 
     def camera12(self) -> np.ndarray:
         return np.array(self.org.tolist() + self.dir_00.tolist() + self.dir_du.tolist()
@@ -122,6 +125,7 @@ def lib() -> C.CDLL:
             "irt_reset_render_stats_total": [P],
             "irt_get_shell": [P, P, P],
             "irt_get_grid": [P, P, P],
+            "irt_build_wedge_accel": [P, P, S],
             "irt_num_tiles": [I, I],
             "irt_load_ic": [C.c_char_p, C.c_long, P, S, C.POINTER(S)],
             "irt_save_ic": [C.c_char_p, P, S],
@@ -422,6 +426,12 @@ class Context:
 
     def reset_stats_total(self):
         _check(lib().irt_reset_render_stats_total(self._h), "irt_reset_render_stats_total")
+
+    def build_wedge_accel(self, cells: np.ndarray):
+        """buildCuBQLAccel (hostCode.cu:557-649): enables LaunchParams.mode = MODE_CUBQL."""
+        cells = np.ascontiguousarray(cells, dtype=CELL_DTYPE)
+        _check(lib().irt_build_wedge_accel(self._h, _ptr(cells), cells.size),
+               "irt_build_wedge_accel")
 
     def grid(self) -> tuple[np.ndarray, np.ndarray]:
         """GRID_ACCEL_MODE grid: (valueRanges (256^3, 2), maxOpacities (256^3,))."""

@@ -56,6 +56,11 @@ typedef struct irt_box3f { irt_vec3f lower, upper; } irt_box3f;
 #define IRT_RAYGEN_AE 1         /* woodcockTrackingAE, deviceCode.cu:239-275 */
 #define IRT_ACCEL_SPHERE 0      /* SPHERE_ACCEL_MODE (Params.h:33): sdda, ShellAccel.h:82-229 */
 #define IRT_ACCEL_GRID 1        /* GRID_ACCEL_MODE (Params.h:34): dda3, DDA.h:35-136 */
+/* Sampler == Volume::mode (Params.h:29-31, 60; the -mode flag, hostCode.cu:125-127). */
+#define IRT_MODE_USER_GEOM 0    /* sample() on the cells (ICONGrid.h:181-208): the CPU build's
+                                   scan (deviceCode.cu:116-123), lowest index wins */
+#define IRT_MODE_TRIANGLES 1    /* OptiX triangle trace (deviceCode.cu:61-76): not supported */
+#define IRT_MODE_CUBQL 2        /* wedges + intersectWedgeEXT (deviceCode.cu:90-115) */
 
 /* Per-frame part of icon_rt::LaunchParams (icon_rt/Params.h:92-119).  The volume,
  * accelerator and transfer-function members live in the context (set by irt_create /
@@ -74,6 +79,8 @@ typedef struct irt_launch_params {
                                "Accel mode" UI option 853-857): IRT_ACCEL_SPHERE (sdda over
                                the shell grid, the default) or IRT_ACCEL_GRID (dda3 over the
                                256^3 Cartesian grid) */
+  int32_t mode;             /* volume.mode: IRT_MODE_USER_GEOM (default) or IRT_MODE_CUBQL
+                               (needs irt_build_wedge_accel) */
 } irt_launch_params;
 
 /* Scene facts computed at irt_create exactly as hostCode.cu:792-808, 838-840. */
@@ -168,6 +175,16 @@ int irt_get_render_stats(const irt_context *ctx, irt_render_stats *stats);
 int irt_get_render_stats_total(const irt_context *ctx, irt_render_stats *total,
                                long long *launches);
 int irt_reset_render_stats_total(irt_context *ctx);
+
+/* buildCuBQLAccel (hostCode.cu:557-649) for IRT_MODE_CUBQL: the wedges of every (cell,
+ * layer) -- corners toCartesian(height[h|h+1], lat, lon), scalar
+ * h == 0 ? getValue(height[0]) : (getValue(height[h-1]) + getValue(height[h])) * 0.5 on
+ * all six vertices -- behind a cube-map locator of their primBounds (replacing the cuBQL
+ * BVH).  `cells` must be the array given to irt_create.  A sample takes the first wedge,
+ * in (cell, layer) order, whose bounds contain it and whose intersectWedgeEXT
+ * (UElems.h:214-311) accepts it; cuBQL's own traversal order is not reproducible here
+ * (the submodule is not vendored), so that order is the documented choice. */
+int irt_build_wedge_accel(irt_context *ctx, const irt_icon_cell *cells, size_t n);
 
 /* Download the GRID_ACCEL_MODE grid (256^3 macrocells over the volume bounds,
  * hostCode.cu:668-682; index x + 256*(y + 256*z)), same conventions as irt_get_shell. */

@@ -51,6 +51,13 @@ int irt_debug_scene_candidates(const irt_debug_scene *s, irt_vec3f p, uint32_t *
 /* Per-record side planes (3 x vec4) as uploaded. */
 int irt_debug_scene_planes(const irt_debug_scene *s, uint32_t record, float *out12);
 void irt_debug_scene_free(irt_debug_scene *s);
+/* CUBQL_MODE (deviceCode.cu:90-115): build the wedge locator irt_build_wedge_accel
+ * uploads, then sampleVolume through it as the kernel does (first wedge in index order
+ * whose primBounds contain p and whose intersectWedgeEXT accepts it). */
+int irt_debug_scene_build_wedges(irt_debug_scene *s, const irt_icon_cell *cells, size_t n);
+int irt_debug_scene_locate_wedge(irt_debug_scene *s, irt_vec3f p, float *value);
+/* intersectWedgeEXT (UElems.h:214-311) as the kernel evaluates it; v24 = 6 x (xyz, scalar). */
+int irt_debug_intersect_wedge(const float *v24, irt_vec3f p, float *value);
 
 /* Select the render-kernel variant (bit set of irt_render.hip's OPT_* flags; every
  * variant gives identical results -- used for in-process A/B timing). */

@@ -432,12 +432,140 @@ inline V4 postClassify(const oc_params &p, float v) {
           v1[2] * frac + v2[2] * om * 1.f, v1[3] * frac + v2[3] * om * p.opacityScale};
 }
 
+// ---------------------------------------------------------------- CUBQL_MODE wedges
+// The unstructured-element sampler (deviceCode.cu:90-115): wedges built per (cell, layer)
+// as buildCuBQLAccel does (hostCode.cu:557-600), each sample the first wedge whose
+// primBounds (534-552) contain the point and whose intersectWedgeEXT (UElems.h:214-311)
+// accepts it.  cuBQL's traversal order is unpinned (the submodule is absent); "first"
+// here is the lowest wedge index, the order a linear scan of the build would give.
+struct Wedge {
+  V4 v[6];
+  B3 box;
+};
+
+// determinant(mat3f) (vecmath.h:733-748) of make_LinearSpace3f(c0, c1, c2) (UElems.h:20-28):
+// m(row, col) is component `row` of column `col`
+inline float det3(V3 c0, V3 c1, V3 c2) {
+  auto det2 = [](float m00, float m01, float m10, float m11) { return m00 * m11 - m10 * m01; };
+  const float a00 = det2(c1.y, c2.y, c1.z, c2.z);
+  const float a01 = det2(c0.y, c2.y, c0.z, c2.z);
+  const float a02 = det2(c0.y, c1.y, c0.z, c1.z);
+  return c0.x * a00 - c1.x * a01 + c2.x * a02;
+}
+
+// intersectWedgeEXT (UElems.h:176-311), the OpenVKL Newton inversion.  Quirks kept:
+// norm2(bbox.size()) binds to norm2(vec2f) through vec2f's converting constructor
+// (vecmath.h:317, 386-389), so the tolerance ignores z; WEDGE_CONVERGED /
+// WEDGE_OUTSIDE_CELL_TOLERANCE are double literals (compared / folded in double).
+inline bool intersectWedgeEXT(float &value, V3 P, const V4 V[6]) {
+  B3 bbox{v3(1e31f), v3(-1e31f)};
+  for (int i = 0; i < 6; ++i) {
+    bbox.lower = vmin(bbox.lower, V3{V[i].x, V[i].y, V[i].z});
+    bbox.upper = vmax(bbox.upper, V3{V[i].x, V[i].y, V[i].z});
+  }
+  const V3 sz = bbox.upper - bbox.lower;
+  const float determinantTolerance = (sz.x * sz.x + sz.y * sz.y) * 1e-6f;
+  float pc[3] = {.5f, .5f, .5f};
+  float w[6], dv[18];
+  bool converged = false;
+  for (int it = 0; !converged && it < 10; ++it) {
+    w[0] = (1.f - pc[0] - pc[1]) * (1.f - pc[2]);  // wedgeInterpolationFunctions (176-184)
+    w[1] = pc[0] * (1.f - pc[2]);
+    w[2] = pc[1] * (1.f - pc[2]);
+    w[3] = (1.f - pc[0] - pc[1]) * pc[2];
+    w[4] = pc[0] * pc[2];
+    w[5] = pc[1] * pc[2];
+    dv[0] = -1.f + pc[2];  // wedgeInterpolationDerivs (187-212)
+    dv[1] = 1.f - pc[2];
+    dv[2] = 0.f;
+    dv[3] = -pc[2];
+    dv[4] = pc[2];
+    dv[5] = 0.f;
+    dv[6] = -1.f + pc[2];
+    dv[7] = 0.f;
+    dv[8] = 1.f - pc[2];
+    dv[9] = -pc[2];
+    dv[10] = 0.f;
+    dv[11] = pc[2];
+    dv[12] = -1.f + pc[0] + pc[1];
+    dv[13] = -pc[0];
+    dv[14] = -pc[1];
+    dv[15] = 1.f - pc[0] - pc[1];
+    dv[16] = pc[0];
+    dv[17] = pc[1];
+    V3 f = v3(0.f), r = v3(0.f), s = v3(0.f), t = v3(0.f);
+    for (int i = 0; i < 6; ++i) {
+      const V3 pt{V[i].x, V[i].y, V[i].z};
+      f = f + pt * w[i];
+      r = r + pt * dv[i];
+      s = s + pt * dv[i + 6];
+      t = t + pt * dv[i + 12];
+    }
+    f = f - P;
+    const float d = det3(r, s, t);
+    if (fabsf(d) < determinantTolerance) return false;
+    const float d0 = det3(f, s, t) / d;
+    const float d1 = det3(r, f, t) / d;
+    const float d2 = det3(r, s, f) / d;
+    pc[0] = pc[0] - d0;
+    pc[1] = pc[1] - d1;
+    pc[2] = pc[2] - d2;
+    if (((double)fabsf(d0) < 1e-4) & ((double)fabsf(d1) < 1e-4) & ((double)fabsf(d2) < 1e-4)) {
+      converged = true;
+    } else if ((fabsf(pc[0]) > 1e6) | (fabsf(pc[1]) > 1e6) | (fabsf(pc[2]) > 1e6)) {
+      return false;
+    }
+  }
+  if (!converged) return false;
+  const float lo = (float)(0.f - 1e-6), hi = (float)(1.f + 1e-6);
+  if (pc[0] >= lo && pc[0] <= hi && pc[1] >= lo && pc[1] <= hi && pc[2] >= lo && pc[2] <= hi &&
+      pc[0] + pc[1] <= hi) {
+    float val = 0.f;
+    for (int i = 0; i < 6; ++i) val += w[i] * V[i].w;
+    value = val;
+    return true;
+  }
+  return false;
+}
+
+// buildCuBQLAccel's wedges (hostCode.cu:557-600) and computeBounds (534-552)
+void buildWedges(const oc_cell *cells, size_t n, std::vector<Wedge> &out) {
+  out.clear();
+  for (size_t i = 0; i < n; ++i) {
+    const oc_cell &cell = cells[i];
+    for (int h = 0; h < cell.numLayers; ++h) {
+      Wedge wd;
+      const float bv = h == 0 ? getValue(cell, cell.height[h])
+                              : (getValue(cell, cell.height[h - 1]) + getValue(cell, cell.height[h])) * 0.5f;
+      for (int k = 0; k < 3; ++k) {
+        const V3 b = toCartesian({cell.height[h], cell.lat[k], cell.lon[k]});
+        const V3 t = toCartesian({cell.height[h + 1], cell.lat[k], cell.lon[k]});
+        wd.v[k] = {b.x, b.y, b.z, bv};
+        wd.v[k + 3] = {t.x, t.y, t.z, bv};  // `#if 1`: the top takes bv too (574-577)
+      }
+      wd.box = B3{v3(1e31f), v3(-1e31f)};
+      for (int k = 0; k < 6; ++k) {
+        wd.box.lower = vmin(wd.box.lower, V3{wd.v[k].x, wd.v[k].y, wd.v[k].z});
+        wd.box.upper = vmax(wd.box.upper, V3{wd.v[k].x, wd.v[k].y, wd.v[k].z});
+      }
+      out.push_back(wd);
+    }
+  }
+}
+
+inline bool boxContains(const B3 &b, V3 p) {  // box3f::contains (vecmath.h:1088-1092)
+  return b.lower.x <= p.x && p.x <= b.upper.x && b.lower.y <= p.y && p.y <= b.upper.y &&
+         b.lower.z <= p.z && p.z <= b.upper.z;
+}
+
 // ---------------------------------------------------------------- renderer
 struct Scene {
   const oc_cell *cells;
   size_t n;
   bool fast;
   std::vector<CellPlanes> planes;  // fast mode only
+  std::vector<Wedge> wedges;       // CUBQL_MODE only
+  bool useWedges = false;
 };
 
 struct ThreadStats {
@@ -446,6 +574,11 @@ struct ThreadStats {
 
 // sampleVolume, CPU branch: first cell index wins (deviceCode.cu:116-123)
 inline bool sampleVolume(const Scene &S, V3 pos, float &value) {
+  if (S.useWedges) {  // CUBQL_MODE (deviceCode.cu:90-115)
+    for (const Wedge &wd : S.wedges)
+      if (boxContains(wd.box, pos) && intersectWedgeEXT(value, pos, wd.v)) return true;
+    return false;
+  }
   if (S.fast) {
     for (size_t i = 0; i < S.n; ++i)
       if (sampleFast(S.cells[i], S.planes[i], pos, value)) return true;
@@ -836,10 +969,14 @@ int oracle_render(const oc_cell *cells, size_t n, const oc_params *p, int W, int
                   oc_stats *stats) {
   if (!p || W <= 0 || H <= 0 || x0 < 0 || y0 < 0 || x1 > W || y1 > H) return -1;
   if (x1 <= x0 || y1 <= y0) return 0;
-  Scene S{cells, n, fast != 0, {}};
+  Scene S{cells, n, fast != 0, {}, {}, false};
   if (S.fast) {
     S.planes.resize(n);
     for (size_t i = 0; i < n; ++i) S.planes[i] = cellPlanes(cells[i]);
+  }
+  if (p->mode == 2) {
+    S.useWedges = true;
+    buildWedges(cells, n, S.wedges);
   }
   // parallel::for_each over 64x64 tiles (common/for_each.h:70-85,
   // parallel_for.h:62-82), dynamic via an atomic counter (thread_pool.h:146-161)
@@ -885,10 +1022,14 @@ int oracle_render_pixels(const oc_cell *cells, size_t n, const oc_params *p, int
   if (!p || W <= 0 || H <= 0 || numPixels < 0) return -1;
   for (int i = 0; i < numPixels; ++i)
     if (xy[2 * i] < 0 || xy[2 * i] >= W || xy[2 * i + 1] < 0 || xy[2 * i + 1] >= H) return -1;
-  Scene S{cells, n, fast != 0, {}};
+  Scene S{cells, n, fast != 0, {}, {}, false};
   if (S.fast) {
     S.planes.resize(n);
     for (size_t i = 0; i < n; ++i) S.planes[i] = cellPlanes(cells[i]);
+  }
+  if (p->mode == 2) {
+    S.useWedges = true;
+    buildWedges(cells, n, S.wedges);
   }
   std::atomic<int> counter{0};
   if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
@@ -977,6 +1118,21 @@ int oracle_dda3_trace(oc_vec3 org, oc_vec3 dir, float tmin, float tmax, const in
     return count < 100000;
   });
   return count;
+}
+
+int oracle_intersect_wedge(const float *v24, oc_vec3 p, float *value) {
+  V4 V[6];
+  for (int i = 0; i < 6; ++i) V[i] = {v24[4 * i], v24[4 * i + 1], v24[4 * i + 2], v24[4 * i + 3]};
+  float v = 0.f;
+  const bool hit = intersectWedgeEXT(v, toV3(p), V);
+  if (hit) *value = v;
+  return hit;
+}
+
+int oracle_wedge_sample(const oc_cell *cells, size_t n, oc_vec3 p, float *value) {
+  Scene S{cells, n, false, {}, {}, true};
+  buildWedges(cells, n, S.wedges);
+  return sampleVolume(S, toV3(p), *value);
 }
 
 float oracle_linear_to_srgb(float x) { return linear_to_srgb(x); }

@@ -57,6 +57,9 @@ typedef struct oc_params {
   int32_t gridDims[3];
   oc_box3 gridBounds;
   const float *gridMaxOpacities;
+  /* Volume::mode (Params.h:60): 0 the cell sample() scan (the CPU build, deviceCode.cu:
+     116-123), 2 CUBQL_MODE wedges (deviceCode.cu:90-115) */
+  int32_t mode;
 } oc_params;
 
 typedef struct oc_stats {
@@ -141,6 +144,10 @@ int oracle_sdda_trace(oc_vec3 org, oc_vec3 dir, float tmin, float tmax, const in
 /* dda3 (DDA.h:35-136) leaf sequence over a dims grid of worldBounds. */
 int oracle_dda3_trace(oc_vec3 org, oc_vec3 dir, float tmin, float tmax, const int32_t dims[3],
                       oc_box3 worldBounds, int maxOut, int32_t *leaf, float *t0, float *t1);
+/* intersectWedgeEXT (UElems.h:214-311): v24 = 6 vertices as (x,y,z,scalar). */
+int oracle_intersect_wedge(const float *v24, oc_vec3 p, float *value);
+/* CUBQL_MODE sampleVolume over the wedges of `cells` (hostCode.cu:557-600). */
+int oracle_wedge_sample(const oc_cell *cells, size_t n, oc_vec3 p, float *value);
 float oracle_linear_to_srgb(float x);                                          /* dvr_course-common-both.h:30-35 */
 uint32_t oracle_make_rgba(const float *rgba4);                                 /* dvr_course-common-both.h:103-110 */
 void oracle_to_spherical(oc_vec3 c, oc_vec3 *out);                             /* ICONGrid.h:36-42 */

@@ -37,7 +37,7 @@ class OParams(C.Structure):
                 ("maxOpacities", C.c_void_p), ("tf_lower", C.c_float), ("tf_upper", C.c_float),
                 ("opacityScale", C.c_float), ("lut", C.c_void_p), ("lut_size", C.c_int32),
                 ("accelMode", C.c_int32), ("gridDims", C.c_int32 * 3), ("gridBounds", OBox3),
-                ("gridMaxOpacities", C.c_void_p)]
+                ("gridMaxOpacities", C.c_void_p), ("mode", C.c_int32)]
 
 
 class OStats(C.Structure):
@@ -98,6 +98,8 @@ def olib() -> C.CDLL:
         L.oracle_sdda_trace.argtypes = [OVec3, OVec3, F, F, P, OBox3, I, P, P, P]
         L.oracle_dda3_trace.argtypes = [OVec3, OVec3, F, F, P, OBox3, I, P, P, P]
         L.oracle_build_grid.argtypes = [P, S, P, OBox3, P]
+        L.oracle_intersect_wedge.argtypes = [P, OVec3, C.POINTER(C.c_float)]
+        L.oracle_wedge_sample.argtypes = [P, S, OVec3, C.POINTER(C.c_float)]
         L.oracle_linear_to_srgb.argtypes = [F]
         L.oracle_linear_to_srgb.restype = F
         L.oracle_make_rgba.argtypes = [P]
@@ -135,6 +137,9 @@ def rlib() -> C.CDLL:
         L.ref_dda3_trace.argtypes = [P, P, F, F, P, P, I, P, P, P]
         L.ref_build_grid.argtypes = [P, I, P, P, P]
         L.ref_set_accel.argtypes = [I, P, P, P]
+        L.ref_set_sampler.argtypes = [I, P, I]
+        L.ref_intersect_wedge.argtypes = [P, P, C.POINTER(C.c_float)]
+        L.ref_wedge_sample.argtypes = [P, I, P, C.POINTER(C.c_float)]
         L.ref_linear_to_srgb.argtypes = [F]
         L.ref_linear_to_srgb.restype = F
         L.ref_make_rgba.argtypes = [P]
@@ -229,7 +234,8 @@ class OracleScene:
         v = np.array([out[3].x, out[3].y, out[3].z], dtype=np.float32) / np.float32(dh)
         return (np.array(org, np.float32), np.array(ll, np.float32), h, v)
 
-    def params(self, cam, accum_id=0, raygen=0, unit_distance=None, accel_mode=0) -> OParams:
+    def params(self, cam, accum_id=0, raygen=0, unit_distance=None, accel_mode=0,
+               mode=0) -> OParams:
         org, ll, du, dv = cam
         p = OParams()
         p.org, p.dir_00, p.dir_du, p.dir_dv = v3(org), v3(ll), v3(du), v3(dv)
@@ -248,6 +254,7 @@ class OracleScene:
         p.lut = self.lut.ctypes.data
         p.lut_size = self.lut.shape[0]
         p.accelMode = accel_mode
+        p.mode = mode
         if accel_mode == 1:
             self.build_grid()
             for i in range(3):
@@ -312,6 +319,7 @@ def ref_render(scene: OracleScene, params: OParams, width, height, rect=None, ac
         R.ref_set_accel(1, _p(gd), _p(wb6), C.c_void_p(params.gridMaxOpacities))
     else:
         R.ref_set_accel(0, None, None, None)
+    R.ref_set_sampler(params.mode, _p(scene.cells), scene.cells.size)
     R.ref_render(_p(scene.cells), scene.cells.size, _p(cam), params.accumID, _p(amb),
                  params.unitDistance, params.raygen, _p(bounds6), _p(scene.dims), _p(sb6),
                  _p(scene.max_op), _p(tf3), _p(scene.lut), scene.lut.shape[0], width, height,

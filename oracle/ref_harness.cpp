@@ -7,7 +7,7 @@
 // common/thread_pool.h + common/for_each.h (the CPU parallel_for),
 // icon_rt/ICONGrid.h (ICONCell, sample, toSpherical/toCartesian),
 // icon_rt/ShellAccel.h (intersectSphere, sdda), icon_rt/DDA.h (linearIndex, projectOnGrid,
-// dda3).
+// dda3), icon_rt/UElems.h (intersectWedgeEXT).
 //
 // icon_rt/deviceCode.cu itself cannot be compiled here: it includes Params.h,
 // which includes cuBQL/traversal/fixedBoxQuery.h from the un-vendored cuBQL
@@ -34,6 +34,7 @@
 #include "DDA.h"
 #include "ICONGrid.h"
 #include "ShellAccel.h"
+#include "UElems.h"
 
 using namespace dvr_course;
 using namespace icon_rt;
@@ -71,6 +72,67 @@ struct GridAccel {
   const float *maxOpacities = nullptr;
 } g_grid;
 
+// CUBQL_MODE (Params.h:31, 60): the wedge UMesh of buildCuBQLAccel (hostCode.cu:557-600)
+// with its primBounds (computeBounds, 534-552), sampled as deviceCode.cu:90-115 does; the
+// cuBQL BVH's traversal order is replaced by wedge index order (cuBQL is not vendored).
+struct WedgeMesh {
+  int mode = 0;
+  std::vector<vec3f> vertices;
+  std::vector<float> scalars;
+  std::vector<int> indices;
+  std::vector<box3f> primBounds;
+} g_wedges;
+
+void buildWedgeMesh(const ICONCell *cells, int numCells) {
+  auto &W = g_wedges;
+  W.vertices.clear();
+  W.scalars.clear();
+  W.indices.clear();
+  W.primBounds.clear();
+  for (int i = 0; i < numCells; ++i) {
+    const ICONCell &cell = cells[i];
+    for (int h = 0; h < cell.numLayers; ++h) {
+      vec3f bv1 = toCartesian({cell.height[h], cell.lat.x, cell.lon.x});
+      vec3f bv2 = toCartesian({cell.height[h], cell.lat.y, cell.lon.y});
+      vec3f bv3 = toCartesian({cell.height[h], cell.lat.z, cell.lon.z});
+      vec3f tv1 = toCartesian({cell.height[h + 1], cell.lat.x, cell.lon.x});
+      vec3f tv2 = toCartesian({cell.height[h + 1], cell.lat.y, cell.lon.y});
+      vec3f tv3 = toCartesian({cell.height[h + 1], cell.lat.z, cell.lon.z});
+      float bv = h == 0 ? cell.getValue(cell.height[h])
+                        : (cell.getValue(cell.height[h - 1]) + cell.getValue(cell.height[h])) * 0.5f;
+      int idx0 = (int)W.vertices.size();
+      for (const vec3f &v : {bv1, bv2, bv3, tv1, tv2, tv3}) {
+        W.vertices.push_back(v);
+        W.scalars.push_back(bv);
+      }
+      for (int k = 0; k < 6; ++k) W.indices.push_back(idx0 + k);
+      box3f b(vec3f(1e31f), vec3f(-1e31f));
+      for (int k = 0; k < 6; ++k) b.extend(W.vertices[idx0 + k]);
+      W.primBounds.push_back(b);
+    }
+  }
+}
+
+inline bool sampleWedges(vec3f pos, float &value) {
+  const auto &W = g_wedges;
+  for (size_t primID = 0; primID < W.primBounds.size(); ++primID) {
+    if (!W.primBounds[primID].contains(pos)) continue;
+    const int *I = W.indices.data() + primID * 6;
+    const vec4f v0(W.vertices[I[0]], W.scalars[I[0]]);
+    const vec4f v1(W.vertices[I[1]], W.scalars[I[1]]);
+    const vec4f v2(W.vertices[I[2]], W.scalars[I[2]]);
+    const vec4f v3(W.vertices[I[3]], W.scalars[I[3]]);
+    const vec4f v4(W.vertices[I[4]], W.scalars[I[4]]);
+    const vec4f v5(W.vertices[I[5]], W.scalars[I[5]]);
+    float v;
+    if (intersectWedgeEXT(v, pos, v0, v1, v2, v3, v4, v5)) {
+      value = v;
+      return true;
+    }
+  }
+  return false;
+}
+
 // deviceCode.cu:36-49 (expression kept as in the reference)
 inline Ray generateRay(const RefParams &lp, const vec2f screen, Random &rnd) {
   vec3f org = lp.org;
@@ -84,6 +146,7 @@ inline Ray generateRay(const RefParams &lp, const vec2f screen, Random &rnd) {
 
 // deviceCode.cu:116-123 (non-RTCORE branch)
 inline bool sampleVolume(const RefParams &lp, vec3f pos, float &value) {
+  if (g_wedges.mode == 2) return sampleWedges(pos, value);
   for (unsigned i = 0; i < (unsigned)lp.numCells; ++i) {
     if (sample(lp.cells[i], pos, value)) return true;
   }
@@ -310,6 +373,25 @@ void ref_build_shell(const void *cellsv, int n, const int *dimsi, const float *s
           }
     }
   }
+}
+
+// ---- Volume::mode for ref_render: 0 the CPU cell scan, 2 CUBQL_MODE wedges
+void ref_set_sampler(int mode, const void *cells, int numCells) {
+  g_wedges.mode = mode;
+  if (mode == 2) buildWedgeMesh((const ICONCell *)cells, numCells);
+}
+
+int ref_intersect_wedge(const float *v24, const float *p3, float *value) {
+  const vec4f *V = (const vec4f *)v24;
+  float v = 0.f;
+  const bool hit = intersectWedgeEXT(v, vec3f(p3[0], p3[1], p3[2]), V[0], V[1], V[2], V[3], V[4], V[5]);
+  if (hit) *value = v;
+  return hit;
+}
+
+int ref_wedge_sample(const void *cells, int numCells, const float *p3, float *value) {
+  buildWedgeMesh((const ICONCell *)cells, numCells);
+  return sampleWedges(vec3f(p3[0], p3[1], p3[2]), *value);
 }
 
 // ---- GRID_ACCEL_MODE selection for ref_render (toggleAccelMode, hostCode.cu:170-199)

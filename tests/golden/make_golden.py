@@ -10,7 +10,9 @@ LaunchParams, accumIDs) and the reference outputs (accumBuffer float32 RGBA, fbP
 RGBA8, sampleVolume call counts).  kats.npz holds single-function known answers from the
 reference functions (LCG, sample, findHeight, intersectSphere, boxTest, sdda,
 linear_to_srgb/make_rgba, toSpherical/toCartesian, getBounds, resampleLUT, Camera);
-kats_grid.npz + f6_*_grid.npz the GRID_ACCEL_MODE path (dda3, buildGrid_ICON, a frame).
+kats_grid.npz + f6_*_grid.npz the GRID_ACCEL_MODE path (dda3, buildGrid_ICON, a frame);
+kats_wedge.npz + f7_*_wedge.npz the CUBQL_MODE sampler (intersectWedgeEXT, the wedge
+sampleVolume, a frame).
 The `.ic` inputs are synthetic grids from icon-ray-tracing_amd's generator (real DWD data
 is not available offline); they are stored verbatim, so the fixtures do not depend on it.
 """
@@ -43,7 +45,7 @@ SPARSE_LUT5 = np.array([[0.1, 0.2, 0.9, 0.05], [0.9, 0.9, 0.2, 0.02], [0.8, 0.1,
                        np.float32)
 
 
-def make_frame(name, spec):
+def make_frame(name, spec, mode=0):
     rn, bis, L, cap, W, H, cam, ids, raygen, tf = spec
     cells = irt.synth_grid(rn, bis, L, noise=0.1 if tf == "sparse" else 0.0)
     if cap >= 0:
@@ -91,7 +93,7 @@ def make_frame(name, spec):
     fb = np.zeros((H, W), np.uint32)
     counts = []
     p = S.params((cam12[0:3], cam12[3:6], cam12[6:9], cam12[9:12]), raygen=raygen,
-                 unit_distance=unit_c)
+                 unit_distance=unit_c, mode=mode)
     for aid in ids:
         p.accumID = aid
         _, _, c = O.ref_render(S, p, W, H, accum=accum, fb=fb, threads=1)
@@ -102,7 +104,7 @@ def make_frame(name, spec):
         lut=lut, value_range=np.array(vrange, np.float32), opacity_scale=np.float32(opacity),
         unit_distance=np.float32(unit_c), spherical_bounds=sb6, volume_bounds=vb6,
         data_range=dr, value_ranges=vr_ref, max_opacities=maxop, accum=accum, fb=fb,
-        counts=np.array(counts, np.uint64))
+        counts=np.array(counts, np.uint64), mode=mode)
     print(f"{name}: {cells.size} records {W}x{H}, hit {(accum[..., 3] > 0).mean():.3f}, "
           f"samples {counts}")
 
@@ -329,13 +331,84 @@ def make_grid_fixtures(frame=True):
           f"hit {(accum[..., 3] > 0).mean():.3f}, samples {c}")
 
 
+def make_wedge_fixtures():
+    """CUBQL_MODE (Params.h:31): intersectWedgeEXT known answers from UElems.h itself, the
+    wedge sampleVolume of deviceCode.cu:90-115 over buildCuBQLAccel's wedges (hostCode.cu:
+    557-600) at points around a scene, and one frame with volume.mode = CUBQL_MODE."""
+    R = O.rlib()
+    rng = np.random.default_rng(20261017)
+    out = {}
+    # single wedges: random prisms (general, thin/flat, and Earth-scale ICON-like)
+    nW = 600
+    V = np.zeros((nW, 6, 4), np.float32)
+    P = np.zeros((nW, 3), np.float32)
+    for k in range(nW):
+        if k < 200:
+            tri = rng.normal(size=(3, 3))
+            off = rng.normal(size=3) * 0.3 + np.array([0, 0, 1.0])
+            V[k, :3, :3] = tri
+            V[k, 3:, :3] = tri + off
+            scale = 1.0
+        else:
+            lat = rng.uniform(-1.5, 1.5) + rng.normal(size=3) * (0.02 if k < 400 else 0.2)
+            lon = rng.uniform(-3.1, 3.1) + rng.normal(size=3) * (0.02 if k < 400 else 0.2)
+            h0 = 6.371229e6 + rng.uniform(0, 7e4)
+            h1 = h0 + rng.uniform(10, 3000)
+            d = np.stack([np.cos(lat) * np.cos(lon), np.cos(lat) * np.sin(lon), np.sin(lat)], 1)
+            V[k, :3, :3] = d * h0
+            V[k, 3:, :3] = d * h1
+            scale = 0.0
+        V[k, :, 3] = rng.uniform(0, 1)
+        w = rng.dirichlet([1, 1, 1]) * 1.3 - 0.1
+        tt = rng.uniform(-0.2, 1.2)
+        P[k] = ((1 - tt) * (w @ V[k, :3, :3]) + tt * (w @ V[k, 3:, :3])).astype(np.float32)
+        del scale
+    hit = np.zeros(nW, np.int32)
+    val = np.zeros(nW, np.float32)
+    for k in range(nW):
+        v = C.c_float(0)
+        hit[k] = R.ref_intersect_wedge(V[k].ctypes.data, P[k].ctypes.data, C.byref(v))
+        val[k] = v.value
+    out.update(wedge_v=V, wedge_p=P, wedge_hit=hit, wedge_value=val)
+    # sampleVolume in CUBQL_MODE over a scene's wedges
+    cells = irt.synth_grid(2, 2, 20, noise=0.3)
+    pts = []
+    for _ in range(4000):
+        c = cells[rng.integers(cells.size)]
+        lat, lon = c["lat"].astype(np.float64), c["lon"].astype(np.float64)
+        d = np.stack([np.cos(lat) * np.cos(lon), np.cos(lat) * np.sin(lon), np.sin(lat)], 1)
+        w = rng.dirichlet([1, 1, 1]) * 1.4 - 0.13
+        r = rng.uniform(c["height"][0] - 2000, c["height"][c["numLayers"]] + 2000)
+        v = w @ d
+        pts.append((v / np.linalg.norm(v) * r).astype(np.float32))
+    pts = np.array(pts, np.float32)
+    shit = np.zeros(len(pts), np.int32)
+    sval = np.zeros(len(pts), np.float32)
+    for k in range(len(pts)):
+        v = C.c_float(0)
+        shit[k] = R.ref_wedge_sample(cells.ctypes.data, cells.size, pts[k].ctypes.data, C.byref(v))
+        sval[k] = v.value
+    out.update(scene_cells=cells.view(np.uint8).reshape(cells.size, 284), scene_points=pts,
+               scene_hit=shit, scene_value=sval)
+    np.savez_compressed(os.path.join(HERE, "kats_wedge.npz"), **out)
+    print("kats_wedge:", int(hit.sum()), "of", nW, "wedge hits;", int(shit.sum()), "of",
+          len(pts), "scene hits")
+    # one CUBQL_MODE frame
+    make_frame("f7_r2b02_l20_wedge", (2, 2, 20, -1, 64, 64, FRAMING, (0,), 0, "default"),
+               mode=2)
+
+
 if __name__ == "__main__":
     if not O.have_ref():
         sys.exit("oracle/_ref/libiconref.so missing: make -C oracle ref (needs /root/reference)")
     if len(sys.argv) > 1 and sys.argv[1] == "grid":
         make_grid_fixtures()
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "wedge":
+        make_wedge_fixtures()
+        sys.exit(0)
     for name, spec in FRAMES.items():
         make_frame(name, spec)
     make_kats()
     make_grid_fixtures()
+    make_wedge_fixtures()

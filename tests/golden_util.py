@@ -28,4 +28,4 @@ def params(S, d, accum_id):
     c = d["camera12"]
     return S.params((c[0:3], c[3:6], c[6:9], c[9:12]), accum_id=int(accum_id),
                     raygen=int(d["raygen"]), unit_distance=float(d["unit_distance"]),
-                    accel_mode=int(d.get("accel_mode", 0)))
+                    accel_mode=int(d.get("accel_mode", 0)), mode=int(d.get("mode", 0)))

@@ -12,7 +12,8 @@ def bits(a):
 
 
 def oracle_frame(cells, W, H, camera=None, accum_ids=(0,), raygen=0, lut=None, value_range=None,
-                 opacity_scale=1.0, unit_distance=None, threads=0, rect=None, accel_mode=0):
+                 opacity_scale=1.0, unit_distance=None, threads=0, rect=None, accel_mode=0,
+                 mode=0):
     """Oracle frames with the reference's main()-style setup; returns (accum, fb, stats, scene)."""
     S = O.OracleScene(cells)
     if lut is None:
@@ -25,7 +26,7 @@ def oracle_frame(cells, W, H, camera=None, accum_ids=(0,), raygen=0, lut=None, v
     stats = []
     for aid in accum_ids:
         p = S.params(cam, accum_id=aid, raygen=raygen, unit_distance=unit_distance,
-                     accel_mode=accel_mode)
+                     accel_mode=accel_mode, mode=mode)
         _, _, st = S.render(p, W, H, rect=rect, accum=accum, fb=fb, threads=threads)
         stats.append(st)
     return accum, fb, stats, S
@@ -54,16 +55,19 @@ class GpuFrame:
 
 
 def gpu_frame(cells, W, H, camera=None, accum_ids=(0,), raygen=0, lut=None, value_range=None,
-              opacity_scale=1.0, device=0, unit_distance=None, accel_mode=0):
+              opacity_scale=1.0, device=0, unit_distance=None, accel_mode=0, mode=0):
     setup = irt.setup_frame(cells, W, H, camera=camera, raygen=raygen)
     if lut is None:
         lut, value_range = setup.lut, setup.value_range
     ctx = irt.Context(cells, device)
     ctx.set_transfunc(lut, value_range, opacity_scale)
+    if mode == irt.MODE_CUBQL:
+        ctx.build_wedge_accel(cells)
     fr = GpuFrame(ctx, W, H)
     stats = []
     lp = setup.lp
     lp.accelMode = accel_mode
+    lp.mode = mode
     if unit_distance is not None:
         lp.unitDistance = unit_distance
     for aid in accum_ids:

@@ -205,6 +205,9 @@ def test_gpu_matches_reference_golden(name):
     lp.unitDistance = float(d["unit_distance"])
     lp.raygen = int(d["raygen"])
     lp.accelMode = int(d.get("accel_mode", 0))
+    lp.mode = int(d.get("mode", 0))
+    if lp.mode == irt.MODE_CUBQL:
+        ctx.build_wedge_accel(d["cells"])
     for k, aid in enumerate(d["accum_ids"]):
         lp.accumID = int(aid)
         st = fr.render(lp)

@@ -277,3 +277,81 @@ def test_binned_locator_on_terrain_following_columns():
             assert found[0] == recb and found[1] == np.float32(vb), (p, found, recb)
             n_sph += found[0] in zt
     assert n_hit > len(pts) // 3 and n_sph >= 3
+
+
+# ------------------------------------------------------------------ CUBQL_MODE wedges
+def _wedge_lib():
+    import ctypes as C
+    L = irt.lib()
+    P = C.c_void_p
+    L.irt_debug_scene_build.argtypes = [P, C.c_size_t, C.POINTER(P)]
+    L.irt_debug_scene_build_wedges.argtypes = [P, P, C.c_size_t]
+    L.irt_debug_scene_locate_wedge.argtypes = [P, irt.Vec3, C.POINTER(C.c_float)]
+    L.irt_debug_intersect_wedge.argtypes = [P, irt.Vec3, C.POINTER(C.c_float)]
+    L.irt_debug_scene_free.argtypes = [P]
+    return L
+
+
+def test_product_intersect_wedge_matches_reference_kats():
+    """The kernels' intersect_wedge (irt_common.h), host-compiled, vs UElems.h's answers."""
+    import ctypes as C
+    npz = np.load(os.path.join(os.path.dirname(__file__), "golden", "kats_wedge.npz"))
+    z = {k: npz[k] for k in npz.files}  # NpzFile re-reads on every access
+    L = _wedge_lib()
+    for k in range(len(z["wedge_p"])):
+        v = C.c_float(0)
+        V = np.ascontiguousarray(z["wedge_v"][k])
+        h = L.irt_debug_intersect_wedge(V.ctypes.data, irt.Vec3(*z["wedge_p"][k].tolist()),
+                                        C.byref(v))
+        assert h == z["wedge_hit"][k], k
+        if h:
+            assert np.float32(v.value).view(np.uint32) == z["wedge_value"][k].view(np.uint32), k
+
+
+def test_wedge_locator_matches_reference_scan():
+    """The wedge locator irt_build_wedge_accel uploads (cube map of record wedge boxes)
+    finds exactly the reference's wedge (first in index order) at the fixture points."""
+    import ctypes as C
+    npz = np.load(os.path.join(os.path.dirname(__file__), "golden", "kats_wedge.npz"))
+    z = {k: npz[k] for k in npz.files}
+    cells = np.ascontiguousarray(z["scene_cells"]).view(irt.CELL_DTYPE).ravel()
+    L = _wedge_lib()
+    h = C.c_void_p()
+    assert L.irt_debug_scene_build(cells.ctypes.data, cells.size, C.byref(h)) == 0
+    assert L.irt_debug_scene_build_wedges(h, cells.ctypes.data, cells.size) == 0
+    for k, p in enumerate(z["scene_points"]):
+        v = C.c_float(0)
+        hit = L.irt_debug_scene_locate_wedge(h, irt.Vec3(*p.tolist()), C.byref(v))
+        assert hit == z["scene_hit"][k], k
+        if hit:
+            assert np.float32(v.value).view(np.uint32) == z["scene_value"][k].view(np.uint32), k
+    L.irt_debug_scene_free(h)
+
+
+def test_wedge_locator_matches_oracle_on_coarse_and_fine_grids():
+    """Locator vs the oracle's brute-force wedge scan, incl. the 20-face icosahedron (boxes
+    spanning whole cube faces) and points outside every column."""
+    import ctypes as C
+    import oracle as O
+    L = _wedge_lib()
+    rng = np.random.default_rng(4)
+    for rn, bis, lev in ((1, 0, 4), (2, 0, 9), (2, 3, 47)):
+        cells = irt.synth_grid(rn, bis, lev, noise=0.3)
+        h = C.c_void_p()
+        assert L.irt_debug_scene_build(cells.ctypes.data, cells.size, C.byref(h)) == 0
+        assert L.irt_debug_scene_build_wedges(h, cells.ctypes.data, cells.size) == 0
+        for _ in range(400):
+            c = cells[rng.integers(cells.size)]
+            lat, lon = c["lat"].astype(np.float64), c["lon"].astype(np.float64)
+            d = np.stack([np.cos(lat) * np.cos(lon), np.cos(lat) * np.sin(lon), np.sin(lat)], 1)
+            w = rng.dirichlet([1, 1, 1]) * 1.6 - 0.2
+            r = rng.uniform(c["height"][0] - 3000, c["height"][c["numLayers"]] + 3000)
+            v = w @ d
+            p = (v / np.linalg.norm(v) * r).astype(np.float32)
+            a, b = C.c_float(0), C.c_float(0)
+            h1 = L.irt_debug_scene_locate_wedge(h, irt.Vec3(*p.tolist()), C.byref(a))
+            h2 = O.olib().oracle_wedge_sample(O._p(cells), cells.size, O.v3(p), C.byref(b))
+            assert h1 == h2
+            if h1:
+                assert np.float32(a.value).view(np.uint32) == np.float32(b.value).view(np.uint32)
+        L.irt_debug_scene_free(h)

@@ -191,3 +191,40 @@ def test_kat_grid_build_and_majorants(kats_grid):
     S.set_transfunc(d["grid_lut"], tuple(float(v) for v in d["grid_value_range"]), 1.0)
     assert np.array_equal(bits(S.grid_max_op[d["grid_pick"]]), bits(d["grid_pick_maxop"]))
     assert hashlib.sha256(S.grid_max_op.tobytes()).digest() == d["grid_maxop_sha256"].tobytes()
+
+
+# ------------------------------------------------------------------ CUBQL_MODE wedges
+@pytest.fixture(scope="module")
+def kats_wedge():
+    z = np.load(O.os.path.join(O.os.path.dirname(O.HERE), "tests", "golden", "kats_wedge.npz"))
+    d = {k: z[k] for k in z.files}
+    d["scene_cells"] = np.ascontiguousarray(d["scene_cells"]).view(O.CELL_DTYPE).ravel()
+    return d
+
+
+def test_kat_intersect_wedge(kats_wedge):
+    """intersectWedgeEXT (UElems.h:214-311): hit and interpolated value, bit for bit, for
+    unit-scale prisms and Earth-scale ICON wedges (where the float Newton often fails to
+    converge -- the reference's behaviour, kept)."""
+    d = kats_wedge
+    L = O.olib()
+    for k in range(len(d["wedge_p"])):
+        v = C.c_float(0)
+        V = np.ascontiguousarray(d["wedge_v"][k])
+        h = L.oracle_intersect_wedge(O._p(V), O.v3(d["wedge_p"][k]), C.byref(v))
+        assert h == d["wedge_hit"][k], k
+        if h:
+            assert bits([v.value])[0] == bits([d["wedge_value"][k]])[0], k
+
+
+def test_kat_wedge_sample_volume(kats_wedge):
+    """CUBQL_MODE sampleVolume (deviceCode.cu:90-115) over buildCuBQLAccel's wedges."""
+    d = kats_wedge
+    L = O.olib()
+    cells = d["scene_cells"]
+    for k in range(0, len(d["scene_points"]), 4):
+        v = C.c_float(0)
+        h = L.oracle_wedge_sample(O._p(cells), cells.size, O.v3(d["scene_points"][k]), C.byref(v))
+        assert h == d["scene_hit"][k], k
+        if h:
+            assert bits([v.value])[0] == bits([d["scene_value"][k]])[0], k
