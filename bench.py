@@ -21,7 +21,7 @@ One step:
 Frames are enqueued back to back: per-launch statistics come back through a ring, never
 stalling the host between launches.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
        torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -46,7 +46,10 @@ CONFIGS = {
     "c2": (2, 5, 47, 512, 512, "C2: R2B05 (81,920 cells) x 47 levels, 512x512"),
     "c3": (2, 7, 90, 1024, 1024, "C3: R2B07 (1,310,720 cells) x 90 levels, 1024x1024"),
     "c4": (2, 7, 90, 2048, 2048, "C4: R2B07 (1,310,720 cells) x 90 levels, 2048x2048"),
+    "c5": (2, 9, 90, 1024, 1024, "C5: R2B09 (20,971,520 cells) x 90 levels, 1024x1024, "
+                                 "60-frame orbit"),
 }
+ORBIT_FRAMES = 60  # C5: eye = 1.4e7 (sin t, 0, cos t), t = 2 pi k / 60, looking at the origin
 FRAMING = ((0.0, 0.0, 1.4e7), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0)
 
 
@@ -153,6 +156,13 @@ def main():
         f"{ctx.info.locatorFaceRes} entries={ctx.info.locatorEntries} ({time.time() - t0:.1f} s)")
 
     lp = setup.lp
+    orbit = None
+    if args.config == "c5":  # one orbit frame per step (a new view: accumID 0)
+        orbit = []
+        for k in range(ORBIT_FRAMES):
+            th = 2.0 * np.pi * k / ORBIT_FRAMES
+            orbit.append(irt.camera_look_at((1.4e7 * np.sin(th), 0.0, 1.4e7 * np.cos(th)),
+                                            (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0, W, H))
     ntiles = irt.num_tiles(W, H)
     stream = torch.cuda.current_stream(device).cuda_stream
     # frames per step: 1 on one GPU; N on N GPUs (weak scaling: N frames of the
@@ -175,6 +185,10 @@ def main():
 
     def step(s):
         lp.accumID = s * frames
+        if orbit is not None:
+            c = orbit[s % ORBIT_FRAMES]
+            lp.org, lp.dir_00, lp.dir_du, lp.dir_dv = c.org, c.dir_00, c.dir_du, c.dir_dv
+            lp.accumID = 0
         if world == 1:
             ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
             return
@@ -216,7 +230,9 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     tot, launches = ctx.stats_total()
-    log(f"[rank {rank}] timed {args.steps} steps ({launches} launches) in {elapsed:.3f} s")
+    import resource
+    log(f"[rank {rank}] timed {args.steps} steps ({launches} launches) in {elapsed:.3f} s; "
+        f"peak host RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.1f} GiB")
     samples, in_box = tot.samplesFound, tot.raysInBox
     if world > 1:
         rdev = dev if args.dist_backend == "nccl" else "cpu"
@@ -252,8 +268,12 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": desc + ", framing camera --camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60, "
-                           "woodcockTrackingWithAccel, default TF, one frame per step",
+                "workload": desc + (", orbit camera (eye 1.4e7 (sin t, 0, cos t), -fovy 60), "
+                                    "one orbit frame per step"
+                                    if orbit is not None else
+                                    ", framing camera --camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60, "
+                                    "one frame per step") +
+                           ", woodcockTrackingWithAccel, default TF",
                 "records": int(cells.size), "width": W, "height": H,
                 "parallelism": (f"{world} GPUs x 64x64 interleaved frame tiles, {frames} progressive "
                                 f"frames per step in one launch per rank, RCCL gather of the "

@@ -30,6 +30,7 @@ enum : int {
   OPT_PF = 2,         // next sample's cell header prefetched (woodcock_pf)
   OPT_ACCPF = 64,     // read the old accum value at ray start
   OPT_WEDGE = 16384,  // CUBQL_MODE sampler (locate_wedge); kept out of the default kernels
+  OPT_GRID = 8192,    // GRID_ACCEL_MODE traversal (render_grid); likewise
   OPT_STATS = 32768,  // per-wave statistics into counters[5..9] (measurement only)
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
@@ -786,9 +787,11 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
       }
     }
   }
-  if (!ae && A.accelMode == IRT_ACCEL_GRID) {
-    render_grid(A, T, ray, t0, t1, st, cr, cg, cb, alpha);
-    numRanges = 0;
+  if constexpr ((OPT & OPT_GRID) != 0) {
+    if (!ae) {
+      render_grid(A, T, ray, t0, t1, st, cr, cg, cb, alpha);
+      numRanges = 0;
+    }
   }
   const float sceneEPS = A.sbLo.x * 1e-6f;
   for (int i = 0; i < numRanges; ++i) {
@@ -999,11 +1002,19 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
     // progressive batch (one frame per grid row, then the lerp chain), the grid accel or
     // the wedge sampler: the one-kernel raygen
     constexpr int M = (N & OPT_MONO) != 0 ? K : (kDefaultVariant & ~OPT_MONO);
-    if (A.sampler == IRT_MODE_CUBQL)
-      hipLaunchKernelGGL(k_render<(kDefaultVariant & ~OPT_MONO) | OPT_WEDGE>,
-                         dim3(numBlocks, A.numSamples), dim3(256), 0, s, A, 0);
+    constexpr int D = kDefaultVariant & ~OPT_MONO;
+    const dim3 grid(numBlocks, A.numSamples);
+    const bool g = A.accelMode == IRT_ACCEL_GRID;
+    // the wedge kernels hold a 6-vertex Newton state: no waves-per-SIMD floor (no spills)
+    constexpr int DW = (D & ~0xF00) | OPT_WEDGE;
+    if (A.sampler == IRT_MODE_CUBQL && g)
+      hipLaunchKernelGGL(k_render<DW | OPT_GRID>, grid, dim3(256), 0, s, A, 0);
+    else if (A.sampler == IRT_MODE_CUBQL)
+      hipLaunchKernelGGL(k_render<DW>, grid, dim3(256), 0, s, A, 0);
+    else if (g)
+      hipLaunchKernelGGL(k_render<D | OPT_GRID>, grid, dim3(256), 0, s, A, 0);
     else
-      hipLaunchKernelGGL(k_render<M>, dim3(numBlocks, A.numSamples), dim3(256), 0, s, A, 0);
+      hipLaunchKernelGGL(k_render<M>, grid, dim3(256), 0, s, A, 0);
     if (A.numSamples > 1) hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);
     return;
   }
