@@ -273,7 +273,7 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads)
   double scale = 1.5;
   if (const char *e = getenv("IRT_LOCATOR_SCALE")) scale = atof(e);
   int G = (int)llround(sqrt((double)std::max<size_t>(numRuns, 1) / 6.0) * scale);
-  G = std::max(4, std::min(G, 2048));
+  G = std::max(4, std::min(G, 4096));
   if (const char *e = getenv("IRT_LOCATOR_G")) G = std::max(1, std::min(4096, atoi(e)));
   S.G = G;
   const uint32_t numGridCells = 6u * G * G;
@@ -785,7 +785,7 @@ int build_wedges(const irt_icon_cell *cells, size_t n, WedgeScene &W, int thread
   for (size_t i = 0; i < n; ++i)
     if (i == 0 || !same_column(cells[i], cells[i - 1])) ++numRuns;
   int G = (int)llround(sqrt((double)std::max<size_t>(numRuns, 1) / 6.0) * 1.5);
-  G = std::max(4, std::min(G, 2048));
+  G = std::max(4, std::min(G, 4096));
   W.G = G;
   const uint32_t numGridCells = 6u * G * G;
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> parts(threads);

@@ -566,7 +566,29 @@ struct Scene {
   std::vector<CellPlanes> planes;  // fast mode only
   std::vector<Wedge> wedges;       // CUBQL_MODE only
   bool useWedges = false;
+  std::vector<float> rr;           // fast mode: {height[0], height[numLayers]} per record
 };
+
+// Fast mode's per-record tables (the same tests in the same order, read from compact
+// arrays), built on nthreads threads.
+void buildFast(Scene &S, int nthreads) {
+  S.planes.resize(S.n);
+  S.rr.resize(2 * S.n);
+  if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
+  if (nthreads <= 0) nthreads = 1;
+  const size_t chunk = (S.n + nthreads - 1) / nthreads;
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nthreads; ++t)
+    ts.emplace_back([&S, t, chunk] {
+      const size_t b = t * chunk, e = std::min(S.n, b + chunk);
+      for (size_t i = b; i < e; ++i) {
+        S.planes[i] = cellPlanes(S.cells[i]);
+        S.rr[2 * i] = S.cells[i].height[0];
+        S.rr[2 * i + 1] = S.cells[i].height[S.cells[i].numLayers];
+      }
+    });
+  for (auto &th : ts) th.join();
+}
 
 struct ThreadStats {
   uint64_t launched = 0, inBox = 0, locate = 0, found = 0, draws = 0, leaves = 0;
@@ -580,8 +602,11 @@ inline bool sampleVolume(const Scene &S, V3 pos, float &value) {
     return false;
   }
   if (S.fast) {
-    for (size_t i = 0; i < S.n; ++i)
+    const float r = length(pos);
+    for (size_t i = 0; i < S.n; ++i) {
+      if (r < S.rr[2 * i] || r > S.rr[2 * i + 1]) continue;  // sampleFast's first test
       if (sampleFast(S.cells[i], S.planes[i], pos, value)) return true;
+    }
   } else {
     for (size_t i = 0; i < S.n; ++i)
       if (sampleLiteral(S.cells[i], pos, value)) return true;
@@ -857,9 +882,16 @@ void oracle_build_shell(const oc_cell *cells, size_t n, const int32_t dims[3],
     valueRanges[2 * i + 1] = -FLT_MAX;
   }
   const B3 sb = toB3(sphericalBounds);
-  // buildShell_ICON (hostCode.cu:299-336); float atomicMin/Max (36-56) only
-  // store when strictly smaller/larger.
-  for (size_t ci = 0; ci < n; ++ci) {
+  // buildShell_ICON (hostCode.cu:299-336); float atomicMin/Max (36-56) only store when
+  // strictly smaller/larger -- an order-independent min/max (up to the sign of a zero,
+  // which depends on atomic arrival order in the reference too), so cells are split over
+  // threads with private grids, merged the same way.
+  int nthreads = (int)std::thread::hardware_concurrency();
+  if (nthreads <= 0) nthreads = 1;
+  if (n < 100000) nthreads = 1;
+  std::vector<std::vector<float>> priv(nthreads - 1);
+  auto rasterize = [&](size_t c0, size_t c1, float *vrBase) {
+  for (size_t ci = c0; ci < c1; ++ci) {
     const oc_cell &cell = cells[ci];
     for (int i = 0; i < cell.numLayers; ++i) {
       I3 c1 = projectToSphericalGrid({cell.height[i], cell.lat[0], cell.lon[0]}, d, sb);
@@ -877,12 +909,31 @@ void oracle_build_shell(const oc_cell *cells, size_t n, const int32_t dims[3],
         for (int mcy = lo.y; mcy <= up.y; ++mcy)
           for (int mcx = lo.x; mcx <= up.x; ++mcx) {
             size_t id = linearIndex({mcx, mcy, mcz}, d);
-            float *vr = valueRanges + 2 * id;
+            float *vr = vrBase + 2 * id;
             if (range.lower < vr[0]) vr[0] = range.lower;
             if (range.upper > vr[1]) vr[1] = range.upper;
           }
     }
   }
+  };
+  const size_t chunk = (n + nthreads - 1) / nthreads;
+  std::vector<std::thread> ts;
+  for (int t = 1; t < nthreads; ++t) {
+    priv[t - 1].resize(2 * numMCs);
+    float *p = priv[t - 1].data();
+    for (size_t i = 0; i < numMCs; ++i) {
+      p[2 * i] = FLT_MAX;
+      p[2 * i + 1] = -FLT_MAX;
+    }
+    ts.emplace_back(rasterize, std::min(n, t * chunk), std::min(n, (t + 1) * chunk), p);
+  }
+  rasterize(0, std::min(n, chunk), valueRanges);
+  for (auto &th : ts) th.join();
+  for (auto &p : priv)
+    for (size_t i = 0; i < numMCs; ++i) {
+      if (p[2 * i] < valueRanges[2 * i]) valueRanges[2 * i] = p[2 * i];
+      if (p[2 * i + 1] > valueRanges[2 * i + 1]) valueRanges[2 * i + 1] = p[2 * i + 1];
+    }
 }
 
 void oracle_build_grid(const oc_cell *cells, size_t n, const int32_t dims[3], oc_box3 worldBounds,
@@ -969,11 +1020,8 @@ int oracle_render(const oc_cell *cells, size_t n, const oc_params *p, int W, int
                   oc_stats *stats) {
   if (!p || W <= 0 || H <= 0 || x0 < 0 || y0 < 0 || x1 > W || y1 > H) return -1;
   if (x1 <= x0 || y1 <= y0) return 0;
-  Scene S{cells, n, fast != 0, {}, {}, false};
-  if (S.fast) {
-    S.planes.resize(n);
-    for (size_t i = 0; i < n; ++i) S.planes[i] = cellPlanes(cells[i]);
-  }
+  Scene S{cells, n, fast != 0, {}, {}, false, {}};
+  if (S.fast) buildFast(S, nthreads);
   if (p->mode == 2) {
     S.useWedges = true;
     buildWedges(cells, n, S.wedges);
@@ -1022,11 +1070,8 @@ int oracle_render_pixels(const oc_cell *cells, size_t n, const oc_params *p, int
   if (!p || W <= 0 || H <= 0 || numPixels < 0) return -1;
   for (int i = 0; i < numPixels; ++i)
     if (xy[2 * i] < 0 || xy[2 * i] >= W || xy[2 * i + 1] < 0 || xy[2 * i + 1] >= H) return -1;
-  Scene S{cells, n, fast != 0, {}, {}, false};
-  if (S.fast) {
-    S.planes.resize(n);
-    for (size_t i = 0; i < n; ++i) S.planes[i] = cellPlanes(cells[i]);
-  }
+  Scene S{cells, n, fast != 0, {}, {}, false, {}};
+  if (S.fast) buildFast(S, nthreads);
   if (p->mode == 2) {
     S.useWedges = true;
     buildWedges(cells, n, S.wedges);
@@ -1130,7 +1175,7 @@ int oracle_intersect_wedge(const float *v24, oc_vec3 p, float *value) {
 }
 
 int oracle_wedge_sample(const oc_cell *cells, size_t n, oc_vec3 p, float *value) {
-  Scene S{cells, n, false, {}, {}, true};
+  Scene S{cells, n, false, {}, {}, true, {}};
   buildWedges(cells, n, S.wedges);
   return sampleVolume(S, toV3(p), *value);
 }
