@@ -107,7 +107,7 @@ def profiled_traffic(kernel, records, width):
         b = s.get("bench") or {}
         if not any(k.endswith(kernel) for k in s.get("kernels", {})):
             continue
-        if s.get("records") not in (None, records) or s.get("width") not in (None, width):
+        if s.get("records") != records or s.get("width") != width:
             continue
         if "traffic_bytes_per_launch_fetch_x2" in s and b:
             best = (s["traffic_bytes_per_launch_fetch_x2"], os.path.relpath(p, ROOT))
