@@ -26,6 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--config", default="c3")
+    ap.add_argument("--cases", default="away,empty,dense,default,viewall")
     args = ap.parse_args()
     import torch
     import irt
@@ -44,6 +45,8 @@ def main():
         "viewall": (irt.setup_frame(cells, W, W).lp, lut0),
     }
     for name, (lp, lut) in cases.items():
+        if name not in args.cases.split(","):
+            continue
         ctx.set_transfunc(np.ascontiguousarray(lut, np.float32), base.value_range)
         ms = []
         for _ in range(args.frames):
