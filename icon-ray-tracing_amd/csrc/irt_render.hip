@@ -28,7 +28,6 @@ namespace irt {
 enum : int {
   OPT_BATCH = 1,      // two fat entries per round trip
   OPT_PF = 2,         // next sample's cell header prefetched (woodcock_pf)
-  OPT_ACCPF = 64,     // read the old accum value at ray start
   OPT_WEDGE = 16384,  // CUBQL_MODE sampler (locate_wedge); kept out of the default kernels
   OPT_GRID = 8192,    // GRID_ACCEL_MODE traversal (render_grid); likewise
   OPT_STATS = 32768,  // per-wave statistics into counters[5..9] (measurement only)
