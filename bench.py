@@ -59,9 +59,12 @@ def log(*a):
 
 def cpu_baseline(cells, setup, W, H, budget_s=15.0):
     """The reference's CPU path (brute-force sampleVolume, deviceCode.cu:116-123) on the
-    host cores, on a bounded strided sample of the same frame's pixels."""
+    host cores, on a bounded strided sample of the same frame's pixels: the reference's own
+    raygen compiled from /root/reference headers (oracle/_ref, built by __graft_entry__.build)
+    when present ("reference"), else the oracle's restatement ("port")."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
+    use_ref = O.have_ref()
     threads = max(1, min(16, os.cpu_count() or 1))
     S = O.OracleScene(cells)
     S.set_transfunc(setup.lut, setup.value_range, setup.opacity_scale)
@@ -76,7 +79,12 @@ def cpu_baseline(cells, setup, W, H, budget_s=15.0):
         ys, xs = np.mgrid[stride // 2:H:stride, stride // 2:W:stride]
         xy = np.stack([xs.ravel(), ys.ravel()], axis=1).astype(np.int32)
         t = time.perf_counter()
-        _, _, st = S.render_pixels(params, W, H, xy, threads=threads, fast=False)
+        if use_ref:
+            _, _, cnt = O.ref_render_pixels(S, params, W, H, xy, threads=threads)
+            locate = int(cnt[0])
+        else:
+            _, _, st = S.render_pixels(params, W, H, xy, threads=threads, fast=False)
+            locate = st.locate_calls
         elapsed = time.perf_counter() - t
         pix = xy.shape[0]
         log(f"[cpu baseline] stride {stride}: {pix} rays in {elapsed:.2f} s")
@@ -85,11 +93,13 @@ def cpu_baseline(cells, setup, W, H, budget_s=15.0):
         stride //= 2
     mray = pix / elapsed / 1e6
     sample = (f"every {stride}th pixel in x and y of the {W}x{H} frame ({pix} rays, "
-              f"{st.locate_calls} sampleVolume calls, {elapsed:.1f} s on {threads} threads): "
+              f"{locate} sampleVolume calls, {elapsed:.1f} s on {threads} threads): "
               f"the reference's CPU raygen with its brute-force first-hit cell scan over "
-              f"{cells.size} records (deviceCode.cu:116-123), oracle restatement, literal "
-              f"sample() incl. toSpherical")
-    kind = "port"
+              f"{cells.size} records (deviceCode.cu:116-123), " +
+              ("compiled from the reference's own headers (oracle/_ref: ICONGrid.h sample(), "
+               "ShellAccel.h sdda, vecmath), one host thread per pixel chunk"
+               if use_ref else "oracle restatement, literal sample() incl. toSpherical"))
+    kind = "reference" if use_ref else "port"
     return {"value": mray, "unit": "Mray/s", "cores": threads, "kind": kind, "sample": sample,
             "ms_per_frame_extrapolated": W * H / (mray * 1e6) * 1e3}
 

@@ -123,6 +123,8 @@ def rlib() -> C.CDLL:
         P, I, F = C.c_void_p, C.c_int, C.c_float
         L.ref_render.argtypes = [P, I, P, I, P, F, I, P, P, P, P, P, P, I, I, I, I, I, I, I, P, P,
                                  I, P]
+        L.ref_render_pixels.argtypes = [P, I, P, I, P, F, I, P, P, P, P, P, P, I, I, I, P, I,
+                                        P, P, P]
         L.ref_compute_bounds.argtypes = [P, I, P, P, P]
         L.ref_build_shell.argtypes = [P, I, P, P, P]
         L.ref_max_opacities.argtypes = [P, C.c_long, P, I, F, F, P]
@@ -325,3 +327,43 @@ def ref_render(scene: OracleScene, params: OParams, width, height, rect=None, ac
                  _p(scene.max_op), _p(tf3), _p(scene.lut), scene.lut.shape[0], width, height,
                  x0, y0, x1, y1, _p(accum), _p(fb), threads, _p(counters))
     return accum, fb, counters
+
+
+def ref_render_pixels(scene: OracleScene, params: OParams, width, height, xy: np.ndarray,
+                      threads=1):
+    """The reference's own raygen (oracle/_ref, compiled from /root/reference headers) over
+    a pixel list, split over `threads` host threads (ctypes releases the GIL); returns
+    (accum, fb, [sampleVolume calls, found])."""
+    import threading
+    R = rlib()
+    xy = np.ascontiguousarray(xy, dtype=np.int32).reshape(-1, 2)
+    accum = np.zeros((height, width, 4), dtype=np.float32)
+    fb = np.zeros((height, width), dtype=np.uint32)
+    cam = np.array([params.org.x, params.org.y, params.org.z, params.dir_00.x, params.dir_00.y,
+                    params.dir_00.z, params.dir_du.x, params.dir_du.y, params.dir_du.z,
+                    params.dir_dv.x, params.dir_dv.y, params.dir_dv.z], dtype=np.float32)
+    amb = np.array([1, 1, 1, 1], dtype=np.float32)
+    bounds6 = np.array([scene.vb.lower.x, scene.vb.lower.y, scene.vb.lower.z, scene.vb.upper.x,
+                        scene.vb.upper.y, scene.vb.upper.z], dtype=np.float32)
+    sb6 = np.array([scene.sb.lower.x, scene.sb.lower.y, scene.sb.lower.z, scene.sb.upper.x,
+                    scene.sb.upper.y, scene.sb.upper.z], dtype=np.float32)
+    tf3 = np.array([params.tf_lower, params.tf_upper, params.opacityScale], dtype=np.float32)
+    R.ref_set_accel(0, None, None, None)
+    R.ref_set_sampler(0, None, 0)
+    chunks = np.array_split(np.arange(xy.shape[0]), max(1, threads))
+    counts = np.zeros((len(chunks), 2), dtype=np.uint64)
+    parts = [np.ascontiguousarray(xy[c]) for c in chunks]
+
+    def run(k):
+        R.ref_render_pixels(_p(scene.cells), scene.cells.size, _p(cam), params.accumID, _p(amb),
+                            params.unitDistance, params.raygen, _p(bounds6), _p(scene.dims),
+                            _p(sb6), _p(scene.max_op), _p(tf3), _p(scene.lut),
+                            scene.lut.shape[0], width, height, _p(parts[k]), parts[k].shape[0],
+                            _p(accum), _p(fb), _p(counts[k]))
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(len(chunks))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return accum, fb, counts.sum(axis=0)

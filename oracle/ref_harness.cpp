@@ -251,6 +251,11 @@ inline void fmax_store(float *a, float v) { if (v > *a) *a = v; }
 
 extern "C" {
 
+static RefParams make_params(const void *cells, int numCells, const float *camera12, int accumID,
+                      const float *ambient4, float unitDistance, int raygenKind,
+                      const float *bounds6, const int *dims, const float *sphericalBounds6,
+                      const float *maxOpacities, const float *tf3, const float *lut, int lutSize);
+
 // ---- full frame on the reference's CPU parallel_for (64x64 tiles, thread_pool)
 int ref_render(const void *cells, int numCells, const float *camera12, int accumID,
                const float *ambient4, float unitDistance, int raygenKind,
@@ -258,31 +263,9 @@ int ref_render(const void *cells, int numCells, const float *camera12, int accum
                const float *maxOpacities, const float *tf3, const float *lut, int lutSize,
                int W, int H, int x0, int y0, int x1, int y1, float *accum, uint32_t *fb,
                int nthreads, unsigned long long *counters2) {
-  RefParams lp;
-  lp.org = vec3f(camera12[0], camera12[1], camera12[2]);
-  lp.dir_00 = vec3f(camera12[3], camera12[4], camera12[5]);
-  lp.dir_du = vec3f(camera12[6], camera12[7], camera12[8]);
-  lp.dir_dv = vec3f(camera12[9], camera12[10], camera12[11]);
-  lp.accumID = accumID;
-  lp.ambientColor = vec3f(ambient4[0], ambient4[1], ambient4[2]);
-  lp.ambientRadiance = ambient4[3];
-  lp.unitDistance = unitDistance;
-  lp.raygen = raygenKind;
-  lp.bounds = box3f(vec3f(bounds6[0], bounds6[1], bounds6[2]),
-                    vec3f(bounds6[3], bounds6[4], bounds6[5]));
-  lp.accel.dims = vec3i(dims[0], dims[1], dims[2]);
-  lp.accel.sphericalBounds =
-      box3f(vec3f(sphericalBounds6[0], sphericalBounds6[1], sphericalBounds6[2]),
-            vec3f(sphericalBounds6[3], sphericalBounds6[4], sphericalBounds6[5]));
-  lp.accel.valueRanges = nullptr;
-  lp.accel.maxOpacities = const_cast<float *>(maxOpacities);
-  lp.tfRange = box1f(tf3[0], tf3[1]);
-  lp.opacityScale = tf3[2];
-  lp.lut = (const vec4f *)lut;
-  lp.lutSize = lutSize;
-  lp.cells = (const ICONCell *)cells;
-  lp.numCells = numCells;
-
+  const RefParams lp = make_params(cells, numCells, camera12, accumID, ambient4, unitDistance,
+                                   raygenKind, bounds6, dims, sphericalBounds6, maxOpacities,
+                                   tf3, lut, lutSize);
   if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
   std::mutex mtx;
   Counters total;
@@ -308,6 +291,57 @@ int ref_render(const void *cells, int numCells, const float *camera12, int accum
     counters2[1] = total.found;
   }
   return 0;
+}
+
+// ---- the reference raygen over an explicit pixel list, serially (the caller may run
+// several calls on disjoint pixel lists concurrently: each only reads the scene)
+int ref_render_pixels(const void *cells, int numCells, const float *camera12, int accumID,
+                      const float *ambient4, float unitDistance, int raygenKind,
+                      const float *bounds6, const int *dims, const float *sphericalBounds6,
+                      const float *maxOpacities, const float *tf3, const float *lut, int lutSize,
+                      int W, int H, const int *xy, int numPixels, float *accum, uint32_t *fb,
+                      unsigned long long *counters2) {
+  const RefParams lp = make_params(cells, numCells, camera12, accumID, ambient4, unitDistance,
+                                   raygenKind, bounds6, dims, sphericalBounds6, maxOpacities,
+                                   tf3, lut, lutSize);
+  Counters total;
+  for (int i = 0; i < numPixels; ++i) raygen(lp, xy[2 * i], xy[2 * i + 1], W, H, (vec4f *)accum, fb, total);
+  if (counters2) {
+    counters2[0] = total.locate;
+    counters2[1] = total.found;
+  }
+  return 0;
+}
+
+static RefParams make_params(const void *cells, int numCells, const float *camera12, int accumID,
+                      const float *ambient4, float unitDistance, int raygenKind,
+                      const float *bounds6, const int *dims, const float *sphericalBounds6,
+                      const float *maxOpacities, const float *tf3, const float *lut, int lutSize) {
+  RefParams lp;
+  lp.org = vec3f(camera12[0], camera12[1], camera12[2]);
+  lp.dir_00 = vec3f(camera12[3], camera12[4], camera12[5]);
+  lp.dir_du = vec3f(camera12[6], camera12[7], camera12[8]);
+  lp.dir_dv = vec3f(camera12[9], camera12[10], camera12[11]);
+  lp.accumID = accumID;
+  lp.ambientColor = vec3f(ambient4[0], ambient4[1], ambient4[2]);
+  lp.ambientRadiance = ambient4[3];
+  lp.unitDistance = unitDistance;
+  lp.raygen = raygenKind;
+  lp.bounds = box3f(vec3f(bounds6[0], bounds6[1], bounds6[2]),
+                    vec3f(bounds6[3], bounds6[4], bounds6[5]));
+  lp.accel.dims = vec3i(dims[0], dims[1], dims[2]);
+  lp.accel.sphericalBounds =
+      box3f(vec3f(sphericalBounds6[0], sphericalBounds6[1], sphericalBounds6[2]),
+            vec3f(sphericalBounds6[3], sphericalBounds6[4], sphericalBounds6[5]));
+  lp.accel.valueRanges = nullptr;
+  lp.accel.maxOpacities = const_cast<float *>(maxOpacities);
+  lp.tfRange = box1f(tf3[0], tf3[1]);
+  lp.opacityScale = tf3[2];
+  lp.lut = (const vec4f *)lut;
+  lp.lutSize = lutSize;
+  lp.cells = (const ICONCell *)cells;
+  lp.numCells = numCells;
+  return lp;
 }
 
 // ---- host setup restated from hostCode.cu:792-808 with the reference's types

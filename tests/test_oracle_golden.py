@@ -228,3 +228,22 @@ def test_kat_wedge_sample_volume(kats_wedge):
         assert h == d["scene_hit"][k], k
         if h:
             assert bits([v.value])[0] == bits([d["scene_value"][k]])[0], k
+
+
+@pytest.mark.skipif(not O.have_ref(), reason="oracle/_ref not built (needs /root/reference)")
+def test_reference_pixel_list_render_matches_oracle():
+    """bench.py's CPU baseline runs the reference's own raygen (oracle/_ref) over a strided
+    pixel list on several threads; it must equal the oracle pixel for pixel."""
+    import irt
+    cells = irt.synth_grid(2, 2, 30)
+    S = O.OracleScene(cells)
+    lut, vr = S.default_lut()
+    S.set_transfunc(lut, vr)
+    W = 64
+    p = S.params(S.camera(W, W, irt.FRAMING_CAMERA))
+    ys, xs = np.mgrid[0:W:3, 1:W:3]
+    xy = np.stack([xs.ravel(), ys.ravel()], 1).astype(np.int32)
+    a1, f1, cnt = O.ref_render_pixels(S, p, W, W, xy, threads=4)
+    a2, f2, st = S.render_pixels(p, W, W, xy, threads=4, fast=False)
+    assert np.array_equal(bits(a1), bits(a2)) and np.array_equal(f1, f2)
+    assert int(cnt[0]) == st.locate_calls and int(cnt[1]) == st.samples_found
