@@ -73,7 +73,7 @@ def cpu_baseline(cells, setup, W, H, budget_s=15.0):
            np.array(lp.dir_du.tolist(), np.float32), np.array(lp.dir_dv.tolist(), np.float32))
     params = S.params(cam, accum_id=0, raygen=lp.raygen, unit_distance=lp.unitDistance)
     # An unbiased bounded sample: a regular sub-grid of the frame's pixels, refined until
-    # the run takes about budget_s/4 .. budget_s of CPU time.
+    # the run takes about budget_s/2 .. 2 budget_s of CPU time.
     stride, elapsed, pix, st = 128, 0.0, 0, None
     while True:
         ys, xs = np.mgrid[stride // 2:H:stride, stride // 2:W:stride]
@@ -88,7 +88,7 @@ def cpu_baseline(cells, setup, W, H, budget_s=15.0):
         elapsed = time.perf_counter() - t
         pix = xy.shape[0]
         log(f"[cpu baseline] stride {stride}: {pix} rays in {elapsed:.2f} s")
-        if elapsed > budget_s / 4 or stride <= 8:
+        if elapsed > budget_s / 2 or stride <= 8:
             break
         stride //= 2
     mray = pix / elapsed / 1e6
