@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <vector>
 
@@ -77,6 +78,22 @@ struct irt_context {
   long long totalLaunches = 0;
   size_t bytes = 0;
   int variant = kDefaultVariant;  // render-kernel variant (irt_render.hip OPT_* bits)
+  // Measured-cost workgroup scheduling of the one-kernel raygen: every launch records its
+  // workgroups' durations (d_schedCost); now and then a launch copies them back
+  // (h_schedCost, pinned, in the stats ring), and once that copy has landed the host
+  // orders the frame tiles by descending cost (longest-processing-time first) and uploads
+  // the order (d_schedOrder) for later launches with the same grid.
+  uint32_t *d_schedOrder = nullptr, *d_schedCost = nullptr;  // 2 x cap (ping-pong), cap
+  uint32_t *h_schedCost = nullptr, *h_schedOrder = nullptr;  // pinned: kSlots x cap, 2 x cap
+  int schedBuf = 0;             // the order buffer launches read now
+  long long schedSwitch = 0;    // first launch reading it
+  size_t schedCap = 0;
+  bool schedOn = true;         // IRT_SCHED=0 disables
+  bool schedOrderValid = false;
+  long long schedKey[8] = {};
+  long long schedSrc = -1;      // launch whose costs the current order came from
+  long long schedCopied[kSlots] = {};  // launch index whose costs slot i holds (-1: none)
+  long long schedLastCopy = -1000;
 };
 
 namespace {
@@ -102,11 +119,13 @@ void free_all(irt_context *c) {
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
-                  c->d_sphBits, c->d_queue, c->d_contList, c->d_segCount, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_srgb, c->d_valueRanges,
+                  c->d_sphBits, c->d_queue, c->d_contList, c->d_segCount, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
                   c->d_lut, c->d_counters};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
+  if (c->h_schedCost) (void)hipHostFree(c->h_schedCost);
+  if (c->h_schedOrder) (void)hipHostFree(c->h_schedOrder);
   for (int i = 0; i < irt_context::kSlots; ++i) {
     if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
@@ -148,6 +167,78 @@ int finish_stats(irt_context *c) {
     int rc = finish_slot(c, (int)(j % irt_context::kSlots));
     if (rc) return rc;
   }
+  return IRT_OK;
+}
+
+// Measured-cost scheduling, host side (see irt_context::d_schedOrder): (re)allocate for
+// the grid, drop the order when the grid changes, and rebuild it from the newest landed
+// cost copy of a launch with the same grid.
+int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int tileBegin,
+                  int tileStride, int numTiles, const irt_launch_params *lp, hipStream_t s) {
+  if ((size_t)numBlocks > c->schedCap) {
+    IRT_HIP(hipStreamSynchronize(s));
+    if (c->d_schedOrder) IRT_HIP(hipFree(c->d_schedOrder));
+    if (c->d_schedCost) IRT_HIP(hipFree(c->d_schedCost));
+    if (c->h_schedCost) IRT_HIP(hipHostFree(c->h_schedCost));
+    if (c->h_schedOrder) IRT_HIP(hipHostFree(c->h_schedOrder));
+    c->d_schedOrder = c->d_schedCost = c->h_schedCost = c->h_schedOrder = nullptr;
+    c->bytes -= 3 * c->schedCap * sizeof(uint32_t);
+    c->schedCap = 0;
+    int rc;
+    if ((rc = dalloc(c, &c->d_schedOrder, 2 * (size_t)numBlocks)) ||
+        (rc = dalloc(c, &c->d_schedCost, numBlocks)))
+      return rc;
+    IRT_HIP(hipHostMalloc((void **)&c->h_schedCost, (size_t)irt_context::kSlots * numBlocks * sizeof(uint32_t)));
+    IRT_HIP(hipHostMalloc((void **)&c->h_schedOrder, 2 * (size_t)numBlocks * sizeof(uint32_t)));
+    c->schedCap = numBlocks;
+    c->schedOrderValid = false;
+    for (auto &v : c->schedCopied) v = -1;
+    c->info.deviceBytes = c->bytes;
+  }
+  const long long key[8] = {numBlocks, W, H, packed, tileBegin, tileStride, numTiles,
+                            lp->accelMode * 4 + lp->mode};
+  if (memcmp(key, c->schedKey, sizeof(key)) != 0) {
+    memcpy(c->schedKey, key, sizeof(key));
+    c->schedOrderValid = false;
+    c->schedSrc = c->launches;  // costs of launches before this one belong to another grid
+    for (auto &v : c->schedCopied) v = -1;
+  }
+  // the newest cost copy that has landed -- from a launch no older than the first reader
+  // of the current order buffer, so every launch reading the other buffer has finished and
+  // it (and its pinned staging copy) may be rewritten without a stall
+  long long best = -1;
+  int bestSlot = -1;
+  for (int i = 0; i < irt_context::kSlots; ++i)
+    if (c->schedCopied[i] > c->schedSrc && c->schedCopied[i] >= c->schedSwitch &&
+        c->schedCopied[i] > best && hipEventQuery(c->evDone[i]) == hipSuccess) {
+      best = c->schedCopied[i];
+      bestSlot = i;
+    }
+  if (bestSlot < 0) return IRT_OK;
+  // longest-processing-time first over whole 64x64 tiles (16 consecutive workgroups, kept
+  // together for the locator's cache locality)
+  const uint32_t *cost = c->h_schedCost + (size_t)bestSlot * c->schedCap;
+  const int nt = numBlocks / 16;
+  std::vector<std::pair<uint64_t, int>> tiles(nt);
+  for (int t = 0; t < nt; ++t) {
+    uint64_t sum = 0;
+    for (int j = 0; j < 16; ++j) sum += cost[16 * t + j];
+    tiles[t] = {sum, t};
+  }
+  std::stable_sort(tiles.begin(), tiles.end(),
+                   [](const std::pair<uint64_t, int> &a, const std::pair<uint64_t, int> &b) {
+                     return a.first > b.first;
+                   });
+  const int nb = c->schedOrderValid ? 1 - c->schedBuf : c->schedBuf;
+  uint32_t *h = c->h_schedOrder + (size_t)nb * c->schedCap;
+  for (int p = 0; p < nt; ++p)
+    for (int j = 0; j < 16; ++j) h[16 * p + j] = (uint32_t)(16 * tiles[p].second + j);
+  IRT_HIP(hipMemcpyAsync(c->d_schedOrder + (size_t)nb * c->schedCap, h,
+                         (size_t)numBlocks * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  c->schedBuf = nb;
+  c->schedSwitch = c->launches;
+  c->schedOrderValid = true;
+  c->schedSrc = best;
   return IRT_OK;
 }
 
@@ -283,6 +374,21 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     }
   }
   A.sampleBuf = c->d_samples;
+  // measured-cost scheduling: single-frame launches of the one-kernel raygen only
+  A.schedOrder = nullptr;
+  A.schedCost = nullptr;
+  const int numBlocks = numTiles * 16;
+  const bool mono = (c->variant & 4096) != 0 || lp->accelMode != IRT_ACCEL_SPHERE ||
+                    lp->mode != IRT_MODE_USER_GEOM;
+  bool copyCosts = false;
+  if (c->schedOn && mono && numFrames == 1 && numBlocks > 0) {
+    int rc = sched_prepare(c, numBlocks, W, H, packed, tileBegin, tileStride, numTiles, lp, s);
+    if (rc) return rc;
+    A.schedOrder = c->schedOrderValid ? c->d_schedOrder + (size_t)c->schedBuf * c->schedCap : nullptr;
+    A.schedCost = c->d_schedCost;
+    // copy the costs back every 8th launch (a 4*numBlocks-byte D2H on the stream)
+    copyCosts = c->launches - c->schedLastCopy >= 8;
+  }
   IRT_HIP(hipMemsetAsync(A.counters, 0, 16 * sizeof(unsigned long long), s));
   IRT_HIP(hipEventRecord(c->ev0[slot], s));
   if (numTiles > 0) {
@@ -292,6 +398,13 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   IRT_HIP(hipEventRecord(c->ev1[slot], s));
   IRT_HIP(hipMemcpyAsync(c->h_counters + 16 * slot, A.counters, 16 * sizeof(unsigned long long),
                          hipMemcpyDeviceToHost, s));
+  c->schedCopied[slot] = -1;
+  if (copyCosts) {
+    IRT_HIP(hipMemcpyAsync(c->h_schedCost + (size_t)slot * c->schedCap, c->d_schedCost,
+                           (size_t)numBlocks * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    c->schedCopied[slot] = c->launches;
+    c->schedLastCopy = c->launches;
+  }
   IRT_HIP(hipEventRecord(c->evDone[slot], s));
   c->pending[slot] = true;
   ++c->launches;
@@ -338,6 +451,7 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
     set_error("irt_create: cannot initialise device %d", device);
     return fail(IRT_E_HIP);
   }
+  if (const char *e = getenv("IRT_SCHED")) c->schedOn = atoi(e) != 0;
   c->info = S.info;
   c->n = (uint32_t)S.n;
   c->G = S.G;

@@ -66,6 +66,10 @@ struct RenderArgs {
   // progressive batch (irt_render_accumulate): frames accumID .. accumID+numSamples-1;
   // for numSamples > 1 each frame's colour goes to sampleBuf[frame][lane] first
   int numSamples;
+  // measured-cost workgroup scheduling of the one-kernel raygen (irt_context.hip): the
+  // block order to render (null: identity) and this launch's per-block durations
+  const uint32_t *schedOrder;
+  uint32_t *schedCost;
   float4 *sampleBuf;    // rays per 256-slot queue segment (one per setup workgroup)
   uint32_t *contList;
 };

@@ -924,6 +924,7 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   if (tid < 8) s_cnt[tid] = 0;
   __syncthreads();
   Tracer<OPT> T{A, s_logf, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
+  const uint64_t c0 = A.schedCost ? wall_clock64() : 0;
   if (listMode) {
     for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
       const uint32_t j = base + (uint32_t)tid;
@@ -934,8 +935,10 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
     }
   } else {
     // grid.y = frame k of a progressive batch (accumID + k), whose colour goes to the
-    // sample buffer for k_accumulate; a single frame writes accum/fb directly
-    const uint32_t gid = blockIdx.x * 256u + (uint32_t)tid;
+    // sample buffer for k_accumulate; a single frame writes accum/fb directly.  With
+    // measured-cost scheduling (irt_context.hip) workgroup b renders block order[b].
+    const uint32_t blk = A.schedOrder ? A.schedOrder[blockIdx.x] : blockIdx.x;
+    const uint32_t gid = blk * 256u + (uint32_t)tid;
     const Pixel px = pixel_of(A, gid);
     float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + gid : nullptr;
     if (px.active)
@@ -943,6 +946,14 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
     if (A.counters && px.active) atomicAdd(&s_cnt[0], 1u);
   }
   if (A.counters) flush_counters(A, s_cnt, tid);
+  if (A.schedCost && !listMode) {  // this workgroup's duration, for the next launches' order
+    __syncthreads();
+    if (tid == 0) {
+      const uint64_t dt = wall_clock64() - c0;
+      A.schedCost[A.schedOrder ? A.schedOrder[blockIdx.x] : blockIdx.x] =
+          dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ progressive batch
