@@ -89,6 +89,7 @@ struct irt_context {
   long long schedSwitch = 0;    // first launch reading it
   size_t schedCap = 0;
   bool schedOn = true;         // IRT_SCHED=0 disables
+  int schedPolicy = 1;         // IRT_SCHED: 1 tiles, 2 bands of tiles (a tile row), 3 reversed
   bool schedOrderValid = false;
   long long schedKey[8] = {};
   long long schedSrc = -1;      // launch whose costs the current order came from
@@ -219,20 +220,27 @@ int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int t
   // together for the locator's cache locality)
   const uint32_t *cost = c->h_schedCost + (size_t)bestSlot * c->schedCap;
   const int nt = numBlocks / 16;
-  std::vector<std::pair<uint64_t, int>> tiles(nt);
-  for (int t = 0; t < nt; ++t) {
+  // group size in tiles: 1, or a band of consecutive launch tiles (one image row of tiles)
+  const int tilesX = (W + 63) / 64;
+  const int band = c->schedPolicy == 2 ? std::max(1, tilesX / std::max(1, tileStride)) : 1;
+  const int ng = (nt + band - 1) / band;
+  std::vector<std::pair<uint64_t, int>> groups(ng);
+  for (int g = 0; g < ng; ++g) {
     uint64_t sum = 0;
-    for (int j = 0; j < 16; ++j) sum += cost[16 * t + j];
-    tiles[t] = {sum, t};
+    for (int t = g * band; t < std::min(nt, (g + 1) * band); ++t)
+      for (int j = 0; j < 16; ++j) sum += cost[16 * t + j];
+    groups[g] = {c->schedPolicy == 3 ? (uint64_t)g : sum, g};
   }
-  std::stable_sort(tiles.begin(), tiles.end(),
+  std::stable_sort(groups.begin(), groups.end(),
                    [](const std::pair<uint64_t, int> &a, const std::pair<uint64_t, int> &b) {
                      return a.first > b.first;
                    });
   const int nb = c->schedOrderValid ? 1 - c->schedBuf : c->schedBuf;
   uint32_t *h = c->h_schedOrder + (size_t)nb * c->schedCap;
-  for (int p = 0; p < nt; ++p)
-    for (int j = 0; j < 16; ++j) h[16 * p + j] = (uint32_t)(16 * tiles[p].second + j);
+  int p = 0;
+  for (const auto &g : groups)
+    for (int t = g.second * band; t < std::min(nt, (g.second + 1) * band); ++t, ++p)
+      for (int j = 0; j < 16; ++j) h[16 * p + j] = (uint32_t)(16 * t + j);
   IRT_HIP(hipMemcpyAsync(c->d_schedOrder + (size_t)nb * c->schedCap, h,
                          (size_t)numBlocks * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   c->schedBuf = nb;
@@ -451,7 +459,10 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
     set_error("irt_create: cannot initialise device %d", device);
     return fail(IRT_E_HIP);
   }
-  if (const char *e = getenv("IRT_SCHED")) c->schedOn = atoi(e) != 0;
+  if (const char *e = getenv("IRT_SCHED")) {
+    c->schedOn = atoi(e) != 0;
+    c->schedPolicy = atoi(e);
+  }
   c->info = S.info;
   c->n = (uint32_t)S.n;
   c->G = S.G;
