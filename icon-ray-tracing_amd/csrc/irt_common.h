@@ -533,3 +533,29 @@ IRT_HD bool intersect_wedge(float &value, float px, float py, float pz, const WV
   return false;
 }
 }  // namespace irt
+
+// ---------------------------------------------------------------------------------
+// TRIANGLE_MODE (deviceCode.cu:61-76): from the sample point, a ray toward the Earth's
+// centre (direction -normalize(pos)) against the bottom triangles of buildTriangleAccel
+// (hostCode.cu:445-450), back faces culled, the closest hit wins.  OptiX's watertight
+// triangle test is not reproducible here; this is the definition both the oracle and the
+// kernel use (parity unpinned): Moller-Trumbore without division except for t, front face
+// iff det > 0 (counter-clockwise seen from the ray origin), edges inclusive, t > 0.
+namespace irt {
+IRT_HD bool ray_triangle(float ox, float oy, float oz, float dx, float dy, float dz,
+                         const float *v0, const float *v1, const float *v2, float &t) {
+  const float e1x = v1[0] - v0[0], e1y = v1[1] - v0[1], e1z = v1[2] - v0[2];
+  const float e2x = v2[0] - v0[0], e2y = v2[1] - v0[1], e2z = v2[2] - v0[2];
+  const float px = dy * e2z - dz * e2y, py = dz * e2x - dx * e2z, pz = dx * e2y - dy * e2x;
+  const float det = e1x * px + e1y * py + e1z * pz;
+  if (!(det > 0.f)) return false;  // back face or parallel: culled
+  const float tx = ox - v0[0], ty = oy - v0[1], tz = oz - v0[2];
+  const float u = tx * px + ty * py + tz * pz;
+  if (u < 0.f || u > det) return false;
+  const float qx = ty * e1z - tz * e1y, qy = tz * e1x - tx * e1z, qz = tx * e1y - ty * e1x;
+  const float v = dx * qx + dy * qy + dz * qz;
+  if (v < 0.f || u + v > det) return false;
+  t = (e2x * qx + e2y * qy + e2z * qz) / det;
+  return t > 0.f;
+}
+}  // namespace irt

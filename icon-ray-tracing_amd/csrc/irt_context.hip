@@ -270,14 +270,14 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     set_error("irt_render: unknown accelMode %d", lp->accelMode);
     return IRT_E_INVALID;
   }
-  if (lp->mode != IRT_MODE_USER_GEOM && lp->mode != IRT_MODE_CUBQL) {
-    set_error("irt_render: sampler mode %d not supported (IRT_MODE_USER_GEOM or IRT_MODE_CUBQL)",
-              lp->mode);
+  if (lp->mode != IRT_MODE_USER_GEOM && lp->mode != IRT_MODE_CUBQL &&
+      lp->mode != IRT_MODE_TRIANGLES) {
+    set_error("irt_render: unknown sampler mode %d", lp->mode);
     return IRT_E_INVALID;
   }
-  if (lp->mode == IRT_MODE_CUBQL && c->wG == 0 && c->n != 0) {
-    set_error("irt_render: IRT_MODE_CUBQL needs irt_build_wedge_accel first (buildCuBQLAccel, "
-              "hostCode.cu:557-649)");
+  if (lp->mode != IRT_MODE_USER_GEOM && c->wG == 0 && c->n != 0) {
+    set_error("irt_render: sampler mode %d needs irt_build_wedge_accel first (buildCuBQLAccel / "
+              "buildTriangleAccel, hostCode.cu:557-649, 440-484)", lp->mode);
     return IRT_E_INVALID;
   }
   IRT_HIP(hipSetDevice(c->device));

@@ -71,10 +71,12 @@ int sample_host(const HostScene &s, uint32_t rec, float px, float py, float pz, 
 int locate_host(const HostScene &s, float px, float py, float pz, float &value,
                 uint32_t *record);
 
-// CUBQL_MODE (Params.h:31; deviceCode.cu:90-115) wedge locator, the replacement of
-// buildCuBQLAccel's cuBQL BVH (hostCode.cu:557-649): per record the glibc corner trig and
-// the union of its wedges' primBounds, and a gnomonic cube map listing, per cell, every
-// record with a wedge whose box can contain a point of that direction (sorted by index).
+// The unstructured-element locator of CUBQL_MODE (Params.h:31; deviceCode.cu:90-115) and
+// TRIANGLE_MODE (61-76), the replacement of buildCuBQLAccel's cuBQL BVH and
+// buildTriangleAccel's OptiX BVH (hostCode.cu:557-649, 440-484): per record the glibc corner
+// trig and the union box of its wedges' primBounds and its bottom triangle, and a gnomonic
+// cube map listing, per cell, every record whose box can hold a point of that direction
+// (sorted by index).
 struct WedgeScene {
   int G = 0;
   std::vector<float> trig;       // n * 12: per corner {cosf lat, sinf lat, cosf lon, sinf lon}
@@ -86,6 +88,9 @@ int build_wedges(const irt_icon_cell *cells, size_t n, WedgeScene &W, int thread
 // CUBQL_MODE sampleVolume over the wedge locator, as the kernel does it (host check).
 bool wedge_locate_host(const WedgeScene &W, const irt_icon_cell *cells, float px, float py,
                        float pz, float &value);
+// TRIANGLE_MODE sampleVolume over the same locator, as the kernel does it (host check).
+bool triangle_locate_host(const WedgeScene &W, const irt_icon_cell *cells, float px, float py,
+                          float pz, float &value, uint32_t *record);
 
 int default_threads();
 

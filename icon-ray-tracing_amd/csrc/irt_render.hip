@@ -28,7 +28,8 @@ namespace irt {
 enum : int {
   OPT_BATCH = 1,      // two fat entries per round trip
   OPT_PF = 2,         // next sample's cell header prefetched (woodcock_pf)
-  OPT_WEDGE = 16384,  // CUBQL_MODE sampler (locate_wedge); kept out of the default kernels
+  OPT_WEDGE = 16384,  // CUBQL / TRIANGLE samplers (locate_wedge, locate_tri); kept out of
+                      // the default kernels
   OPT_GRID = 8192,    // GRID_ACCEL_MODE traversal (render_grid); likewise
   OPT_STATS = 32768,  // per-wave statistics into counters[5..9] (measurement only)
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
@@ -239,9 +240,45 @@ struct Tracer {
     return false;
   }
 
+  // TRIANGLE_MODE sampleVolume (deviceCode.cu:61-76): the ray from the sample toward the
+  // Earth's centre against the listed records' bottom triangles (hostCode.cu:445-450),
+  // closest front-face hit (ray_triangle, irt_common.h), then its radial range and getValue.
+  __device__ __forceinline__ bool locate_tri(float px, float py, float pz, float &value) {
+    const float len = sqrtf(dot3(px, py, pz, px, py, pz));
+    const float dx = -(px / len), dy = -(py / len), dz = -(pz / len);
+    const uint32_t cell = cubemap_cell_fast(px, py, pz, A.wG);
+    const uint32_t qe = A.wOff[cell + 1];
+    float best = __builtin_inff();
+    uint32_t hit = 0xFFFFFFFFu;
+    for (uint32_t q = A.wOff[cell]; q < qe; ++q) {
+      const uint32_t rec = A.wRec[q];
+      const float4 t0 = A.wTrig[3 * (size_t)rec], t1 = A.wTrig[3 * (size_t)rec + 1],
+                   t2 = A.wTrig[3 * (size_t)rec + 2];
+      const float h0 = reinterpret_cast<const float *>(A.blocks + (size_t)rec * kBlk4)[blk_height_pos(0)];
+      const float v0[3] = {(h0 * t0.x) * t0.z, (h0 * t0.x) * t0.w, h0 * t0.y};
+      const float v1[3] = {(h0 * t1.x) * t1.z, (h0 * t1.x) * t1.w, h0 * t1.y};
+      const float v2[3] = {(h0 * t2.x) * t2.z, (h0 * t2.x) * t2.w, h0 * t2.y};
+      float t;
+      if (ray_triangle(px, py, pz, dx, dy, dz, v0, v1, v2, t) && t < best) {
+        best = t;
+        hit = rec;
+      }
+    }
+    if (hit == 0xFFFFFFFFu) return false;
+    const float4 *B = A.blocks + (size_t)hit * kBlk4;
+    const float *Bf = reinterpret_cast<const float *>(B);
+    const int nl = (int)__float_as_uint(A.wBox[2 * (size_t)hit].w);
+    if (len < Bf[blk_height_pos(0)] || len > Bf[blk_height_pos(nl)]) return false;
+    value = find_value_literal(B, nl, len);
+    return true;
+  }
+
   __device__ __forceinline__ bool locate(float px, float py, float pz, float &value) {
     if (A.numCells == 0) return false;
-    if constexpr ((OPT & OPT_WEDGE) != 0) return locate_wedge(px, py, pz, value);
+    if constexpr ((OPT & OPT_WEDGE) != 0) {
+      if (A.sampler == IRT_MODE_TRIANGLES) return locate_tri(px, py, pz, value);
+      return locate_wedge(px, py, pz, value);
+    }
     const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
     const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G);
     const uint4 H0 = A.binHdr[2 * (size_t)cell], H1 = A.binHdr[2 * (size_t)cell + 1];
@@ -1017,9 +1054,9 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
     const bool g = A.accelMode == IRT_ACCEL_GRID;
     // the wedge kernels hold a 6-vertex Newton state: no waves-per-SIMD floor (no spills)
     constexpr int DW = (D & ~0xF00) | OPT_WEDGE;
-    if (A.sampler == IRT_MODE_CUBQL && g)
+    if (A.sampler != IRT_MODE_USER_GEOM && g)  // CUBQL or TRIANGLES: the unstructured locator
       hipLaunchKernelGGL(k_render<DW | OPT_GRID>, grid, dim3(256), 0, s, A, 0);
-    else if (A.sampler == IRT_MODE_CUBQL)
+    else if (A.sampler != IRT_MODE_USER_GEOM)
       hipLaunchKernelGGL(k_render<DW>, grid, dim3(256), 0, s, A, 0);
     else if (g)
       hipLaunchKernelGGL(k_render<D | OPT_GRID>, grid, dim3(256), 0, s, A, 0);

@@ -3,7 +3,7 @@
 // ABI of include/icon_rt_hip.h.
 //
 //   icon_rt <file.ic> [--num-cells N] [--lat-range a:b] [--lon-range a:b]
-//           [-mode 0|2]                         (0 cell sample(), 2 cuBQL wedges)
+//           [-mode 0|1|2]                       (0 cell sample(), 1 triangles, 2 wedges)
 //           [Pipeline flags: --size W H, --camera ..., -fovy f, --xf f, --sample-limit N]
 //           [--synth rootN bisections levels]   (no .ic file: synthetic ICON grid)
 //           [--bench K]                         (render K extra frames, print timing)
@@ -156,12 +156,12 @@ int main(int argc, char *argv[]) {
   lp.unitDistance = info.unitDistance;
   lp.raygen = IRT_RAYGEN_WITH_ACCEL;  // setRayGen(woodcockTrackingWithAccel) (863)
   lp.accelMode = g.accelMode;         // toggleAccelMode (hostCode.cu:170-199)
-  if (g.mode == IRT_MODE_CUBQL) {     // toggleMode (hostCode.cu:152-168) + buildCuBQLAccel
+  if (g.mode == IRT_MODE_CUBQL || g.mode == IRT_MODE_TRIANGLES) {
+    // toggleMode (hostCode.cu:152-168): buildCuBQLAccel / buildTriangleAccel's geometry
     if (irt_build_wedge_accel(ctx, cells.data(), cells.size())) die("irt_build_wedge_accel");
-    lp.mode = IRT_MODE_CUBQL;
+    lp.mode = g.mode;
   } else if (g.mode != IRT_MODE_USER_GEOM) {
-    fprintf(stderr, "icon_rt: -mode %d (OptiX triangles) is not available; using the cell "
-                    "sampler (-mode 0)\n", g.mode);
+    fprintf(stderr, "icon_rt: unknown -mode %d; using the cell sampler (-mode 0)\n", g.mode);
   }
 
   pl.clearFramebuffer = [&] {

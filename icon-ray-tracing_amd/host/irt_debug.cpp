@@ -162,6 +162,16 @@ int irt_debug_scene_build_wedges(irt_debug_scene *s, const irt_icon_cell *cells,
   return build_wedges(cells, n, s->w);
 }
 
+int irt_debug_scene_locate_triangle(irt_debug_scene *s, irt_vec3f p, float *value,
+                                    uint32_t *record) {
+  if (!s || !value) return IRT_E_INVALID;
+  if (s->w.G == 0) {
+    set_error("irt_debug_scene_locate_triangle: call irt_debug_scene_build_wedges first");
+    return IRT_E_INVALID;
+  }
+  return triangle_locate_host(s->w, s->cells.data(), p.x, p.y, p.z, *value, record) ? 1 : 0;
+}
+
 int irt_debug_intersect_wedge(const float *v24, irt_vec3f p, float *value) {
   WV4 V[6];
   memcpy(V, v24, sizeof(V));

@@ -806,6 +806,13 @@ int build_wedges(const irt_icon_cell *cells, size_t n, WedgeScene &W, int thread
           tr[4 * k + 3] = sinf(c.lon[k]);
         }
         float lo[3] = {1e31f, 1e31f, 1e31f}, hi[3] = {-1e31f, -1e31f, -1e31f};
+        // the bottom triangle (TRIANGLE_MODE's geometry, hostCode.cu:445-450), also of
+        // records without layers
+        for (int k = 0; k < 3; ++k) {
+          const V3 b = wedge_vertex(c.height[0], tr + 4 * k);
+          lo[0] = fminf(lo[0], b.x), lo[1] = fminf(lo[1], b.y), lo[2] = fminf(lo[2], b.z);
+          hi[0] = fmaxf(hi[0], b.x), hi[1] = fmaxf(hi[1], b.y), hi[2] = fmaxf(hi[2], b.z);
+        }
         for (int h = 0; h < c.numLayers; ++h) {
           WV4 V[6];
           float wl[3], wh[3];
@@ -820,7 +827,6 @@ int build_wedges(const irt_icon_cell *cells, size_t n, WedgeScene &W, int thread
         bx[0] = lo[0], bx[1] = lo[1], bx[2] = lo[2];
         memcpy(bx + 3, &nl, 4);
         bx[4] = hi[0], bx[5] = hi[1], bx[6] = hi[2];
-        if (c.numLayers == 0) continue;  // no wedges
         // pad the union box by a relative 1e-6 against the double evaluation
         double dl[3], dh[3];
         for (int a = 0; a < 3; ++a) {
@@ -851,6 +857,37 @@ int build_wedges(const irt_icon_cell *cells, size_t n, WedgeScene &W, int thread
   for (auto &p : parts)
     for (auto &e : p) W.recs[cursor[e.first]++] = e.second;
   return IRT_OK;
+}
+
+bool triangle_locate_host(const WedgeScene &W, const irt_icon_cell *cells, float px, float py,
+                          float pz, float &value, uint32_t *record) {
+  if (W.G == 0) return false;
+  // ray.direction = -normalize(pos) (deviceCode.cu:67; vecmath normalize = u / |u|)
+  const float len = sqrtf(px * px + py * py + pz * pz);
+  const float dx = -(px / len), dy = -(py / len), dz = -(pz / len);
+  const uint32_t cell = cubemap_cell(px, py, pz, W.G);
+  float best = INFINITY;
+  uint32_t hit = 0xFFFFFFFFu;
+  for (uint32_t q = W.offsets[cell]; q < W.offsets[cell + 1]; ++q) {
+    const uint32_t rec = W.recs[q];
+    const float *tr = &W.trig[12 * (size_t)rec];
+    float v[3][3];
+    for (int k = 0; k < 3; ++k) {
+      const V3 b = wedge_vertex(cells[rec].height[0], tr + 4 * k);
+      v[k][0] = b.x, v[k][1] = b.y, v[k][2] = b.z;
+    }
+    float t;
+    if (ray_triangle(px, py, pz, dx, dy, dz, v[0], v[1], v[2], t) && t < best) {
+      best = t;
+      hit = rec;
+    }
+  }
+  if (hit == 0xFFFFFFFFu) return false;
+  const irt_icon_cell &c = cells[hit];
+  if (len < c.height[0] || len > c.height[c.numLayers]) return false;
+  value = cell_value(c, len);
+  if (record) *record = hit;
+  return true;
 }
 
 bool wedge_locate_host(const WedgeScene &W, const irt_icon_cell *cells, float px, float py,

@@ -29,6 +29,7 @@ RAYGEN_AE = 1          # woodcockTrackingAE (deviceCode.cu:239-275)
 ACCEL_SPHERE = 0       # SPHERE_ACCEL_MODE (Params.h:33): sdda over the shell grid
 ACCEL_GRID = 1         # GRID_ACCEL_MODE (Params.h:34): dda3 over the 256^3 grid
 MODE_USER_GEOM = 0     # Volume::mode (Params.h:29-31): sample() on the cells (default)
+MODE_TRIANGLES = 1     # closest bottom triangle toward the centre (deviceCode.cu:61-76)
 MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
 # compiled variants of the raygen (irt_render.hip OPT_* bits; 4096 = one monolithic
 # kernel instead of the setup -> march -> continuation pipeline); all bit-identical

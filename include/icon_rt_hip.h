@@ -59,7 +59,10 @@ typedef struct irt_box3f { irt_vec3f lower, upper; } irt_box3f;
 /* Sampler == Volume::mode (Params.h:29-31, 60; the -mode flag, hostCode.cu:125-127). */
 #define IRT_MODE_USER_GEOM 0    /* sample() on the cells (ICONGrid.h:181-208): the CPU build's
                                    scan (deviceCode.cu:116-123), lowest index wins */
-#define IRT_MODE_TRIANGLES 1    /* OptiX triangle trace (deviceCode.cu:61-76): not supported */
+#define IRT_MODE_TRIANGLES 1    /* the OptiX triangle trace (deviceCode.cu:61-76): closest
+                                   bottom triangle toward the Earth's centre (needs
+                                   irt_build_wedge_accel); OptiX's own intersection test is
+                                   not reproducible, see ray_triangle in csrc/irt_common.h */
 #define IRT_MODE_CUBQL 2        /* wedges + intersectWedgeEXT (deviceCode.cu:90-115) */
 
 /* Per-frame part of icon_rt::LaunchParams (icon_rt/Params.h:92-119).  The volume,
@@ -79,8 +82,8 @@ typedef struct irt_launch_params {
                                "Accel mode" UI option 853-857): IRT_ACCEL_SPHERE (sdda over
                                the shell grid, the default) or IRT_ACCEL_GRID (dda3 over the
                                256^3 Cartesian grid) */
-  int32_t mode;             /* volume.mode: IRT_MODE_USER_GEOM (default) or IRT_MODE_CUBQL
-                               (needs irt_build_wedge_accel) */
+  int32_t mode;             /* volume.mode: IRT_MODE_USER_GEOM (default), IRT_MODE_TRIANGLES
+                               or IRT_MODE_CUBQL (both need irt_build_wedge_accel) */
 } irt_launch_params;
 
 /* Scene facts computed at irt_create exactly as hostCode.cu:792-808, 838-840. */
@@ -185,6 +188,8 @@ int irt_reset_render_stats_total(irt_context *ctx);
  * (UElems.h:214-311) accepts it; cuBQL's own traversal order is not reproducible here
  * (the submodule is not vendored), so that order is the documented choice. */
 int irt_build_wedge_accel(irt_context *ctx, const irt_icon_cell *cells, size_t n);
+/* The same locator also serves IRT_MODE_TRIANGLES (buildTriangleAccel, hostCode.cu:440-484):
+ * every cell's bottom triangle toCartesian(height[0], lat, lon) is listed too. */
 
 /* Download the GRID_ACCEL_MODE grid (256^3 macrocells over the volume bounds,
  * hostCode.cu:668-682; index x + 256*(y + 256*z)), same conventions as irt_get_shell. */

@@ -56,6 +56,10 @@ void irt_debug_scene_free(irt_debug_scene *s);
  * whose primBounds contain p and whose intersectWedgeEXT accepts it). */
 int irt_debug_scene_build_wedges(irt_debug_scene *s, const irt_icon_cell *cells, size_t n);
 int irt_debug_scene_locate_wedge(irt_debug_scene *s, irt_vec3f p, float *value);
+/* TRIANGLE_MODE sampleVolume (deviceCode.cu:61-76) through the same locator, as the kernel
+ * does it; *record = the hit cell. */
+int irt_debug_scene_locate_triangle(irt_debug_scene *s, irt_vec3f p, float *value,
+                                    uint32_t *record);
 /* intersectWedgeEXT (UElems.h:214-311) as the kernel evaluates it; v24 = 6 x (xyz, scalar). */
 int irt_debug_intersect_wedge(const float *v24, irt_vec3f p, float *value);
 

@@ -558,6 +558,31 @@ inline bool boxContains(const B3 &b, V3 p) {  // box3f::contains (vecmath.h:1088
          b.lower.z <= p.z && p.z <= b.upper.z;
 }
 
+// ---------------------------------------------------------------- TRIANGLE_MODE
+// deviceCode.cu:61-76 with buildTriangleAccel's triangles (hostCode.cu:445-450): a ray from
+// the sample toward the Earth's centre, back faces culled, the closest hit's cell, then its
+// radial range and getValue.  OptiX's triangle test is not available: Moller-Trumbore (the
+// product's definition, csrc/irt_common.h ray_triangle; parity unpinned), the lowest index
+// winning equal distances.
+inline bool rayTriangle(V3 o, V3 d, V3 a, V3 b, V3 c, float &t) {
+  const V3 e1 = b - a, e2 = c - a;
+  const V3 p{d.y * e2.z - d.z * e2.y, d.z * e2.x - d.x * e2.z, d.x * e2.y - d.y * e2.x};
+  const float det = e1.x * p.x + e1.y * p.y + e1.z * p.z;
+  if (!(det > 0.f)) return false;
+  const V3 tv = o - a;
+  const float u = tv.x * p.x + tv.y * p.y + tv.z * p.z;
+  if (u < 0.f || u > det) return false;
+  const V3 q{tv.y * e1.z - tv.z * e1.y, tv.z * e1.x - tv.x * e1.z, tv.x * e1.y - tv.y * e1.x};
+  const float v = d.x * q.x + d.y * q.y + d.z * q.z;
+  if (v < 0.f || u + v > det) return false;
+  t = (e2.x * q.x + e2.y * q.y + e2.z * q.z) / det;
+  return t > 0.f;
+}
+
+struct Tri {
+  V3 v[3];
+};
+
 // ---------------------------------------------------------------- renderer
 struct Scene {
   const oc_cell *cells;
@@ -567,7 +592,35 @@ struct Scene {
   std::vector<Wedge> wedges;       // CUBQL_MODE only
   bool useWedges = false;
   std::vector<float> rr;           // fast mode: {height[0], height[numLayers]} per record
+  std::vector<Tri> tris;           // TRIANGLE_MODE only
+  bool useTriangles = false;
 };
+
+void buildTriangles(Scene &S) {
+  S.tris.resize(S.n);
+  for (size_t i = 0; i < S.n; ++i)
+    for (int k = 0; k < 3; ++k)
+      S.tris[i].v[k] = toCartesian({S.cells[i].height[0], S.cells[i].lat[k], S.cells[i].lon[k]});
+}
+
+inline bool sampleTriangles(const Scene &S, V3 pos, float &value) {
+  const V3 d = -normalize(pos);  // ray.direction = -normalize(ray.origin) (deviceCode.cu:67)
+  float best = INFINITY;
+  size_t hit = (size_t)-1;
+  for (size_t i = 0; i < S.n; ++i) {
+    float t;
+    if (rayTriangle(pos, d, S.tris[i].v[0], S.tris[i].v[1], S.tris[i].v[2], t) && t < best) {
+      best = t;
+      hit = i;
+    }
+  }
+  if (hit == (size_t)-1) return false;
+  const oc_cell &cell = S.cells[hit];
+  const float r = length(pos);  // toSpherical(pos).x (deviceCode.cu:70)
+  if (r < cell.height[0] || r > cell.height[cell.numLayers]) return false;
+  value = getValue(cell, r);
+  return true;
+}
 
 // Fast mode's per-record tables (the same tests in the same order, read from compact
 // arrays), built on nthreads threads.
@@ -596,6 +649,7 @@ struct ThreadStats {
 
 // sampleVolume, CPU branch: first cell index wins (deviceCode.cu:116-123)
 inline bool sampleVolume(const Scene &S, V3 pos, float &value) {
+  if (S.useTriangles) return sampleTriangles(S, pos, value);  // TRIANGLE_MODE
   if (S.useWedges) {  // CUBQL_MODE (deviceCode.cu:90-115)
     for (const Wedge &wd : S.wedges)
       if (boxContains(wd.box, pos) && intersectWedgeEXT(value, pos, wd.v)) return true;
@@ -1020,11 +1074,15 @@ int oracle_render(const oc_cell *cells, size_t n, const oc_params *p, int W, int
                   oc_stats *stats) {
   if (!p || W <= 0 || H <= 0 || x0 < 0 || y0 < 0 || x1 > W || y1 > H) return -1;
   if (x1 <= x0 || y1 <= y0) return 0;
-  Scene S{cells, n, fast != 0, {}, {}, false, {}};
+  Scene S{cells, n, fast != 0, {}, {}, false, {}, {}, false};
   if (S.fast) buildFast(S, nthreads);
   if (p->mode == 2) {
     S.useWedges = true;
     buildWedges(cells, n, S.wedges);
+  }
+  if (p->mode == 1) {
+    S.useTriangles = true;
+    buildTriangles(S);
   }
   // parallel::for_each over 64x64 tiles (common/for_each.h:70-85,
   // parallel_for.h:62-82), dynamic via an atomic counter (thread_pool.h:146-161)
@@ -1070,11 +1128,15 @@ int oracle_render_pixels(const oc_cell *cells, size_t n, const oc_params *p, int
   if (!p || W <= 0 || H <= 0 || numPixels < 0) return -1;
   for (int i = 0; i < numPixels; ++i)
     if (xy[2 * i] < 0 || xy[2 * i] >= W || xy[2 * i + 1] < 0 || xy[2 * i + 1] >= H) return -1;
-  Scene S{cells, n, fast != 0, {}, {}, false, {}};
+  Scene S{cells, n, fast != 0, {}, {}, false, {}, {}, false};
   if (S.fast) buildFast(S, nthreads);
   if (p->mode == 2) {
     S.useWedges = true;
     buildWedges(cells, n, S.wedges);
+  }
+  if (p->mode == 1) {
+    S.useTriangles = true;
+    buildTriangles(S);
   }
   std::atomic<int> counter{0};
   if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
@@ -1175,8 +1237,14 @@ int oracle_intersect_wedge(const float *v24, oc_vec3 p, float *value) {
 }
 
 int oracle_wedge_sample(const oc_cell *cells, size_t n, oc_vec3 p, float *value) {
-  Scene S{cells, n, false, {}, {}, true, {}};
+  Scene S{cells, n, false, {}, {}, true, {}, {}, false};
   buildWedges(cells, n, S.wedges);
+  return sampleVolume(S, toV3(p), *value);
+}
+
+int oracle_triangle_sample(const oc_cell *cells, size_t n, oc_vec3 p, float *value) {
+  Scene S{cells, n, false, {}, {}, false, {}, {}, true};
+  buildTriangles(S);
   return sampleVolume(S, toV3(p), *value);
 }
 

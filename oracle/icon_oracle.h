@@ -58,7 +58,7 @@ typedef struct oc_params {
   oc_box3 gridBounds;
   const float *gridMaxOpacities;
   /* Volume::mode (Params.h:60): 0 the cell sample() scan (the CPU build, deviceCode.cu:
-     116-123), 2 CUBQL_MODE wedges (deviceCode.cu:90-115) */
+     116-123), 1 TRIANGLE_MODE (61-76), 2 CUBQL_MODE wedges (90-115) */
   int32_t mode;
 } oc_params;
 
@@ -148,6 +148,8 @@ int oracle_dda3_trace(oc_vec3 org, oc_vec3 dir, float tmin, float tmax, const in
 int oracle_intersect_wedge(const float *v24, oc_vec3 p, float *value);
 /* CUBQL_MODE sampleVolume over the wedges of `cells` (hostCode.cu:557-600). */
 int oracle_wedge_sample(const oc_cell *cells, size_t n, oc_vec3 p, float *value);
+/* TRIANGLE_MODE sampleVolume over the cells' bottom triangles (deviceCode.cu:61-76). */
+int oracle_triangle_sample(const oc_cell *cells, size_t n, oc_vec3 p, float *value);
 float oracle_linear_to_srgb(float x);                                          /* dvr_course-common-both.h:30-35 */
 uint32_t oracle_make_rgba(const float *rgba4);                                 /* dvr_course-common-both.h:103-110 */
 void oracle_to_spherical(oc_vec3 c, oc_vec3 *out);                             /* ICONGrid.h:36-42 */

@@ -100,6 +100,7 @@ def olib() -> C.CDLL:
         L.oracle_build_grid.argtypes = [P, S, P, OBox3, P]
         L.oracle_intersect_wedge.argtypes = [P, OVec3, C.POINTER(C.c_float)]
         L.oracle_wedge_sample.argtypes = [P, S, OVec3, C.POINTER(C.c_float)]
+        L.oracle_triangle_sample.argtypes = [P, S, OVec3, C.POINTER(C.c_float)]
         L.oracle_linear_to_srgb.argtypes = [F]
         L.oracle_linear_to_srgb.restype = F
         L.oracle_make_rgba.argtypes = [P]

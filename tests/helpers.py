@@ -61,7 +61,7 @@ def gpu_frame(cells, W, H, camera=None, accum_ids=(0,), raygen=0, lut=None, valu
         lut, value_range = setup.lut, setup.value_range
     ctx = irt.Context(cells, device)
     ctx.set_transfunc(lut, value_range, opacity_scale)
-    if mode == irt.MODE_CUBQL:
+    if mode != irt.MODE_USER_GEOM:
         ctx.build_wedge_accel(cells)
     fr = GpuFrame(ctx, W, H)
     stats = []

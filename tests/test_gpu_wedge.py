@@ -1,4 +1,6 @@
-"""GPU parity of the CUBQL_MODE sampler (Params.h:31; deviceCode.cu:90-115): sampleVolume
+"""GPU parity of the unstructured samplers: TRIANGLE_MODE (deviceCode.cu:61-76; the
+product's ray_triangle definition, parity unpinned) and the CUBQL_MODE sampler
+(Params.h:31; deviceCode.cu:90-115): sampleVolume
 through the wedges of buildCuBQLAccel (hostCode.cu:557-600) and intersectWedgeEXT
 (UElems.h:214-311), against the oracle's brute-force wedge scan and the reference's own
 outputs (tests/golden/kats_wedge.npz, f7_*_wedge.npz).  Bar: bit-exact.
@@ -47,8 +49,11 @@ def test_wedge_mode_needs_its_accel():
     setup.lp.mode = irt.MODE_CUBQL
     with pytest.raises(irt.IrtError, match="irt_build_wedge_accel"):
         fr.render(setup.lp)
-    setup.lp.mode = 1  # TRIANGLE_MODE (OptiX): not supported
-    with pytest.raises(irt.IrtError, match="not supported"):
+    setup.lp.mode = irt.MODE_TRIANGLES  # needs the same accel
+    with pytest.raises(irt.IrtError, match="irt_build_wedge_accel"):
+        fr.render(setup.lp)
+    setup.lp.mode = 7
+    with pytest.raises(irt.IrtError, match="unknown sampler"):
         fr.render(setup.lp)
     with pytest.raises(irt.IrtError):
         ctx.build_wedge_accel(cells[:-1])
@@ -85,4 +90,26 @@ def test_wedge_c2_strided_pixels_match_oracle():
     bad = np.any(bits(a[ys, xs]) != bits(a_ref[ys, xs]), axis=-1) | (f[ys, xs] != f_ref[ys, xs])
     assert not bad.any(), f"{int(bad.sum())} of {len(xy)} sampled pixels differ"
     assert (a_ref[ys, xs, 3] > 0).sum() > len(xy) // 3
+    ctx.close()
+
+
+TRI_CASES = [
+    # (rootN, bisections, levels, W, camera, accelMode)
+    (2, 2, 30, 64, FRAMING, 0),
+    (2, 3, 47, 64, None, 0),
+    (2, 2, 20, 48, FRAMING, 1),  # with GRID_ACCEL_MODE traversal
+    (1, 0, 4, 48, FRAMING, 0),
+]
+
+
+@pytest.mark.parametrize("rn,bis,L,W,cam,accel", TRI_CASES)
+def test_triangle_frame_bit_exact(rn, bis, L, W, cam, accel):
+    cells = irt.synth_grid(rn, bis, L, noise=0.2)
+    a_ref, f_ref, st_ref, _ = oracle_frame(cells, W, W, camera=cam, accel_mode=accel, mode=1,
+                                           threads=16)
+    a_gpu, f_gpu, st_gpu, ctx = gpu_frame(cells, W, W, camera=cam, accel_mode=accel,
+                                          mode=irt.MODE_TRIANGLES)
+    assert_same_frame(a_gpu, f_gpu, a_ref, f_ref, f"triangles R{rn}B{bis:02d}L{L}")
+    assert (st_gpu[0].locateCalls, st_gpu[0].samplesFound) == (st_ref[0].locate_calls,
+                                                               st_ref[0].samples_found)
     ctx.close()

@@ -355,3 +355,46 @@ def test_wedge_locator_matches_oracle_on_coarse_and_fine_grids():
             if h1:
                 assert np.float32(a.value).view(np.uint32) == np.float32(b.value).view(np.uint32)
         L.irt_debug_scene_free(h)
+
+
+# ------------------------------------------------------------------ TRIANGLE_MODE
+def test_triangle_locator_matches_oracle_and_cell_sampler():
+    """TRIANGLE_MODE (deviceCode.cu:61-76) through the locator vs the oracle's scan over
+    every bottom triangle (the same ray_triangle definition; OptiX's test is not available,
+    parity unpinned), and against the cell sampler, which it matches away from record
+    boundaries."""
+    import ctypes as C
+    import oracle as O
+    L = _wedge_lib()
+    L.irt_debug_scene_locate_triangle.argtypes = [C.c_void_p, irt.Vec3, C.POINTER(C.c_float),
+                                                  C.POINTER(C.c_uint32)]
+    L.irt_debug_scene_locate.argtypes = [C.c_void_p, irt.Vec3, C.POINTER(C.c_float),
+                                         C.POINTER(C.c_uint32)]
+    rng = np.random.default_rng(8)
+    for rn, bis, lev in ((1, 0, 4), (2, 0, 9), (2, 3, 47)):
+        cells = irt.synth_grid(rn, bis, lev, noise=0.3)
+        h = C.c_void_p()
+        assert L.irt_debug_scene_build(cells.ctypes.data, cells.size, C.byref(h)) == 0
+        assert L.irt_debug_scene_build_wedges(h, cells.ctypes.data, cells.size) == 0
+        same_as_cells = 0
+        for _ in range(300):
+            c = cells[rng.integers(cells.size)]
+            lat, lon = c["lat"].astype(np.float64), c["lon"].astype(np.float64)
+            d = np.stack([np.cos(lat) * np.cos(lon), np.cos(lat) * np.sin(lon), np.sin(lat)], 1)
+            w = rng.dirichlet([1, 1, 1]) * 1.4 - 0.13
+            r = rng.uniform(c["height"][0] - 3000, c["height"][c["numLayers"]] + 3000)
+            v = w @ d
+            p = (v / np.linalg.norm(v) * r).astype(np.float32)
+            a, b, e = C.c_float(0), C.c_float(0), C.c_float(0)
+            rec = C.c_uint32(0)
+            h1 = L.irt_debug_scene_locate_triangle(h, irt.Vec3(*p.tolist()), C.byref(a), C.byref(rec))
+            h2 = O.olib().oracle_triangle_sample(O._p(cells), cells.size, O.v3(p), C.byref(b))
+            assert h1 == h2
+            if h1:
+                assert np.float32(a.value).view(np.uint32) == np.float32(b.value).view(np.uint32)
+            rc = C.c_uint32(0)
+            h3 = L.irt_debug_scene_locate(h, irt.Vec3(*p.tolist()), C.byref(e), C.byref(rc))
+            if h3 == h1 and (not h1 or e.value == a.value):
+                same_as_cells += 1
+        assert same_as_cells >= 0.8 * 300, same_as_cells  # chord vs sphere bands differ
+        L.irt_debug_scene_free(h)
