@@ -68,6 +68,18 @@ struct irt_context {
   static constexpr int kSlots = 32;
   unsigned long long *d_counters = nullptr;  // kSlots x 16
   unsigned long long *h_counters = nullptr;  // pinned, kSlots x 16
+  unsigned long long *dh_counters = nullptr; // h_counters as the device sees it
+  // statsKernel: k_stats_out writes the counters to h_counters and zeroes the next slot
+  // (every slot starts zeroed); otherwise a memset + D2H copy per launch (IRT_STATS_COPY=1)
+  bool statsKernel = true;
+  hipStream_t lastStream = nullptr;  // stream of the previous launch
+  // kernel-timing events on every n-th launch only (irt_set_timing_interval): an event
+  // pair around every frame costs ~10 us of stream gaps against a 0.17 ms kernel
+  int timingEvery = 8;
+  bool timed[kSlots] = {};
+  float lastMs = 0.f;          // most recent timed launch
+  double timedMs = 0.0;        // sum over the timed launches since the last reset
+  long long timedLaunches = 0;
   hipEvent_t ev0[kSlots] = {}, ev1[kSlots] = {};  // kernel timing
   hipEvent_t evDone[kSlots] = {};                  // counters landed in h_counters
   bool pending[kSlots] = {};
@@ -139,7 +151,12 @@ int finish_slot(irt_context *c, int i) {
   if (!c->pending[i]) return IRT_OK;
   IRT_HIP(hipEventSynchronize(c->evDone[i]));
   float ms = 0.f;
-  IRT_HIP(hipEventElapsedTime(&ms, c->ev0[i], c->ev1[i]));
+  if (c->timed[i]) {
+    IRT_HIP(hipEventElapsedTime(&ms, c->ev0[i], c->ev1[i]));
+    c->lastMs = ms;
+    c->timedMs += ms;
+    ++c->timedLaunches;
+  }
   const unsigned long long *h = c->h_counters + 16 * i;
   irt_render_stats st;
   st.raysLaunched = h[0];
@@ -147,7 +164,7 @@ int finish_slot(irt_context *c, int i) {
   st.locateCalls = h[2];
   st.samplesFound = h[3];
   st.candidatesTested = h[4];
-  st.kernelMs = ms;
+  st.kernelMs = c->lastMs;
   c->stats = st;
   memcpy(c->h_last, h, sizeof(c->h_last));
   c->total.raysLaunched += st.raysLaunched;
@@ -155,7 +172,6 @@ int finish_slot(irt_context *c, int i) {
   c->total.locateCalls += st.locateCalls;
   c->total.samplesFound += st.samplesFound;
   c->total.candidatesTested += st.candidatesTested;
-  c->total.kernelMs += ms;
   ++c->totalLaunches;
   c->pending[i] = false;
   return IRT_OK;
@@ -241,8 +257,15 @@ int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int t
   for (const auto &g : groups)
     for (int t = g.second * band; t < std::min(nt, (g.second + 1) * band); ++t, ++p)
       for (int j = 0; j < 16; ++j) h[16 * p + j] = (uint32_t)(16 * t + j);
-  IRT_HIP(hipMemcpyAsync(c->d_schedOrder + (size_t)nb * c->schedCap, h,
-                         (size_t)numBlocks * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  if (c->statsKernel) {
+    uint32_t *dh = nullptr;
+    IRT_HIP(hipHostGetDevicePointer((void **)&dh, h, 0));
+    launch_copy_u32(dh, c->d_schedOrder + (size_t)nb * c->schedCap, (size_t)numBlocks, s);
+    IRT_HIP(hipGetLastError());
+  } else {
+    IRT_HIP(hipMemcpyAsync(c->d_schedOrder + (size_t)nb * c->schedCap, h,
+                           (size_t)numBlocks * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  }
   c->schedBuf = nb;
   c->schedSwitch = c->launches;
   c->schedOrderValid = true;
@@ -397,19 +420,39 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     // copy the costs back every 8th launch (a 4*numBlocks-byte D2H on the stream)
     copyCosts = c->launches - c->schedLastCopy >= 8;
   }
-  IRT_HIP(hipMemsetAsync(A.counters, 0, 16 * sizeof(unsigned long long), s));
-  IRT_HIP(hipEventRecord(c->ev0[slot], s));
+  if (!c->statsKernel) {
+    IRT_HIP(hipMemsetAsync(A.counters, 0, 16 * sizeof(unsigned long long), s));
+  } else if (c->launches > 0 && s != c->lastStream) {
+    // this slot was zeroed by the previous launch's k_stats_out on another stream
+    IRT_HIP(hipStreamWaitEvent(s, c->evDone[(c->launches - 1) % irt_context::kSlots], 0));
+  }
+  c->lastStream = s;
+  c->timed[slot] = c->launches % c->timingEvery == 0;
+  if (c->timed[slot]) IRT_HIP(hipEventRecord(c->ev0[slot], s));
   if (numTiles > 0) {
     launch_render(A, numTiles * 16, s, c->variant);
   }
   IRT_HIP(hipGetLastError());
-  IRT_HIP(hipEventRecord(c->ev1[slot], s));
-  IRT_HIP(hipMemcpyAsync(c->h_counters + 16 * slot, A.counters, 16 * sizeof(unsigned long long),
-                         hipMemcpyDeviceToHost, s));
+  if (c->timed[slot]) IRT_HIP(hipEventRecord(c->ev1[slot], s));
+  if (c->statsKernel) {
+    launch_stats_out(A.counters, c->dh_counters + 16 * slot,
+                     c->d_counters + 16 * ((c->launches + 1) % irt_context::kSlots), s);
+    IRT_HIP(hipGetLastError());
+  } else {
+    IRT_HIP(hipMemcpyAsync(c->h_counters + 16 * slot, A.counters, 16 * sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, s));
+  }
   c->schedCopied[slot] = -1;
   if (copyCosts) {
-    IRT_HIP(hipMemcpyAsync(c->h_schedCost + (size_t)slot * c->schedCap, c->d_schedCost,
-                           (size_t)numBlocks * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (c->statsKernel) {
+      uint32_t *dh = nullptr;
+      IRT_HIP(hipHostGetDevicePointer((void **)&dh, c->h_schedCost + (size_t)slot * c->schedCap, 0));
+      launch_copy_u32(c->d_schedCost, dh, (size_t)numBlocks, s);
+      IRT_HIP(hipGetLastError());
+    } else {
+      IRT_HIP(hipMemcpyAsync(c->h_schedCost + (size_t)slot * c->schedCap, c->d_schedCost,
+                             (size_t)numBlocks * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    }
     c->schedCopied[slot] = c->launches;
     c->schedLastCopy = c->launches;
   }
@@ -499,6 +542,15 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
       return fail(IRT_E_HIP);
     }
   memset(c->h_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long));
+  if (const char *e = getenv("IRT_STATS_COPY")) c->statsKernel = atoi(e) == 0;
+  if (const char *e = getenv("IRT_TIMING_EVERY")) c->timingEvery = std::max(1, atoi(e));
+  if (hipHostGetDevicePointer((void **)&c->dh_counters, c->h_counters, 0) != hipSuccess ||
+      hipMemsetAsync(c->d_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long),
+                     c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess) {
+    set_error("irt_create: statistics ring setup failed");
+    return fail(IRT_E_HIP);
+  }
 
   // ShellAccel{vec3i(1,1024,1024), sphericalBounds} + initGrid + buildShell_ICON
   // (hostCode.cu:652-666), majorants zero until a transfer function arrives
@@ -667,7 +719,19 @@ int irt_get_render_stats_total(const irt_context *cc, irt_render_stats *total, l
   int rc = finish_stats(c);
   if (rc) return rc;
   *total = c->total;
+  total->kernelMs = c->timedLaunches
+                        ? (float)(c->timedMs / (double)c->timedLaunches * (double)c->totalLaunches)
+                        : 0.f;
   if (launches) *launches = c->totalLaunches;
+  return IRT_OK;
+}
+
+int irt_set_timing_interval(irt_context *c, int every) {
+  if (!c || every < 1) {
+    set_error("irt_set_timing_interval: null context or interval < 1");
+    return IRT_E_INVALID;
+  }
+  c->timingEvery = every;
   return IRT_OK;
 }
 
@@ -680,6 +744,8 @@ int irt_reset_render_stats_total(irt_context *c) {
   if (rc) return rc;
   c->total = irt_render_stats{};
   c->totalLaunches = 0;
+  c->timedMs = 0.0;
+  c->timedLaunches = 0;
   return IRT_OK;
 }
 

@@ -87,6 +87,9 @@ void launch_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n,
 void launch_max_opacities(const float *valueRanges, size_t numMCs, const float4 *lut, int size,
                           float lo, float hi, float *maxOp, hipStream_t s);
 void launch_clear(uint32_t *fb, float4 *accum, size_t n, hipStream_t s);
+void launch_stats_out(const unsigned long long *cur, unsigned long long *host,
+                      unsigned long long *next, hipStream_t s);
+void launch_copy_u32(const uint32_t *src, uint32_t *dst, size_t n, hipStream_t s);
 void launch_unpack(const uint32_t *gathered, int numRanks, int maxTiles, int W, int H,
                    uint32_t *fb, hipStream_t s);
 

@@ -3,6 +3,8 @@
 // framebuffer clear, and the multi-GPU tile unpack.  The raygen itself is irt_render.hip.
 
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "irt_device.h"
@@ -203,6 +205,19 @@ __global__ void k_unpack(const uint32_t *gathered, int numRanks, int maxTiles, i
   }
 }
 
+// Per-launch statistics hand-off (irt_context.hip render_impl): this launch's 16 counters
+// into the pinned host ring (vector stores over the mapped pointer, visible to the host at
+// the kernel's end-of-kernel release) and the next ring slot zeroed for the next launch.
+// One dispatch instead of a fill kernel plus an SDMA copy per frame.
+__global__ void k_stats_out(const unsigned long long *cur, unsigned long long *host,
+                            unsigned long long *next) {
+  const int i = threadIdx.x;
+  if (i < 16) {
+    host[i] = cur[i];
+    if (next != cur) next[i] = 0ull;
+  }
+}
+
 void launch_shell_init(float *vr, size_t numMCs, hipStream_t s) {
   hipLaunchKernelGGL(k_shell_init, dim3((unsigned)((numMCs + 255) / 256)), dim3(256), 0, s,
                      (float2 *)vr, numMCs);
@@ -222,6 +237,21 @@ void launch_max_opacities(const float *vr, size_t numMCs, const float4 *lut, int
                           float hi, float *maxOp, hipStream_t s) {
   hipLaunchKernelGGL(k_max_opacities, dim3((unsigned)((numMCs + 255) / 256)), dim3(256), 0, s,
                      (const float2 *)vr, numMCs, lut, size, lo, hi, maxOp);
+}
+void launch_stats_out(const unsigned long long *cur, unsigned long long *host,
+                      unsigned long long *next, hipStream_t s) {
+  hipLaunchKernelGGL(k_stats_out, dim3(1), dim3(64), 0, s, cur, host, next);
+}
+// a u32 array between device memory and mapped pinned host memory (either direction):
+// the scheduling costs and block orders, without an SDMA copy on the render stream
+__global__ void k_copy_u32(const uint32_t *src, uint32_t *dst, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+void launch_copy_u32(const uint32_t *src, uint32_t *dst, size_t n, hipStream_t s) {
+  if (n == 0) return;
+  const unsigned blocks = (unsigned)std::min<size_t>(64, (n + 255) / 256);
+  hipLaunchKernelGGL(k_copy_u32, dim3(blocks), dim3(256), 0, s, src, dst, n);
 }
 void launch_clear(uint32_t *fb, float4 *accum, size_t n, hipStream_t s) {
   if (n == 0) return;

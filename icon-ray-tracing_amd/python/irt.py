@@ -124,6 +124,7 @@ def lib() -> C.CDLL:
             "irt_get_render_stats": [P, C.POINTER(RenderStats)],
             "irt_get_render_stats_total": [P, C.POINTER(RenderStats), C.POINTER(C.c_longlong)],
             "irt_reset_render_stats_total": [P],
+            "irt_set_timing_interval": [P, C.c_int],
             "irt_get_shell": [P, P, P],
             "irt_get_grid": [P, P, P],
             "irt_build_wedge_accel": [P, P, S],
@@ -427,6 +428,10 @@ class Context:
 
     def reset_stats_total(self):
         _check(lib().irt_reset_render_stats_total(self._h), "irt_reset_render_stats_total")
+
+    def set_timing_interval(self, every: int):
+        """Kernel-timing events on every `every`-th launch only (default 8)."""
+        _check(lib().irt_set_timing_interval(self._h, int(every)), "irt_set_timing_interval")
 
     def build_wedge_accel(self, cells: np.ndarray):
         """buildCuBQLAccel (hostCode.cu:557-649): enables LaunchParams.mode = MODE_CUBQL."""

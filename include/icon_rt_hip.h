@@ -107,7 +107,8 @@ typedef struct irt_render_stats {
   uint64_t locateCalls;         /* sampleVolume calls (deviceCode.cu:173) */
   uint64_t samplesFound;        /* sampleVolume calls that found a cell */
   uint64_t candidatesTested;    /* locator candidate-list entries examined */
-  float kernelMs;               /* render kernel time, HIP events on the launch stream */
+  float kernelMs;               /* render kernel time, HIP events on the launch stream
+                                   (most recent timed launch, irt_set_timing_interval) */
 } irt_render_stats;
 
 typedef struct irt_context irt_context;
@@ -174,10 +175,16 @@ int irt_unpack_tiles(irt_context *ctx, const uint32_t *d_gathered, int numRanks,
  * ones' statistics: counters are read back through a ring, so frames queue back to back
  * like the reference's GPU path (owlLaunch2D is asynchronous, pipeline.cu:1064). */
 int irt_get_render_stats(const irt_context *ctx, irt_render_stats *stats);
-/* Sums over every launch since the last reset (kernelMs summed too); *launches = count. */
+/* Sums over every launch since the last reset; *launches = count.  kernelMs is the mean
+ * of the timed launches times the launch count (see irt_set_timing_interval). */
 int irt_get_render_stats_total(const irt_context *ctx, irt_render_stats *total,
                                long long *launches);
 int irt_reset_render_stats_total(irt_context *ctx);
+/* Kernel timing (HIP events on the launch stream) on every `every`-th launch only (default
+ * 8; 1 = every launch): an event pair per frame adds ~10 us of stream gaps to a 0.17 ms
+ * frame.  irt_render_stats.kernelMs of a launch is that of the most recent timed launch.
+ * No counterpart in the reference, which times on the host (pipeline.cu:1062-1073). */
+int irt_set_timing_interval(irt_context *ctx, int every);
 
 /* buildCuBQLAccel (hostCode.cu:557-649) for IRT_MODE_CUBQL: the wedges of every (cell,
  * layer) -- corners toCartesian(height[h|h+1], lat, lon), scalar
