@@ -44,3 +44,13 @@ def test_errors_are_reported_not_raised():
     info = irt.VolumeInfo()
     rc = L.irt_compute_volume_info(cells.ctypes.data, cells.size, C.byref(info))
     assert rc == -3 and b"numLayers" in L.irt_last_error()
+
+
+def test_context_calls_reject_a_null_context():
+    """Context entry points check their handle before touching a device (no GPU needed)."""
+    L = irt.lib()
+    assert L.irt_set_timing_interval(None, 8) == -1
+    assert b"irt_set_timing_interval" in L.irt_last_error()
+    assert L.irt_reset_render_stats_total(None) == -1
+    st = irt.RenderStats()
+    assert L.irt_get_render_stats(None, C.byref(st)) == -1
