@@ -101,7 +101,7 @@ struct irt_context {
   long long schedSwitch = 0;    // first launch reading it
   size_t schedCap = 0;
   bool schedOn = true;         // IRT_SCHED=0 disables
-  int schedPolicy = 1;         // IRT_SCHED: 1 tiles, 2 bands of tiles (a tile row), 3 reversed
+  int schedPolicy = 2;         // IRT_SCHED: 1 tiles, 2 bands of tiles (a tile row; default), 3 reversed
   bool schedOrderValid = false;
   long long schedKey[8] = {};
   long long schedSrc = -1;      // launch whose costs the current order came from
