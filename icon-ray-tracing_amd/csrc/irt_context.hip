@@ -40,12 +40,13 @@ struct irt_context {
   uint32_t *d_sphOff = nullptr;
   uint2 *d_sphRec = nullptr;
   uint32_t *d_sphBits = nullptr;
-  uint4 *d_queue = nullptr;      // march queue and continuation list (irt_render.hip),
-  uint32_t *d_contList = nullptr;  // sized for the largest launch so far
-  uint32_t *d_segCount = nullptr;
+  // per-workgroup event counts of the launches in flight: kSlots x wgCap x kCnt u32
+  // (a slot is rewritten only once its launch's statistics landed, see finish_slot)
+  uint32_t *d_wgCounts = nullptr;
+  size_t wgCap = 0;             // workgroups per slot
+  bool wgCountsOn = true;       // IRT_COUNTERS=atomic: device-scope atomics instead
   float4 *d_samples = nullptr;   // per-frame colours of a progressive batch
   size_t sampleCap = 0;
-  size_t queueCap = 0;
   float *d_srgb = nullptr;
   float *d_valueRanges = nullptr;
   float *d_maxOp = nullptr;
@@ -69,9 +70,6 @@ struct irt_context {
   unsigned long long *d_counters = nullptr;  // kSlots x 16
   unsigned long long *h_counters = nullptr;  // pinned, kSlots x 16
   unsigned long long *dh_counters = nullptr; // h_counters as the device sees it
-  // statsKernel: k_stats_out writes the counters to h_counters and zeroes the next slot
-  // (every slot starts zeroed); otherwise a memset + D2H copy per launch (IRT_STATS_COPY=1)
-  bool statsKernel = true;
   hipStream_t lastStream = nullptr;  // stream of the previous launch
   // kernel-timing events on every n-th launch only (irt_set_timing_interval): an event
   // pair around every frame costs ~10 us of stream gaps against a 0.17 ms kernel
@@ -132,7 +130,7 @@ void free_all(irt_context *c) {
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
-                  c->d_sphBits, c->d_queue, c->d_contList, c->d_segCount, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
+                  c->d_sphBits, c->d_wgCounts, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
                   c->d_lut, c->d_counters};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -257,15 +255,10 @@ int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int t
   for (const auto &g : groups)
     for (int t = g.second * band; t < std::min(nt, (g.second + 1) * band); ++t, ++p)
       for (int j = 0; j < 16; ++j) h[16 * p + j] = (uint32_t)(16 * t + j);
-  if (c->statsKernel) {
-    uint32_t *dh = nullptr;
-    IRT_HIP(hipHostGetDevicePointer((void **)&dh, h, 0));
-    launch_copy_u32(dh, c->d_schedOrder + (size_t)nb * c->schedCap, (size_t)numBlocks, s);
-    IRT_HIP(hipGetLastError());
-  } else {
-    IRT_HIP(hipMemcpyAsync(c->d_schedOrder + (size_t)nb * c->schedCap, h,
-                           (size_t)numBlocks * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-  }
+  uint32_t *dh = nullptr;
+  IRT_HIP(hipHostGetDevicePointer((void **)&dh, h, 0));
+  launch_copy_u32(dh, c->d_schedOrder + (size_t)nb * c->schedCap, (size_t)numBlocks, s);
+  IRT_HIP(hipGetLastError());
   c->schedBuf = nb;
   c->schedSwitch = c->launches;
   c->schedOrderValid = true;
@@ -304,7 +297,9 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     return IRT_E_INVALID;
   }
   IRT_HIP(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  // NULL is the null stream itself (ordered with the caller's blocking streams), never the
+  // context's private non-blocking stream
+  hipStream_t s = (hipStream_t)stream;
   const int tilesX = (W + 63) / 64, tilesY = (H + 63) / 64;
   const int total = tilesX * tilesY;
   int numTiles = tileBegin < total ? (total - tileBegin + tileStride - 1) / tileStride : 0;
@@ -369,26 +364,21 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     if (rc) return rc;
   }
   const size_t lanes = (size_t)numTiles * 4096;
-  if (lanes > c->queueCap) {
-    IRT_HIP(hipStreamSynchronize(s));
-    if (c->d_queue) IRT_HIP(hipFree(c->d_queue));
-    if (c->d_contList) IRT_HIP(hipFree(c->d_contList));
-    if (c->d_segCount) IRT_HIP(hipFree(c->d_segCount));
-    c->d_queue = nullptr;
-    c->d_contList = nullptr;
-    c->d_segCount = nullptr;
-    c->bytes -= c->queueCap * (sizeof(uint4) + sizeof(uint32_t)) + c->queueCap / 256 * sizeof(uint32_t);
-    c->queueCap = 0;
-    int rc = dalloc(c, &c->d_queue, lanes);
-    if (rc == IRT_OK) rc = dalloc(c, &c->d_contList, lanes);
-    if (rc == IRT_OK) rc = dalloc(c, &c->d_segCount, lanes / 256);
+  const size_t numWG = (size_t)numTiles * 16 * (size_t)numFrames;
+  if (c->wgCountsOn && numWG > c->wgCap) {
+    // every slot's launch must be done before the ring is reallocated
+    int rc = finish_stats(c);
     if (rc) return rc;
-    c->queueCap = lanes;
+    if (c->d_wgCounts) IRT_HIP(hipFree(c->d_wgCounts));
+    c->d_wgCounts = nullptr;
+    c->bytes -= c->wgCap * irt_context::kSlots * kCnt * sizeof(uint32_t);
+    c->wgCap = 0;
+    rc = dalloc(c, &c->d_wgCounts, numWG * irt_context::kSlots * kCnt);
+    if (rc) return rc;
+    c->wgCap = numWG;
     c->info.deviceBytes = c->bytes;
   }
-  A.queue = c->d_queue;
-  A.contList = c->d_contList;
-  A.segCount = c->d_segCount;
+  A.wgCounts = c->wgCountsOn ? c->d_wgCounts + (size_t)slot * c->wgCap * kCnt : nullptr;
   A.numSamples = numFrames;
   if (numFrames > 1) {
     const size_t need = lanes * (size_t)numFrames;
@@ -409,10 +399,8 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.schedOrder = nullptr;
   A.schedCost = nullptr;
   const int numBlocks = numTiles * 16;
-  const bool mono = (c->variant & 4096) != 0 || lp->accelMode != IRT_ACCEL_SPHERE ||
-                    lp->mode != IRT_MODE_USER_GEOM;
   bool copyCosts = false;
-  if (c->schedOn && mono && numFrames == 1 && numBlocks > 0) {
+  if (c->schedOn && numFrames == 1 && numBlocks > 0) {
     int rc = sched_prepare(c, numBlocks, W, H, packed, tileBegin, tileStride, numTiles, lp, s);
     if (rc) return rc;
     A.schedOrder = c->schedOrderValid ? c->d_schedOrder + (size_t)c->schedBuf * c->schedCap : nullptr;
@@ -420,9 +408,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     // copy the costs back every 8th launch (a 4*numBlocks-byte D2H on the stream)
     copyCosts = c->launches - c->schedLastCopy >= 8;
   }
-  if (!c->statsKernel) {
-    IRT_HIP(hipMemsetAsync(A.counters, 0, 16 * sizeof(unsigned long long), s));
-  } else if (c->launches > 0 && s != c->lastStream) {
+  if (c->launches > 0 && s != c->lastStream) {
     // this slot was zeroed by the previous launch's k_stats_out on another stream
     IRT_HIP(hipStreamWaitEvent(s, c->evDone[(c->launches - 1) % irt_context::kSlots], 0));
   }
@@ -434,25 +420,15 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   }
   IRT_HIP(hipGetLastError());
   if (c->timed[slot]) IRT_HIP(hipEventRecord(c->ev1[slot], s));
-  if (c->statsKernel) {
-    launch_stats_out(A.counters, c->dh_counters + 16 * slot,
-                     c->d_counters + 16 * ((c->launches + 1) % irt_context::kSlots), s);
-    IRT_HIP(hipGetLastError());
-  } else {
-    IRT_HIP(hipMemcpyAsync(c->h_counters + 16 * slot, A.counters, 16 * sizeof(unsigned long long),
-                           hipMemcpyDeviceToHost, s));
-  }
+  launch_stats_out(A.counters, A.wgCounts, numTiles > 0 ? numWG : 0, c->dh_counters + 16 * slot,
+                   c->d_counters + 16 * ((c->launches + 1) % irt_context::kSlots), s);
+  IRT_HIP(hipGetLastError());
   c->schedCopied[slot] = -1;
   if (copyCosts) {
-    if (c->statsKernel) {
-      uint32_t *dh = nullptr;
-      IRT_HIP(hipHostGetDevicePointer((void **)&dh, c->h_schedCost + (size_t)slot * c->schedCap, 0));
-      launch_copy_u32(c->d_schedCost, dh, (size_t)numBlocks, s);
-      IRT_HIP(hipGetLastError());
-    } else {
-      IRT_HIP(hipMemcpyAsync(c->h_schedCost + (size_t)slot * c->schedCap, c->d_schedCost,
-                             (size_t)numBlocks * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    }
+    uint32_t *dh = nullptr;
+    IRT_HIP(hipHostGetDevicePointer((void **)&dh, c->h_schedCost + (size_t)slot * c->schedCap, 0));
+    launch_copy_u32(c->d_schedCost, dh, (size_t)numBlocks, s);
+    IRT_HIP(hipGetLastError());
     c->schedCopied[slot] = c->launches;
     c->schedLastCopy = c->launches;
   }
@@ -542,7 +518,7 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
       return fail(IRT_E_HIP);
     }
   memset(c->h_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long));
-  if (const char *e = getenv("IRT_STATS_COPY")) c->statsKernel = atoi(e) == 0;
+  if (const char *e = getenv("IRT_COUNTERS")) c->wgCountsOn = strcmp(e, "atomic") != 0;
   if (const char *e = getenv("IRT_TIMING_EVERY")) c->timingEvery = std::max(1, atoi(e));
   if (hipHostGetDevicePointer((void **)&c->dh_counters, c->h_counters, 0) != hipSuccess ||
       hipMemsetAsync(c->d_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long),
@@ -624,6 +600,9 @@ int irt_set_transfunc(irt_context *c, const irt_vec4f *lut, int size, irt_box1f 
     return IRT_E_INVALID;
   }
   IRT_HIP(hipSetDevice(c->device));
+  // frames still in flight on the caller's stream read the LUT and the majorants: the
+  // update is serialized after them, as the reference's TF handler is after its launches
+  if (c->launches > 0) IRT_HIP(hipEventSynchronize(c->evDone[(c->launches - 1) % irt_context::kSlots]));
   if (size > c->lutCap) {
     if (c->d_lut) {
       IRT_HIP(hipStreamSynchronize(c->stream));
@@ -659,7 +638,7 @@ int irt_clear_frame(irt_context *c, uint32_t *fb, irt_vec4f *accum, size_t n, vo
     return IRT_E_INVALID;
   }
   IRT_HIP(hipSetDevice(c->device));
-  launch_clear(fb, (float4 *)accum, n, stream ? (hipStream_t)stream : c->stream);
+  launch_clear(fb, (float4 *)accum, n, (hipStream_t)stream);
   IRT_HIP(hipGetLastError());
   return IRT_OK;
 }
@@ -693,7 +672,7 @@ int irt_unpack_tiles(irt_context *c, const uint32_t *g, int numRanks, int maxTil
     return IRT_E_INVALID;
   }
   IRT_HIP(hipSetDevice(c->device));
-  if (maxTiles > 0) launch_unpack(g, numRanks, maxTiles, W, H, fb, stream ? (hipStream_t)stream : c->stream);
+  if (maxTiles > 0) launch_unpack(g, numRanks, maxTiles, W, H, fb, (hipStream_t)stream);
   IRT_HIP(hipGetLastError());
   return IRT_OK;
 }

@@ -58,11 +58,9 @@ struct RenderArgs {
   const uint32_t *sphOff;
   const uint2 *sphRec;
   const uint32_t *sphBits;
-  // the setup -> march -> continuation pipeline (irt_render.hip): the march queue
-  // ({gid | flags, t0, t1, majorant} per ray, one compacted segment per setup workgroup)
-  // and the continuation list (gids, count in counters[11])
-  uint4 *queue;
-  uint32_t *segCount;
+  // per-workgroup event counts (kCnt u32 per workgroup, summed by k_stats_out); null:
+  // device-scope atomics into `counters`
+  uint32_t *wgCounts;
   // progressive batch (irt_render_accumulate): frames accumID .. accumID+numSamples-1;
   // for numSamples > 1 each frame's colour goes to sampleBuf[frame][lane] first
   int numSamples;
@@ -70,9 +68,11 @@ struct RenderArgs {
   // block order to render (null: identity) and this launch's per-block durations
   const uint32_t *schedOrder;
   uint32_t *schedCost;
-  float4 *sampleBuf;    // rays per 256-slot queue segment (one per setup workgroup)
-  uint32_t *contList;
+  float4 *sampleBuf;
 };
+
+// Event counts kept per workgroup: [0] launched [1] inBox [2] locate [3] found [4] candidates
+constexpr int kCnt = 8;
 
 // Render-kernel variants: the bit set of irt_render.hip's OPT_* flags (bits 8-11: minimum
 // waves per SIMD).  All give identical results.
@@ -87,8 +87,8 @@ void launch_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n,
 void launch_max_opacities(const float *valueRanges, size_t numMCs, const float4 *lut, int size,
                           float lo, float hi, float *maxOp, hipStream_t s);
 void launch_clear(uint32_t *fb, float4 *accum, size_t n, hipStream_t s);
-void launch_stats_out(const unsigned long long *cur, unsigned long long *host,
-                      unsigned long long *next, hipStream_t s);
+void launch_stats_out(const unsigned long long *cur, const uint32_t *wgCounts, size_t numWG,
+                      unsigned long long *host, unsigned long long *next, hipStream_t s);
 void launch_copy_u32(const uint32_t *src, uint32_t *dst, size_t n, hipStream_t s);
 void launch_unpack(const uint32_t *gathered, int numRanks, int maxTiles, int W, int H,
                    uint32_t *fb, hipStream_t s);

@@ -205,16 +205,36 @@ __global__ void k_unpack(const uint32_t *gathered, int numRanks, int maxTiles, i
   }
 }
 
-// Per-launch statistics hand-off (irt_context.hip render_impl): this launch's 16 counters
-// into the pinned host ring (vector stores over the mapped pointer, visible to the host at
-// the kernel's end-of-kernel release) and the next ring slot zeroed for the next launch.
-// One dispatch instead of a fill kernel plus an SDMA copy per frame.
-__global__ void k_stats_out(const unsigned long long *cur, unsigned long long *host,
-                            unsigned long long *next) {
-  const int i = threadIdx.x;
-  if (i < 16) {
-    host[i] = cur[i];
-    if (next != cur) next[i] = 0ull;
+// Per-launch statistics hand-off (irt_context.hip render_impl): the workgroups' event
+// counts (kCnt u32 each) summed, plus this launch's 16-counter block, into the pinned host
+// ring (vector stores over the mapped pointer, visible to the host at the kernel's
+// end-of-kernel release), and the next ring slot zeroed for the next launch.  One dispatch
+// instead of a fill kernel plus an SDMA copy per frame.
+__global__ void __launch_bounds__(256) k_stats_out(const unsigned long long *cur, const uint32_t *wg,
+                                                   size_t numWG, unsigned long long *host,
+                                                   unsigned long long *next) {
+  __shared__ unsigned long long s_sum[256 / 64][kCnt];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  unsigned long long acc[kCnt];
+#pragma unroll
+  for (int k = 0; k < kCnt; ++k) acc[k] = 0ull;
+  if (wg)
+    for (size_t b = t; b < numWG; b += 256) {
+#pragma unroll
+      for (int k = 0; k < kCnt; ++k) acc[k] += wg[b * kCnt + k];
+    }
+#pragma unroll
+  for (int k = 0; k < kCnt; ++k) {
+    unsigned long long v = acc[k];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) s_sum[w][k] = v;
+  }
+  __syncthreads();
+  if (t < 16) {
+    unsigned long long v = cur[t];
+    if (t < kCnt) v += s_sum[0][t] + s_sum[1][t] + s_sum[2][t] + s_sum[3][t];
+    host[t] = v;
+    if (next != cur) next[t] = 0ull;
   }
 }
 
@@ -238,9 +258,9 @@ void launch_max_opacities(const float *vr, size_t numMCs, const float4 *lut, int
   hipLaunchKernelGGL(k_max_opacities, dim3((unsigned)((numMCs + 255) / 256)), dim3(256), 0, s,
                      (const float2 *)vr, numMCs, lut, size, lo, hi, maxOp);
 }
-void launch_stats_out(const unsigned long long *cur, unsigned long long *host,
-                      unsigned long long *next, hipStream_t s) {
-  hipLaunchKernelGGL(k_stats_out, dim3(1), dim3(64), 0, s, cur, host, next);
+void launch_stats_out(const unsigned long long *cur, const uint32_t *wgCounts, size_t numWG,
+                      unsigned long long *host, unsigned long long *next, hipStream_t s) {
+  hipLaunchKernelGGL(k_stats_out, dim3(1), dim3(256), 0, s, cur, wgCounts, numWG, host, next);
 }
 // a u32 array between device memory and mapped pinned host memory (either direction):
 // the scheduling costs and block orders, without an SDMA copy on the render stream

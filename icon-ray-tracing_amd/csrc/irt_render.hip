@@ -27,7 +27,6 @@ namespace irt {
 
 enum : int {
   OPT_BATCH = 1,      // two fat entries per round trip
-  OPT_PF = 2,         // next sample's cell header prefetched (woodcock_pf)
   OPT_WEDGE = 16384,  // CUBQL / TRIANGLE samplers (locate_wedge, locate_tri); kept out of
                       // the default kernels
   OPT_GRID = 8192,    // GRID_ACCEL_MODE traversal (render_grid); likewise
@@ -67,8 +66,6 @@ __device__ __forceinline__ uint32_t cubemap_cell_fast(float px, float py, float 
   return face * (uint32_t)G * (uint32_t)G + (uint32_t)j * (uint32_t)G + (uint32_t)i;
 }
 
-constexpr int kLutAlphaLds = 1024;
-
 template <int OPT>
 struct Tracer {
   const RenderArgs &A;
@@ -76,7 +73,6 @@ struct Tracer {
   const uint32_t *s_sph;
   uint32_t *s_cnt;  // [0] launched [1] inBox [2] locate [3] found [4] candidates
   Counts cnt;       // per-lane statistics (OPT_STATS)
-  const float *s_lutA = nullptr;  // LUT alpha column in LDS (march kernel)
 
   // one wave-aggregated LDS add per event site
   __device__ __forceinline__ void count(int k) {
@@ -285,13 +281,6 @@ struct Tracer {
     return locate_hdr(px, py, pz, r, H0, H1, value);
   }
 
-  // the cell header of a sample point (one gather), for locate_hdr
-  __device__ __forceinline__ void fetch_hdr(float px, float py, float pz, uint4 &H0, uint4 &H1) {
-    const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G);
-    H0 = A.binHdr[2 * (size_t)cell];
-    H1 = A.binHdr[2 * (size_t)cell + 1];
-  }
-
   __device__ __forceinline__ bool locate_hdr(float px, float py, float pz, float r, const uint4 &H0,
                                              const uint4 &H1, float &value) {
     const float e0 = __uint_as_float(H0.x), e1 = __uint_as_float(H0.y), e2 = __uint_as_float(H0.z);
@@ -334,8 +323,8 @@ struct Tracer {
     return hit;
   }
 
-  // postClassify's alpha only (the acceptance test needs nothing else), from the LUT's
-  // alpha column in LDS when it fits; the colour comes from post_classify on acceptance
+  // postClassify's alpha only (the acceptance test needs nothing else); the colour comes
+  // from post_classify on acceptance
   __device__ __forceinline__ float classify_alpha(float v) {
     v = (v - A.tfLo) / (A.tfHi - A.tfLo);
     const int size = A.lutSize;
@@ -344,8 +333,7 @@ struct Tracer {
     const int i1 = idx < 0 ? 0 : (idx > size - 1 ? size - 1 : idx);
     const int idx2 = (int)((uint32_t)idx + 1u);
     const int i2 = idx2 < 0 ? 0 : (idx2 > size - 1 ? size - 1 : idx2);
-    const bool lds = s_lutA && size <= kLutAlphaLds;
-    const float a = lds ? s_lutA[i1] : A.lut[i1].w, b = lds ? s_lutA[i2] : A.lut[i2].w;
+    const float a = A.lut[i1].w, b = A.lut[i2].w;
     return a * frac + b * (1.f - frac) * A.opacityScale;
   }
 
@@ -368,54 +356,6 @@ struct Tracer {
     return o;
   }
 
-  // woodcockTracking with the next sample's cell header in flight while the current
-  // sample is located: the next position depends only on the RNG state after this
-  // sample's acceptance draw, which exists whenever the sample lands in a cell (all but
-  // ~0.1% of samples).  Same draws, same samples, same result; one gather less per step.
-  __device__ __forceinline__ float woodcock_pf(float dx, float dy, float dz, float t, float tmax,
-                                               uint32_t &st, float majorant, float q,
-                                               float4 &sampleOut, bool counted) {
-    uint32_t sN = lcg_next(st);                        // this step's xi
-    float tN = t - (woodcock_log(sN, s_logf) / q);     // deviceCode.cu:165
-    uint4 H0 = make_uint4(0u, 0u, 0u, 0u), H1 = H0;
-    if (tN <= tmax) fetch_hdr(A.org.x + dx * tN, A.org.y + dy * tN, A.org.z + dz * tN, H0, H1);
-    while (true) {
-      if constexpr ((OPT & OPT_STATS) != 0) ++cnt.steps;
-      st = sN;
-      t = tN;
-      if (t > tmax) break;                             // 167-168
-      const float px = A.org.x + dx * t, py = A.org.y + dy * t, pz = A.org.z + dz * t;
-      // speculate: this sample is found, so the acceptance draw sU precedes the next xi
-      const uint32_t sU = lcg_next(st), sN2 = lcg_next(sU);
-      const float tN2 = t - (woodcock_log(sN2, s_logf) / q);
-      uint4 G0 = make_uint4(0u, 0u, 0u, 0u), G1 = G0;
-      if (tN2 <= tmax) fetch_hdr(A.org.x + dx * tN2, A.org.y + dy * tN2, A.org.z + dz * tN2, G0, G1);
-      if (counted) count(2);
-      float value = 0.f;
-      const float r = sqrtf(dot3(px, py, pz, px, py, pz));
-      if (!locate_hdr(px, py, pz, r, H0, H1, value)) {
-        // not in any cell: no acceptance draw (172-173), the next xi follows directly
-        sN = lcg_next(st);
-        tN = t - (woodcock_log(sN, s_logf) / q);
-        if (tN <= tmax) fetch_hdr(A.org.x + dx * tN, A.org.y + dy * tN, A.org.z + dz * tN, H0, H1);
-        continue;
-      }
-      if (counted) count(3);
-      const float sw = classify_alpha(value);  // postClassify(value).w (175)
-      st = sU;
-      const float u = lcg_float(st);           // 176
-      if (sw >= u * majorant) {                // 177-181
-        sampleOut = post_classify(value);
-        break;
-      }
-      sN = sN2;
-      tN = tN2;
-      H0 = G0;
-      H1 = G1;
-    }
-    return fminf(t, tmax);
-  }
-
   // woodcockTracking (deviceCode.cu:149-186) over [tmin, tmax].  `counted` is false in
   // zero-length sdda leaves, whose sampleVolume calls the statistics leave out.
   __device__ __forceinline__ float woodcock(float dx, float dy, float dz, float tmin, float tmax,
@@ -424,10 +364,6 @@ struct Tracer {
     float t = tmin;
     if (majorant <= 0.f) return fminf(t, tmax);
     const float q = majorant / A.unitDistance;  // the same value every iteration (165)
-    if constexpr ((OPT & OPT_PF) != 0) {
-      if constexpr ((OPT & OPT_WEDGE) == 0)
-        if (A.numCells != 0) return woodcock_pf(dx, dy, dz, t, tmax, st, majorant, q, sampleOut, counted);
-    }
     while (true) {
       if constexpr ((OPT & OPT_STATS) != 0) ++cnt.steps;
       st = lcg_next(st);
@@ -514,205 +450,22 @@ __device__ __forceinline__ void write_pixel(const RenderArgs &A, size_t outIdx, 
                  (srgb_byte(s_th, nv.z) << 16) + (make_8bit(nv.w) << 24);
 }
 
-// Wave-aggregated append: lanes with `want` get consecutive slots of queue counter *ctr
-// (one atomic per wave).  Call with the whole wave converged.
-__device__ __forceinline__ uint32_t wave_append(unsigned long long *ctr, bool want) {
-  const unsigned long long m = __ballot(want);
-  if (!m) return 0;
-  const int leader = __ffsll((long long)m) - 1;
-  uint32_t base = 0;
-  if ((int)__lane_id() == leader) base = (uint32_t)atomicAdd(ctr, (unsigned long long)__popcll(m));
-  base = __shfl(base, leader, 64);
-  const unsigned long long below = m & ((1ull << __lane_id()) - 1ull);
-  return base + (uint32_t)__popcll(below);
-}
-
+// The workgroup's event counts (LDS) out to the launch's statistics.  Default: one plain
+// store of the kCnt counts per workgroup into wgCounts (k_stats_out sums them), so no two
+// workgroups ever touch the same line.  Without wgCounts: device-scope atomics into the
+// counter block -- 4 096 workgroups x 5 same-line atomics per 1024^2 frame.
 __device__ __forceinline__ void flush_counters(const RenderArgs &A, uint32_t *s_cnt, int tid) {
   __syncthreads();
-  if (tid < 5 && s_cnt[tid]) atomicAdd(&A.counters[tid], (unsigned long long)s_cnt[tid]);
+  if (A.wgCounts) {
+    const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    if (tid < kCnt) A.wgCounts[wg * kCnt + tid] = s_cnt[tid];
+  } else if (tid < 5 && s_cnt[tid]) {
+    atomicAdd(&A.counters[tid], (unsigned long long)s_cnt[tid]);
+  }
 }
 
-// march-queue record: {gid | flags, t0, t1, majorant} -- the first leaf of a ray's first
-// range, where (for the default data and cameras) nearly every ray ends
-constexpr uint32_t kRecLast = 0x80000000u;  // nothing after this leaf can change the pixel
-constexpr uint32_t kRecAE = 0x40000000u;    // woodcockTrackingAE semantics
-constexpr uint32_t kRecGid = 0x3FFFFFFFu;
 // sample-buffer marker of a frame whose ray missed the box (alpha is 0 or 1 otherwise)
 constexpr float kNoSample = -1.f;
-// continuation-list counter (in RenderArgs::counters)
-constexpr int kCtrCont = 11;
-
-// ------------------------------------------------------------------ kernel 1: setup
-// Per pixel: the ray, boxTest, the shell ranges (ShellAccel.h:94-111) and the first leaf
-// of the first range (121-124, 163-170).  Pixels the raygen leaves without a Woodcock step
-// are written here; rays with a first leaf to march are appended to the march queue
-// (compacted: only in-shell rays occupy lanes of the march kernel); rays whose first leaf
-// cannot decide them go to the continuation list.
-template <int OPT>
-__global__ void __launch_bounds__(256) k_setup(RenderArgs A) {
-  __shared__ float s_th[256];
-  __shared__ uint32_t s_cnt[8];
-  __shared__ uint32_t s_wcnt[4];
-  const int tid = threadIdx.x;
-  s_th[tid] = A.srgbTh[tid];
-  if (tid < 8) s_cnt[tid] = 0;
-  __syncthreads();
-  const uint32_t gid = blockIdx.x * 256u + (uint32_t)tid;
-  const Pixel px = pixel_of(A, gid);
-  int action = 0;  // 0 nothing, 1 write a zero sample, 2 march queue, 3 continuation
-  uint4 rec = make_uint4(0u, 0u, 0u, 0u);
-  if (px.active) {
-    uint32_t st;
-    float dx, dy, dz;
-    gen_ray(A, A.accumID, px.x, px.y, st, dx, dy, dz);
-    const Ray ray = {A.org.x, A.org.y, A.org.z, 0.f, dx, dy, dz, 1e10f};
-    float t0, t1;
-    if (box_test(ray, A, t0, t1)) {
-      {
-        const unsigned long long m = __ballot(1);
-        if (__lane_id() == (unsigned)(__ffsll((long long)m) - 1)) atomicAdd(&s_cnt[1], (uint32_t)__popcll(m));
-      }
-      if (A.raygen == 1) {  // woodcockTrackingAE: one leaf, the box interval, majorant 1
-        action = 2;
-        rec = make_uint4(gid | kRecAE | kRecLast, __float_as_uint(t0), __float_as_uint(t1), __float_as_uint(1.f));
-      } else {
-        float st1 = 0.f, st2 = 0.f, st3 = 0.f, st4 = 0.f;
-        const bool s1 = intersect_sphere(ray, A.sbHi.x, st1, st4);
-        const bool s2 = intersect_sphere(ray, A.sbLo.x, st2, st3);
-        float lower = 0.f, upper = -1.f;
-        bool twoRanges = false;
-        if ((s1 || s2) && !(st4 < t0)) {
-          if (s1 && !s2) {
-            lower = st1; upper = st4;
-          } else if (t0 < st2) {
-            lower = st1; upper = st2;
-            twoRanges = !(st4 <= st3);  // range 1 not box1f::empty (lastRange's test)
-          } else {
-            lower = st3; upper = st4;
-          }
-        }
-        if (upper <= lower) {
-          action = 1;  // no range: the pixel accumulates a zero sample
-        } else {
-          const float e1 = lower + A.sbLo.x * 1e-6f;
-          float r1, la1, lo1;
-          to_spherical(ray.ox + ray.dx * e1, ray.oy + ray.dy * e1, ray.oz + ray.dz * e1, r1, la1, lo1);
-          const int cx = project_axis(r1, A.sbLo.x, A.sbHi.x, A.dims.x);
-          const int cy = project_axis(la1, A.sbLo.y, A.sbHi.y, A.dims.y);
-          const int cz = project_axis(lo1, A.sbLo.z, A.sbHi.z, A.dims.z);
-          // first leaf: tt1 = the least of tnext = {upper, 0, 0} that is >= lower
-          float tt1 = IRT_FLT_MAX;
-          if (upper < tt1 && upper >= lower) tt1 = upper;
-          if (0.f < tt1 && 0.f >= lower) tt1 = 0.f;
-          const uint32_t leaf = (uint32_t)wrap_coord(cz, A.dims.z) * (uint32_t)A.dims.x * (uint32_t)A.dims.y +
-                                (uint32_t)wrap_coord(cy, A.dims.y) * (uint32_t)A.dims.x +
-                                (uint32_t)wrap_coord(cx, A.dims.x);
-          const float maj = A.maxOp[leaf];
-          if (tt1 == lower || !(maj > 0.f)) {
-            // a zero-length first leaf or a zero majorant: no sample can hit here
-            action = twoRanges ? 3 : 1;
-          } else {
-            action = 2;
-            rec = make_uint4(gid | (twoRanges ? 0u : kRecLast), __float_as_uint(lower),
-                             __float_as_uint(tt1), __float_as_uint(maj));
-          }
-        }
-      }
-    }
-  }
-  // march queue: this workgroup's rays, compacted to the front of its own 256-slot
-  // segment (an LDS prefix over the waves, no global atomics); the count per segment
-  // tells the march kernel how many of its lanes have work
-  {
-    const unsigned long long m = __ballot(action == 2);
-    const int w = tid >> 6;
-    if ((tid & 63) == 0) s_wcnt[w] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t off = 0;
-    for (int k = 0; k < w; ++k) off += s_wcnt[k];
-    const uint32_t pos = off + (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
-    if (action == 2) A.queue[blockIdx.x * 256u + pos] = rec;
-    if (tid == 0) A.segCount[blockIdx.x] = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
-  }
-  const uint32_t ci = wave_append(&A.counters[kCtrCont], action == 3);
-  if (action == 3) A.contList[ci] = gid;
-  if (action == 1) write_pixel(A, px.outIdx, 0.f, 0.f, 0.f, 0.f, s_th);
-  if (A.counters) {
-    if (px.active) atomicAdd(&s_cnt[0], 1u);
-    flush_counters(A, s_cnt, tid);
-  }
-}
-
-// ------------------------------------------------------------------ kernel 2: march
-// One lane per queued ray: woodcockTracking over the first leaf (deviceCode.cu:149-186
-// via the woodcockFunc lambda, 304-323, or the AE raygen, 239-275) with the binned
-// locator; writes the pixel, or hands an undecided ray with a later range on.
-template <int OPT>
-__global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1) k_march(RenderArgs A) {
-  const uint32_t count = A.segCount[blockIdx.x];  // rays of setup workgroup blockIdx.x
-  if (count == 0) return;                         // whole workgroup: nothing to march
-  __shared__ float s_th[256];
-  __shared__ uint32_t s_cnt[8];
-  __shared__ LogfTab s_logf[16];
-  __shared__ uint32_t s_sph[kSphBitWords];
-  __shared__ float s_lutA[kLutAlphaLds];
-  const int tid = threadIdx.x;
-  if (A.numSph)
-    for (int i = tid; i < kSphBitWords; i += 256) s_sph[i] = A.sphBits[i];
-  if (A.lutSize <= kLutAlphaLds)
-    for (int i = tid; i < A.lutSize; i += 256) s_lutA[i] = A.lut[i].w;
-  s_th[tid] = A.srgbTh[tid];
-  if (tid < 16) s_logf[tid] = kLogfTab[tid];
-  if (tid < 8) s_cnt[tid] = 0;
-  __syncthreads();
-  Tracer<OPT> T{A, s_logf, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}, s_lutA};
-  const uint32_t j = (uint32_t)tid;
-  bool cont = false;
-  uint32_t gid = 0;
-  if (j < count) {
-    const uint4 rec = A.queue[blockIdx.x * 256u + j];
-    gid = rec.x & kRecGid;
-    const Pixel px = pixel_of(A, gid);
-    uint32_t st;
-    float dx, dy, dz;
-    gen_ray(A, A.accumID, px.x, px.y, st, dx, dy, dz);
-    const float t0 = __uint_as_float(rec.y), t1 = __uint_as_float(rec.z);
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float tw = T.woodcock(dx, dy, dz, t0, t1, st, __uint_as_float(rec.w), s, true);
-    const bool hit = (rec.x & kRecAE) || (tw > t0 && tw < t1);
-    if (hit || (rec.x & kRecLast)) {
-      float cr = 0.f, cg = 0.f, cb = 0.f, alpha = 0.f;
-      if (hit) {
-        cr = s.x * A.amb.x * A.ambRad;
-        cg = s.y * A.amb.y * A.ambRad;
-        cb = s.z * A.amb.z * A.ambRad;
-        alpha = s.w > 0.f ? 1.f : 0.f;
-      }
-      write_pixel(A, px.outIdx, cr, cg, cb, alpha, s_th);
-    } else {
-      cont = true;
-    }
-  }
-  const uint32_t ci = wave_append(&A.counters[kCtrCont], cont);
-  if (cont) A.contList[ci] = gid;
-  if (A.counters) flush_counters(A, s_cnt, tid);
-  if constexpr ((OPT & OPT_STATS) != 0) {
-    uint32_t ss = T.cnt.steps, sm = T.cnt.steps;
-    for (int off = 32; off > 0; off >>= 1) {
-      ss += __shfl_down(ss, off, 64);
-      sm = max(sm, (uint32_t)__shfl_down(sm, off, 64));
-    }
-    if ((tid & 63) == 0) {
-      atomicAdd(&A.counters[5], (unsigned long long)ss);
-      atomicAdd(&A.counters[6], (unsigned long long)sm);
-      atomicMax(&A.counters[9], (unsigned long long)sm);  // longest ray (draws)
-    }
-    if (j < count) {  // draws histogram: <= 2, 3-5, 6-10, > 10
-      const int bkt = T.cnt.steps <= 2 ? 12 : (T.cnt.steps <= 5 ? 13 : (T.cnt.steps <= 10 ? 14 : 15));
-      atomicAdd(&A.counters[bkt], 1ull);
-    }
-  }
-}
 
 // The woodcockTrackingWithAccel raygen in GRID_ACCEL_MODE (deviceCode.cu:326-328): dda3
 // (DDA.h:35-136) over the 256^3 Cartesian grid, each cell handed to the woodcockFunc
@@ -780,14 +533,11 @@ __device__ __forceinline__ void render_grid(const RenderArgs &A, Tracer<OPT> &T,
 }
 
 // ------------------------------------------------------------------ the full raygen
-// One pixel of woodcockTrackingWithAccel / woodcockTrackingAE, every range and leaf.  Used
-// alone (variant bit OPT_MONO) or as the continuation pass for the rays the march kernel
-// could not decide (skipFirst: the first leaf's sampleVolume calls were counted there).
+// One pixel of woodcockTrackingWithAccel / woodcockTrackingAE, every range and leaf.
 template <int OPT>
 __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
                                              const float *s_th, int4 *s_dda, float4 *s_entry,
-                                             int tid, bool skipFirst, int accumID,
-                                             float4 *sampleOut) {
+                                             int tid, int accumID, float4 *sampleOut) {
   uint32_t st;
   float dx, dy, dz;
   gen_ray(A, accumID, px.x, px.y, st, dx, dy, dz);
@@ -797,7 +547,7 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
     if (sampleOut) *sampleOut = make_float4(0.f, 0.f, 0.f, kNoSample);
     return;
   }
-  if (!skipFirst) T.count(1);
+  T.count(1);
   float cr = 0.f, cg = 0.f, cb = 0.f, alpha = 0.f;
   const bool ae = A.raygen == 1;
   // The ranges the raygen tracks.  woodcockTrackingAE (deviceCode.cu:239-275): the box
@@ -886,7 +636,7 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
       }
       if (!fast) {  // woodcockFunc(leafID, t, tt1)
         float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        const bool counted = !zeroLen && !(skipFirst && i == 0 && iter == 0);
+        const bool counted = !zeroLen;
         const float tw = T.woodcock(ray.dx, ray.dy, ray.dz, t, tt1, st, maj, s, counted);
         if (!zeroLen && (ae || (tw > t && tw < tt1))) {
           // AE: colour/alpha from the last accepted sample, zero if none (239-275)
@@ -938,17 +688,11 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
     write_pixel(A, px.outIdx, cr, cg, cb, alpha, s_th);
 }
 
-// The full raygen per pixel: alone over the frame grid (OPT_MONO), or as the continuation
-// pass over A.contList (a workgroup-stride loop over the list).
+// The raygen over the frame grid: one lane per pixel (see pixel_of).
 template <int OPT>
-__global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1) k_render(RenderArgs A, int listMode) {
-  uint32_t n = 0;
-  if (listMode) {
-    n = (uint32_t)A.counters[kCtrCont];
-    if (blockIdx.x * 256u >= n) return;  // whole workgroup: nothing to continue
-  }
+__global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1) k_render(RenderArgs A) {
   __shared__ float s_th[256];
-  __shared__ uint32_t s_cnt[8];
+  __shared__ uint32_t s_cnt[kCnt];
   __shared__ LogfTab s_logf[16];
   __shared__ uint32_t s_sph[kSphBitWords];
   __shared__ int4 s_dda[256];       // sdda state needed only after a range's first leaf
@@ -958,37 +702,44 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
     for (int i = tid; i < kSphBitWords; i += 256) s_sph[i] = A.sphBits[i];
   s_th[tid] = A.srgbTh[tid];
   if (tid < 16) s_logf[tid] = kLogfTab[tid];
-  if (tid < 8) s_cnt[tid] = 0;
+  if (tid < kCnt) s_cnt[tid] = 0;
   __syncthreads();
   Tracer<OPT> T{A, s_logf, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
   const uint64_t c0 = A.schedCost ? wall_clock64() : 0;
-  if (listMode) {
-    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
-      const uint32_t j = base + (uint32_t)tid;
-      if (j < n) {
-        const Pixel px = pixel_of(A, A.contList[j]);
-        render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, true, A.accumID, nullptr);
-      }
+  // grid.y = frame k of a progressive batch (accumID + k), whose colour goes to the sample
+  // buffer for k_accumulate; a single frame writes accum/fb directly.  With measured-cost
+  // scheduling (irt_context.hip) workgroup b renders block order[b].
+  const uint32_t blk = A.schedOrder ? A.schedOrder[blockIdx.x] : blockIdx.x;
+  const uint32_t gid = blk * 256u + (uint32_t)tid;
+  const Pixel px = pixel_of(A, gid);
+  float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + gid : nullptr;
+  if (px.active) render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, A.accumID + (int)blockIdx.y, slot);
+  if constexpr ((OPT & OPT_STATS) != 0) {  // Woodcock draws: sum, per-wave max, histogram
+    uint32_t ss = T.cnt.steps, sm = T.cnt.steps;
+    for (int off = 32; off > 0; off >>= 1) {
+      ss += __shfl_down(ss, off, 64);
+      sm = max(sm, (uint32_t)__shfl_down(sm, off, 64));
     }
-  } else {
-    // grid.y = frame k of a progressive batch (accumID + k), whose colour goes to the
-    // sample buffer for k_accumulate; a single frame writes accum/fb directly.  With
-    // measured-cost scheduling (irt_context.hip) workgroup b renders block order[b].
-    const uint32_t blk = A.schedOrder ? A.schedOrder[blockIdx.x] : blockIdx.x;
-    const uint32_t gid = blk * 256u + (uint32_t)tid;
-    const Pixel px = pixel_of(A, gid);
-    float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + gid : nullptr;
-    if (px.active)
-      render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, false, A.accumID + (int)blockIdx.y, slot);
-    if (A.counters && px.active) atomicAdd(&s_cnt[0], 1u);
+    if ((tid & 63) == 0) {
+      atomicAdd(&A.counters[5], (unsigned long long)ss);
+      atomicAdd(&A.counters[6], (unsigned long long)sm);
+      atomicMax(&A.counters[9], (unsigned long long)sm);
+    }
+    if (px.active) {  // draws histogram: 0, 1-2, 3-5, > 5
+      const uint32_t d = T.cnt.steps;
+      atomicAdd(&A.counters[d == 0 ? 12 : (d <= 2 ? 13 : (d <= 5 ? 14 : 15))], 1ull);
+    }
   }
-  if (A.counters) flush_counters(A, s_cnt, tid);
-  if (A.schedCost && !listMode) {  // this workgroup's duration, for the next launches' order
+  if (A.counters) {
+    const unsigned long long m = __ballot(px.active);  // rays launched, once per wave
+    if (__lane_id() == 0 && m) atomicAdd(&s_cnt[0], (uint32_t)__popcll(m));
+    flush_counters(A, s_cnt, tid);
+  }
+  if (A.schedCost) {  // this workgroup's duration, for the next launches' order
     __syncthreads();
     if (tid == 0) {
       const uint64_t dt = wall_clock64() - c0;
-      A.schedCost[A.schedOrder ? A.schedOrder[blockIdx.x] : blockIdx.x] =
-          dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
+      A.schedCost[blk] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
     }
   }
 }
@@ -1025,15 +776,14 @@ __global__ void __launch_bounds__(256) k_accumulate(RenderArgs A) {
 }
 
 // ------------------------------------------------------------------ variants / launcher
-// Variant bits: irt_render.hip OPT_* (bits 8-11: minimum waves per SIMD of the march
-// kernel).  OPT_MONO = 4096 runs the full raygen per pixel in one kernel instead of the
-// setup -> march -> continuation pipeline.  All variants give identical results.
+// Variant bits: irt_render.hip OPT_* (bits 8-11: minimum waves per SIMD asked of the
+// register allocator).  OPT_MONO (4096) is kept in the numbering of round 1 (the one-kernel
+// raygen; the setup -> march -> continuation pipeline it distinguished from was removed).
+// All variants give identical results.
 constexpr int OPT_MONO = 4096;
-constexpr int kContBlocks = 128;
-static_assert((kDefaultVariant & OPT_MONO) != 0, "progressive batches use the default kernel");
+static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
-#define IRT_VARIANTS(X) \
-  X(0) X(1) X(2) X(1536) X(2048) X(32768) X(4096) X(4097) X(4098) X(5120) X(5376) X(5632) X(6144) X(36864)
+#define IRT_VARIANTS(X) X(4096) X(4097) X(5120) X(5376) X(36864)
 
 bool render_variant_available(int v) {
 #define IRT_CASE(N) if (v == N) return true;
@@ -1045,33 +795,23 @@ bool render_variant_available(int v) {
 template <int N>
 void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
   constexpr int K = N & ~OPT_MONO;
-  if (A.numSamples > 1 || A.accelMode != IRT_ACCEL_SPHERE || A.sampler != IRT_MODE_USER_GEOM) {
-    // progressive batch (one frame per grid row, then the lerp chain), the grid accel or
-    // the wedge sampler: the one-kernel raygen
-    constexpr int M = (N & OPT_MONO) != 0 ? K : (kDefaultVariant & ~OPT_MONO);
-    constexpr int D = kDefaultVariant & ~OPT_MONO;
-    const dim3 grid(numBlocks, A.numSamples);
-    const bool g = A.accelMode == IRT_ACCEL_GRID;
-    // the wedge kernels hold a 6-vertex Newton state: no waves-per-SIMD floor (no spills)
-    constexpr int DW = (D & ~0xF00) | OPT_WEDGE;
-    if (A.sampler != IRT_MODE_USER_GEOM && g)  // CUBQL or TRIANGLES: the unstructured locator
-      hipLaunchKernelGGL(k_render<DW | OPT_GRID>, grid, dim3(256), 0, s, A, 0);
-    else if (A.sampler != IRT_MODE_USER_GEOM)
-      hipLaunchKernelGGL(k_render<DW>, grid, dim3(256), 0, s, A, 0);
-    else if (g)
-      hipLaunchKernelGGL(k_render<D | OPT_GRID>, grid, dim3(256), 0, s, A, 0);
-    else
-      hipLaunchKernelGGL(k_render<M>, grid, dim3(256), 0, s, A, 0);
-    if (A.numSamples > 1) hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);
-    return;
-  }
-  if constexpr ((N & OPT_MONO) != 0) {
-    hipLaunchKernelGGL(k_render<K>, dim3(numBlocks), dim3(256), 0, s, A, 0);
-  } else {
-    hipLaunchKernelGGL(k_setup<K>, dim3(numBlocks), dim3(256), 0, s, A);
-    hipLaunchKernelGGL(k_march<K>, dim3(numBlocks), dim3(256), 0, s, A);
-    hipLaunchKernelGGL(k_render<K & ~0xF00>, dim3(kContBlocks), dim3(256), 0, s, A, 1);
-  }
+  // the grid accel or the unstructured samplers: their own instantiations of the raygen
+  // (kept out of the default kernel, whose registers they would cost); the wedge kernels
+  // hold a 6-vertex Newton state: no waves-per-SIMD floor
+  constexpr int D = kDefaultVariant & ~OPT_MONO;
+  constexpr int DW = (D & ~0xF00) | OPT_WEDGE;
+  const dim3 grid(numBlocks, A.numSamples);
+  const bool g = A.accelMode == IRT_ACCEL_GRID;
+  if (A.sampler != IRT_MODE_USER_GEOM && g)  // CUBQL or TRIANGLES: the unstructured locator
+    hipLaunchKernelGGL(k_render<DW | OPT_GRID>, grid, dim3(256), 0, s, A);
+  else if (A.sampler != IRT_MODE_USER_GEOM)
+    hipLaunchKernelGGL(k_render<DW>, grid, dim3(256), 0, s, A);
+  else if (g)
+    hipLaunchKernelGGL(k_render<D | OPT_GRID>, grid, dim3(256), 0, s, A);
+  else
+    hipLaunchKernelGGL(k_render<K>, grid, dim3(256), 0, s, A);
+  // progressive batch: the lerp chain over the frames' samples
+  if (A.numSamples > 1) hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);
 }
 
 void launch_render(const RenderArgs &A, int numBlocks, hipStream_t s, int variant) {
@@ -1083,7 +823,7 @@ void launch_render(const RenderArgs &A, int numBlocks, hipStream_t s, int varian
     IRT_VARIANTS(IRT_CASE)
 #undef IRT_CASE
     default:
-      launch_variant<0>(A, numBlocks, s);
+      launch_variant<kDefaultVariant>(A, numBlocks, s);
   }
 }
 

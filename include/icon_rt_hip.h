@@ -18,7 +18,9 @@
  *    (the reference's LaunchParams borrow pointers owned by Buffer/Frame/Transfunc).
  *  - Framebuffer pointers passed to irt_render* are DEVICE pointers on the context's
  *    device (HBM-resident, as the reference's fbPointer/accumBuffer in RTCORE builds).
- *  - `stream` is a hipStream_t passed as void* (NULL = the context's own stream).
+ *  - `stream` is a hipStream_t passed as void*; NULL is HIP's null (legacy default) stream,
+ *    so work launched there is ordered with every blocking stream of the process (torch's
+ *    default stream included).
  *  - A context is single-caller.  Multi-GPU = one process (one context) per GPU.
  */
 #ifndef ICON_RT_HIP_H
