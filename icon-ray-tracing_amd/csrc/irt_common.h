@@ -294,13 +294,38 @@ IRT_HD uint32_t cubemap_cell(float px, float py, float pz, int G) {
   return (uint32_t)face * (uint32_t)G * (uint32_t)G + (uint32_t)j * (uint32_t)G + (uint32_t)i;
 }
 
-// One candidate-list entry: the record's radial extent (for the cheap first test of
-// sample(), ICONGrid.h:184), its index, and meta = numLayers | sortedHeights << 31.
-struct LocEntry {
-  float h0, hN;
-  uint32_t idx;
-  uint32_t meta;
-};
+constexpr int kSubCells = 4;  // sub-cells per cell edge (irt_build.h kSub)
+constexpr int kMaskCand = 8;  // candidates per radial bin with a sub-cell mask (irt_build.h)
+
+// cubemap_cell on the kSubCells-times finer grid: the same cell (the scaling by a power of
+// two is exact) and the sub-cell s = sj * kSubCells + si within it.
+IRT_HD uint32_t cubemap_cell_sub(float px, float py, float pz, int G, uint32_t &sub) {
+  const float ax = __builtin_fabsf(px), ay = __builtin_fabsf(py), az = __builtin_fabsf(pz);
+  int face;
+  float u, v;
+  if (ax >= ay && ax >= az) {
+    face = px >= 0.f ? 0 : 1;
+    u = py / ax;
+    v = pz / ax;
+  } else if (ay >= az) {
+    face = py >= 0.f ? 2 : 3;
+    u = px / ay;
+    v = pz / ay;
+  } else {
+    face = pz >= 0.f ? 4 : 5;
+    u = px / az;
+    v = py / az;
+  }
+  const int GS = G * kSubCells;
+  const float fg = (float)G;
+  int i = (int)((u + 1.f) * 0.5f * fg * (float)kSubCells);
+  int j = (int)((v + 1.f) * 0.5f * fg * (float)kSubCells);
+  i = i < 0 ? 0 : (i >= GS ? GS - 1 : i);
+  j = j < 0 ? 0 : (j >= GS ? GS - 1 : j);
+  sub = (uint32_t)((j % kSubCells) * kSubCells + (i % kSubCells));
+  return (uint32_t)face * (uint32_t)G * (uint32_t)G + (uint32_t)(j / kSubCells) * (uint32_t)G +
+         (uint32_t)(i / kSubCells);
+}
 
 // Per-record height/value block: 64 floats = 256 B, two 128-B lines.
 //   [0..31]  height[0..31]   (ICONCell::height)
@@ -308,19 +333,6 @@ struct LocEntry {
 //                             path -- findHeight() < numLayers <= 31 after the radial test)
 //   [63]     numLayers (int bits)
 constexpr int kHV = 64;
-
-// Render record: everything sample() + getValue() read for one record, kRec4 float4 =
-// 320 B, laid out for the state-machine kernel (irt_trace.hip) so that a point-in-record
-// test is one gather step and the value another:
-//   [0..2]   the three side planes (n.xyz, w)                       ICONGrid.h:197-203
-//   [3]      coarse keys {height[7], height[15], height[23], height[31]}
-//   [4+4b .. 7+4b], b = 0..3:  block b =
-//            {height[8b..8b+3]}, {height[8b+4..8b+7]},
-//            {value[8b-1..8b+2]}, {value[8b+3..8b+6]}   (value[-1] := 0)
-// height[j] sits at float (4+4(j>>3))*4 + (j&7); value[c] at (4+4((c+1)>>3)+2)*4 + ((c+1)&7).
-constexpr int kRec4 = 20;
-IRT_HD int rec_height_pos(int j) { return (4 + 4 * (j >> 3)) * 4 + (j & 7); }
-IRT_HD int rec_value_pos(int c) { return (4 + 4 * ((c + 1) >> 3) + 2) * 4 + ((c + 1) & 7); }
 
 // ---------------------------------------------------------------------------------
 // Radially binned candidate lists (the product locator).  Each cube-map cell splits the
@@ -333,7 +345,9 @@ IRT_HD int rec_value_pos(int c) { return (4 + 4 * ((c + 1) >> 3) + 2) * 4 + ((c 
 // the lower first hit.  Either way the first record passing sample() is the reference's
 // lowest-index answer (deviceCode.cu:119-122).
 constexpr int kMaxEdges = 3;
-constexpr int kBinHdrWords = 8;  // {e0, e1, e2, base} {end0, end1, end2, end3}: 32 B per cell
+// Cell header (irt_build.h): {e0, e1, e2, base} {end0, end1, end2, end3}, then the sub-cell
+// candidate masks: 128 B per cell
+constexpr int kBinHdrWords = 32;
 IRT_HD int bin_of(float r, float e0, float e1, float e2) {
   return (e0 < r ? 1 : 0) + (e1 < r ? 1 : 0) + (e2 < r ? 1 : 0);
 }

@@ -16,25 +16,26 @@ namespace irt {
 void set_error(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 void clear_error();
 
-struct Plane4 {
-  float x, y, z, w;
-};
 
-// Everything the GPU needs, prepared on the host.
+// The scene build's arrays (irt_build.h), restated on the host: the device build
+// (irt_build.hip) produces the same bytes.
 struct HostScene {
   size_t n = 0;
   irt_volume_info info{};
-  std::vector<float> hv;          // n * kHV floats (see irt_common.h)
-  std::vector<Plane4> planes;     // n * 3 side planes of sample() (ICONGrid.h:197-199)
+  std::vector<float> hv;          // n * kHV floats (see irt_common.h), for host checks
   std::vector<float> trig;        // n * 12: per corner {cosf lat, sinf lat, cosf lon, sinf lon}
-                                  // (glibc, for toCartesian in the grid build)
+  std::vector<float> planes;      // n * 12: the side planes of sample() (ICONGrid.h:197-199)
+  std::vector<float> rng;         // n * 2: {height[0], height[numLayers]}
+  std::vector<uint32_t> meta;     // n: numLayers | sorted << 31
+  std::vector<float> keys;        // n * 4: coarse findHeight keys
+  std::vector<float> blocks;      // n * kBlk4 * 4: height/value blocks
   int G = 0;                      // cube-map cells per face edge
   std::vector<uint32_t> offsets;  // 6*G*G + 1 CSR offsets
-  std::vector<LocEntry> entries;  // candidate lists, each sorted by record index
-  // the product locator (irt_common.h "radially binned candidate lists")
+  std::vector<uint32_t> entryRec; // candidate lists (each sorted by record index) ...
+  std::vector<uint32_t> entrySub; // ... and each entry's sub-cell mask
+  // the product locator (irt_build.h)
   std::vector<uint32_t> binHdr;   // 6*G*G * kBinHdrWords
   std::vector<float> fat;         // binEntries * kFat4 * 4
-  std::vector<float> blocks;      // n * kBlk4 * 4
   size_t binEntries = 0;
   // zero-thickness records (spheres): distinct radii, CSR into record indices (ascending),
   // and a hash bitmap of the radii (irt_common.h sph_hash) the kernel keeps in LDS
@@ -42,8 +43,10 @@ struct HostScene {
   std::vector<uint32_t> sphOff, sphRec, sphBits;
 };
 
-// Build the binned locator (binHdr, fat, blocks) from the CSR lists; build_scene calls it.
+// Build the binned locator (binHdr, fat) from the CSR lists; build_scene calls it.
 int build_bins(HostScene &S, int threads);
+// Cube-map resolution for a scene with numRuns columns (IRT_LOCATOR_SCALE / _G override).
+int locator_resolution(size_t numRuns);
 // Point location over the binned locator, as the kernel does it (host restatement).
 int locate_bins_host(const HostScene &s, float px, float py, float pz, float &value,
                      uint32_t *record, uint32_t *tested);
@@ -51,8 +54,6 @@ int locate_bins_host(const HostScene &s, float px, float py, float pz, float &va
 // Validate, compute volume facts, per-record planes/heights, and the locator.
 int build_scene(const irt_icon_cell *cells, size_t n, HostScene &out, int threads = 0);
 
-// Render records (irt_common.h, kRec4 float4 = 4*kRec4 floats each) from hv + planes.
-void build_records(const HostScene &s, std::vector<float> &out);
 
 // Volume facts only (hostCode.cu:792-808, 838-840).
 void compute_volume_info(const irt_icon_cell *cells, size_t n, irt_volume_info &info);

@@ -26,7 +26,6 @@
 namespace irt {
 
 enum : int {
-  OPT_BATCH = 1,      // two fat entries per round trip
   OPT_WEDGE = 16384,  // CUBQL / TRIANGLE samplers (locate_wedge, locate_tri); kept out of
                       // the default kernels
   OPT_GRID = 8192,    // GRID_ACCEL_MODE traversal (render_grid); likewise
@@ -34,10 +33,13 @@ enum : int {
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
-// cube-map cell of a sample point.  The lists are rasterised with 1e-5 padding in face
-// coordinates (host/irt_scene.cpp), so the hardware reciprocal (1 ulp) is exact enough:
-// any cell it picks lists every record that can contain the point.
-__device__ __forceinline__ uint32_t cubemap_cell_fast(float px, float py, float pz, int G) {
+// cube-map cell of a sample point, and its sub-cell (irt_build.h).  The lists are
+// rasterised with 1e-5 padding in face coordinates, so the hardware reciprocal (1 ulp) is
+// exact enough: any (sub-)cell it picks lists every record that can contain the point.
+// The kSubCells-times finer index is exact scaling by a power of two: its cell is the
+// coarse grid's cell.
+__device__ __forceinline__ uint32_t cubemap_cell_fast(float px, float py, float pz, int G,
+                                                      uint32_t &sub) {
   const float ax = __builtin_fabsf(px), ay = __builtin_fabsf(py), az = __builtin_fabsf(pz);
   uint32_t face;
   float num0, num1, den;
@@ -58,12 +60,19 @@ __device__ __forceinline__ uint32_t cubemap_cell_fast(float px, float py, float 
     den = az;
   }
   const float inv = __builtin_amdgcn_rcpf(den);
-  const float fg = 0.5f * (float)G;
+  const int GS = G * kSubCells;
+  const float fg = 0.5f * (float)GS;
   int i = (int)((num0 * inv + 1.f) * fg);
   int j = (int)((num1 * inv + 1.f) * fg);
-  i = i < 0 ? 0 : (i >= G ? G - 1 : i);
-  j = j < 0 ? 0 : (j >= G ? G - 1 : j);
-  return face * (uint32_t)G * (uint32_t)G + (uint32_t)j * (uint32_t)G + (uint32_t)i;
+  i = i < 0 ? 0 : (i >= GS ? GS - 1 : i);
+  j = j < 0 ? 0 : (j >= GS ? GS - 1 : j);
+  sub = (uint32_t)((j & (kSubCells - 1)) * kSubCells + (i & (kSubCells - 1)));
+  return face * (uint32_t)G * (uint32_t)G + (uint32_t)(j / kSubCells) * (uint32_t)G +
+         (uint32_t)(i / kSubCells);
+}
+__device__ __forceinline__ uint32_t cubemap_cell_fast(float px, float py, float pz, int G) {
+  uint32_t sub;
+  return cubemap_cell_fast(px, py, pz, G, sub);
 }
 
 template <int OPT>
@@ -114,38 +123,25 @@ struct Tracer {
     float4 ck;
   };
 
-  // First entry of fat entries [q, qe) whose point test passes, among records < limit.
-  // Only the point test runs in the (lane-divergent) loop; getValue's gathers come after.
-  __device__ __forceinline__ bool scan_fat(uint32_t q, uint32_t qe, uint32_t limit, float px,
-                                           float py, float pz, float r, Found &f) {
-    if constexpr ((OPT & OPT_BATCH) != 0) {
-      for (; q < qe; q += 2) {
-        const float4 *F = A.fat + (size_t)q * kFat4;
-        const float4 *F1 = A.fat + (size_t)min(q + 1, qe - 1) * kFat4;
-        const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3], ak = F[4];
-        const float4 b0 = F1[0], b1 = F1[1], b2 = F1[2], bm = F1[3], bk = F1[4];
-        if (__float_as_uint(am.z) >= limit) return false;
-        if (pass_fat(a0, a1, a2, am, px, py, pz, r)) {
-          f = {__float_as_uint(am.z), __float_as_uint(am.w), ak};
-          return true;
-        }
-        if (q + 1 < qe) {
-          if (__float_as_uint(bm.z) >= limit) return false;
-          if (pass_fat(b0, b1, b2, bm, px, py, pz, r)) {
-            f = {__float_as_uint(bm.z), __float_as_uint(bm.w), bk};
-            return true;
-          }
-        }
+  // First entry of fat entries [q, qe) whose point test passes, among records < limit:
+  // of the first kMaskCand entries only those whose bit is set in `mask` (the candidates
+  // that can reach the sample's sub-cell, irt_build.h), then every later one.  Only the
+  // point test runs in the (lane-divergent) loop; getValue's gathers come after.
+  __device__ __forceinline__ bool scan_fat(uint32_t q, uint32_t qe, uint32_t mask, uint32_t limit,
+                                           float px, float py, float pz, float r, Found &f) {
+    const uint32_t n = qe - q;
+    for (uint32_t j = 0;; ++j) {
+      if (j < (uint32_t)kMaskCand) {
+        const uint32_t m = mask >> j;
+        j = m ? j + (uint32_t)__builtin_ctz(m) : (uint32_t)kMaskCand;
       }
-    } else {
-      for (; q < qe; ++q) {
-        const float4 *F = A.fat + (size_t)q * kFat4;
-        const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3], ak = F[4];
-        if (__float_as_uint(am.z) >= limit) return false;
-        if (pass_fat(a0, a1, a2, am, px, py, pz, r)) {
-          f = {__float_as_uint(am.z), __float_as_uint(am.w), ak};
-          return true;
-        }
+      if (j >= n) break;
+      const float4 *F = A.fat + (size_t)(q + j) * kFat4;
+      const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3], ak = F[4];
+      if (__float_as_uint(am.z) >= limit) return false;
+      if (pass_fat(a0, a1, a2, am, px, py, pz, r)) {
+        f = {__float_as_uint(am.z), __float_as_uint(am.w), ak};
+        return true;
       }
     }
     return false;
@@ -276,13 +272,17 @@ struct Tracer {
       return locate_wedge(px, py, pz, value);
     }
     const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
-    const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G);
-    const uint4 H0 = A.binHdr[2 * (size_t)cell], H1 = A.binHdr[2 * (size_t)cell + 1];
-    return locate_hdr(px, py, pz, r, H0, H1, value);
+    uint32_t sub;
+    const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G, sub);
+    // the cell header's words 0..7 and the sub-cell's mask word: one 128-B line
+    const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
+    const uint4 H0 = Hc[0], H1 = Hc[1];
+    const uint32_t M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
+    return locate_hdr(px, py, pz, r, H0, H1, M, value);
   }
 
   __device__ __forceinline__ bool locate_hdr(float px, float py, float pz, float r, const uint4 &H0,
-                                             const uint4 &H1, float &value) {
+                                             const uint4 &H1, uint32_t M, float &value) {
     const float e0 = __uint_as_float(H0.x), e1 = __uint_as_float(H0.y), e2 = __uint_as_float(H0.z);
     const int b = bin_of(r, e0, e1, e2);
     // bin b's [beg, end) from the cumulative ends, and its upper edge, selected with masks
@@ -300,7 +300,7 @@ struct Tracer {
     bool hit = false;
     for (int pass = 0; pass < 2; ++pass) {
       Found g;
-      if (scan_fat(qb, qe, f.rec, px, py, pz, r, g)) {
+      if (scan_fat(qb, qe, (M >> (8 * (b + pass))) & 0xFFu, f.rec, px, py, pz, r, g)) {
         f = g;
         hit = true;
       }
@@ -783,7 +783,7 @@ __global__ void __launch_bounds__(256) k_accumulate(RenderArgs A) {
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
-#define IRT_VARIANTS(X) X(4096) X(4097) X(5120) X(5376) X(36864)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864)
 
 bool render_variant_available(int v) {
 #define IRT_CASE(N) if (v == N) return true;

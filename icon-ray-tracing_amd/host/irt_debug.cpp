@@ -92,35 +92,27 @@ int irt_debug_scene_values(const irt_debug_scene *s, uint32_t rec, float r, floa
   int32_t nl;
   memcpy(&nl, hv + 63, 4);
   out2[0] = hv[32 + find_height(hv, nl, r)];
-  // the render-record path of irt_trace.hip (S_PLN -> S_BLK, or S_HS/S_VAL)
-  std::vector<float> R(kRec4 * 4);
-  {
-    HostScene one;
-    one.n = 1;
-    one.hv.assign(hv, hv + kHV);
-    one.planes.assign(s->s.planes.begin() + 3 * (size_t)rec, s->s.planes.begin() + 3 * (size_t)rec + 3);
-    build_records(one, R);
-  }
-  bool sorted = true;
-  for (int j = 2; j <= nl; ++j)
-    if (!(hv[j - 1] <= hv[j])) sorted = false;
-  if (sorted) {
-    const int b = rec_coarse_block(R[12], R[13], R[14], R[15], nl, r);
-    const float *B = &R[(4 + 4 * b) * 4];
-    const int m = rec_block_index(B[0], B[1], B[2], B[3], B[4], B[5], B[6], b, nl, r);
-    out2[1] = select8(m, B[8], B[9], B[10], B[11], B[12], B[13], B[14], B[15]);
+  // the kernel's path: coarse keys + one 64-B block for sorted heights, else the literal
+  // binary search over the block (irt_render.hip record_value)
+  const float *B = &s->s.blocks[(size_t)rec * kBlk4 * 4];
+  const float *K = &s->s.keys[4 * (size_t)rec];
+  if (s->s.meta[rec] >> 31) {
+    const int b = rec_coarse_block(K[0], K[1], K[2], K[3], nl, r);
+    const float *Q = B + 16 * b;
+    const int m = rec_block_index(Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], Q[6], b, nl, r);
+    out2[1] = select8(m, Q[8], Q[9], Q[10], Q[11], Q[12], Q[13], Q[14], Q[15]);
   } else {
-    uint32_t first = 0, count = (uint32_t)nl;
+    int first = 0, count = nl;
     while (count > 0) {
-      const uint32_t stp = count / 2, it = first + stp;
-      if (!(r <= R[rec_height_pos((int)it + 1)])) {
+      const int stp = count / 2, it = first + stp;
+      if (!(r <= B[blk_height_pos(it + 1)])) {
         first = it + 1;
         count -= stp + 1;
       } else {
         count = stp;
       }
     }
-    out2[1] = R[rec_value_pos((int)first)];
+    out2[1] = B[blk_value_pos(first)];
   }
   return IRT_OK;
 }
@@ -132,13 +124,13 @@ int irt_debug_scene_candidates(const irt_debug_scene *s, irt_vec3f p, uint32_t *
   const uint32_t b = s->s.offsets[cell], e = s->s.offsets[cell + 1];
   int k = 0;
   for (uint32_t i = b; i < e; ++i, ++k)
-    if (records && k < capacity) records[k] = s->s.entries[i].idx;
+    if (records && k < capacity) records[k] = s->s.entryRec[i];
   return k;
 }
 
 int irt_debug_scene_planes(const irt_debug_scene *s, uint32_t record, float *out12) {
   if (!s || !out12 || record >= s->s.n) return IRT_E_INVALID;
-  memcpy(out12, &s->s.planes[3 * (size_t)record], 12 * sizeof(float));
+  memcpy(out12, &s->s.planes[12 * (size_t)record], 12 * sizeof(float));
   return IRT_OK;
 }
 

@@ -33,7 +33,7 @@ MODE_TRIANGLES = 1     # closest bottom triangle toward the centre (deviceCode.c
 MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
 # compiled variants of the raygen (irt_render.hip OPT_* bits; 4096 = one monolithic
 # kernel instead of the setup -> march -> continuation pipeline); all bit-identical
-BIN_VARIANTS = (4096, 4097, 5120, 5376, 36864)
+BIN_VARIANTS = (4096, 5120, 5376, 36864)
 
 
 class IrtError(RuntimeError):
