@@ -25,6 +25,8 @@
 //     cone-versus-cell test; records whose planes carve out no cone go into every cell.
 #pragma once
 
+#include <math.h>
+
 #include "irt_common.h"
 
 namespace irt {
@@ -302,15 +304,17 @@ IRT_HD uint32_t float_key(float v) {
 
 // Expected number of list entries a radius drawn uniformly from [rmin, rmax] meets, for
 // the given edges: sum over bins of (bin length within [rmin, rmax]) * count.
-IRT_HD double bin_cost(const float *h0, const float *hN, int n, const float *edges, int ne,
-                       double rmin, double rmax) {
+// Entries are read through an accessor E: e.h0(k), e.hN(k) (radial extent of the cell's k-th
+// entry, record order) and e.sub(k) (its sub-cell mask) -- host vectors or device arrays.
+template <class E>
+IRT_HD double bin_cost(const E &en, int n, const float *edges, int ne, double rmin, double rmax) {
   double cost = 0;
   for (int k = 0; k <= ne; ++k) {
     const float lo = k ? edges[k - 1] : -__builtin_inff(), hi = k < ne ? edges[k] : __builtin_inff();
     const double a = dmax(rmin, (double)lo), b = dmin(rmax, (double)hi);
     if (!(b > a)) continue;
     int cnt = 0;
-    for (int e = 0; e < n; ++e) cnt += in_bin(h0[e], hN[e], lo, hi) ? 1 : 0;
+    for (int e = 0; e < n; ++e) cnt += in_bin(en.h0(e), en.hN(e), lo, hi) ? 1 : 0;
     cost += (b - a) * (double)cnt;
   }
   return cost;
@@ -319,8 +323,9 @@ IRT_HD double bin_cost(const float *h0, const float *hN, int n, const float *edg
 // Up to kMaxEdges radial edges for one cell, greedily among the records' bottom heights.
 // cand: the distinct bottom heights strictly inside (rmin, rmax), ascending (float_key
 // order), nc of them.  Returns the number of edges, ascending in edges[].
-IRT_HD int choose_edges(const float *h0, const float *hN, int n, const float *cand, int nc,
-                        double rmin, double rmax, float *edges) {
+template <class E>
+IRT_HD int choose_edges(const E &en, int n, const float *cand, int nc, double rmin, double rmax,
+                        float *edges) {
   if (n <= 2) return 0;
   // bound the search: 48 quantiles
   float q[48];
@@ -331,7 +336,7 @@ IRT_HD int choose_edges(const float *h0, const float *hN, int n, const float *ca
     if (nq == 0 || !(q[nq - 1] == v)) q[nq++] = v;
   }
   int ne = 0;
-  double best = bin_cost(h0, hN, n, edges, 0, rmin, rmax);
+  double best = bin_cost(en, n, edges, 0, rmin, rmax);
   while (ne < kMaxEdges) {
     int bi = -1;
     double bc = best;
@@ -352,7 +357,7 @@ IRT_HD int choose_edges(const float *h0, const float *hN, int n, const float *ca
       }
       tr[at] = q[i];
       ++m;
-      const double c = bin_cost(h0, hN, n, tr, m, rmin, rmax);
+      const double c = bin_cost(en, n, tr, m, rmin, rmax);
       if (c < bc * 0.98) {
         bc = c;
         bi = i;
@@ -371,19 +376,19 @@ IRT_HD int choose_edges(const float *h0, const float *hN, int n, const float *ca
   return ne;
 }
 
-// The radial range a cell's entries span and its sorted distinct inner bottom heights
-// (insertion sort: the device path, n small; the host sorts with the same key).
-IRT_HD int cell_candidates(const float *h0, const float *hN, int n, float *cand, double &rmin,
-                           double &rmax) {
+// The radial range a cell's entries span and its distinct bottom heights strictly inside
+// it, ascending (float_key order; insertion sort, so cand needs room for n).
+template <class E>
+IRT_HD int cell_candidates(const E &en, int n, float *cand, double &rmin, double &rmax) {
   rmin = __builtin_inf();
   rmax = -__builtin_inf();
   for (int e = 0; e < n; ++e) {
-    rmin = dmin(rmin, (double)h0[e]);
-    rmax = dmax(rmax, (double)hN[e]);
+    rmin = dmin(rmin, (double)en.h0(e));
+    rmax = dmax(rmax, (double)en.hN(e));
   }
   int nc = 0;
   for (int e = 0; e < n; ++e) {
-    const float v = h0[e];
+    const float v = en.h0(e);
     if (!((double)v > rmin && (double)v < rmax)) continue;
     bool dup = false;
     for (int k = 0; k < nc; ++k)
@@ -411,8 +416,8 @@ IRT_HD int cell_candidates(const float *h0, const float *hN, int n, float *cand,
 //
 // Fills every word but the base from a cell's n entries (in record order: bottom/top
 // heights and sub-cell masks) and its ne edges; returns the cell's number of fat entries.
-IRT_HD uint32_t cell_header(const float *h0, const float *hN, const uint32_t *sub, int n,
-                            const float *edges, int ne, uint32_t *H) {
+template <class E>
+IRT_HD uint32_t cell_header(const E &en, int n, const float *edges, int ne, uint32_t *H) {
   for (int w = 0; w < kBinHdrWords; ++w) H[w] = 0u;
   for (int k = 0; k < kMaxEdges; ++k) H[k] = f2u(k < ne ? edges[k] : __builtin_inff());
   uint32_t cum = 0;
@@ -421,10 +426,12 @@ IRT_HD uint32_t cell_header(const float *h0, const float *hN, const uint32_t *su
       const float lo = k ? edges[k - 1] : -__builtin_inff(), hi = k < ne ? edges[k] : __builtin_inff();
       int j = 0;
       for (int e = 0; e < n; ++e) {
-        if (!in_bin(h0[e], hN[e], lo, hi)) continue;
-        if (j < kMaskCand)
+        if (!in_bin(en.h0(e), en.hN(e), lo, hi)) continue;
+        if (j < kMaskCand) {
+          const uint32_t sm = en.sub(e);
           for (int s = 0; s < kSub * kSub; ++s)
-            if ((sub[e] >> s) & 1u) H[8 + s] |= 1u << (8 * k + j);
+            if ((sm >> s) & 1u) H[8 + s] |= 1u << (8 * k + j);
+        }
         ++j;
         ++cum;
       }

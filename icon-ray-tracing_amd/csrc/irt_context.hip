@@ -7,8 +7,12 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
+#include <cstdio>
+#include <thread>
 #include <vector>
 
+#include "irt_build.h"
 #include "irt_internal.h"
 #include "icon_rt_hip_debug.h"
 #include "irt_kernels.h"
@@ -35,7 +39,9 @@ struct irt_context {
   uint4 *d_binHdr = nullptr;   // binned locator (irt_common.h)
   float4 *d_fat = nullptr;
   float4 *d_blocks = nullptr;
-  uint32_t numSph = 0;         // zero-thickness records (spheres)
+  size_t binEntries = 0;       // fat entries
+  uint32_t numSph = 0;         // zero-thickness records (spheres): distinct radii
+  uint32_t numSphRec = 0;      // ... and records
   float *d_sphR = nullptr;
   uint32_t *d_sphOff = nullptr;
   uint2 *d_sphRec = nullptr;
@@ -105,6 +111,22 @@ struct irt_context {
   long long schedSrc = -1;      // launch whose costs the current order came from
   long long schedCopied[kSlots] = {};  // launch index whose costs slot i holds (-1: none)
   long long schedLastCopy = -1000;
+  // streaming creation (irt_create_begin / _append / _end): the cells and their glibc
+  // corner trig go to HBM chunk by chunk; the volume facts, column count and sphere
+  // records are folded on the host in record order
+  bool building = false;
+  size_t expected = 0, received = 0;
+  irt_icon_cell *d_cells = nullptr;  // freed once the scene is built
+  float4 *d_trig = nullptr;
+  VolumeAcc vacc{};
+  size_t numRuns = 0;
+  irt_icon_cell last{};
+  struct Sphere {
+    float r;
+    uint32_t rec;
+    int32_t nl;
+  };
+  std::vector<Sphere> sph;  // zero-thickness records
 };
 
 namespace {
@@ -134,6 +156,8 @@ void free_all(irt_context *c) {
                   c->d_lut, c->d_counters};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
+  if (c->d_cells) (void)hipFree(c->d_cells);
+  if (c->d_trig) (void)hipFree(c->d_trig);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   if (c->h_schedCost) (void)hipHostFree(c->h_schedCost);
   if (c->h_schedOrder) (void)hipHostFree(c->h_schedOrder);
@@ -442,12 +466,16 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
 
 extern "C" {
 
-int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_context **out) {
-  if (!out || (numCells && !cells)) {
+int irt_create_begin(size_t numCells, int device, irt_context **out) {
+  if (!out) {
     set_error("irt_create: null argument");
     return IRT_E_INVALID;
   }
   *out = nullptr;
+  if (numCells > 0xFFFFFFF0ull) {
+    set_error("too many cells (%zu)", numCells);
+    return IRT_E_INVALID;
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
     set_error("irt_create: no HIP device visible (this product has no CPU fallback)");
@@ -457,12 +485,6 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
     set_error("irt_create: device %d out of range (%d devices)", device, ndev);
     return IRT_E_INVALID;
   }
-  HostScene S;
-  int rc = build_scene(cells, numCells, S);
-  if (rc) return rc;
-  float th[256];
-  srgb_thresholds(th);
-
   irt_context *c = new irt_context();
   c->device = device;
   if (const char *v = getenv("IRT_RENDER_VARIANT")) {
@@ -482,98 +504,287 @@ int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_cont
     c->schedOn = atoi(e) != 0;
     c->schedPolicy = atoi(e);
   }
-  c->info = S.info;
-  c->n = (uint32_t)S.n;
-  c->G = S.G;
-  if ((rc = upload(c, &c->d_binHdr, (const uint4 *)S.binHdr.data(), S.binHdr.size() / 4))) return fail(rc);
-  if ((rc = upload(c, &c->d_fat, (const float4 *)S.fat.data(), S.fat.size() / 4))) return fail(rc);
-  if ((rc = upload(c, &c->d_blocks, (const float4 *)S.blocks.data(), S.blocks.size() / 4))) return fail(rc);
-  {
-    std::vector<uint2> sr(S.sphRec.size());
-    for (size_t k = 0; k < sr.size(); ++k) {
-      const uint32_t rec = S.sphRec[k];
-      sr[k] = make_uint2(rec, (uint32_t)cells[rec].numLayers);
-    }
-    c->numSph = (uint32_t)S.sphR.size();
-    if ((rc = upload(c, &c->d_sphR, S.sphR.data(), S.sphR.size()))) return fail(rc);
-    if ((rc = upload(c, &c->d_sphOff, S.sphOff.data(), S.sphOff.size()))) return fail(rc);
-    if ((rc = upload(c, &c->d_sphRec, sr.data(), sr.size()))) return fail(rc);
-    if ((rc = upload(c, &c->d_sphBits, S.sphBits.data(), S.sphBits.size()))) return fail(rc);
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(IRT_E_HIP);  // sr
-  }
-  const int dims[3] = {S.info.shellDims[0], S.info.shellDims[1], S.info.shellDims[2]};
-  c->numMCs = (size_t)dims[0] * dims[1] * dims[2];
-  if ((rc = dalloc(c, &c->d_maxOp, c->numMCs))) return fail(rc);
-  if (hipMemsetAsync(c->d_maxOp, 0, c->numMCs * sizeof(float), c->stream) != hipSuccess) return fail(IRT_E_HIP);
-  if ((rc = upload(c, &c->d_srgb, th, 256))) return fail(rc);
-  if ((rc = dalloc(c, &c->d_counters, 16 * irt_context::kSlots))) return fail(rc);
-  if (hipHostMalloc((void **)&c->h_counters, 16 * irt_context::kSlots * sizeof(unsigned long long)) != hipSuccess) {
-    set_error("irt_create: pinned allocation failed");
+  if (hipMalloc((void **)&c->d_cells, std::max<size_t>(numCells, 1) * sizeof(irt_icon_cell)) != hipSuccess ||
+      hipMalloc((void **)&c->d_trig, std::max<size_t>(numCells, 1) * 3 * sizeof(float4)) != hipSuccess) {
+    set_error("irt_create: cannot allocate %zu cells in HBM", numCells);
     return fail(IRT_E_HIP);
   }
-  for (int i = 0; i < irt_context::kSlots; ++i)
-    if (hipEventCreate(&c->ev0[i]) != hipSuccess || hipEventCreate(&c->ev1[i]) != hipSuccess ||
-        hipEventCreate(&c->evDone[i]) != hipSuccess) {
-      set_error("irt_create: event creation failed");
-      return fail(IRT_E_HIP);
+  volume_acc_init(c->vacc);
+  c->expected = numCells;
+  c->building = true;
+  *out = c;
+  return IRT_OK;
+}
+
+int irt_create_append(irt_context *c, const irt_icon_cell *cells, size_t n) {
+  if (!c || !c->building || (n && !cells)) {
+    set_error("irt_create_append: no context being created, or null cells");
+    return IRT_E_INVALID;
+  }
+  if (n > c->expected - c->received) {
+    set_error("irt_create_append: %zu more cells than irt_create_begin announced", n - (c->expected - c->received));
+    return IRT_E_INVALID;
+  }
+  if (n == 0) return IRT_OK;
+  const size_t base = c->received;
+  for (size_t i = 0; i < n; ++i) {
+    if (cells[i].numLayers < 0 || cells[i].numLayers > 31) {
+      set_error("cell %zu: numLayers %d outside [0,31] (MAX_LAYERS 32, ICONGrid.h:57)", base + i,
+                cells[i].numLayers);
+      return IRT_E_DATA;
     }
+    const irt_icon_cell &x = cells[i];
+    bool finite = true;
+    for (int k = 0; k < 3; ++k) finite = finite && std::isfinite(x.lat[k]) && std::isfinite(x.lon[k]);
+    for (int j = 0; j <= x.numLayers; ++j) finite = finite && std::isfinite(x.height[j]);
+    if (!finite) {
+      set_error("cell %zu: non-finite lat/lon/height", base + i);
+      return IRT_E_DATA;
+    }
+  }
+  // corner trig (host glibc: the only libm values the device build needs) and getBounds,
+  // per record in parallel; then the order-dependent folds in record order
+  std::vector<float> trig(n * 12), bnd(n * 6);
+  {
+    const int threads = n < 4096 ? 1 : default_threads();
+    std::vector<std::thread> ts;
+    const size_t chunk = (n + threads - 1) / threads;
+    for (int t = 0; t < threads; ++t)
+      ts.emplace_back([&, t] {
+        for (size_t i = t * chunk; i < std::min(n, (t + 1) * chunk); ++i) {
+          float *tr = &trig[12 * i];
+          if (i > 0 && same_corners(cells[i].lat, cells[i].lon, cells[i - 1].lat, cells[i - 1].lon) &&
+              i != t * chunk)
+            memcpy(tr, tr - 12, 12 * sizeof(float));  // same column, same corners
+          else
+            corner_trig(cells[i], tr);
+          cell_bounds(cells[i], tr, &bnd[6 * i], &bnd[6 * i + 3]);
+        }
+      });
+    for (auto &t : ts) t.join();
+  }
+  for (size_t i = 0; i < n; ++i) {
+    volume_acc_add(c->vacc, cells[i], &bnd[6 * i], &bnd[6 * i + 3]);
+    const irt_icon_cell &prev = i ? cells[i - 1] : c->last;
+    if (base + i == 0 || !same_corners(cells[i].lat, cells[i].lon, prev.lat, prev.lon)) ++c->numRuns;
+    if (cells[i].height[0] == cells[i].height[cells[i].numLayers])  // a sphere record
+      c->sph.push_back({cells[i].height[0], (uint32_t)(base + i), cells[i].numLayers});
+  }
+  IRT_HIP(hipSetDevice(c->device));
+  IRT_HIP(hipMemcpy(c->d_cells + base, cells, n * sizeof(irt_icon_cell), hipMemcpyHostToDevice));
+  IRT_HIP(hipMemcpy(c->d_trig + 3 * base, trig.data(), n * 12 * sizeof(float), hipMemcpyHostToDevice));
+  c->last = cells[n - 1];
+  c->received += n;
+  return IRT_OK;
+}
+
+int irt_create_end(irt_context *c) {
+  if (!c || !c->building) {
+    set_error("irt_create_end: no context being created");
+    return IRT_E_INVALID;
+  }
+  if (c->received != c->expected) {
+    set_error("irt_create_end: %zu of %zu cells appended", c->received, c->expected);
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(c->device));
+  const size_t numCells = c->expected;
+  const bool verbose = getenv("IRT_BUILD_VERBOSE") != nullptr;
+  auto t0 = std::chrono::steady_clock::now();
+  auto mark = [&](const char *what) {
+    if (!verbose) return;
+    (void)hipStreamSynchronize(c->stream);
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "[irt create] %-20s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+    t0 = t;
+  };
+  volume_acc_finish(c->vacc, c->info);
+  c->n = (uint32_t)numCells;
+  c->G = locator_resolution(c->numRuns);
+  // the scene build on the device (irt_build.hip)
+  DeviceScene D;
+  int rc = build_scene_device(c->d_cells, c->d_trig, numCells, c->numRuns, c->G, c->stream, D);
+  c->d_blocks = D.blocks;
+  c->d_binHdr = D.binHdr;
+  c->d_fat = D.fat;
+  c->bytes += D.bytes;
+  if (rc) return rc;
+  c->info.locatorFaceRes = c->G;
+  c->info.locatorEntries = D.entries;
+  c->binEntries = D.binEntries;
+  mark("device scene build");
+  // zero-thickness records (spheres): sorted by (radius, record) -- see host/irt_scene.cpp
+  {
+    std::sort(c->sph.begin(), c->sph.end(), [](const irt_context::Sphere &a, const irt_context::Sphere &b) {
+      return a.r < b.r || (a.r == b.r && a.rec < b.rec);
+    });
+    std::vector<float> R;
+    std::vector<uint32_t> off(1, 0u), bits(kSphBitWords, 0u);
+    std::vector<uint2> rec;
+    for (size_t k = 0; k < c->sph.size(); ++k) {
+      if (k == 0 || c->sph[k].r != c->sph[k - 1].r) {
+        if (k) off.push_back((uint32_t)rec.size());
+        R.push_back(c->sph[k].r);
+      }
+      rec.push_back(make_uint2(c->sph[k].rec, (uint32_t)c->sph[k].nl));
+    }
+    if (!c->sph.empty()) off.push_back((uint32_t)rec.size());
+    for (float r : R) {
+      const uint32_t h = sph_hash(r);
+      bits[h >> 5] |= 1u << (h & 31);
+    }
+    c->numSph = (uint32_t)R.size();
+    c->numSphRec = (uint32_t)rec.size();
+    if ((rc = upload(c, &c->d_sphR, R.data(), R.size())) || (rc = upload(c, &c->d_sphOff, off.data(), off.size())) ||
+        (rc = upload(c, &c->d_sphRec, rec.data(), rec.size())) ||
+        (rc = upload(c, &c->d_sphBits, bits.data(), bits.size())))
+      return rc;
+    IRT_HIP(hipStreamSynchronize(c->stream));
+    std::vector<irt_context::Sphere>().swap(c->sph);
+  }
+  mark("sphere table");
+  float th[256];
+  srgb_thresholds(th);
+  mark("sRGB thresholds");
+  const int dims[3] = {c->info.shellDims[0], c->info.shellDims[1], c->info.shellDims[2]};
+  c->numMCs = (size_t)dims[0] * dims[1] * dims[2];
+  if ((rc = dalloc(c, &c->d_maxOp, c->numMCs))) return rc;
+  IRT_HIP(hipMemsetAsync(c->d_maxOp, 0, c->numMCs * sizeof(float), c->stream));
+  if ((rc = upload(c, &c->d_srgb, th, 256))) return rc;
+  if ((rc = dalloc(c, &c->d_counters, 16 * irt_context::kSlots))) return rc;
+  IRT_HIP(hipHostMalloc((void **)&c->h_counters, 16 * irt_context::kSlots * sizeof(unsigned long long)));
+  for (int i = 0; i < irt_context::kSlots; ++i) {
+    IRT_HIP(hipEventCreate(&c->ev0[i]));
+    IRT_HIP(hipEventCreate(&c->ev1[i]));
+    IRT_HIP(hipEventCreate(&c->evDone[i]));
+  }
   memset(c->h_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long));
   if (const char *e = getenv("IRT_COUNTERS")) c->wgCountsOn = strcmp(e, "atomic") != 0;
   if (const char *e = getenv("IRT_TIMING_EVERY")) c->timingEvery = std::max(1, atoi(e));
-  if (hipHostGetDevicePointer((void **)&c->dh_counters, c->h_counters, 0) != hipSuccess ||
-      hipMemsetAsync(c->d_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long),
-                     c->stream) != hipSuccess ||
-      hipStreamSynchronize(c->stream) != hipSuccess) {
-    set_error("irt_create: statistics ring setup failed");
-    return fail(IRT_E_HIP);
-  }
+  IRT_HIP(hipHostGetDevicePointer((void **)&c->dh_counters, c->h_counters, 0));
+  IRT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long), c->stream));
 
   // ShellAccel{vec3i(1,1024,1024), sphericalBounds} + initGrid + buildShell_ICON
   // (hostCode.cu:652-666), majorants zero until a transfer function arrives
-  if ((rc = dalloc(c, &c->d_valueRanges, 2 * c->numMCs))) return fail(rc);
+  if ((rc = dalloc(c, &c->d_valueRanges, 2 * c->numMCs))) return rc;
   launch_shell_init(c->d_valueRanges, c->numMCs, c->stream);
   const size_t gridMCs = (size_t)kGridDim * kGridDim * kGridDim;
-  if ((rc = dalloc(c, &c->d_gridVR, 2 * gridMCs))) return fail(rc);
-  if ((rc = dalloc(c, &c->d_gridMaxOp, gridMCs))) return fail(rc);
+  if ((rc = dalloc(c, &c->d_gridVR, 2 * gridMCs))) return rc;
+  if ((rc = dalloc(c, &c->d_gridMaxOp, gridMCs))) return rc;
   launch_shell_init(c->d_gridVR, gridMCs, c->stream);  // initGrid(Grid) (hostCode.cu:205-214)
-  if (hipMemsetAsync(c->d_gridMaxOp, 0, gridMCs * sizeof(float), c->stream) != hipSuccess) return fail(IRT_E_HIP);
+  IRT_HIP(hipMemsetAsync(c->d_gridMaxOp, 0, gridMCs * sizeof(float), c->stream));
   if (numCells) {
-    irt_icon_cell *d_cells = nullptr;
-    if (hipMalloc((void **)&d_cells, numCells * sizeof(irt_icon_cell)) != hipSuccess ||
-        hipMemcpyAsync(d_cells, cells, numCells * sizeof(irt_icon_cell), hipMemcpyHostToDevice,
-                       c->stream) != hipSuccess) {
-      set_error("irt_create: cell upload failed");
-      if (d_cells) (void)hipFree(d_cells);
-      return fail(IRT_E_HIP);
-    }
-    const irt_box3f &sb = S.info.sphericalBounds;
-    launch_shell_build(d_cells, numCells, make_int3(dims[0], dims[1], dims[2]),
+    const irt_box3f &sb = c->info.sphericalBounds;
+    launch_shell_build(c->d_cells, numCells, make_int3(dims[0], dims[1], dims[2]),
                        make_float3(sb.lower.x, sb.lower.y, sb.lower.z),
                        make_float3(sb.upper.x, sb.upper.y, sb.upper.z), c->d_valueRanges, c->stream);
     // buildICONGrid (hostCode.cu:668-682): initGrid + buildGrid_ICON over volbounds
-    float4 *d_trig = nullptr;
-    hipError_t e = hipMalloc((void **)&d_trig, numCells * 3 * sizeof(float4));
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(d_trig, S.trig.data(), numCells * 3 * sizeof(float4), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) {
-      const irt_box3f &vb = S.info.bounds;
-      launch_grid_build(d_cells, d_trig, numCells, make_float3(vb.lower.x, vb.lower.y, vb.lower.z),
-                        make_float3(vb.upper.x, vb.upper.y, vb.upper.z), c->d_gridVR, c->stream);
-      e = hipStreamSynchronize(c->stream);
-    }
-    if (d_trig) (void)hipFree(d_trig);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    (void)hipFree(d_cells);
-    if (e != hipSuccess || hipGetLastError() != hipSuccess) {
-      set_error("irt_create: shell build failed: %s", hipGetErrorString(e));
-      return fail(IRT_E_HIP);
-    }
+    const irt_box3f &vb = c->info.bounds;
+    launch_grid_build(c->d_cells, c->d_trig, numCells, make_float3(vb.lower.x, vb.lower.y, vb.lower.z),
+                      make_float3(vb.upper.x, vb.upper.y, vb.upper.z), c->d_gridVR, c->stream);
   }
-  if (hipStreamSynchronize(c->stream) != hipSuccess) {
-    set_error("irt_create: upload failed");
-    return fail(IRT_E_HIP);
-  }
+  IRT_HIP(hipGetLastError());
+  IRT_HIP(hipStreamSynchronize(c->stream));
+  mark("shell + grid builds");
+  IRT_HIP(hipFree(c->d_cells));
+  IRT_HIP(hipFree(c->d_trig));
+  c->d_cells = nullptr;
+  c->d_trig = nullptr;
+  c->building = false;
   c->info.deviceBytes = c->bytes;
+  return IRT_OK;
+}
+
+int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_context **out) {
+  if (!out || (numCells && !cells)) {
+    set_error("irt_create: null argument");
+    return IRT_E_INVALID;
+  }
+  irt_context *c = nullptr;
+  int rc = irt_create_begin(numCells, device, &c);
+  if (rc) return rc;
+  if ((rc = irt_create_append(c, cells, numCells)) || (rc = irt_create_end(c))) {
+    irt_destroy(c);
+    *out = nullptr;
+    return rc;
+  }
+  *out = c;
+  return IRT_OK;
+}
+
+// streamed creation helpers: records arrive in chunks of kChunk
+static constexpr size_t kChunk = size_t(1) << 20;
+
+int irt_create_from_file(const char *path, long maxNumCells, int device, irt_context **out) {
+  if (!path || !out) {
+    set_error("irt_create_from_file: null argument");
+    return IRT_E_INVALID;
+  }
+  *out = nullptr;
+  FILE *f = fopen(path, "rb");
+  if (!f) {
+    set_error("irt_create_from_file: cannot open %s", path);
+    return IRT_E_IO;
+  }
+  fseek(f, 0, SEEK_END);
+  const long size = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  size_t n = (size_t)size / sizeof(irt_icon_cell);  // hostCode.cu:725
+  if (maxNumCells >= 0) n = std::min(n, (size_t)maxNumCells);  // hostCode.cu:728-730
+  irt_context *c = nullptr;
+  int rc = irt_create_begin(n, device, &c);
+  if (rc) {
+    fclose(f);
+    return rc;
+  }
+  std::vector<irt_icon_cell> buf(std::min(n, kChunk));
+  for (size_t at = 0; at < n && !rc; at += buf.size()) {
+    const size_t m = std::min(buf.size(), n - at);
+    if (fread(buf.data(), sizeof(irt_icon_cell), m, f) != m) {
+      set_error("irt_create_from_file: short read at record %zu", at);
+      rc = IRT_E_IO;
+      break;
+    }
+    rc = irt_create_append(c, buf.data(), m);
+  }
+  fclose(f);
+  if (!rc) rc = irt_create_end(c);
+  if (rc) {
+    irt_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return IRT_OK;
+}
+
+int irt_create_synth(int rootN, int bisections, int levels, float topHeight, float noise,
+                     uint32_t seed, int device, irt_context **out) {
+  if (!out) {
+    set_error("irt_create_synth: null argument");
+    return IRT_E_INVALID;
+  }
+  *out = nullptr;
+  void *gen = nullptr;
+  size_t n = 0;
+  int rc = synth_open(rootN, bisections, levels, topHeight, noise, seed, &gen, &n);
+  if (rc) return rc;
+  irt_context *c = nullptr;
+  if ((rc = irt_create_begin(n, device, &c))) {
+    synth_close(gen);
+    return rc;
+  }
+  std::vector<irt_icon_cell> buf(std::min(n, kChunk));
+  for (size_t at = 0; at < n && !rc; at += buf.size()) {
+    const size_t m = std::min(buf.size(), n - at);
+    synth_fill(gen, at, m, buf.data());
+    rc = irt_create_append(c, buf.data(), m);
+  }
+  synth_close(gen);
+  if (!rc) rc = irt_create_end(c);
+  if (rc) {
+    irt_destroy(c);
+    return rc;
+  }
   *out = c;
   return IRT_OK;
 }
@@ -864,6 +1075,35 @@ extern "C" int irt_debug_counters(irt_context *c, unsigned long long *out16) {
 }
 
 extern "C" int irt_debug_default_variant(void) { return kDefaultVariant; }
+
+extern "C" int irt_debug_context_array(const irt_context *c, int which, void *dst, size_t capacity,
+                                       size_t *bytes) {
+  if (!c || !bytes || c->building) {
+    set_error("irt_debug_context_array: null argument or context not built");
+    return IRT_E_INVALID;
+  }
+  const void *src = nullptr;
+  size_t n = 0;
+  switch (which) {
+    case IRT_DEBUG_ARRAY_BIN_HDR: src = c->d_binHdr; n = (size_t)6 * c->G * c->G * kBinHdrWords * 4; break;
+    case IRT_DEBUG_ARRAY_FAT: src = c->d_fat; n = c->binEntries * kFat4 * 16; break;
+    case IRT_DEBUG_ARRAY_BLOCKS: src = c->d_blocks; n = (size_t)c->n * kBlk4 * 16; break;
+    case IRT_DEBUG_ARRAY_SPH_R: src = c->d_sphR; n = (size_t)c->numSph * 4; break;
+    case IRT_DEBUG_ARRAY_SPH_OFF: src = c->d_sphOff; n = c->numSph ? ((size_t)c->numSph + 1) * 4 : 4; break;
+    case IRT_DEBUG_ARRAY_SPH_REC: src = c->d_sphRec; n = (size_t)c->numSphRec * 8; break;
+    case IRT_DEBUG_ARRAY_SPH_BITS: src = c->d_sphBits; n = (size_t)kSphBitWords * 4; break;
+    default:
+      set_error("irt_debug_context_array: unknown array %d", which);
+      return IRT_E_INVALID;
+  }
+  *bytes = n;
+  if (dst && capacity >= n && n) {
+    IRT_HIP(hipSetDevice(c->device));
+    IRT_HIP(hipStreamSynchronize(c->stream));
+    IRT_HIP(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
+  }
+  return IRT_OK;
+}
 
 extern "C" int irt_debug_set_variant(irt_context *c, int variant) {
   if (!c || !render_variant_available(variant)) {

@@ -57,6 +57,17 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &out, int thread
 
 // Volume facts only (hostCode.cu:792-808, 838-840).
 void compute_volume_info(const irt_icon_cell *cells, size_t n, irt_volume_info &info);
+// ... as a fold over records in order, for chunked input: per record the corner trig
+// (glibc cosf/sinf) and getBounds (ICONGrid.h:78-115), then volume_acc_add in record order.
+struct VolumeAcc {
+  float vlo[3], vhi[3], slo[3], shi[3], dlo, dhi;
+  size_t n;
+};
+void corner_trig(const irt_icon_cell &c, float *t12);
+void cell_bounds(const irt_icon_cell &c, const float *t12, float lo[3], float hi[3]);
+void volume_acc_init(VolumeAcc &a);
+void volume_acc_add(VolumeAcc &a, const irt_icon_cell &c, const float blo[3], const float bhi[3]);
+void volume_acc_finish(const VolumeAcc &a, irt_volume_info &info);
 
 // glibc logf(1 - k/2^24) for k in [0, 2^24): the only arguments woodcockTracking's
 // `logf(1.f - rnd())` (deviceCode.cu:165) can ever see.
@@ -94,5 +105,11 @@ bool triangle_locate_host(const WedgeScene &W, const irt_icon_cell *cells, float
                           float pz, float &value, uint32_t *record);
 
 int default_threads();
+
+// Synthetic RnBk grid generator (host/irt_synth.cpp): open once, fill any record range.
+int synth_open(int rootN, int bisections, int levels, float topHeight, float noise, uint32_t seed,
+               void **gen, size_t *total);
+void synth_fill(const void *gen, size_t first, size_t count, irt_icon_cell *out);
+void synth_close(void *gen);
 
 }  // namespace irt

@@ -90,6 +90,17 @@ void launch_clear(uint32_t *fb, float4 *accum, size_t n, hipStream_t s);
 void launch_stats_out(const unsigned long long *cur, const uint32_t *wgCounts, size_t numWG,
                       unsigned long long *host, unsigned long long *next, hipStream_t s);
 void launch_copy_u32(const uint32_t *src, uint32_t *dst, size_t n, hipStream_t s);
+// The scene build on the device (irt_build.hip): per-record blocks and the binned cube-map
+// locator (irt_build.h) from the cells and their glibc corner trig in HBM.  On success the
+// caller owns blocks / binHdr / fat; on failure it frees whatever is non-null.
+struct DeviceScene {
+  float4 *blocks = nullptr;
+  uint4 *binHdr = nullptr;
+  float4 *fat = nullptr;
+  size_t entries = 0, binEntries = 0, bigCells = 0, bytes = 0;
+};
+int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_t n, size_t numRuns,
+                       int G, hipStream_t s, DeviceScene &out);
 void launch_unpack(const uint32_t *gathered, int numRanks, int maxTiles, int W, int H,
                    uint32_t *fb, hipStream_t s);
 

@@ -91,14 +91,17 @@ __global__ void k_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, f
 // cosf/sinf come precomputed from the host (trig = {cos lat, sin lat, cos lon, sin lon}
 // per corner, host/irt_scene.cpp), the rest is the same float expressions.  Consecutive
 // layers covering the same macrocell box are merged before the CAS-loop min/max (the
-// same min/max).  One lane per cell.
+// same min/max).
 __device__ __forceinline__ float3 to_cartesian_trig(float r, const float4 &t) {
   return make_float3((r * t.x) * t.z, (r * t.x) * t.w, r * t.y);  // ICONGrid.h:44-54
 }
 
-__global__ void k_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n, int dim,
-                             float3 lo, float3 hi, float *valueRanges) {
-  const size_t ci = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(64) k_grid_build(const irt_icon_cell *cells, const float4 *trig,
+                                                   size_t n, int dim, float3 lo, float3 hi,
+                                                   float *valueRanges) {
+  // one wave per cell: every lane walks the layers (the merge logic is uniform), the lanes
+  // share each merged box's macrocells
+  const size_t ci = blockIdx.x;
   if (ci >= n) return;
   const irt_icon_cell &c = cells[ci];
   const float4 t0 = trig[3 * ci], t1 = trig[3 * ci + 1], t2 = trig[3 * ci + 2];
@@ -106,13 +109,16 @@ __global__ void k_grid_build(const irt_icon_cell *cells, const float4 *trig, siz
   float rLo = 0.f, rHi = 0.f;
   bool have = false;
   auto flush = [&]() {
-    for (int mz = pLo.z; mz <= pHi.z; ++mz)
-      for (int my = pLo.y; my <= pHi.y; ++my)
-        for (int mx = pLo.x; mx <= pHi.x; ++mx) {
-          float *vr = valueRanges + 2 * ((size_t)mz * dim * dim + (size_t)my * dim + mx);
-          atomic_min_f(vr, rLo);
-          atomic_max_f(vr + 1, rHi);
-        }
+    const int nx = pHi.x - pLo.x + 1, ny = pHi.y - pLo.y + 1, nz = pHi.z - pLo.z + 1;
+    const long total = (long)nx * ny * nz;
+    for (long q = threadIdx.x; q < total; q += blockDim.x) {
+      const int mx = pLo.x + (int)(q % nx);
+      const int my = pLo.y + (int)((q / nx) % ny);
+      const int mz = pLo.z + (int)(q / ((long)nx * ny));
+      float *vr = valueRanges + 2 * ((size_t)mz * dim * dim + (size_t)my * dim + mx);
+      atomic_min_f(vr, rLo);
+      atomic_max_f(vr + 1, rHi);
+    }
   };
   for (int i = 0; i < c.numLayers; ++i) {
     const float hb = c.height[i], ht = c.height[i + 1];
@@ -250,8 +256,8 @@ void launch_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, float3 
 void launch_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n, float3 lo,
                        float3 hi, float *vr, hipStream_t s) {
   if (n == 0) return;
-  hipLaunchKernelGGL(k_grid_build, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, cells, trig,
-                     n, kGridDim, lo, hi, vr);
+  hipLaunchKernelGGL(k_grid_build, dim3((unsigned)n), dim3(64), 0, s, cells, trig, n, kGridDim, lo,
+                     hi, vr);
 }
 void launch_max_opacities(const float *vr, size_t numMCs, const float4 *lut, int size, float lo,
                           float hi, float *maxOp, hipStream_t s) {

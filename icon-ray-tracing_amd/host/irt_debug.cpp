@@ -136,6 +136,42 @@ int irt_debug_scene_planes(const irt_debug_scene *s, uint32_t record, float *out
 
 void irt_debug_scene_free(irt_debug_scene *s) { delete s; }
 
+int irt_debug_scene_array(const irt_debug_scene *s, int which, void *dst, size_t capacity,
+                          size_t *bytes) {
+  if (!s || !bytes) {
+    set_error("irt_debug_scene_array: null argument");
+    return IRT_E_INVALID;
+  }
+  const HostScene &S = s->s;
+  std::vector<uint32_t> rec;
+  const void *src = nullptr;
+  size_t n = 0;
+  switch (which) {
+    case IRT_DEBUG_ARRAY_BIN_HDR: src = S.binHdr.data(); n = S.binHdr.size() * 4; break;
+    case IRT_DEBUG_ARRAY_FAT: src = S.fat.data(); n = S.fat.size() * 4; break;
+    case IRT_DEBUG_ARRAY_BLOCKS: src = S.blocks.data(); n = S.blocks.size() * 4; break;
+    case IRT_DEBUG_ARRAY_SPH_R: src = S.sphR.data(); n = S.sphR.size() * 4; break;
+    case IRT_DEBUG_ARRAY_SPH_OFF: src = S.sphOff.data(); n = S.sphOff.size() * 4; break;
+    case IRT_DEBUG_ARRAY_SPH_REC:
+      for (uint32_t r : S.sphRec) {
+        int32_t nl;
+        memcpy(&nl, &S.hv[(size_t)r * kHV + 63], 4);
+        rec.push_back(r);
+        rec.push_back((uint32_t)nl);
+      }
+      src = rec.data();
+      n = rec.size() * 4;
+      break;
+    case IRT_DEBUG_ARRAY_SPH_BITS: src = S.sphBits.data(); n = S.sphBits.size() * 4; break;
+    default:
+      set_error("irt_debug_scene_array: unknown array %d", which);
+      return IRT_E_INVALID;
+  }
+  *bytes = n;
+  if (dst && capacity >= n && n) memcpy(dst, src, n);
+  return IRT_OK;
+}
+
 int irt_debug_scene_locate_wedge(irt_debug_scene *s, irt_vec3f p, float *value) {
   if (!s || !value) return IRT_E_INVALID;
   if (s->w.G == 0) {

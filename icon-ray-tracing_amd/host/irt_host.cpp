@@ -88,18 +88,32 @@ inline V3 toCartesian(float r, float lat, float lon) {
 }
 }  // namespace
 
-// ICONCell::getBounds (ICONGrid.h:78-115)
-static void cell_bounds(const irt_icon_cell &c, V3 &lo, V3 &hi) {
-  lo = splat(INFINITY);
-  hi = splat(-INFINITY);
+// corner trig {cosf lat, sinf lat, cosf lon, sinf lon} x 3 (host glibc)
+void corner_trig(const irt_icon_cell &c, float *t12) {
+  for (int k = 0; k < 3; ++k) {
+    t12[4 * k + 0] = cosf(c.lat[k]);
+    t12[4 * k + 1] = sinf(c.lat[k]);
+    t12[4 * k + 2] = cosf(c.lon[k]);
+    t12[4 * k + 3] = sinf(c.lon[k]);
+  }
+}
+
+// ICONCell::getBounds (ICONGrid.h:78-115); toCartesian from the corner trig is the same
+// float expression as r * cosf(lat) * cosf(lon) etc.
+void cell_bounds(const irt_icon_cell &c, const float *t12, float lo3[3], float hi3[3]) {
+  auto tc = [&](float r, int k) {
+    const float *t = t12 + 4 * k;
+    return V3{(r * t[0]) * t[2], (r * t[0]) * t[3], r * t[1]};
+  };
+  V3 lo = splat(INFINITY), hi = splat(-INFINITY);
   const float h0 = c.height[0], hN = c.height[c.numLayers];
   V3 tv[3];
   for (int k = 0; k < 3; ++k) {
-    V3 b = toCartesian(h0, c.lat[k], c.lon[k]);
+    V3 b = tc(h0, k);
     lo = vmin(lo, b);
     hi = vmax(hi, b);
   }
-  for (int k = 0; k < 3; ++k) tv[k] = toCartesian(hN, c.lat[k], c.lon[k]);
+  for (int k = 0; k < 3; ++k) tv[k] = tc(hN, k);
   V3 bary = (tv[0] + tv[1] + tv[2]) / 3.f;
   float R = hN;
   float D = R - length(bary);
@@ -109,45 +123,68 @@ static void cell_bounds(const irt_icon_cell &c, V3 &lo, V3 &hi) {
     lo = vmin(lo, tv[k]);
     hi = vmax(hi, tv[k]);
   }
+  lo3[0] = lo.x, lo3[1] = lo.y, lo3[2] = lo.z;
+  hi3[0] = hi.x, hi3[1] = hi.y, hi3[2] = hi.z;
 }
 
-// hostCode.cu:792-808 (bounds, dataRange) and 838-840 (unitDistance)
-void compute_volume_info(const irt_icon_cell *cells, size_t n, irt_volume_info &info) {
-  memset(&info, 0, sizeof(info));
-  V3 vlo = splat(INFINITY), vhi = splat(-INFINITY);
-  V3 slo = splat(INFINITY), shi = splat(-INFINITY);
-  float dlo = INFINITY, dhi = -INFINITY;
-  for (size_t i = 0; i < n; ++i) {
-    const irt_icon_cell &c = cells[i];
-    float minLat = fminf(c.lat[0], fminf(c.lat[1], c.lat[2]));
-    float maxLat = fmaxf(c.lat[0], fmaxf(c.lat[1], c.lat[2]));
-    float minLon = fminf(c.lon[0], fminf(c.lon[1], c.lon[2]));
-    float maxLon = fmaxf(c.lon[0], fmaxf(c.lon[1], c.lon[2]));
-    slo.x = fminf(slo.x, c.height[0]);
-    shi.x = fmaxf(shi.x, c.height[c.numLayers]);
-    slo.y = fminf(slo.y, minLat);
-    shi.y = fmaxf(shi.y, maxLat);
-    slo.z = fminf(slo.z, minLon);
-    shi.z = fmaxf(shi.z, maxLon);
-    V3 blo, bhi;
-    cell_bounds(c, blo, bhi);
-    vlo = vmin(vlo, blo);
-    vhi = vmax(vhi, bhi);
-    for (int j = 0; j < c.numLayers; ++j) {
-      dlo = fminf(dlo, c.value[j]);
-      dhi = fmaxf(dhi, c.value[j]);
-    }
+// hostCode.cu:792-808 (bounds, dataRange) and 838-840 (unitDistance), as a fold over the
+// records in order (so chunked input gives the same result)
+void volume_acc_init(VolumeAcc &a) {
+  for (int k = 0; k < 3; ++k) {
+    a.vlo[k] = a.slo[k] = INFINITY;
+    a.vhi[k] = a.shi[k] = -INFINITY;
   }
-  info.numCells = n;
-  info.bounds = {iv(vlo), iv(vhi)};
-  info.sphericalBounds = {iv(slo), iv(shi)};
-  info.dataRange = {dlo, dhi};
-  float magnitude = floorf(log10f(slo.x));
+  a.dlo = INFINITY;
+  a.dhi = -INFINITY;
+  a.n = 0;
+}
+
+void volume_acc_add(VolumeAcc &a, const irt_icon_cell &c, const float blo[3], const float bhi[3]) {
+  float minLat = fminf(c.lat[0], fminf(c.lat[1], c.lat[2]));
+  float maxLat = fmaxf(c.lat[0], fmaxf(c.lat[1], c.lat[2]));
+  float minLon = fminf(c.lon[0], fminf(c.lon[1], c.lon[2]));
+  float maxLon = fmaxf(c.lon[0], fmaxf(c.lon[1], c.lon[2]));
+  a.slo[0] = fminf(a.slo[0], c.height[0]);
+  a.shi[0] = fmaxf(a.shi[0], c.height[c.numLayers]);
+  a.slo[1] = fminf(a.slo[1], minLat);
+  a.shi[1] = fmaxf(a.shi[1], maxLat);
+  a.slo[2] = fminf(a.slo[2], minLon);
+  a.shi[2] = fmaxf(a.shi[2], maxLon);
+  for (int k = 0; k < 3; ++k) {
+    a.vlo[k] = fminf(a.vlo[k], blo[k]);
+    a.vhi[k] = fmaxf(a.vhi[k], bhi[k]);
+  }
+  for (int j = 0; j < c.numLayers; ++j) {
+    a.dlo = fminf(a.dlo, c.value[j]);
+    a.dhi = fmaxf(a.dhi, c.value[j]);
+  }
+  ++a.n;
+}
+
+void volume_acc_finish(const VolumeAcc &a, irt_volume_info &info) {
+  memset(&info, 0, sizeof(info));
+  info.numCells = a.n;
+  info.bounds = {{a.vlo[0], a.vlo[1], a.vlo[2]}, {a.vhi[0], a.vhi[1], a.vhi[2]}};
+  info.sphericalBounds = {{a.slo[0], a.slo[1], a.slo[2]}, {a.shi[0], a.shi[1], a.shi[2]}};
+  info.dataRange = {a.dlo, a.dhi};
+  float magnitude = floorf(log10f(a.slo[0]));
   float scale = powf(10.f, magnitude - 3);
   info.unitDistance = 1.0f * scale;
   info.shellDims[0] = 1;
   info.shellDims[1] = 1024;
   info.shellDims[2] = 1024;
+}
+
+void compute_volume_info(const irt_icon_cell *cells, size_t n, irt_volume_info &info) {
+  VolumeAcc a;
+  volume_acc_init(a);
+  for (size_t i = 0; i < n; ++i) {
+    float t[12], lo[3], hi[3];
+    corner_trig(cells[i], t);
+    cell_bounds(cells[i], t, lo, hi);
+    volume_acc_add(a, cells[i], lo, hi);
+  }
+  volume_acc_finish(a, info);
 }
 
 const std::vector<float> &logf_table() {

@@ -222,29 +222,33 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads)
 }
 
 // ---------------------------------------------------------------- radially binned lists
+namespace {
+// irt_build.h entry accessor over a cell's CSR range
+struct CellEntries {
+  const HostScene &S;
+  uint32_t q0;
+  float h0(int k) const { return S.rng[2 * (size_t)S.entryRec[q0 + k]]; }
+  float hN(int k) const { return S.rng[2 * (size_t)S.entryRec[q0 + k] + 1]; }
+  uint32_t sub(int k) const { return S.entrySub[q0 + k]; }
+};
+}  // namespace
+
 int build_bins(HostScene &S, int threads) {
   const uint32_t numGridCells = 6u * S.G * S.G;
   S.binHdr.assign((size_t)numGridCells * kBinHdrWords, 0u);
   std::vector<uint64_t> cellCount(numGridCells + 1, 0);
   // pass 1: edges, per-bin counts and sub-cell masks per cell (irt_build.h)
   parallel_ranges(numGridCells, threads, [&](int, size_t b, size_t e) {
-    std::vector<float> h0, hN, cand;
+    std::vector<float> cand;
     for (size_t cell = b; cell < e; ++cell) {
       const uint32_t q0 = S.offsets[cell], n = S.offsets[cell + 1] - q0;
-      h0.resize(n);
-      hN.resize(n);
+      const CellEntries en{S, q0};
       cand.resize(n);
-      for (uint32_t k = 0; k < n; ++k) {
-        const uint32_t rec = S.entryRec[q0 + k];
-        h0[k] = S.rng[2 * (size_t)rec];
-        hN[k] = S.rng[2 * (size_t)rec + 1];
-      }
       double rmin, rmax;
-      const int nc = cell_candidates(h0.data(), hN.data(), (int)n, cand.data(), rmin, rmax);
+      const int nc = cell_candidates(en, (int)n, cand.data(), rmin, rmax);
       float edges[kMaxEdges] = {0.f, 0.f, 0.f};
-      const int ne = choose_edges(h0.data(), hN.data(), (int)n, cand.data(), nc, rmin, rmax, edges);
-      cellCount[cell + 1] = cell_header(h0.data(), hN.data(), &S.entrySub[q0], (int)n, edges, ne,
-                                        &S.binHdr[cell * kBinHdrWords]);
+      const int ne = choose_edges(en, (int)n, cand.data(), nc, rmin, rmax, edges);
+      cellCount[cell + 1] = cell_header(en, (int)n, edges, ne, &S.binHdr[cell * kBinHdrWords]);
     }
   });
   for (uint32_t k = 0; k < numGridCells; ++k) cellCount[k + 1] += cellCount[k];

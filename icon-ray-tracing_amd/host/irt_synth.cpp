@@ -23,6 +23,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "irt_internal.h"
@@ -45,16 +46,20 @@ struct Tri {
   D3 a, b, c;
 };
 
-void bisect(const Tri &t, int depth, std::vector<Tri> &out) {
-  if (depth == 0) {
-    out.push_back(t);
-    return;
+// Triangle `leaf` of the depth-first 4-way bisection of root t: children (a,ab,ca),
+// (ab,b,bc), (ca,bc,c), (ab,bc,ca), the first level's choice in the leaf index's highest
+// base-4 digit.  Every midpoint is computed from the same parent doubles as a recursive
+// descent would, so any leaf comes out identical without generating the others.
+Tri descend(Tri t, int depth, size_t leaf) {
+  for (int d = depth - 1; d >= 0; --d) {
+    const int c = (int)((leaf >> (2 * d)) & 3);
+    const D3 ab = unit(add(t.a, t.b)), bc = unit(add(t.b, t.c)), ca = unit(add(t.c, t.a));
+    if (c == 0) t = {t.a, ab, ca};
+    else if (c == 1) t = {ab, t.b, bc};
+    else if (c == 2) t = {ca, bc, t.c};
+    else t = {ab, bc, ca};
   }
-  D3 ab = unit(add(t.a, t.b)), bc = unit(add(t.b, t.c)), ca = unit(add(t.c, t.a));
-  bisect({t.a, ab, ca}, depth - 1, out);
-  bisect({ab, t.b, bc}, depth - 1, out);
-  bisect({ca, bc, t.c}, depth - 1, out);
-  bisect({ab, bc, ca}, depth - 1, out);
+  return t;
 }
 
 inline uint32_t hash32(uint32_t x) {
@@ -66,7 +71,164 @@ inline uint32_t hash32(uint32_t x) {
   return x;
 }
 
+// The grid generator: root triangles, level heights and the value normalisation once; then
+// any range of records on demand (irt_create_synth streams them into HBM chunk by chunk).
+struct SynthGen {
+  int rootN = 0, bisections = 0, levels = 0, recsPerCol = 0;
+  float noise = 0.f;
+  uint32_t seed = 0;
+  size_t numTris = 0, total = 0;
+  std::vector<Tri> roots;
+  std::vector<float> H;
+  double vmin = INFINITY, vmax = -INFINITY, vscale = 0.0;
+
+  int init(int rn, int bis, int lev, float topHeight, float nz, uint32_t sd) {
+    using irt::set_error;
+    if (rn < 1 || bis < 0 || bis > 12 || lev < 1 || lev > 100000) {
+      set_error("irt_synth_grid: bad argument");
+      return IRT_E_INVALID;
+    }
+    rootN = rn, bisections = bis, levels = lev, noise = nz, seed = sd;
+    numTris = 20ull * rootN * rootN * (1ull << (2 * bisections));
+    recsPerCol = (levels + 30) / 31;
+    total = numTris * recsPerCol;
+    const double phi = (1.0 + sqrt(5.0)) / 2.0;
+    const D3 V[12] = {{-1, phi, 0}, {1, phi, 0}, {-1, -phi, 0}, {1, -phi, 0},
+                      {0, -1, phi}, {0, 1, phi}, {0, -1, -phi}, {0, 1, -phi},
+                      {phi, 0, -1}, {phi, 0, 1}, {-phi, 0, -1}, {-phi, 0, 1}};
+    const int F[20][3] = {{0, 11, 5}, {0, 5, 1},  {0, 1, 7},   {0, 7, 10}, {0, 10, 11},
+                          {1, 5, 9},  {5, 11, 4}, {11, 10, 2}, {10, 7, 6}, {7, 1, 8},
+                          {3, 9, 4},  {3, 4, 2},  {3, 2, 6},   {3, 6, 8},  {3, 8, 9},
+                          {4, 9, 5},  {2, 4, 11}, {6, 2, 10},  {8, 6, 7},  {9, 8, 1}};
+    roots.clear();
+    roots.reserve(20 * rootN * rootN);
+    for (int f = 0; f < 20; ++f) {
+      D3 a = unit(V[F[f][0]]), b = unit(V[F[f][1]]), c = unit(V[F[f][2]]);
+      if (dotd(crossd(sub(b, a), sub(c, a)), add(add(a, b), c)) < 0) std::swap(b, c);
+      auto P = [&](int i, int j) {  // barycentric lattice point, on the sphere
+        double s = (double)i / rootN, t = (double)j / rootN;
+        return unit(add(a, add(mul(sub(b, a), s), mul(sub(c, a), t))));
+      };
+      for (int j = 0; j < rootN; ++j)
+        for (int i = 0; i + j < rootN; ++i) {
+          roots.push_back({P(i, j), P(i + 1, j), P(i, j + 1)});
+          if (i + j + 1 < rootN) roots.push_back({P(i + 1, j), P(i + 1, j + 1), P(i, j + 1)});
+        }
+    }
+    const float R = 6.371229E6f;
+    H.assign(levels + 1, 0.f);
+    for (int l = 0; l <= levels; ++l) {
+      double f = (double)l / levels;
+      H[l] = (float)((double)R + (double)topHeight * f * f);
+    }
+    // value range over the whole grid (min/max: any evaluation order gives the same)
+    const int threads = irt::default_threads();
+    std::vector<double> lo(threads, INFINITY), hi(threads, -INFINITY);
+    std::vector<std::thread> ts;
+    const size_t chunk = (numTris + threads - 1) / threads;
+    for (int t = 0; t < threads; ++t)
+      ts.emplace_back([&, t] {
+        std::vector<double> v(levels);
+        double l = INFINITY, h = -INFINITY;  // thread-local: no false sharing
+        for (size_t k = t * chunk; k < std::min(numTris, (t + 1) * chunk); ++k) {
+          values(k, v.data());
+          for (double x : v) {
+            l = std::min(l, x);
+            h = std::max(h, x);
+          }
+        }
+        lo[t] = l;
+        hi[t] = h;
+      });
+    for (auto &t : ts) t.join();
+    for (int t = 0; t < threads; ++t) {
+      vmin = std::min(vmin, lo[t]);
+      vmax = std::max(vmax, hi[t]);
+    }
+    vscale = vmax > vmin ? 1.0 / (vmax - vmin) : 0.0;
+    return IRT_OK;
+  }
+
+  Tri tri(size_t t) const {
+    const size_t per = (size_t)1 << (2 * bisections);
+    return descend(roots[t / per], bisections, t % per);
+  }
+
+  // un-normalised values of column t's layers
+  void values(size_t t, double *v) const {
+    const Tri tr = tri(t);
+    D3 c = unit(add(add(tr.a, tr.b), tr.c));
+    double base = sin(4 * c.x + 3 * c.y) * cos(5 * c.z);
+    for (int l = 0; l < levels; ++l) {
+      double h = (l + 0.5) / levels;
+      double x = 0.5 + 0.35 * base * (1 - h) + 0.1 * h;
+      if (noise != 0.f) {
+        uint32_t k = hash32((uint32_t)t * 2654435761u ^ hash32((uint32_t)l + seed * 97u));
+        x += (double)noise * ((k >> 8) * (1.0 / 16777216.0) - 0.5);
+      }
+      v[l] = x;
+    }
+  }
+
+  // records [first, first + count), in parallel over columns
+  void fill(size_t first, size_t count, irt_icon_cell *out) const {
+    if (!count) return;
+    const size_t t0 = first / recsPerCol, t1 = (first + count - 1) / recsPerCol + 1;
+    const int threads = count < 4096 ? 1 : irt::default_threads();
+    std::vector<std::thread> ts;
+    const size_t chunk = (t1 - t0 + threads - 1) / threads;
+    for (int th = 0; th < threads; ++th)
+      ts.emplace_back([&, th] {
+        std::vector<double> v(levels);
+        for (size_t t = t0 + th * chunk; t < std::min(t1, t0 + (th + 1) * chunk); ++t) {
+          const Tri tr = tri(t);
+          const D3 cs[3] = {tr.a, tr.b, tr.c};
+          float lat[3], lon[3];
+          for (int k = 0; k < 3; ++k) {
+            double z = std::max(-1.0, std::min(1.0, cs[k].z));
+            lat[k] = (float)asin(z);
+            lon[k] = (float)atan2(cs[k].y, cs[k].x);
+          }
+          values(t, v.data());
+          for (int rc = 0; rc < recsPerCol; ++rc) {
+            const size_t r = t * recsPerCol + rc;
+            if (r < first || r >= first + count) continue;
+            irt_icon_cell &cell = out[r - first];
+            memset(&cell, 0, sizeof(cell));
+            memcpy(cell.lat, lat, sizeof(lat));
+            memcpy(cell.lon, lon, sizeof(lon));
+            const int l0 = rc * 31;
+            const int nl = std::min(31, levels - l0);
+            cell.numLayers = nl;
+            for (int j = 0; j <= nl; ++j) cell.height[j] = H[l0 + j];
+            for (int j = 0; j < nl; ++j) cell.value[j] = (float)((v[l0 + j] - vmin) * vscale);
+          }
+        }
+      });
+    for (auto &t : ts) t.join();
+  }
+};
+
 }  // namespace
+
+namespace irt {
+int synth_open(int rootN, int bisections, int levels, float topHeight, float noise, uint32_t seed,
+               void **gen, size_t *total) {
+  SynthGen *g = new SynthGen();
+  int rc = g->init(rootN, bisections, levels, topHeight, noise, seed);
+  if (rc) {
+    delete g;
+    return rc;
+  }
+  *gen = g;
+  *total = g->total;
+  return IRT_OK;
+}
+void synth_fill(const void *gen, size_t first, size_t count, irt_icon_cell *out) {
+  static_cast<const SynthGen *>(gen)->fill(first, count, out);
+}
+void synth_close(void *gen) { delete static_cast<SynthGen *>(gen); }
+}  // namespace irt
 
 extern "C" int irt_synth_grid(int rootN, int bisections, int levels, float topHeight,
                               float noise, uint32_t seed, irt_icon_cell *out, size_t capacity,
@@ -78,94 +240,16 @@ extern "C" int irt_synth_grid(int rootN, int bisections, int levels, float topHe
     return IRT_E_INVALID;
   }
   const size_t numTris = 20ull * rootN * rootN * (1ull << (2 * bisections));
-  const int recsPerCol = (levels + 30) / 31;
-  const size_t total = numTris * recsPerCol;
+  const size_t total = numTris * ((levels + 30) / 31);
   *count = total;
   if (!out) return IRT_OK;
   if (capacity < total) {
     set_error("irt_synth_grid: capacity %zu < %zu", capacity, total);
     return IRT_E_INVALID;
   }
-
-  const double phi = (1.0 + sqrt(5.0)) / 2.0;
-  const D3 V[12] = {{-1, phi, 0}, {1, phi, 0}, {-1, -phi, 0}, {1, -phi, 0},
-                    {0, -1, phi}, {0, 1, phi}, {0, -1, -phi}, {0, 1, -phi},
-                    {phi, 0, -1}, {phi, 0, 1}, {-phi, 0, -1}, {-phi, 0, 1}};
-  const int F[20][3] = {{0, 11, 5}, {0, 5, 1},  {0, 1, 7},   {0, 7, 10}, {0, 10, 11},
-                        {1, 5, 9},  {5, 11, 4}, {11, 10, 2}, {10, 7, 6}, {7, 1, 8},
-                        {3, 9, 4},  {3, 4, 2},  {3, 2, 6},   {3, 6, 8},  {3, 8, 9},
-                        {4, 9, 5},  {2, 4, 11}, {6, 2, 10},  {8, 6, 7},  {9, 8, 1}};
-  std::vector<Tri> roots;
-  roots.reserve(20 * rootN * rootN);
-  for (int f = 0; f < 20; ++f) {
-    D3 a = unit(V[F[f][0]]), b = unit(V[F[f][1]]), c = unit(V[F[f][2]]);
-    if (dotd(crossd(sub(b, a), sub(c, a)), add(add(a, b), c)) < 0) std::swap(b, c);
-    auto P = [&](int i, int j) {  // barycentric lattice point, on the sphere
-      double s = (double)i / rootN, t = (double)j / rootN;
-      return unit(add(a, add(mul(sub(b, a), s), mul(sub(c, a), t))));
-    };
-    for (int j = 0; j < rootN; ++j)
-      for (int i = 0; i + j < rootN; ++i) {
-        roots.push_back({P(i, j), P(i + 1, j), P(i, j + 1)});
-        if (i + j + 1 < rootN) roots.push_back({P(i + 1, j), P(i + 1, j + 1), P(i, j + 1)});
-      }
-  }
-  std::vector<Tri> tris;
-  tris.reserve(numTris);
-  for (const Tri &t : roots) bisect(t, bisections, tris);
-  if (tris.size() != numTris) {
-    set_error("irt_synth_grid: internal triangle count mismatch");
-    return IRT_E_INVALID;
-  }
-
-  const float R = 6.371229E6f;
-  std::vector<float> H(levels + 1);
-  for (int l = 0; l <= levels; ++l) {
-    double f = (double)l / levels;
-    H[l] = (float)((double)R + (double)topHeight * f * f);
-  }
-
-  // values (double), then normalise to [0,1]
-  std::vector<double> val(numTris * (size_t)levels);
-  double vmin = INFINITY, vmax = -INFINITY;
-  for (size_t t = 0; t < numTris; ++t) {
-    D3 c = unit(add(add(tris[t].a, tris[t].b), tris[t].c));
-    double base = sin(4 * c.x + 3 * c.y) * cos(5 * c.z);
-    for (int l = 0; l < levels; ++l) {
-      double h = (l + 0.5) / levels;
-      double v = 0.5 + 0.35 * base * (1 - h) + 0.1 * h;
-      if (noise != 0.f) {
-        uint32_t k = hash32((uint32_t)t * 2654435761u ^ hash32((uint32_t)l + seed * 97u));
-        v += (double)noise * ((k >> 8) * (1.0 / 16777216.0) - 0.5);
-      }
-      val[t * levels + l] = v;
-      vmin = std::min(vmin, v);
-      vmax = std::max(vmax, v);
-    }
-  }
-  const double vscale = vmax > vmin ? 1.0 / (vmax - vmin) : 0.0;
-
-  size_t r = 0;
-  for (size_t t = 0; t < numTris; ++t) {
-    const D3 cs[3] = {tris[t].a, tris[t].b, tris[t].c};
-    float lat[3], lon[3];
-    for (int k = 0; k < 3; ++k) {
-      double z = std::max(-1.0, std::min(1.0, cs[k].z));
-      lat[k] = (float)asin(z);
-      lon[k] = (float)atan2(cs[k].y, cs[k].x);
-    }
-    for (int rc = 0; rc < recsPerCol; ++rc) {
-      irt_icon_cell &cell = out[r++];
-      memset(&cell, 0, sizeof(cell));
-      memcpy(cell.lat, lat, sizeof(lat));
-      memcpy(cell.lon, lon, sizeof(lon));
-      const int l0 = rc * 31;
-      const int nl = std::min(31, levels - l0);
-      cell.numLayers = nl;
-      for (int j = 0; j <= nl; ++j) cell.height[j] = H[l0 + j];
-      for (int j = 0; j < nl; ++j)
-        cell.value[j] = (float)((val[t * levels + l0 + j] - vmin) * vscale);
-    }
-  }
+  SynthGen g;
+  int rc = g.init(rootN, bisections, levels, topHeight, noise, seed);
+  if (rc) return rc;
+  g.fill(0, total, out);
   return IRT_OK;
 }

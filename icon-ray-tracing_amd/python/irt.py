@@ -110,6 +110,13 @@ def lib() -> C.CDLL:
         L.irt_last_error.restype = C.c_char_p
         sig = {
             "irt_create": [P, S, I, C.POINTER(P)],
+            "irt_create_begin": [S, I, C.POINTER(P)],
+            "irt_create_append": [P, P, S],
+            "irt_create_end": [P],
+            "irt_create_from_file": [C.c_char_p, C.c_long, I, C.POINTER(P)],
+            "irt_create_synth": [I, I, I, F, F, C.c_uint32, I, C.POINTER(P)],
+            "irt_debug_context_array": [P, I, P, S, C.POINTER(S)],
+            "irt_debug_scene_array": [P, I, P, S, C.POINTER(S)],
             "irt_destroy": [P],
             "irt_get_volume_info": [P, C.POINTER(VolumeInfo)],
             "irt_set_transfunc": [P, P, I, Box1, F],
@@ -313,15 +320,19 @@ FRAMING_CAMERA = ((0.0, 0.0, 1.4e7), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0)
 
 
 def setup_frame(cells: np.ndarray, width: int, height: int, camera=None,
-                camera_div=None, raygen: int = RAYGEN_WITH_ACCEL) -> FrameSetup:
+                camera_div=None, raygen: int = RAYGEN_WITH_ACCEL, info: VolumeInfo = None) -> FrameSetup:
     """Mirror hostCode.cu main(): volume facts, default TF, unitDistance, camera.
+
+    info: the volume facts when already known (Context.info: a streamed context never
+          holds the whole cell array on the host); otherwise computed from `cells`.
 
     camera: None -> Camera::viewAll(volbounds) with fovy 90 (hostCode.cu:819-821);
             (vp, vi, vu, fovyDeg) -> Pipeline --camera/-fovy (pipeline.cu:444-454).
     camera_div: the image size dir_du/dir_dv are divided by; the reference hard-codes
             512 (hostCode.cu:815,944-945); default: the real (width, height).
     """
-    info = volume_info(cells)
+    if info is None:
+        info = volume_info(cells)
     lut, vr = default_transfunc((info.dataRange.lower, info.dataRange.upper))
     dw, dh = camera_div if camera_div is not None else (width, height)
     if camera is None:
@@ -337,18 +348,73 @@ def setup_frame(cells: np.ndarray, width: int, height: int, camera=None,
     return FrameSetup(lp=lp, lut=lut, value_range=vr, opacity_scale=1.0, info=info)
 
 
+# scene arrays the render kernel reads (irt_debug_context_array / irt_debug_scene_array)
+SCENE_ARRAYS = {"bin_hdr": 0, "fat": 1, "blocks": 2, "sph_r": 3, "sph_off": 4, "sph_rec": 5,
+                "sph_bits": 6}
+
+
+def _array(fn, h, name):
+    n = C.c_size_t()
+    _check(fn(h, SCENE_ARRAYS[name], None, 0, C.byref(n)), "scene array")
+    out = np.zeros(n.value, np.uint8)
+    _check(fn(h, SCENE_ARRAYS[name], _ptr(out), n.value, C.byref(n)), "scene array")
+    return out
+
+
 # ----------------------------------------------------------------------- GPU context
 class Context:
-    """One renderer context on one HIP device (irt_create ... irt_destroy)."""
+    """One renderer context on one HIP device (irt_create ... irt_destroy).
 
-    def __init__(self, cells: np.ndarray, device: int = 0):
-        cells = np.ascontiguousarray(cells, dtype=CELL_DTYPE)
-        h = C.c_void_p()
-        _check(lib().irt_create(_ptr(cells), cells.size, device, C.byref(h)), "irt_create")
-        self._h = h
+    Context(cells) uploads a host array; Context.synth / Context.from_file /
+    Context.streamed feed the cells to HBM chunk by chunk (irt_create_begin / _append /
+    _end), so host memory stays at one chunk."""
+
+    def __init__(self, cells: np.ndarray = None, device: int = 0, _handle=None):
+        if _handle is None:
+            cells = np.ascontiguousarray(cells, dtype=CELL_DTYPE)
+            _handle = C.c_void_p()
+            _check(lib().irt_create(_ptr(cells), cells.size, device, C.byref(_handle)),
+                   "irt_create")
+        self._h = _handle
         self.device = device
         self.info = VolumeInfo()
         _check(lib().irt_get_volume_info(self._h, C.byref(self.info)), "irt_get_volume_info")
+
+    @classmethod
+    def synth(cls, root_n: int, bisections: int, levels: int, device: int = 0,
+              top_height: float = 75e3, noise: float = 0.0, seed: int = 1234) -> "Context":
+        """The grid of synth_grid(...), generated straight into HBM (irt_create_synth)."""
+        h = C.c_void_p()
+        _check(lib().irt_create_synth(root_n, bisections, levels, top_height, noise, seed, device,
+                                      C.byref(h)), "irt_create_synth")
+        return cls(device=device, _handle=h)
+
+    @classmethod
+    def from_file(cls, path: str, max_num_cells: int = -1, device: int = 0) -> "Context":
+        """A `.ic` file streamed into HBM (irt_create_from_file, hostCode.cu:717-734)."""
+        h = C.c_void_p()
+        _check(lib().irt_create_from_file(path.encode(), max_num_cells, device, C.byref(h)),
+               "irt_create_from_file")
+        return cls(device=device, _handle=h)
+
+    @classmethod
+    def streamed(cls, chunks, num_cells: int, device: int = 0) -> "Context":
+        """`num_cells` records from an iterable of record arrays, in order."""
+        h = C.c_void_p()
+        _check(lib().irt_create_begin(num_cells, device, C.byref(h)), "irt_create_begin")
+        try:
+            for ch in chunks:
+                ch = np.ascontiguousarray(ch, dtype=CELL_DTYPE)
+                _check(lib().irt_create_append(h, _ptr(ch), ch.size), "irt_create_append")
+            _check(lib().irt_create_end(h), "irt_create_end")
+        except Exception:
+            lib().irt_destroy(h)
+            raise
+        return cls(device=device, _handle=h)
+
+    def array(self, name: str) -> np.ndarray:
+        """A scene array as the device built it (bytes; irt_debug_context_array)."""
+        return _array(lib().irt_debug_context_array, self._h, name)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -495,6 +561,10 @@ class DebugScene:
         _check(lib().irt_debug_scene_values(self._h, rec, C.c_float(r), _ptr(out)),
                "irt_debug_scene_values")
         return out
+
+    def array(self, name: str) -> np.ndarray:
+        """A scene array as the host restatement built it (bytes)."""
+        return _array(lib().irt_debug_scene_array, self._h, name)
 
     def planes(self, rec: int) -> np.ndarray:
         out = np.zeros(12, dtype=np.float32)

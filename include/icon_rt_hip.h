@@ -123,8 +123,27 @@ const char *irt_last_error(void);
  * compute the volume facts (hostCode.cu:792-808), build the cell locator that replaces the
  * OptiX/cuBQL accelerators (hostCode.cu:440-650), upload to HBM on `device`, and build the
  * spherical-shell accelerator on the GPU: initGrid + buildShell_ICON
- * (hostCode.cu:216-225, 299-336, 652-666).  Majorants stay zero until irt_set_transfunc. */
+ * (hostCode.cu:216-225, 299-336, 652-666).  Majorants stay zero until irt_set_transfunc.
+ * Everything but the per-record glibc corner trig (toCartesian's cosf/sinf) is built on
+ * the device.  irt_create = irt_create_begin + irt_create_append(all) + irt_create_end. */
 int irt_create(const irt_icon_cell *cells, size_t numCells, int device, irt_context **out);
+
+/* Streaming creation, for scenes larger than host memory should hold at once (the cells
+ * go to HBM chunk by chunk, host memory stays at one chunk): `numCells` records arrive
+ * through any number of irt_create_append calls, in record order; irt_create_end builds
+ * the scene on the device.  The context is unusable (and irt_create_end fails) unless
+ * exactly numCells records were appended. */
+int irt_create_begin(size_t numCells, int device, irt_context **out);
+int irt_create_append(irt_context *ctx, const irt_icon_cell *cells, size_t n);
+int irt_create_end(irt_context *ctx);
+
+/* The load of hostCode.cu:717-734 streamed straight into a context: records of the `.ic`
+ * file (N = filesize / 284, truncated to maxNumCells when >= 0, `--num-cells`). */
+int irt_create_from_file(const char *path, long maxNumCells, int device, irt_context **out);
+
+/* A synthetic RnBk grid (irt_synth_grid) generated chunk by chunk straight into a context. */
+int irt_create_synth(int rootN, int bisections, int levels, float topHeight, float noise,
+                     uint32_t seed, int device, irt_context **out);
 void irt_destroy(irt_context *ctx);
 int irt_get_volume_info(const irt_context *ctx, irt_volume_info *info);
 

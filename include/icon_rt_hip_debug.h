@@ -38,12 +38,12 @@ int irt_debug_scene_info(const irt_debug_scene *s, irt_volume_info *info);
 int irt_debug_scene_locate(const irt_debug_scene *s, irt_vec3f p, float *value,
                            uint32_t *record);
 /* The same query through the binned locator the render kernel uses (radial bins of fat
- * entries, irt_common.h); *tested = candidate entries examined. */
+ * entries and sub-cell masks, irt_build.h); *tested = candidate entries examined. */
 int irt_debug_scene_locate_binned(const irt_debug_scene *s, irt_vec3f p, float *value,
                                   uint32_t *record, uint32_t *tested);
 /* findHeight + value of record `rec` at radius r two ways: out2[0] from the literal
- * binary search (ICONGrid.h:117-164), out2[1] from the render-record layout the
- * state-machine kernel gathers (irt_common.h).  They must agree bit for bit. */
+ * binary search (ICONGrid.h:117-164), out2[1] the way the render kernel reads it (coarse
+ * keys + one 64-B block of the height/value blocks, irt_common.h).  Bit for bit equal. */
 int irt_debug_scene_values(const irt_debug_scene *s, uint32_t rec, float r, float *out2);
 /* Candidate list of the cube-map cell containing direction p. */
 int irt_debug_scene_candidates(const irt_debug_scene *s, irt_vec3f p, uint32_t *records,
@@ -62,6 +62,24 @@ int irt_debug_scene_locate_triangle(irt_debug_scene *s, irt_vec3f p, float *valu
                                     uint32_t *record);
 /* intersectWedgeEXT (UElems.h:214-311) as the kernel evaluates it; v24 = 6 x (xyz, scalar). */
 int irt_debug_intersect_wedge(const float *v24, irt_vec3f p, float *value);
+
+/* The scene arrays the render kernel reads, byte for byte: from a context (the device
+ * build, csrc/irt_build.hip; waits for it) or from the host restatement of the build
+ * (host/irt_scene.cpp).  which: IRT_DEBUG_ARRAY_*.  With dst null (or capacity too small)
+ * only *bytes is set. */
+enum {
+  IRT_DEBUG_ARRAY_BIN_HDR = 0,  /* cube-map cell headers, kBinHdrWords u32 each */
+  IRT_DEBUG_ARRAY_FAT = 1,      /* fat candidate entries, 80 B each */
+  IRT_DEBUG_ARRAY_BLOCKS = 2,   /* per-record height/value blocks, 256 B each */
+  IRT_DEBUG_ARRAY_SPH_R = 3,    /* sphere radii (f32) */
+  IRT_DEBUG_ARRAY_SPH_OFF = 4,  /* CSR offsets (u32) */
+  IRT_DEBUG_ARRAY_SPH_REC = 5,  /* (record, numLayers) u32 pairs */
+  IRT_DEBUG_ARRAY_SPH_BITS = 6  /* radius hash bitmap (u32) */
+};
+int irt_debug_context_array(const irt_context *ctx, int which, void *dst, size_t capacity,
+                            size_t *bytes);
+int irt_debug_scene_array(const irt_debug_scene *s, int which, void *dst, size_t capacity,
+                          size_t *bytes);
 
 /* Select the render-kernel variant (bit set of irt_render.hip's OPT_* flags; every
  * variant gives identical results -- used for in-process A/B timing). */

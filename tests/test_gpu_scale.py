@@ -1,16 +1,17 @@
-"""GPU parity at BASELINE sizes (C2, C3; C5 with IRT_TEST_C5=1) through size-independent
-checks.
+"""GPU parity at the BASELINE sizes (C2, C3, C4, C5) through size-independent checks.
 
 The oracle's brute-force cell scan (the reference's own CPU algorithm) cannot render a
-full 1024^2 frame over 3.9 M records in test time, so at full size the GPU frame is checked
-  - pixel-for-pixel against the oracle on a strided sample of pixels (the raygen is
-    per-pixel independent, so any pixel subset is a valid parity sample),
+full frame over millions of records in test time, so at full size the GPU frame is checked
+  - pixel-for-pixel against the oracle on a strided sample of pixels plus a dense patch
+    across the limb (the raygen is per-pixel independent, so any pixel subset is a valid
+    parity sample),
   - for determinism (two launches bit-identical), and
   - for frame-tile invariance (the 8-GPU split rendered in one process reproduces the
     1-GPU frame bit for bit).
+C4 is C3's grid at 2048^2 (BASELINE configs[3]); C5 is R2B09 x 90 (62.9 M records,
+configs[4]), created by streaming the grid into HBM (irt_create_synth) and rendered from
+one of its 60 orbit cameras.
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -21,26 +22,36 @@ from helpers import FRAMING, GpuFrame, bits
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
 SCALE = {
-    "c2": (2, 5, 47, 512),
-    "c3": (2, 7, 90, 1024),
+    # name: (rootN, bisections, levels, W, orbit frame or None)
+    "c2": (2, 5, 47, 512, None),
+    "c3": (2, 7, 90, 1024, None),
+    "c4": (2, 7, 90, 2048, None),
+    "c5": (2, 9, 90, 1024, 5),
 }
-# C5 (R2B09 x 90 = 62.9 M records, 41 GiB HBM, ~90 GiB host RAM, ~2 min): opt-in
-if os.environ.get("IRT_TEST_C5"):
-    SCALE["c5"] = (2, 9, 90, 1024)
+
+
+def orbit_camera(k, n=60):
+    th = 2.0 * np.pi * k / n  # bench.py: eye = 1.4e7 (sin t, 0, cos t), looking at the origin
+    return ((1.4e7 * np.sin(th), 0.0, 1.4e7 * np.cos(th)), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0)
 
 
 @pytest.fixture(scope="module", params=sorted(SCALE))
 def scene(request):
-    rn, bis, L, W = SCALE[request.param]
+    rn, bis, L, W, orbit = SCALE[request.param]
     cells = irt.synth_grid(rn, bis, L)
-    setup = irt.setup_frame(cells, W, W, camera=FRAMING)
-    ctx = irt.Context(cells, 0)
+    cam = FRAMING if orbit is None else orbit_camera(orbit)
+    if request.param == "c5":
+        ctx = irt.Context.synth(rn, bis, L, 0)  # streamed: host memory stays at one chunk
+        setup = irt.setup_frame(cells, W, W, camera=cam, info=ctx.info)
+    else:
+        ctx = irt.Context(cells, 0)
+        setup = irt.setup_frame(cells, W, W, camera=cam)
     ctx.set_transfunc(setup.lut, setup.value_range)
     fr = GpuFrame(ctx, W, W)
     st = fr.render(setup.lp)
     a, f = fr.host()
     yield dict(name=request.param, cells=cells, setup=setup, ctx=ctx, W=W, accum=a, fb=f,
-               stats=st, frame=fr)
+               stats=st, frame=fr, camera=cam)
     ctx.close()
 
 
@@ -53,7 +64,7 @@ def test_strided_pixels_match_oracle(scene):
     cam = tuple(np.array(v.tolist(), np.float32) for v in (lp.org, lp.dir_00, lp.dir_du, lp.dir_dv))
     p = S.params(cam, accum_id=0, raygen=0, unit_distance=lp.unitDistance)
     big = scene["cells"].size > 10_000_000  # C5: every oracle sample scans 62.9 M records
-    stride = 96 if big else (32 if W >= 1024 else 16)
+    stride = 96 if big else (32 * W // 1024 if W >= 1024 else 16)
     ys, xs = np.mgrid[3:W:stride, 5:W:stride]
     xy = np.stack([xs.ravel(), ys.ravel()], 1)
     # plus a dense patch across the limb, where rays graze the shell
@@ -100,7 +111,21 @@ def test_sample_statistics_are_plausible(scene):
     st = scene["stats"]
     W = scene["W"]
     assert st.raysLaunched == W * W
-    # framing camera: ~63 % of pixels see the globe; ~1 Woodcock sample per launched pixel
+    # framing / orbit camera: ~63 % of pixels see the globe; ~1 Woodcock sample per pixel
     hit = (scene["accum"][..., 3] > 0).mean()
     assert 0.55 < hit < 0.7, hit
     assert 0.7 < st.samplesFound / (W * W) < 1.4
+    # the sub-cell masks keep the candidate tests near one per sample
+    assert st.candidatesTested / st.samplesFound < 1.5
+
+
+def test_streamed_context_equals_array_context(scene):
+    """The streamed creation keeps host memory at one chunk: the scene's HBM arrays match
+    a context created from the full host array (C2 only: the same code path at any size)."""
+    if scene["name"] != "c2":
+        pytest.skip("checked once, at C2")
+    rn, bis, L, _, _ = SCALE["c2"]
+    streamed = irt.Context.synth(rn, bis, L, 0)
+    for name in irt.SCENE_ARRAYS:
+        assert np.array_equal(streamed.array(name), scene["ctx"].array(name)), name
+    streamed.close()
