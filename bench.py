@@ -2,26 +2,35 @@
 """bench.py -- Mray/s + ms/frame of the MI355X ICON renderer (BASELINE.json metric).
 
 The hot path is the raygen woodcockTrackingWithAccel (icon_rt/deviceCode.cu:281-341) over
-every pixel of a 1024x1024 frame.  Inputs (cells, locator, shell accelerator, transfer
-function) are resident in HBM before the timed region.
+every pixel of a frame.  Inputs (cells, locator, shell accelerator, transfer function) are
+resident in HBM before the timed region; the grid is streamed into HBM and the scene built
+on the device (irt_create_synth), so host memory stays at one chunk at any size.
 
-Default workload (configs[2] of BASELINE.json, C3): synthetic R2B07 ICON grid (1,310,720
+Default workload (BASELINE.json configs[2], C3): synthetic R2B07 ICON grid (1,310,720
 cells) x 90 levels (3,932,160 `.ic` records), 1024x1024, framing camera
 `--camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60`, the reference's default transfer function.
+Other configs (--config): c2 (R2B05 x 47, 512^2), c3s (C3 with a sparse "comb" transfer
+function: alpha 0.01 except every 50th LUT entry at 1.0, so every macrocell's majorant stays
+1 while ~95 % of tentative collisions are rejected -- ~13x C3's samples, the sample-heavy
+regime where HBM bandwidth matters), c4 (C3's grid at 2048^2), c5 (R2B09 x 90 = 62.9 M
+records, one of 60 orbit cameras per step).
 
-One step:
-  * 1 GPU: one frame (one launch of the raygen over the 1024x1024 frame);
-  * N GPUs (weak scaling, one process per GPU under torchrun): N consecutive frames of the
-    reference's progressive accumulation (--sample-limit, accumID = step*N + k), tile-split:
-    every rank renders its interleaved 64x64 tiles of all N frames in ONE launch
-    (irt_render_tiles_accumulate), and rank 0 gathers the final RGBA8 tiles over RCCL
-    (torch.distributed "nccl") and unpacks the framebuffer.  The gather of step s runs on
-    the collective's stream while step s+1 renders (double-buffered tiles).  Per-GPU work
-    is one frame's rays per step at every N; `value` counts all ranks' rays.
+One step (--mode):
+  * progressive (default; "weak"): N consecutive frames of the reference's progressive
+    accumulation (--sample-limit, accumID = step*N + k); with N GPUs (one process per GPU
+    under torchrun) every rank renders its interleaved 64x64 tiles of all N frames in ONE
+    launch (irt_render_tiles_accumulate) and rank 0 gathers the final RGBA8 tiles over RCCL
+    (torch.distributed "nccl") into rank-major storage and unpacks the framebuffer.  The
+    gather of step s runs on the collective's stream while step s+1 renders
+    (double-buffered tiles).  Per-GPU work is one frame's rays per step at every N.
+  * frame ("strong"): ONE frame per step, its 64x64 tiles dealt round-robin to the N ranks
+    (irt_render_tiles), gathered and unpacked the same way: single-frame latency, the
+    BASELINE's C4 "frame-tile split with RCCL framebuffer gather".
 Frames are enqueued back to back: per-launch statistics come back through a ring, never
 stalling the host between launches.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c3s|c2|c4|c5]
+       [--mode progressive|frame]
        torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -42,13 +51,28 @@ BYTES_PER_SAMPLE = 92  # geometry 36 + findHeight 20 + value 4 + 2 LUT entries 3
 BYTES_PER_RAY = 44     # accum read 16 + write 16 + RGBA8 4 + 2 majorants 8
 
 CONFIGS = {
-    # name: (rootN, bisections, levels, W, H, description)
-    "c2": (2, 5, 47, 512, 512, "C2: R2B05 (81,920 cells) x 47 levels, 512x512"),
-    "c3": (2, 7, 90, 1024, 1024, "C3: R2B07 (1,310,720 cells) x 90 levels, 1024x1024"),
-    "c4": (2, 7, 90, 2048, 2048, "C4: R2B07 (1,310,720 cells) x 90 levels, 2048x2048"),
-    "c5": (2, 9, 90, 1024, 1024, "C5: R2B09 (20,971,520 cells) x 90 levels, 1024x1024, "
-                                 "60-frame orbit"),
+    # name: (rootN, bisections, levels, W, H, transfer function, orbit, description)
+    "c2": (2, 5, 47, 512, 512, "default", False, "C2: R2B05 (81,920 cells) x 47 levels, 512x512"),
+    "c3": (2, 7, 90, 1024, 1024, "default", False,
+           "C3: R2B07 (1,310,720 cells) x 90 levels, 1024x1024"),
+    "c3s": (2, 7, 90, 1024, 1024, "comb", False,
+            "C3s: R2B07 (1,310,720 cells) x 90 levels, 1024x1024, sparse comb TF (alpha 0.01, "
+            "every 50th of the 300 LUT entries 1.0: sample-heavy)"),
+    "c4": (2, 7, 90, 2048, 2048, "default", False,
+           "C4: R2B07 (1,310,720 cells) x 90 levels, 2048x2048"),
+    "c5": (2, 9, 90, 1024, 1024, "default", True,
+           "C5: R2B09 (20,971,520 cells) x 90 levels, 1024x1024, 60-frame orbit"),
 }
+
+
+def make_lut(kind, lut):
+    """The config's LUT from the reference's default (hostCode.cu:823-836, resampled to 300
+    entries): "default" as is; "comb" with alpha 0.01 except every 50th entry 1.0."""
+    lut = np.array(lut, dtype=np.float32, copy=True)
+    if kind == "comb":
+        lut[:, 3] = 0.01
+        lut[::50, 3] = 1.0
+    return lut
 ORBIT_FRAMES = 60  # C5: eye = 1.4e7 (sin t, 0, cos t), t = 2 pi k / 60, looking at the origin
 FRAMING = ((0.0, 0.0, 1.4e7), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0)
 
@@ -57,54 +81,101 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cells, setup, W, H, budget_s=15.0):
-    """The reference's CPU path (brute-force sampleVolume, deviceCode.cu:116-123) on the
-    host cores, on a bounded strided sample of the same frame's pixels: the reference's own
-    raygen compiled from /root/reference headers (oracle/_ref, built by __graft_entry__.build)
-    when present ("reference"), else the oracle's restatement ("port")."""
+def available_cores():
+    """CPUs this process may use: os.cpu_count() capped by the affinity mask and the
+    cgroup CPU quota (a GPU box shows the whole machine's CPUs, of which it gets a share)."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(rn, bis, L, W, H, camera, tf, budget_s=15.0):
+    """The reference's CPU path on the host cores, two ways (test-infrastructure oracle,
+    oracle/; only this leg of bench.py touches it):
+      * "port" (the primary number): the oracle's restatement of the reference raygen with
+        a direction-voxel cell locator in place of the brute-force scan (same first-index
+        answer, pinned against the reference's fixtures), 64x64 tiles pulled from an atomic
+        counter by one thread per available core (common/pipeline.cu:767,
+        thread_pool.h:146-161); whole frames, render time only (pipeline.cu:1062-1073);
+      * "reference": the reference's own raygen and brute-force first-hit scan
+        (deviceCode.cu:116-123), compiled from its headers (oracle/_ref), on a strided pixel
+        sample of the frame (a whole frame would take hours)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import irt
     import oracle as O
-    use_ref = O.have_ref()
-    threads = max(1, min(16, os.cpu_count() or 1))
+    cores = available_cores()
+    cells = irt.synth_grid(rn, bis, L)
     S = O.OracleScene(cells)
-    S.set_transfunc(setup.lut, setup.value_range, setup.opacity_scale)
-    lp = setup.lp
-    cam = (np.array(lp.org.tolist(), np.float32), np.array(lp.dir_00.tolist(), np.float32),
-           np.array(lp.dir_du.tolist(), np.float32), np.array(lp.dir_dv.tolist(), np.float32))
-    params = S.params(cam, accum_id=0, raygen=lp.raygen, unit_distance=lp.unitDistance)
-    # An unbiased bounded sample: a regular sub-grid of the frame's pixels, refined until
-    # the run takes about budget_s/2 .. 2 budget_s of CPU time.
-    stride, elapsed, pix, st = 128, 0.0, 0, None
-    while True:
-        ys, xs = np.mgrid[stride // 2:H:stride, stride // 2:W:stride]
-        xy = np.stack([xs.ravel(), ys.ravel()], axis=1).astype(np.int32)
+    lut, vr = S.default_lut()
+    S.set_transfunc(make_lut(tf, lut), vr)
+    cam = S.camera(W, H, camera)
+    params = S.params(cam, accum_id=0, raygen=0)
+    T = O.TimedScene(S, 2, cores)
+    T.render(params, W, H, rect=(0, 0, 64, 64), threads=cores)  # build + warm
+    frames, elapsed = 0, 0.0
+    while elapsed < budget_s / 2 or frames < 1:
         t = time.perf_counter()
-        if use_ref:
-            _, _, cnt = O.ref_render_pixels(S, params, W, H, xy, threads=threads)
-            locate = int(cnt[0])
-        else:
-            _, _, st = S.render_pixels(params, W, H, xy, threads=threads, fast=False)
-            locate = st.locate_calls
-        elapsed = time.perf_counter() - t
-        pix = xy.shape[0]
-        log(f"[cpu baseline] stride {stride}: {pix} rays in {elapsed:.2f} s")
-        if elapsed > budget_s / 2 or stride <= 8:
+        _, _, st = T.render(params, W, H, threads=cores)
+        elapsed += time.perf_counter() - t
+        frames += 1
+        if frames >= 200:
             break
-        stride //= 2
-    mray = pix / elapsed / 1e6
-    sample = (f"every {stride}th pixel in x and y of the {W}x{H} frame ({pix} rays, "
-              f"{locate} sampleVolume calls, {elapsed:.1f} s on {threads} threads): "
-              f"the reference's CPU raygen with its brute-force first-hit cell scan over "
-              f"{cells.size} records (deviceCode.cu:116-123), " +
-              ("compiled from the reference's own headers (oracle/_ref: ICONGrid.h sample(), "
-               "ShellAccel.h sdda, vecmath), one host thread per pixel chunk"
-               if use_ref else "oracle restatement, literal sample() incl. toSpherical"))
-    kind = "reference" if use_ref else "port"
-    return {"value": mray, "unit": "Mray/s", "cores": threads, "kind": kind, "sample": sample,
-            "ms_per_frame_extrapolated": W * H / (mray * 1e6) * 1e3}
+    T.close()
+    port_mray = W * H * frames / elapsed / 1e6
+    out = {"value": port_mray, "unit": "Mray/s", "cores": cores, "kind": "port",
+           "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+           "sample": (f"{frames} whole {W}x{H} frames ({elapsed:.1f} s of render time on "
+                      f"{cores} threads, 64x64 tiles from an atomic counter): the oracle's "
+                      f"restatement of woodcockTrackingWithAccel over {cells.size} records, "
+                      f"cells located through a direction-voxel locator (first index wins, "
+                      f"as the reference's scan; oracle/icon_oracle.cpp DirGrid)"),
+           "ms_per_frame": elapsed / frames * 1e3,
+           "samples_per_frame": int(st.samples_found)}
+    # the reference's own code and brute-force scan, on a strided pixel sample
+    if O.have_ref():
+        stride, t_ref, pix, locate = 128, 0.0, 0, 0
+        while True:
+            ys, xs = np.mgrid[stride // 2:H:stride, stride // 2:W:stride]
+            xy = np.stack([xs.ravel(), ys.ravel()], axis=1).astype(np.int32)
+            t = time.perf_counter()
+            _, _, cnt = O.ref_render_pixels(S, params, W, H, xy, threads=cores)
+            t_ref = time.perf_counter() - t
+            pix, locate = xy.shape[0], int(cnt[0])
+            log(f"[cpu baseline] reference stride {stride}: {pix} rays in {t_ref:.2f} s")
+            if t_ref > budget_s / 4 or stride <= 8:
+                break
+            stride //= 2
+        ref = pix / t_ref / 1e6
+        out["brute_force_reference"] = {
+            "value": ref, "unit": "Mray/s", "cores": cores, "kind": "reference",
+            "sample": (f"every {stride}th pixel in x and y ({pix} rays, {locate} sampleVolume "
+                       f"calls, {t_ref:.1f} s on {cores} threads): the reference's CPU raygen "
+                       f"with its brute-force first-hit cell scan (deviceCode.cu:116-123), "
+                       f"compiled from its own headers (oracle/_ref)"),
+            "ms_per_frame_extrapolated": W * H / (ref * 1e6) * 1e3}
+    return out
 
 
-def profiled_traffic(kernel, records, width):
+def profiled_traffic(kernel, config):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 summary of the
     same workload (profiles/*/summary.json: FETCH_SIZE x 2 + WRITE_SIZE, per the gfx950
     correction of MI355X_MICROARCH.md), or None."""
@@ -114,14 +185,18 @@ def profiled_traffic(kernel, records, width):
             s = json.load(open(p))
         except (OSError, ValueError):
             continue
-        b = s.get("bench") or {}
+        if s.get("config_name") != config:
+            continue
         if not any(k.endswith(kernel) for k in s.get("kernels", {})):
             continue
-        if s.get("records") != records or s.get("width") != width:
-            continue
-        if "traffic_bytes_per_launch_fetch_x2" in s and b:
+        if "traffic_bytes_per_launch_fetch_x2" in s:
             best = (s["traffic_bytes_per_launch_fetch_x2"], os.path.relpath(p, ROOT))
     return best
+
+
+def orbit_camera(k):
+    th = 2.0 * np.pi * k / ORBIT_FRAMES
+    return ((1.4e7 * np.sin(th), 0.0, 1.4e7 * np.cos(th)), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0)
 
 
 def main():
@@ -130,6 +205,9 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--mode", default="progressive", choices=["progressive", "frame"],
+                    help="progressive: N frames per step (weak); frame: one frame per step "
+                         "split over the N ranks (strong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -154,31 +232,26 @@ def main():
     torch.cuda.set_device(device)
     dev = torch.device(f"cuda:{device}")
 
-    rn, bis, L, W, H, desc = CONFIGS[args.config]
+    rn, bis, L, W, H, tf, orbit_cfg, desc = CONFIGS[args.config]
     t0 = time.time()
-    cells = irt.synth_grid(rn, bis, L)
-    log(f"[rank {rank}] grid: {cells.size} records ({time.time() - t0:.1f} s)")
-    setup = irt.setup_frame(cells, W, H, camera=FRAMING)
-    t0 = time.time()
-    ctx = irt.Context(cells, device)
-    ctx.set_transfunc(setup.lut, setup.value_range, setup.opacity_scale)
-    log(f"[rank {rank}] context: {ctx.info.deviceBytes / 2**30:.2f} GiB HBM, locator G="
-        f"{ctx.info.locatorFaceRes} entries={ctx.info.locatorEntries} ({time.time() - t0:.1f} s)")
+    ctx = irt.Context.synth(rn, bis, L, device)  # streamed into HBM, built on the device
+    info = ctx.info
+    setup = irt.setup_frame(None, W, H, camera=FRAMING, info=info)
+    ctx.set_transfunc(make_lut(tf, setup.lut), setup.value_range)
+    import resource
+    log(f"[rank {rank}] context: {info.numCells} records, {info.deviceBytes / 2**30:.2f} GiB HBM, "
+        f"locator G={info.locatorFaceRes} entries={info.locatorEntries} ({time.time() - t0:.1f} s, "
+        f"peak host RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.2f} GiB)")
 
     lp = setup.lp
     orbit = None
-    if args.config == "c5":  # one orbit frame per step (a new view: accumID 0)
-        orbit = []
-        for k in range(ORBIT_FRAMES):
-            th = 2.0 * np.pi * k / ORBIT_FRAMES
-            orbit.append(irt.camera_look_at((1.4e7 * np.sin(th), 0.0, 1.4e7 * np.cos(th)),
-                                            (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0, W, H))
+    if orbit_cfg:  # one orbit frame per step (a new view: accumID 0)
+        orbit = [irt.camera_look_at(*orbit_camera(k), W, H) for k in range(ORBIT_FRAMES)]
     ntiles = irt.num_tiles(W, H)
     stream = torch.cuda.current_stream(device).cuda_stream
-    # frames per step: 1 on one GPU; N on N GPUs (weak scaling: N frames of the
-    # progressive accumulation per step, each rank rendering its interleaved 64x64 tiles of
-    # all N frames in one launch, rank 0 gathering the final RGBA8 tiles over RCCL)
-    frames = world
+    # frames per step: 1 on one GPU or in frame mode; N in progressive mode on N GPUs
+    strong = args.mode == "frame"
+    frames = 1 if (world == 1 or strong) else world
     if world == 1:
         fb = torch.zeros(W * H, dtype=torch.int32, device=dev)
         accum = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
@@ -205,22 +278,27 @@ def main():
         b = s % 2
         if b in inflight:  # the gather that last read this buffer must be done
             finish(inflight.pop(b), b)
-        ctx.render_tiles_accumulate(lp, W, H, rank, world, frames, fg.bufs[b].data_ptr(),
-                                    tiles_acc.data_ptr(), stream)
-        inflight[b] = fg.gather_async(b)  # RCCL gather of this step's frame, overlapped
+        if strong:
+            ctx.render_tiles(lp, W, H, rank, world, fg.bufs[b].data_ptr(), tiles_acc.data_ptr(),
+                             stream)
+        else:
+            ctx.render_tiles_accumulate(lp, W, H, rank, world, frames, fg.bufs[b].data_ptr(),
+                                        tiles_acc.data_ptr(), stream)
+        inflight[b] = (s, fg.gather_async(b))  # RCCL gather of this step's frame, overlapped
 
-    def finish(work, b):
-        g = fg.finish(work, b)
+    def finish(pending, b):
+        g = fg.finish(pending[1], b)
         if rank == 0:
             ctx.unpack_tiles(g.data_ptr(), world, maxt, W, H, fb.data_ptr(), stream)
 
-    def drain():
-        for b in sorted(inflight):
+    def drain():  # oldest gather first: rank 0's framebuffer ends with the newest frame
+        for b in sorted(inflight, key=lambda k: inflight[k][0]):
             finish(inflight.pop(b), b)
 
     for f in range(args.warmup):
         step(f)
-    drain()
+    if world > 1:
+        drain()
     st = ctx.stats()
     log(f"[rank {rank}] warmup: last launch kernel {st.kernelMs:.3f} ms, {st.samplesFound} "
         f"samples, {st.candidatesTested} candidates")
@@ -240,9 +318,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     tot, launches = ctx.stats_total()
-    import resource
     log(f"[rank {rank}] timed {args.steps} steps ({launches} launches) in {elapsed:.3f} s; "
-        f"peak host RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.1f} GiB")
+        f"peak host RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.2f} GiB")
     samples, in_box = tot.samplesFound, tot.raysInBox
     if world > 1:
         rdev = dev if args.dist_backend == "nccl" else "cpu"
@@ -264,6 +341,15 @@ def main():
     achieved = bytes_per_launch / avg_kernel_s if avg_kernel_s > 0 else float("nan")
 
     if rank == 0:
+        if world == 1:
+            parallelism = "single GPU"
+        elif strong:
+            parallelism = (f"{world} GPUs x 64x64 interleaved tiles of ONE frame per step, RCCL "
+                           f"gather of the RGBA8 tiles to rank 0 overlapped with the next step")
+        else:
+            parallelism = (f"{world} GPUs x 64x64 interleaved frame tiles, {frames} progressive "
+                           f"frames per step in one launch per rank, RCCL gather of the final "
+                           f"RGBA8 tiles to rank 0 overlapped with the next step")
         out = {
             "metric": METRIC,
             "value": round(mray, 3),
@@ -273,26 +359,26 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
             "config": {
+                "name": args.config,
                 "workload": desc + (", orbit camera (eye 1.4e7 (sin t, 0, cos t), -fovy 60), "
                                     "one orbit frame per step"
                                     if orbit is not None else
                                     ", framing camera --camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60, "
                                     "one frame per step") +
-                           ", woodcockTrackingWithAccel, default TF",
-                "records": int(cells.size), "width": W, "height": H,
-                "parallelism": (f"{world} GPUs x 64x64 interleaved frame tiles, {frames} progressive "
-                                f"frames per step in one launch per rank, RCCL gather of the "
-                                f"final RGBA8 tiles to rank 0 overlapped with the next step")
-                if world > 1 else "single GPU",
+                           ", woodcockTrackingWithAccel, " + ("sparse comb TF" if tf == "comb" else "default TF"),
+                "records": int(info.numCells), "width": W, "height": H,
+                "transfer_function": tf,
+                "parallelism": parallelism,
                 "frames_per_step": frames,
                 "ms_per_frame": round(elapsed / (args.steps * frames) * 1e3, 4),
                 "samples_per_frame": samples_all / args.steps / frames,
                 "rays_in_box_per_frame": in_box_all / args.steps / frames,
+                "candidates_per_sample": tot.candidatesTested / max(samples, 1),
                 "kernel_ms_rank0": round(avg_kernel_s * 1e3, 4),
                 "bytes_per_launch_rank0": bytes_per_launch,
             },
@@ -305,14 +391,15 @@ def main():
                 "traffic": None,
             },
         }
-        prof = profiled_traffic(f"k_render<{irt.default_kernel_id()}>", int(cells.size), W)
+        prof = profiled_traffic(f"k_render<{irt.default_kernel_id()}>", args.config)
         if prof and world == 1:
             out["roofline"]["traffic"] = prof[0]
             out["roofline"]["traffic_source"] = (
                 f"{prof[1]}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE per launch "
                 f"of the same kernel and workload")
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cells, setup, W, H, args.cpu_budget)
+            cam = orbit_camera(0) if orbit is not None else FRAMING
+            out["cpu_baseline"] = cpu_baseline(rn, bis, L, W, H, cam, tf, args.cpu_budget)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -216,19 +216,34 @@ __global__ void k_unpack(const uint32_t *gathered, int numRanks, int maxTiles, i
 // ring (vector stores over the mapped pointer, visible to the host at the kernel's
 // end-of-kernel release), and the next ring slot zeroed for the next launch.  One dispatch
 // instead of a fill kernel plus an SDMA copy per frame.
-__global__ void __launch_bounds__(256) k_stats_out(const unsigned long long *cur, const uint32_t *wg,
-                                                   size_t numWG, unsigned long long *host,
-                                                   unsigned long long *next) {
-  __shared__ unsigned long long s_sum[256 / 64][kCnt];
+__global__ void __launch_bounds__(1024) k_stats_out(const unsigned long long *cur, const uint32_t *wg,
+                                                    size_t numWG, unsigned long long *host,
+                                                    unsigned long long *next) {
+  static_assert(kCnt == 8, "two uint4 per workgroup record");
+  __shared__ unsigned long long s_sum[1024 / 64][kCnt];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   unsigned long long acc[kCnt];
 #pragma unroll
   for (int k = 0; k < kCnt; ++k) acc[k] = 0ull;
-  if (wg)
-    for (size_t b = t; b < numWG; b += 256) {
+  if (wg) {
+    // every thread's records loaded four at a time (eight 16-B loads in flight): the
+    // reduction costs one memory round trip per 4096 workgroups, not one per record
+    const uint4 *W4 = reinterpret_cast<const uint4 *>(wg);
+    for (size_t b0 = t; b0 < numWG; b0 += 4 * 1024) {
+      uint4 r[8];
 #pragma unroll
-      for (int k = 0; k < kCnt; ++k) acc[k] += wg[b * kCnt + k];
+      for (int u = 0; u < 4; ++u) {
+        const size_t b = b0 + (size_t)u * 1024;
+        r[2 * u] = b < numWG ? W4[2 * b] : make_uint4(0u, 0u, 0u, 0u);
+        r[2 * u + 1] = b < numWG ? W4[2 * b + 1] : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc[0] += r[2 * u].x, acc[1] += r[2 * u].y, acc[2] += r[2 * u].z, acc[3] += r[2 * u].w;
+        acc[4] += r[2 * u + 1].x, acc[5] += r[2 * u + 1].y, acc[6] += r[2 * u + 1].z, acc[7] += r[2 * u + 1].w;
+      }
     }
+  }
 #pragma unroll
   for (int k = 0; k < kCnt; ++k) {
     unsigned long long v = acc[k];
@@ -238,7 +253,8 @@ __global__ void __launch_bounds__(256) k_stats_out(const unsigned long long *cur
   __syncthreads();
   if (t < 16) {
     unsigned long long v = cur[t];
-    if (t < kCnt) v += s_sum[0][t] + s_sum[1][t] + s_sum[2][t] + s_sum[3][t];
+    if (t < kCnt)
+      for (int j = 0; j < 1024 / 64; ++j) v += s_sum[j][t];
     host[t] = v;
     if (next != cur) next[t] = 0ull;
   }
@@ -266,7 +282,7 @@ void launch_max_opacities(const float *vr, size_t numMCs, const float4 *lut, int
 }
 void launch_stats_out(const unsigned long long *cur, const uint32_t *wgCounts, size_t numWG,
                       unsigned long long *host, unsigned long long *next, hipStream_t s) {
-  hipLaunchKernelGGL(k_stats_out, dim3(1), dim3(256), 0, s, cur, wgCounts, numWG, host, next);
+  hipLaunchKernelGGL(k_stats_out, dim3(1), dim3(1024), 0, s, cur, wgCounts, numWG, host, next);
 }
 // a u32 array between device memory and mapped pinned host memory (either direction):
 // the scheduling costs and block orders, without an SDMA copy on the render stream

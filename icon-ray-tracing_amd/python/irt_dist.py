@@ -68,10 +68,13 @@ def unpack_host(gathered: np.ndarray, split: TileSplit) -> np.ndarray:
 class FrameGather:
     """Per-frame RCCL gather of packed RGBA8 tiles to rank 0 (torch.distributed).
 
-    `buffers` > 1 double-buffers the packed tiles so that the gather of frame s can run
-    (async_op, on the collective's own stream) while frame s+1 renders into the other
-    buffer: gather_async() returns a pending handle, finish() waits for it (making the
-    current stream wait, not the host) and on rank 0 returns the rank-major frame."""
+    Rank 0 receives straight into rank-major storage: the gather list is the per-rank rows
+    of one preallocated (world, tiles) tensor (contiguous views, so the collective writes
+    them in place and no concatenation copy follows).  `buffers` > 1 double-buffers the
+    packed tiles so that the gather of frame s can run (async_op, on the collective's own
+    stream) while frame s+1 renders into the other buffer: gather_async() returns a
+    pending handle, finish() waits for it (making the current stream wait, not the host)
+    and on rank 0 returns the rank-major frame."""
 
     def __init__(self, split: TileSplit, device, buffers: int = 1, stage_cpu: bool = False):
         import torch
@@ -81,10 +84,16 @@ class FrameGather:
         n = split.max_tiles * TILE_PIX
         cdev = "cpu" if stage_cpu else device
         self.bufs = [torch.zeros(n, dtype=torch.int32, device=device) for _ in range(buffers)]
-        self.parts = ([[torch.zeros(n, dtype=torch.int32, device=cdev) for _ in range(split.world)]
-                       for _ in range(buffers)] if split.rank == 0 else None)
-        self.gathered = (torch.zeros(split.world * n, dtype=torch.int32, device=device)
-                         if split.rank == 0 else None)
+        if split.rank == 0:
+            self.gathered = [torch.zeros(split.world * n, dtype=torch.int32, device=device)
+                             for _ in range(buffers)]
+            recv = (self.gathered if not stage_cpu else
+                    [torch.zeros(split.world * n, dtype=torch.int32, device=cdev)
+                     for _ in range(buffers)])
+            self.recv = recv
+            self.parts = [list(r.view(split.world, n).unbind(0)) for r in recv]
+        else:
+            self.gathered = self.recv = self.parts = None
         self.tiles = self.bufs[0]
 
     def gather_async(self, b: int = 0):
@@ -96,11 +105,9 @@ class FrameGather:
         work.wait()
         if self.split.rank != 0:
             return None
-        if self.stage_cpu:
-            self.gathered.copy_(self.torch.cat(self.parts[b]))
-        else:
-            self.torch.cat(self.parts[b], out=self.gathered)
-        return self.gathered
+        if self.stage_cpu:  # host-staged rehearsal: one copy of the gathered frame to HBM
+            self.gathered[b].copy_(self.recv[b])
+        return self.gathered[b]
 
     def gather(self):
         """Collective: every rank calls it after rendering into self.tiles.  On rank 0

@@ -6,11 +6,20 @@
 // may only be loaded by tests/, __graft_entry__.smoke() and bench.py's
 // cpu_baseline leg.  Nothing under icon-ray-tracing_amd/ uses it.
 //
-// Pinning: oracle/ref_harness.cpp compiles the reference's own headers
-// (vecmath.h, dvr_course-common-both.h, ICONGrid.h, ShellAccel.h, DDA.h,
-// camera.h) and pipeline.cu/fb.cu/transfunc.cu from /root/reference into
-// oracle/_ref/; tests/golden/ holds fixtures generated from it and
-// tests/test_oracle_*.py check this restatement against them bit for bit.
+// Pinning: oracle/ref_harness.cpp, compiled into oracle/_ref/ by `make -C oracle ref`,
+// includes the reference's own headers from /root/reference as they are (vecmath.h,
+// dvr_course-common-both.h, dvr_course-common.h, ICONGrid.h, ShellAccel.h, DDA.h,
+// UElems.h, camera.h, thread_pool.h, for_each.h) and restates only the ~60 lines of
+// deviceCode.cu raygen glue and the host shell build (Params.h needs the absent cuBQL, so
+// deviceCode.cu itself does not compile; pipeline.cu / fb.cu / transfunc.cu are not
+// compiled either).  tests/golden/ holds fixtures generated from it and
+// tests/test_oracle_golden.py checks this restatement against them bit for bit.
+//
+// Locators (the `fast` argument of oracle_render*): 0 the reference's literal linear scan
+// (deviceCode.cu:116-123, sample() recomputing its planes), 1 the same scan over
+// precomputed planes, 2 a direction-voxel locator (DirGrid below, the CPU baseline's
+// "BVH or column locator" of BASELINE.md): the same first-index-wins answer, each sample
+// testing only the records listed for its voxel.
 //
 // Numerics: every float expression keeps the reference's evaluation order;
 // libm calls (asinf, atan2f, sinf, cosf, logf, powf, tanf, atanf, log10f) go to
@@ -584,10 +593,29 @@ struct Tri {
 };
 
 // ---------------------------------------------------------------- renderer
+// ---------------------------------------------------------------- direction-voxel locator
+// Every record whose sample() can accept a point with unit direction u is listed in the
+// voxel of u in a V^3 grid over [-1,1]^3, in index order; only occupied voxels are stored
+// (sorted 64-bit keys + CSR).  A record's accepting directions are its corner triangle's
+// geodesic patch (or, for clockwise corners, the antipodal patch; found by probing its own
+// float planes), whose points q/|q| (q on the flat triangle) lie in the corners' box
+// stretched by 1/d, d = the flat triangle's distance from the origin; the box is padded by
+// 1e-5 (> the float error of a sample point's direction).  Records whose planes carve out
+// no cone, or whose patch is too wide for the box bound (d < 0.05), and zero-thickness
+// records (accepting every direction at one radius) are tested for every sample.
+struct DirGrid {
+  int V = 0;
+  std::vector<uint64_t> keys;   // occupied voxels, ascending
+  std::vector<uint32_t> off;    // keys.size() + 1
+  std::vector<uint32_t> recs;   // per voxel, ascending record indices
+  std::vector<uint32_t> always; // tested for every sample, ascending
+};
+
 struct Scene {
   const oc_cell *cells;
   size_t n;
-  bool fast;
+  int fast;
+  DirGrid grid;
   std::vector<CellPlanes> planes;  // fast mode only
   std::vector<Wedge> wedges;       // CUBQL_MODE only
   bool useWedges = false;
@@ -648,6 +676,141 @@ struct ThreadStats {
 };
 
 // sampleVolume, CPU branch: first cell index wins (deviceCode.cu:116-123)
+inline uint64_t dirKey(const DirGrid &G, double x, double y, double z) {
+  auto q = [&](double c) {
+    long v = (long)std::floor((c + 1.0) * 0.5 * G.V);
+    return (uint64_t)std::max(0L, std::min((long)G.V - 1, v));
+  };
+  return (q(z) * (uint64_t)G.V + q(y)) * (uint64_t)G.V + q(x);
+}
+
+void buildDirGrid(Scene &S, int nthreads) {
+  DirGrid &G = S.grid;
+  size_t cols = 0;
+  for (size_t i = 0; i < S.n; ++i)
+    if (i == 0 || memcmp(S.cells[i].lat, S.cells[i - 1].lat, 12) || memcmp(S.cells[i].lon, S.cells[i - 1].lon, 12))
+      ++cols;
+  // a voxel about one corner triangle wide: edge ~ sqrt(4 * (4 pi / cols) / sqrt(3)) radians
+  G.V = (int)std::max(8.0, std::min(2048.0, 2.0 / std::sqrt(29.0 / (double)std::max<size_t>(cols, 1))));
+  if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
+  if (nthreads <= 0) nthreads = 1;
+  std::vector<std::vector<std::pair<uint64_t, uint32_t>>> parts(nthreads);
+  std::vector<std::vector<uint32_t>> alw(nthreads);
+  const size_t chunk = (S.n + nthreads - 1) / nthreads;
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nthreads; ++t)
+    ts.emplace_back([&, t] {
+      for (size_t i = t * chunk; i < std::min(S.n, (t + 1) * chunk); ++i) {
+        const oc_cell &c = S.cells[i];
+        const float h0 = c.height[0], hN = c.height[c.numLayers];
+        if (!(h0 <= hN)) continue;  // inverted: the radial test never passes
+        if (h0 == hN) {             // zero thickness: any direction at r == h0
+          alw[t].push_back((uint32_t)i);
+          continue;
+        }
+        double d[3][3];
+        for (int k = 0; k < 3; ++k) {
+          const double la = c.lat[k], lo = c.lon[k];
+          d[k][0] = std::cos(la) * std::cos(lo), d[k][1] = std::cos(la) * std::sin(lo), d[k][2] = std::sin(la);
+        }
+        // which cone do the float planes carve out: probe the centroid and its antipode
+        double m[3] = {d[0][0] + d[1][0] + d[2][0], d[0][1] + d[1][1] + d[2][1], d[0][2] + d[1][2] + d[2][2]};
+        const double ml = std::sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+        const CellPlanes P = S.fast ? S.planes[i] : cellPlanes(c);
+        int side = -1;
+        const double rm = 0.5 * ((double)h0 + (double)hN);
+        for (int sgn = 0; sgn < 2 && side < 0 && ml > 0; ++sgn) {
+          const double s = (sgn ? -rm : rm) / ml;
+          const V3 p{(float)(m[0] * s), (float)(m[1] * s), (float)(m[2] * s)};
+          if (!(evalPlane(P.p[0], p) > 0.f) && !(evalPlane(P.p[1], p) > 0.f) && !(evalPlane(P.p[2], p) > 0.f))
+            side = sgn;
+        }
+        // distance of the flat triangle's plane from the origin
+        const double e1[3] = {d[1][0] - d[0][0], d[1][1] - d[0][1], d[1][2] - d[0][2]};
+        const double e2[3] = {d[2][0] - d[0][0], d[2][1] - d[0][1], d[2][2] - d[0][2]};
+        const double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+        const double nl = std::sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
+        const double dist = nl > 0 ? std::fabs(nv[0] * d[0][0] + nv[1] * d[0][1] + nv[2] * d[0][2]) / nl : 0.0;
+        if (side < 0 || !(dist >= 0.05)) {
+          alw[t].push_back((uint32_t)i);
+          continue;
+        }
+        const double sg = side ? -1.0 : 1.0;
+        double lo3[3], hi3[3];
+        for (int a = 0; a < 3; ++a) {
+          double mn = 1e9, mx = -1e9;
+          for (int k = 0; k < 3; ++k) {
+            mn = std::min(mn, sg * d[k][a]);
+            mx = std::max(mx, sg * d[k][a]);
+          }
+          lo3[a] = std::min(mn, mn / dist) - 1e-5;
+          hi3[a] = std::max(mx, mx / dist) + 1e-5;
+        }
+        auto q = [&](double c2) {
+          long v = (long)std::floor((c2 + 1.0) * 0.5 * G.V);
+          return std::max(0L, std::min((long)G.V - 1, v));
+        };
+        for (long z = q(lo3[2]); z <= q(hi3[2]); ++z)
+          for (long y = q(lo3[1]); y <= q(hi3[1]); ++y)
+            for (long x = q(lo3[0]); x <= q(hi3[0]); ++x)
+              parts[t].emplace_back(((uint64_t)z * G.V + (uint64_t)y) * G.V + (uint64_t)x, (uint32_t)i);
+      }
+    });
+  for (auto &th : ts) th.join();
+  std::vector<std::pair<uint64_t, uint32_t>> all;
+  size_t total = 0;
+  for (auto &p : parts) total += p.size();
+  all.reserve(total);
+  for (auto &p : parts) {
+    all.insert(all.end(), p.begin(), p.end());
+    std::vector<std::pair<uint64_t, uint32_t>>().swap(p);
+  }
+  std::sort(all.begin(), all.end());  // by voxel, then record index
+  G.recs.resize(all.size());
+  G.off.assign(1, 0u);
+  for (size_t k = 0; k < all.size(); ++k) {
+    if (k == 0 || all[k].first != all[k - 1].first) {
+      if (k) G.off.push_back((uint32_t)k);
+      G.keys.push_back(all[k].first);
+    }
+    G.recs[k] = all[k].second;
+  }
+  G.off.push_back((uint32_t)all.size());
+  for (auto &a : alw) G.always.insert(G.always.end(), a.begin(), a.end());
+  std::sort(G.always.begin(), G.always.end());
+}
+
+// fast == 2: the voxel's records and the always-tested ones, merged in index order
+inline bool sampleGrid(const Scene &S, V3 pos, float &value) {
+  const DirGrid &G = S.grid;
+  const double l = std::sqrt((double)pos.x * pos.x + (double)pos.y * pos.y + (double)pos.z * pos.z);
+  const uint32_t *a = nullptr, *ae = nullptr;
+  if (l > 0) {
+    const uint64_t key = dirKey(G, pos.x / l, pos.y / l, pos.z / l);
+    const auto it = std::lower_bound(G.keys.begin(), G.keys.end(), key);
+    if (it != G.keys.end() && *it == key) {
+      const size_t k = it - G.keys.begin();
+      a = G.recs.data() + G.off[k];
+      ae = G.recs.data() + G.off[k + 1];
+    }
+  }
+  const uint32_t *b = G.always.data(), *be = b + G.always.size();
+  if (l == 0) b = G.always.data(), be = b;  // unreachable for a sample in the shell
+  const float r = length(pos);
+  while (a != ae || b != be) {
+    uint32_t i;
+    if (b == be || (a != ae && *a < *b)) i = *a++;
+    else i = *b++;
+    if (r < S.rr[2 * i] || r > S.rr[2 * i + 1]) continue;
+    if (sampleFast(S.cells[i], S.planes[i], pos, value)) return true;
+  }
+  if (l == 0) {  // direction undefined: the reference's scan, literally
+    for (size_t i = 0; i < S.n; ++i)
+      if (sampleFast(S.cells[i], S.planes[i], pos, value)) return true;
+  }
+  return false;
+}
+
 inline bool sampleVolume(const Scene &S, V3 pos, float &value) {
   if (S.useTriangles) return sampleTriangles(S, pos, value);  // TRIANGLE_MODE
   if (S.useWedges) {  // CUBQL_MODE (deviceCode.cu:90-115)
@@ -655,6 +818,7 @@ inline bool sampleVolume(const Scene &S, V3 pos, float &value) {
       if (boxContains(wd.box, pos) && intersectWedgeEXT(value, pos, wd.v)) return true;
     return false;
   }
+  if (S.fast == 2) return sampleGrid(S, pos, value);
   if (S.fast) {
     const float r = length(pos);
     for (size_t i = 0; i < S.n; ++i) {
@@ -1069,23 +1233,11 @@ void oracle_clear(uint32_t *fb, float *accum, size_t numPixels) {
   }
 }
 
-int oracle_render(const oc_cell *cells, size_t n, const oc_params *p, int W, int H, int x0,
-                  int y0, int x1, int y1, float *accum, uint32_t *fb, int nthreads, int fast,
-                  oc_stats *stats) {
-  if (!p || W <= 0 || H <= 0 || x0 < 0 || y0 < 0 || x1 > W || y1 > H) return -1;
-  if (x1 <= x0 || y1 <= y0) return 0;
-  Scene S{cells, n, fast != 0, {}, {}, false, {}, {}, false};
-  if (S.fast) buildFast(S, nthreads);
-  if (p->mode == 2) {
-    S.useWedges = true;
-    buildWedges(cells, n, S.wedges);
-  }
-  if (p->mode == 1) {
-    S.useTriangles = true;
-    buildTriangles(S);
-  }
-  // parallel::for_each over 64x64 tiles (common/for_each.h:70-85,
-  // parallel_for.h:62-82), dynamic via an atomic counter (thread_pool.h:146-161)
+namespace {
+// the frame over 64x64 tiles pulled from an atomic counter (parallel::for_each,
+// common/for_each.h:70-85, parallel_for.h:62-82, thread_pool.h:146-161)
+int render_tiles(const Scene &S, const oc_params *p, int W, int H, int x0, int y0, int x1, int y1,
+                 float *accum, uint32_t *fb, int nthreads, oc_stats *stats) {
   const int tw = 64, th = 64;
   const int ntx = (x1 - x0 + tw - 1) / tw, nty = (y1 - y0 + th - 1) / th;
   const long numTiles = (long)ntx * nty;
@@ -1122,22 +1274,58 @@ int oracle_render(const oc_cell *cells, size_t n, const oc_params *p, int W, int
   return 0;
 }
 
+void prepare(Scene &S, const oc_params *p, int nthreads) {
+  if (S.fast && S.planes.empty() && S.n) buildFast(S, nthreads);
+  if (S.fast == 2 && S.grid.V == 0) buildDirGrid(S, nthreads);
+  if (p && p->mode == 2 && !S.useWedges) {
+    S.useWedges = true;
+    buildWedges(S.cells, S.n, S.wedges);
+  }
+  if (p && p->mode == 1 && !S.useTriangles) {
+    S.useTriangles = true;
+    buildTriangles(S);
+  }
+}
+}  // namespace
+
+struct oc_scene {
+  Scene S;
+};
+
+oc_scene *oracle_scene_new(const oc_cell *cells, size_t n, int fast, int nthreads) {
+  oc_scene *s = new oc_scene{Scene{cells, n, fast, {}, {}, {}, false, {}, {}, false}};
+  prepare(s->S, nullptr, nthreads);
+  return s;
+}
+
+int oracle_scene_render(oc_scene *s, const oc_params *p, int W, int H, int x0, int y0, int x1,
+                        int y1, float *accum, uint32_t *fb, int nthreads, oc_stats *stats) {
+  if (!s || !p || W <= 0 || H <= 0 || x0 < 0 || y0 < 0 || x1 > W || y1 > H) return -1;
+  if (x1 <= x0 || y1 <= y0) return 0;
+  prepare(s->S, p, nthreads);
+  return render_tiles(s->S, p, W, H, x0, y0, x1, y1, accum, fb, nthreads, stats);
+}
+
+void oracle_scene_free(oc_scene *s) { delete s; }
+
+int oracle_render(const oc_cell *cells, size_t n, const oc_params *p, int W, int H, int x0,
+                  int y0, int x1, int y1, float *accum, uint32_t *fb, int nthreads, int fast,
+                  oc_stats *stats) {
+  if (!p || W <= 0 || H <= 0 || x0 < 0 || y0 < 0 || x1 > W || y1 > H) return -1;
+  if (x1 <= x0 || y1 <= y0) return 0;
+  Scene S{cells, n, fast, {}, {}, {}, false, {}, {}, false};
+  prepare(S, p, nthreads);
+  return render_tiles(S, p, W, H, x0, y0, x1, y1, accum, fb, nthreads, stats);
+}
+
 int oracle_render_pixels(const oc_cell *cells, size_t n, const oc_params *p, int W, int H,
                          const int32_t *xy, int numPixels, float *accum, uint32_t *fb,
                          int nthreads, int fast, oc_stats *stats) {
   if (!p || W <= 0 || H <= 0 || numPixels < 0) return -1;
   for (int i = 0; i < numPixels; ++i)
     if (xy[2 * i] < 0 || xy[2 * i] >= W || xy[2 * i + 1] < 0 || xy[2 * i + 1] >= H) return -1;
-  Scene S{cells, n, fast != 0, {}, {}, false, {}, {}, false};
-  if (S.fast) buildFast(S, nthreads);
-  if (p->mode == 2) {
-    S.useWedges = true;
-    buildWedges(cells, n, S.wedges);
-  }
-  if (p->mode == 1) {
-    S.useTriangles = true;
-    buildTriangles(S);
-  }
+  Scene S{cells, n, fast, {}, {}, {}, false, {}, {}, false};
+  prepare(S, p, nthreads);
   std::atomic<int> counter{0};
   if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
   if (nthreads <= 0) nthreads = 1;
@@ -1237,13 +1425,13 @@ int oracle_intersect_wedge(const float *v24, oc_vec3 p, float *value) {
 }
 
 int oracle_wedge_sample(const oc_cell *cells, size_t n, oc_vec3 p, float *value) {
-  Scene S{cells, n, false, {}, {}, true, {}, {}, false};
+  Scene S{cells, n, 0, {}, {}, {}, true, {}, {}, false};
   buildWedges(cells, n, S.wedges);
   return sampleVolume(S, toV3(p), *value);
 }
 
 int oracle_triangle_sample(const oc_cell *cells, size_t n, oc_vec3 p, float *value) {
-  Scene S{cells, n, false, {}, {}, false, {}, {}, true};
+  Scene S{cells, n, 0, {}, {}, {}, false, {}, {}, true};
   buildTriangles(S);
   return sampleVolume(S, toV3(p), *value);
 }

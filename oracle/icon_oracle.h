@@ -117,11 +117,21 @@ void oracle_clear(uint32_t *fb, float *accum, size_t numPixels);
    on `nthreads` threads pulling 64x64 tiles from an atomic counter (mirrors
    common/thread_pool.h:129-163 + common/parallel_for.h:62-82).  accum (4*W*H floats)
    and fb (W*H) are read/modified in place.  fast!=0 skips the dead asinf/atan2f of
-   toSpherical inside sample() and tests the radius first (identical results).
+   toSpherical inside sample() and tests the radius first (identical results); fast==2
+   locates samples through the direction-voxel locator (identical results).
    Returns 0 on success. */
 int oracle_render(const oc_cell *cells, size_t n, const oc_params *p, int W, int H,
                   int x0, int y0, int x1, int y1, float *accum, uint32_t *fb,
                   int nthreads, int fast, oc_stats *stats);
+
+/* A scene whose locator tables are built once (fast as above; 2 = the direction-voxel
+   locator), then frames rendered on it as oracle_render does: the CPU baseline times the
+   render only, as the reference's own timer does (pipeline.cu:1062-1073). */
+typedef struct oc_scene oc_scene;
+oc_scene *oracle_scene_new(const oc_cell *cells, size_t n, int fast, int nthreads);
+int oracle_scene_render(oc_scene *s, const oc_params *p, int W, int H, int x0, int y0, int x1,
+                        int y1, float *accum, uint32_t *fb, int nthreads, oc_stats *stats);
+void oracle_scene_free(oc_scene *s);
 
 /* The same raygen for an explicit list of pixels (xy pairs), scheduled one pixel at a
    time over `nthreads` threads -- used to time a bounded, unbiased sample of a frame

@@ -276,7 +276,7 @@ class OracleScene:
         x0, y0, x1, y1 = rect if rect is not None else (0, 0, width, height)
         st = OStats()
         rc = olib().oracle_render(_p(self.cells), self.cells.size, C.byref(params), width, height,
-                                  x0, y0, x1, y1, _p(accum), _p(fb), threads, 1 if fast else 0,
+                                  x0, y0, x1, y1, _p(accum), _p(fb), threads, int(fast),
                                   C.byref(st))
         assert rc == 0
         return accum, fb, st
@@ -290,9 +290,40 @@ class OracleScene:
         st = OStats()
         rc = olib().oracle_render_pixels(_p(self.cells), self.cells.size, C.byref(params), width,
                                          height, _p(xy), xy.shape[0], _p(accum), _p(fb), threads,
-                                         1 if fast else 0, C.byref(st))
+                                         int(fast), C.byref(st))
         assert rc == 0
         return accum, fb, st
+
+
+class TimedScene:
+    """An oracle scene whose locator is built once (oracle_scene_new), so that frames can
+    be timed without the build -- bench.py's CPU baseline."""
+
+    def __init__(self, scene: "OracleScene", fast: int = 2, threads: int = 0):
+        L = olib()
+        L.oracle_scene_new.restype = C.c_void_p
+        L.oracle_scene_new.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int]
+        L.oracle_scene_render.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                          C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                          C.c_int, C.c_void_p]
+        L.oracle_scene_free.argtypes = [C.c_void_p]
+        self.scene = scene
+        self._h = L.oracle_scene_new(_p(scene.cells), scene.cells.size, fast, threads)
+
+    def render(self, params, width, height, rect=None, threads=0):
+        accum = np.zeros((height, width, 4), dtype=np.float32)
+        fb = np.zeros((height, width), dtype=np.uint32)
+        x0, y0, x1, y1 = rect if rect is not None else (0, 0, width, height)
+        st = OStats()
+        rc = olib().oracle_scene_render(self._h, C.byref(params), width, height, x0, y0, x1, y1,
+                                        _p(accum), _p(fb), threads, C.byref(st))
+        assert rc == 0
+        return accum, fb, st
+
+    def close(self):
+        if self._h:
+            olib().oracle_scene_free(self._h)
+            self._h = None
 
 
 def ref_render(scene: OracleScene, params: OParams, width, height, rect=None, accum=None,

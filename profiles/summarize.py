@@ -63,6 +63,7 @@ def main(d):
                         "algorithmic_bytes_per_launch": 92 * cfg.get("samples_per_frame", 0)
                         + 44 * cfg.get("rays_in_box_per_frame", 0)}
         out["records"], out["width"] = cfg.get("records"), cfg.get("width")
+        out["config_name"] = cfg.get("name")
     except Exception as e:  # noqa: BLE001
         out["bench_error"] = str(e)
     f = counters(os.path.join(d, "pmc_fetch"), "FETCH_SIZE")

@@ -1,0 +1,112 @@
+"""The multi-GPU frame split with the HIP renderer: world-size-2 processes (gloo,
+host-staged collectives, both ranks on cuda:0) render their interleaved 64x64 tiles
+through irt_render_tiles / irt_render_tiles_accumulate on torch's default stream, gather
+them to rank 0 with irt_dist.FrameGather (two frames in flight, rank-major receive
+buffers), and rank 0 unpacks them with irt_unpack_tiles -- bench.py's two multi-GPU modes:
+  * frame       one frame per step split over the ranks (strong scaling),
+  * progressive N progressive frames per step, each rank rendering its tiles of all N
+                (weak scaling).
+Rank 0's framebuffer must equal a single-process render bit for bit."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GRID = (2, 3, 47)
+W, H = 200, 136  # ragged: partial tiles on the right and bottom
+STEPS = 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, mode, out_path):
+    sys.path[:0] = [os.path.join(HERE, "..", "icon-ray-tracing_amd", "python"), HERE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    import irt
+    import irt_dist
+    from helpers import FRAMING
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    ctx = irt.Context.synth(*GRID, 0)
+    setup = irt.setup_frame(None, W, H, camera=FRAMING, info=ctx.info)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    lp = setup.lp
+    split = irt_dist.TileSplit(W, H, rank, world)
+    fg = irt_dist.FrameGather(split, "cuda:0", buffers=2, stage_cpu=True)
+    acc = torch.zeros(split.max_tiles * 4096 * 4, dtype=torch.float32, device="cuda:0")
+    fb = torch.zeros(W * H, dtype=torch.int32, device="cuda:0")
+    frames = 1 if mode == "frame" else world
+    inflight = {}
+
+    def finish(b):
+        g = fg.finish(inflight.pop(b)[1], b)
+        if rank == 0:  # NULL stream: ordered after the default-stream copy of the gather
+            ctx.unpack_tiles(g.data_ptr(), world, split.max_tiles, W, H, fb.data_ptr())
+
+    for s in range(STEPS):
+        b = s % 2
+        if b in inflight:
+            finish(b)
+        lp.accumID = s * frames
+        if mode == "frame":
+            ctx.render_tiles(lp, W, H, rank, world, fg.bufs[b].data_ptr(), acc.data_ptr())
+        else:
+            ctx.render_tiles_accumulate(lp, W, H, rank, world, frames, fg.bufs[b].data_ptr(),
+                                        acc.data_ptr())
+        inflight[b] = (s, fg.gather_async(b))
+    for b in sorted(inflight, key=lambda k: inflight[k][0]):  # oldest first
+        finish(b)
+    if rank == 0:
+        torch.cuda.synchronize()
+        np.save(out_path, fb.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+    ctx.close()
+
+
+@pytest.mark.parametrize("mode", ["frame", "progressive"])
+def test_two_rank_hip_frame_split(tmp_path, mode):
+    import torch
+    import torch.multiprocessing as mp
+
+    import irt
+    from helpers import FRAMING
+
+    world = 2
+    out = str(tmp_path / "frame.npy")
+    mp.start_processes(_worker, args=(world, _free_port(), mode, out), nprocs=world, join=True,
+                       start_method="spawn")
+    ctx = irt.Context.synth(*GRID, 0)
+    setup = irt.setup_frame(None, W, H, camera=FRAMING, info=ctx.info)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    lp = setup.lp
+    fb = torch.zeros(W * H, dtype=torch.int32, device="cuda:0")
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
+    frames = 1 if mode == "frame" else world
+    for s in range(STEPS):
+        lp.accumID = s * frames
+        if frames == 1:
+            ctx.render(lp, W, H, fb.data_ptr(), acc.data_ptr())
+        else:
+            ctx.render_accumulate(lp, W, H, frames, fb.data_ptr(), acc.data_ptr())
+    torch.cuda.synchronize()
+    ref = fb.cpu().numpy()
+    got = np.load(out)
+    assert (ref != 0).mean() > 0.3
+    assert np.array_equal(got, ref), int((got != ref).sum())
+    ctx.close()

@@ -359,3 +359,48 @@ def test_measured_cost_scheduling_keeps_frames_identical():
         assert_same_frame(a, f, a_ref, f_ref, f"launch {k}")
         assert (st.locateCalls, st.samplesFound) == (st_ref[0].locate_calls, st_ref[0].samples_found)
     ctx.close()
+
+
+def test_null_stream_is_ordered_with_torch_default_stream():
+    """irt_render with stream NULL runs on HIP's null stream, ordered with torch's default
+    stream: a zero_() of the buffers enqueued just before must land before the kernel reads
+    them, and a read-back enqueued just after must see the finished frame (no host sync in
+    between)."""
+    import torch
+    cells = irt.synth_grid(2, 2, 90)
+    W = 96
+    a_ref, f_ref, _, _ = oracle_frame(cells, W, W, camera=FRAMING)
+    setup = irt.setup_frame(cells, W, W, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    fb = torch.full((W * W,), 12345, dtype=torch.int32, device="cuda")
+    acc = torch.full((W * W * 4,), 7.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    for _ in range(3):
+        acc.fill_(7.0)   # garbage the previous frame...
+        fb.fill_(12345)
+        acc.zero_()      # ...then clear: both on torch's default stream
+        fb.zero_()
+        ctx.render(setup.lp, W, W, fb.data_ptr(), acc.data_ptr())  # stream NULL
+        a = acc.cpu().numpy().reshape(W, W, 4)  # default-stream copy, no explicit sync
+        f = fb.cpu().numpy().view(np.uint32).reshape(W, W)
+        assert_same_frame(a, f, a_ref, f_ref, "null stream")
+    ctx.close()
+
+
+def test_comb_transfunc_sample_heavy():
+    """bench.py's C3s transfer function (alpha 0.01 except every 50th LUT entry 1.0): the
+    majorants stay 1 while almost every tentative collision is rejected -- many samples
+    per ray, the long Woodcock chains -- still bit-exact, counts included."""
+    cells = irt.synth_grid(2, 3, 90)
+    setup = irt.setup_frame(cells, 8, 8)
+    lut = setup.lut.copy()
+    lut[:, 3] = 0.01
+    lut[::50, 3] = 1.0
+    a_ref, f_ref, st_ref, _ = oracle_frame(cells, 80, 80, camera=FRAMING, lut=lut,
+                                           value_range=setup.value_range)
+    a_gpu, f_gpu, st_gpu, _ = gpu_frame(cells, 80, 80, camera=FRAMING, lut=lut,
+                                        value_range=setup.value_range)
+    assert_same_frame(a_gpu, f_gpu, a_ref, f_ref, "comb TF")
+    assert st_gpu[0].locateCalls == st_ref[0].locate_calls
+    assert st_ref[0].samples_found > 4 * 80 * 80  # sample-heavy indeed

@@ -10,8 +10,11 @@ from golden_util import FRAME_FIXTURES, load, oracle_scene, params
 from helpers import bits
 
 
+@pytest.mark.parametrize("locator", [1, 2], ids=["scan", "dirgrid"])
 @pytest.mark.parametrize("name", FRAME_FIXTURES)
-def test_frame_fixture(name):
+def test_frame_fixture(name, locator):
+    """Both oracle locators: the reference's scan over precomputed planes (1) and the
+    direction-voxel locator of the CPU baseline (2)."""
     d = load(name)
     S = oracle_scene(d)
     # host setup: bounds, shell accelerator, majorants (hostCode.cu:792-808, 299-397)
@@ -27,7 +30,7 @@ def test_frame_fixture(name):
     accum = np.zeros((H, W, 4), np.float32)
     fb = np.zeros((H, W), np.uint32)
     for k, aid in enumerate(d["accum_ids"]):
-        _, _, st = S.render(params(S, d, aid), W, H, accum=accum, fb=fb, threads=4)
+        _, _, st = S.render(params(S, d, aid), W, H, accum=accum, fb=fb, threads=4, fast=locator)
         assert st.locate_calls == d["counts"][k][0] and st.samples_found == d["counts"][k][1]
     assert np.array_equal(bits(accum), bits(d["accum"]))
     assert np.array_equal(fb, d["fb"])
@@ -247,3 +250,21 @@ def test_reference_pixel_list_render_matches_oracle():
     a2, f2, st = S.render_pixels(p, W, W, xy, threads=4, fast=False)
     assert np.array_equal(bits(a1), bits(a2)) and np.array_equal(f1, f2)
     assert int(cnt[0]) == st.locate_calls and int(cnt[1]) == st.samples_found
+
+
+def test_dirgrid_locator_matches_scan_on_degenerate_scenes():
+    """The CPU baseline's locator (oracle fast=2) == the reference's scan on scenes with
+    cone-mode triangles, terrain, unsorted/zero-thickness/inverted records."""
+    import irt
+    from helpers import FRAMING, terrain_cells
+    for cells, W in ((irt.synth_grid(1, 0, 4), 64), (terrain_cells(11), 80),
+                     (irt.synth_grid(2, 3, 47, noise=0.2), 64)):
+        S = O.OracleScene(cells)
+        lut, vr = S.default_lut()
+        S.set_transfunc(lut, vr)
+        for cam in (FRAMING, None):
+            p = S.params(S.camera(W, W, cam))
+            a1, f1, s1 = S.render(p, W, W, threads=4, fast=1)
+            a2, f2, s2 = S.render(p, W, W, threads=4, fast=2)
+            assert np.array_equal(bits(a1), bits(a2)) and np.array_equal(f1, f2)
+            assert (s1.locate_calls, s1.samples_found) == (s2.locate_calls, s2.samples_found)
