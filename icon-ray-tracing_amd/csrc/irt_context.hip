@@ -46,10 +46,15 @@ struct irt_context {
   uint32_t *d_sphOff = nullptr;
   uint2 *d_sphRec = nullptr;
   uint32_t *d_sphBits = nullptr;
-  // per-workgroup event counts of the launches in flight: kSlots x wgCap x kCnt u32
-  // (a slot is rewritten only once its launch's statistics landed, see finish_slot)
-  uint32_t *d_wgCounts = nullptr;
+  // per-workgroup event counts of the launches in flight, written by the render kernel
+  // straight into pinned host memory (kSlots x wgCap x kCnt u32) and summed on the host
+  // when a launch's statistics are asked for (finish_slot): no statistics kernel, no
+  // same-line atomics per frame.  A slot is rewritten only once its launch is retired.
+  uint32_t *h_wgCounts = nullptr, *dh_wgCounts = nullptr;
   size_t wgCap = 0;             // workgroups per slot
+  size_t slotWG[32] = {};       // workgroups of the launch in each slot
+  bool slotBlock[32] = {};      // whether k_stats_out copied the slot's 16-counter block
+  bool lastBlock = false;       // ... for the previous launch (which zeroed this slot's)
   bool wgCountsOn = true;       // IRT_COUNTERS=atomic: device-scope atomics instead
   float4 *d_samples = nullptr;   // per-frame colours of a progressive batch
   size_t sampleCap = 0;
@@ -152,13 +157,14 @@ void free_all(irt_context *c) {
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
-                  c->d_sphBits, c->d_wgCounts, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
+                  c->d_sphBits, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
                   c->d_lut, c->d_counters};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->d_cells) (void)hipFree(c->d_cells);
   if (c->d_trig) (void)hipFree(c->d_trig);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
+  if (c->h_wgCounts) (void)hipHostFree(c->h_wgCounts);
   if (c->h_schedCost) (void)hipHostFree(c->h_schedCost);
   if (c->h_schedOrder) (void)hipHostFree(c->h_schedOrder);
   for (int i = 0; i < irt_context::kSlots; ++i) {
@@ -179,7 +185,13 @@ int finish_slot(irt_context *c, int i) {
     c->timedMs += ms;
     ++c->timedLaunches;
   }
-  const unsigned long long *h = c->h_counters + 16 * i;
+  unsigned long long h[16] = {};
+  if (c->slotBlock[i]) memcpy(h, c->h_counters + 16 * i, sizeof(h));
+  if (c->slotWG[i]) {  // the workgroups' counts, from pinned host memory
+    const uint32_t *w = c->h_wgCounts + (size_t)i * c->wgCap * kCnt;
+    for (size_t b = 0; b < c->slotWG[i]; ++b)
+      for (int k = 0; k < 5; ++k) h[k] += w[b * kCnt + k];
+  }
   irt_render_stats st;
   st.raysLaunched = h[0];
   st.raysInBox = h[1];
@@ -390,19 +402,17 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   const size_t lanes = (size_t)numTiles * 4096;
   const size_t numWG = (size_t)numTiles * 16 * (size_t)numFrames;
   if (c->wgCountsOn && numWG > c->wgCap) {
-    // every slot's launch must be done before the ring is reallocated
+    // every slot's launch must be retired before the ring is reallocated
     int rc = finish_stats(c);
     if (rc) return rc;
-    if (c->d_wgCounts) IRT_HIP(hipFree(c->d_wgCounts));
-    c->d_wgCounts = nullptr;
-    c->bytes -= c->wgCap * irt_context::kSlots * kCnt * sizeof(uint32_t);
+    if (c->h_wgCounts) IRT_HIP(hipHostFree(c->h_wgCounts));
+    c->h_wgCounts = c->dh_wgCounts = nullptr;
     c->wgCap = 0;
-    rc = dalloc(c, &c->d_wgCounts, numWG * irt_context::kSlots * kCnt);
-    if (rc) return rc;
+    IRT_HIP(hipHostMalloc((void **)&c->h_wgCounts, numWG * irt_context::kSlots * kCnt * sizeof(uint32_t)));
+    IRT_HIP(hipHostGetDevicePointer((void **)&c->dh_wgCounts, c->h_wgCounts, 0));
     c->wgCap = numWG;
-    c->info.deviceBytes = c->bytes;
   }
-  A.wgCounts = c->wgCountsOn ? c->d_wgCounts + (size_t)slot * c->wgCap * kCnt : nullptr;
+  A.wgCounts = c->wgCountsOn ? c->dh_wgCounts + (size_t)slot * c->wgCap * kCnt : nullptr;
   A.numSamples = numFrames;
   if (numFrames > 1) {
     const size_t need = lanes * (size_t)numFrames;
@@ -428,12 +438,23 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     int rc = sched_prepare(c, numBlocks, W, H, packed, tileBegin, tileStride, numTiles, lp, s);
     if (rc) return rc;
     A.schedOrder = c->schedOrderValid ? c->d_schedOrder + (size_t)c->schedBuf * c->schedCap : nullptr;
-    A.schedCost = c->d_schedCost;
-    // copy the costs back every 8th launch (a 4*numBlocks-byte D2H on the stream)
+    // every 8th launch writes its workgroups' durations straight into this slot's pinned
+    // host copy; the others into device memory nobody reads
     copyCosts = c->launches - c->schedLastCopy >= 8;
+    if (copyCosts) {
+      uint32_t *dh = nullptr;
+      IRT_HIP(hipHostGetDevicePointer((void **)&dh, c->h_schedCost + (size_t)slot * c->schedCap, 0));
+      A.schedCost = dh;
+    } else {
+      A.schedCost = c->d_schedCost;
+    }
   }
+  // the 16-counter block (device atomics) is only needed by the statistics variant and the
+  // IRT_COUNTERS=atomic mode; it must start zeroed
+  const bool block = !c->wgCountsOn || (c->variant & 32768) != 0;
+  if (block && !c->lastBlock) IRT_HIP(hipMemsetAsync(A.counters, 0, 16 * sizeof(unsigned long long), s));
   if (c->launches > 0 && s != c->lastStream) {
-    // this slot was zeroed by the previous launch's k_stats_out on another stream
+    // this slot may have been zeroed by the previous launch's k_stats_out on another stream
     IRT_HIP(hipStreamWaitEvent(s, c->evDone[(c->launches - 1) % irt_context::kSlots], 0));
   }
   c->lastStream = s;
@@ -444,15 +465,16 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   }
   IRT_HIP(hipGetLastError());
   if (c->timed[slot]) IRT_HIP(hipEventRecord(c->ev1[slot], s));
-  launch_stats_out(A.counters, A.wgCounts, numTiles > 0 ? numWG : 0, c->dh_counters + 16 * slot,
-                   c->d_counters + 16 * ((c->launches + 1) % irt_context::kSlots), s);
-  IRT_HIP(hipGetLastError());
+  if (block) {
+    launch_stats_out(A.counters, c->dh_counters + 16 * slot,
+                     c->d_counters + 16 * ((c->launches + 1) % irt_context::kSlots), s);
+    IRT_HIP(hipGetLastError());
+  }
+  c->slotBlock[slot] = block;
+  c->lastBlock = block;
+  c->slotWG[slot] = (c->wgCountsOn && numTiles > 0) ? numWG : 0;
   c->schedCopied[slot] = -1;
   if (copyCosts) {
-    uint32_t *dh = nullptr;
-    IRT_HIP(hipHostGetDevicePointer((void **)&dh, c->h_schedCost + (size_t)slot * c->schedCap, 0));
-    launch_copy_u32(c->d_schedCost, dh, (size_t)numBlocks, s);
-    IRT_HIP(hipGetLastError());
     c->schedCopied[slot] = c->launches;
     c->schedLastCopy = c->launches;
   }

@@ -58,8 +58,8 @@ struct RenderArgs {
   const uint32_t *sphOff;
   const uint2 *sphRec;
   const uint32_t *sphBits;
-  // per-workgroup event counts (kCnt u32 per workgroup, summed by k_stats_out); null:
-  // device-scope atomics into `counters`
+  // per-workgroup event counts (kCnt u32 per workgroup, in pinned host memory, summed by
+  // the host); null: device-scope atomics into `counters`
   uint32_t *wgCounts;
   // progressive batch (irt_render_accumulate): frames accumID .. accumID+numSamples-1;
   // for numSamples > 1 each frame's colour goes to sampleBuf[frame][lane] first
@@ -87,8 +87,8 @@ void launch_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n,
 void launch_max_opacities(const float *valueRanges, size_t numMCs, const float4 *lut, int size,
                           float lo, float hi, float *maxOp, hipStream_t s);
 void launch_clear(uint32_t *fb, float4 *accum, size_t n, hipStream_t s);
-void launch_stats_out(const unsigned long long *cur, const uint32_t *wgCounts, size_t numWG,
-                      unsigned long long *host, unsigned long long *next, hipStream_t s);
+void launch_stats_out(const unsigned long long *cur, unsigned long long *host,
+                      unsigned long long *next, hipStream_t s);
 void launch_copy_u32(const uint32_t *src, uint32_t *dst, size_t n, hipStream_t s);
 // The scene build on the device (irt_build.hip): per-record blocks and the binned cube-map
 // locator (irt_build.h) from the cells and their glibc corner trig in HBM.  On success the

@@ -96,12 +96,19 @@ __device__ __forceinline__ float3 to_cartesian_trig(float r, const float4 &t) {
   return make_float3((r * t.x) * t.z, (r * t.x) * t.w, r * t.y);  // ICONGrid.h:44-54
 }
 
-__global__ void __launch_bounds__(64) k_grid_build(const irt_icon_cell *cells, const float4 *trig,
-                                                   size_t n, int dim, float3 lo, float3 hi,
-                                                   float *valueRanges) {
-  // one wave per cell: every lane walks the layers (the merge logic is uniform), the lanes
-  // share each merged box's macrocells
-  const size_t ci = blockIdx.x;
+// A merged layer box with its value range, deferred to k_grid_boxes when it covers more
+// than kSmallBox macrocells (R1B00/R2B00-class columns): one lane would serialise it.
+struct GridBox {
+  int3 lo, hi;
+  float rLo, rHi;
+};
+constexpr long kSmallBox = 256;
+
+__global__ void __launch_bounds__(128) k_grid_build(const irt_icon_cell *cells, const float4 *trig,
+                                                    size_t n, int dim, float3 lo, float3 hi,
+                                                    float *valueRanges, GridBox *big,
+                                                    unsigned long long *numBig, size_t bigCap) {
+  const size_t ci = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (ci >= n) return;
   const irt_icon_cell &c = cells[ci];
   const float4 t0 = trig[3 * ci], t1 = trig[3 * ci + 1], t2 = trig[3 * ci + 2];
@@ -109,16 +116,21 @@ __global__ void __launch_bounds__(64) k_grid_build(const irt_icon_cell *cells, c
   float rLo = 0.f, rHi = 0.f;
   bool have = false;
   auto flush = [&]() {
-    const int nx = pHi.x - pLo.x + 1, ny = pHi.y - pLo.y + 1, nz = pHi.z - pLo.z + 1;
-    const long total = (long)nx * ny * nz;
-    for (long q = threadIdx.x; q < total; q += blockDim.x) {
-      const int mx = pLo.x + (int)(q % nx);
-      const int my = pLo.y + (int)((q / nx) % ny);
-      const int mz = pLo.z + (int)(q / ((long)nx * ny));
-      float *vr = valueRanges + 2 * ((size_t)mz * dim * dim + (size_t)my * dim + mx);
-      atomic_min_f(vr, rLo);
-      atomic_max_f(vr + 1, rHi);
+    const long nx = pHi.x - pLo.x + 1, ny = pHi.y - pLo.y + 1, nz = pHi.z - pLo.z + 1;
+    if (numBig && nx * ny * nz > kSmallBox) {
+      const unsigned long long k = atomicAdd(numBig, 1ull);
+      if (k < bigCap) {
+        big[k] = {pLo, pHi, rLo, rHi};
+        return;
+      }  // list full: this lane does it
     }
+    for (int mz = pLo.z; mz <= pHi.z; ++mz)
+      for (int my = pLo.y; my <= pHi.y; ++my)
+        for (int mx = pLo.x; mx <= pHi.x; ++mx) {
+          float *vr = valueRanges + 2 * ((size_t)mz * dim * dim + (size_t)my * dim + mx);
+          atomic_min_f(vr, rLo);
+          atomic_max_f(vr + 1, rHi);
+        }
   };
   for (int i = 0; i < c.numLayers; ++i) {
     const float hb = c.height[i], ht = c.height[i + 1];
@@ -163,6 +175,24 @@ __global__ void __launch_bounds__(64) k_grid_build(const irt_icon_cell *cells, c
     have = true;
   }
   if (have) flush();
+}
+
+
+// The deferred boxes: one workgroup per box, lanes sharing its macrocells.
+__global__ void __launch_bounds__(256) k_grid_boxes(const GridBox *big, const unsigned long long *numBig,
+                                                    size_t bigCap, int dim, float *valueRanges) {
+  const unsigned long long nb = *numBig < bigCap ? *numBig : bigCap;
+  for (size_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const GridBox q = big[b];
+    const long nx = q.hi.x - q.lo.x + 1, ny = q.hi.y - q.lo.y + 1, nz = q.hi.z - q.lo.z + 1;
+    for (long k = threadIdx.x; k < nx * ny * nz; k += blockDim.x) {
+      const int mx = q.lo.x + (int)(k % nx), my = q.lo.y + (int)((k / nx) % ny),
+                mz = q.lo.z + (int)(k / (nx * ny));
+      float *vr = valueRanges + 2 * ((size_t)mz * dim * dim + (size_t)my * dim + mx);
+      atomic_min_f(vr, q.rLo);
+      atomic_max_f(vr + 1, q.rHi);
+    }
+  }
 }
 
 // computeMaxOpacities(ShellAccel) (hostCode.cu:362-397)
@@ -211,52 +241,17 @@ __global__ void k_unpack(const uint32_t *gathered, int numRanks, int maxTiles, i
   }
 }
 
-// Per-launch statistics hand-off (irt_context.hip render_impl): the workgroups' event
-// counts (kCnt u32 each) summed, plus this launch's 16-counter block, into the pinned host
-// ring (vector stores over the mapped pointer, visible to the host at the kernel's
-// end-of-kernel release), and the next ring slot zeroed for the next launch.  One dispatch
-// instead of a fill kernel plus an SDMA copy per frame.
-__global__ void __launch_bounds__(1024) k_stats_out(const unsigned long long *cur, const uint32_t *wg,
-                                                    size_t numWG, unsigned long long *host,
-                                                    unsigned long long *next) {
-  static_assert(kCnt == 8, "two uint4 per workgroup record");
-  __shared__ unsigned long long s_sum[1024 / 64][kCnt];
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  unsigned long long acc[kCnt];
-#pragma unroll
-  for (int k = 0; k < kCnt; ++k) acc[k] = 0ull;
-  if (wg) {
-    // every thread's records loaded four at a time (eight 16-B loads in flight): the
-    // reduction costs one memory round trip per 4096 workgroups, not one per record
-    const uint4 *W4 = reinterpret_cast<const uint4 *>(wg);
-    for (size_t b0 = t; b0 < numWG; b0 += 4 * 1024) {
-      uint4 r[8];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const size_t b = b0 + (size_t)u * 1024;
-        r[2 * u] = b < numWG ? W4[2 * b] : make_uint4(0u, 0u, 0u, 0u);
-        r[2 * u + 1] = b < numWG ? W4[2 * b + 1] : make_uint4(0u, 0u, 0u, 0u);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        acc[0] += r[2 * u].x, acc[1] += r[2 * u].y, acc[2] += r[2 * u].z, acc[3] += r[2 * u].w;
-        acc[4] += r[2 * u + 1].x, acc[5] += r[2 * u + 1].y, acc[6] += r[2 * u + 1].z, acc[7] += r[2 * u + 1].w;
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kCnt; ++k) {
-    unsigned long long v = acc[k];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    if (lane == 0) s_sum[w][k] = v;
-  }
-  __syncthreads();
-  if (t < 16) {
-    unsigned long long v = cur[t];
-    if (t < kCnt)
-      for (int j = 0; j < 1024 / 64; ++j) v += s_sum[j][t];
-    host[t] = v;
-    if (next != cur) next[t] = 0ull;
+// Per-launch statistics hand-off of the statistics variant and IRT_COUNTERS=atomic
+// (irt_context.hip render_impl): this launch's 16-counter block into the pinned host ring
+// (vector stores over the mapped pointer, visible to the host at the kernel's end-of-kernel
+// release) and the next ring slot zeroed for the next launch.  (The default path needs no
+// such kernel: the render kernel's workgroups write their counts to host memory.)
+__global__ void k_stats_out(const unsigned long long *cur, unsigned long long *host,
+                            unsigned long long *next) {
+  const int i = threadIdx.x;
+  if (i < 16) {
+    host[i] = cur[i];
+    if (next != cur) next[i] = 0ull;
   }
 }
 
@@ -272,17 +267,32 @@ void launch_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, float3 
 void launch_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n, float3 lo,
                        float3 hi, float *vr, hipStream_t s) {
   if (n == 0) return;
-  hipLaunchKernelGGL(k_grid_build, dim3((unsigned)n), dim3(64), 0, s, cells, trig, n, kGridDim, lo,
-                     hi, vr);
+  // the deferred-box list: sized for a few boxes per cell, capped (overflow stays in-lane)
+  const size_t cap = std::min<size_t>(4 * n + 1024, size_t(1) << 22);
+  GridBox *big = nullptr;
+  unsigned long long *numBig = nullptr;
+  if (hipMallocAsync((void **)&big, cap * sizeof(GridBox), s) != hipSuccess ||
+      hipMallocAsync((void **)&numBig, sizeof(unsigned long long), s) != hipSuccess) {
+    // no scratch: every box in-lane
+    hipLaunchKernelGGL(k_grid_build, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, cells, trig,
+                       n, kGridDim, lo, hi, vr, (GridBox *)nullptr, (unsigned long long *)nullptr, (size_t)0);
+    return;
+  }
+  (void)hipMemsetAsync(numBig, 0, sizeof(unsigned long long), s);
+  hipLaunchKernelGGL(k_grid_build, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, cells, trig, n,
+                     kGridDim, lo, hi, vr, big, numBig, cap);
+  hipLaunchKernelGGL(k_grid_boxes, dim3(2048), dim3(256), 0, s, big, numBig, cap, kGridDim, vr);
+  (void)hipFreeAsync(big, s);
+  (void)hipFreeAsync(numBig, s);
 }
 void launch_max_opacities(const float *vr, size_t numMCs, const float4 *lut, int size, float lo,
                           float hi, float *maxOp, hipStream_t s) {
   hipLaunchKernelGGL(k_max_opacities, dim3((unsigned)((numMCs + 255) / 256)), dim3(256), 0, s,
                      (const float2 *)vr, numMCs, lut, size, lo, hi, maxOp);
 }
-void launch_stats_out(const unsigned long long *cur, const uint32_t *wgCounts, size_t numWG,
-                      unsigned long long *host, unsigned long long *next, hipStream_t s) {
-  hipLaunchKernelGGL(k_stats_out, dim3(1), dim3(1024), 0, s, cur, wgCounts, numWG, host, next);
+void launch_stats_out(const unsigned long long *cur, unsigned long long *host,
+                      unsigned long long *next, hipStream_t s) {
+  hipLaunchKernelGGL(k_stats_out, dim3(1), dim3(64), 0, s, cur, host, next);
 }
 // a u32 array between device memory and mapped pinned host memory (either direction):
 // the scheduling costs and block orders, without an SDMA copy on the render stream

@@ -450,10 +450,11 @@ __device__ __forceinline__ void write_pixel(const RenderArgs &A, size_t outIdx, 
                  (srgb_byte(s_th, nv.z) << 16) + (make_8bit(nv.w) << 24);
 }
 
-// The workgroup's event counts (LDS) out to the launch's statistics.  Default: one plain
-// store of the kCnt counts per workgroup into wgCounts (k_stats_out sums them), so no two
-// workgroups ever touch the same line.  Without wgCounts: device-scope atomics into the
-// counter block -- 4 096 workgroups x 5 same-line atomics per 1024^2 frame.
+// The workgroup's event counts (LDS) out to the launch's statistics.  Default: one store of
+// the kCnt counts per workgroup into wgCounts, pinned host memory the host sums when asked
+// (irt_context.hip finish_slot): no statistics kernel, and no two workgroups touch the same
+// line.  Without wgCounts: device-scope atomics into the counter block -- 4 096 workgroups
+// x 5 same-line atomics per 1024^2 frame, ~40 us of serialised atomics.
 __device__ __forceinline__ void flush_counters(const RenderArgs &A, uint32_t *s_cnt, int tid) {
   __syncthreads();
   if (A.wgCounts) {

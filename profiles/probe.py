@@ -8,7 +8,8 @@ launches).  One JSON line per case.
 
 A case is `;`-separated; inside a case, `,`-separated KEY=VALUE items: environment
 variables read at context creation (IRT_*), `cam=framing|viewall|away`, `variant=N`,
-`tf=default|sparse` (alpha x 0.01, the C3s transfer function).
+`tf=default|zero|dense|comb` (alpha 0: the full sdda walk without a sample; alpha 1: one
+accepted sample per in-shell ray; comb: bench.py's C3s sparse comb).
 """
 import argparse
 import ctypes as C
@@ -74,8 +75,13 @@ def main():
                 os.environ[k] = v
         setup = irt.setup_frame(cells, W, W, camera=CAMS[opt["cam"]])
         lut = setup.lut.copy()
-        if opt["tf"] == "sparse":
-            lut[:, 3] *= 0.01
+        if opt["tf"] == "zero":
+            lut[:, 3] = 0.0
+        elif opt["tf"] == "dense":
+            lut[:, 3] = 1.0
+        elif opt["tf"] == "comb":
+            lut[:, 3] = 0.01
+            lut[::50, 3] = 1.0
         ctx.set_transfunc(lut, setup.value_range)
         ctx.set_timing_interval(1)
         if opt["variant"]:
