@@ -617,6 +617,7 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
       }
       const bool zeroLen = tt1 == t;
       if (zeroLen && lastRange) break;
+      if constexpr ((OPT & OPT_STATS) != 0) T.cnt.deg += zeroLen ? 1u : 0u;
       float maj = 1.f;
       if (!ae) {
         const uint32_t leaf = (uint32_t)wrap_coord(cz, A.dims.z) * (uint32_t)A.dims.x * (uint32_t)A.dims.y +
@@ -715,20 +716,28 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   const Pixel px = pixel_of(A, gid);
   float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + gid : nullptr;
   if (px.active) render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, A.accumID + (int)blockIdx.y, slot);
-  if constexpr ((OPT & OPT_STATS) != 0) {  // Woodcock draws: sum, per-wave max, histogram
-    uint32_t ss = T.cnt.steps, sm = T.cnt.steps;
+  if constexpr ((OPT & OPT_STATS) != 0) {
+    // Woodcock draws and zero-length sdda leaves: sums, per-wave maxima, draws histogram
+    uint32_t ss = T.cnt.steps, sm = T.cnt.steps, ds = T.cnt.deg, dm = T.cnt.deg;
     for (int off = 32; off > 0; off >>= 1) {
       ss += __shfl_down(ss, off, 64);
       sm = max(sm, (uint32_t)__shfl_down(sm, off, 64));
+      ds += __shfl_down(ds, off, 64);
+      dm = max(dm, (uint32_t)__shfl_down(dm, off, 64));
     }
+    const uint32_t d = T.cnt.steps;  // draws histogram: 0, 1-2, 3-5, > 5
+    const int bkt = d == 0 ? 0 : (d <= 2 ? 1 : (d <= 5 ? 2 : 3));
+    uint32_t hist[4];
+    for (int k = 0; k < 4; ++k) hist[k] = (uint32_t)__popcll(__ballot(px.active && bkt == k));
     if ((tid & 63) == 0) {
       atomicAdd(&A.counters[5], (unsigned long long)ss);
       atomicAdd(&A.counters[6], (unsigned long long)sm);
+      atomicAdd(&A.counters[7], (unsigned long long)ds);
+      atomicAdd(&A.counters[8], (unsigned long long)dm);
       atomicMax(&A.counters[9], (unsigned long long)sm);
-    }
-    if (px.active) {  // draws histogram: 0, 1-2, 3-5, > 5
-      const uint32_t d = T.cnt.steps;
-      atomicAdd(&A.counters[d == 0 ? 12 : (d <= 2 ? 13 : (d <= 5 ? 14 : 15))], 1ull);
+      atomicMax(&A.counters[10], (unsigned long long)dm);
+      for (int k = 0; k < 4; ++k)
+        if (hist[k]) atomicAdd(&A.counters[12 + k], (unsigned long long)hist[k]);
     }
   }
   if (A.counters) {

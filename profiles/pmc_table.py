@@ -9,8 +9,9 @@ import re
 import sys
 
 root = sys.argv[1]
+prefix = sys.argv[2] if len(sys.argv) > 2 else ""
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in glob.glob(os.path.join(root, "*", "run_counter_collection.csv")):
+for f in glob.glob(os.path.join(root, prefix + "*", "run_counter_collection.csv")):
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
     for r in csv.DictReader(open(f)):
