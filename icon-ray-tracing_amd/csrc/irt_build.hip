@@ -275,8 +275,9 @@ __global__ void k_cell_fill(const uint32_t *offsets, uint32_t numCells, const un
         if (!in_bin(h.x, h.y, lo, hi)) continue;
         float F[20];
         fat_entry(rec, planes, reinterpret_cast<const float *>(rng), meta, keys, F);
-        float4 *o = fat + (size_t)(at++) * kFat4;
+        float4 *o = fat + (size_t)(at++) * kFatStride4;
         for (int j = 0; j < kFat4; ++j) o[j] = make_float4(F[4 * j], F[4 * j + 1], F[4 * j + 2], F[4 * j + 3]);
+        for (int j = kFat4; j < kFatStride4; ++j) o[j] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
   }
@@ -555,8 +556,8 @@ int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_
     return IRT_E_INVALID;
   }
   // --- 9. fat entries
-  BHIP(hipMalloc((void **)&out.fat, std::max<uint64_t>(numFat, 1) * kFat4 * sizeof(float4)));
-  out.bytes += std::max<uint64_t>(numFat, 1) * kFat4 * sizeof(float4);
+  BHIP(hipMalloc((void **)&out.fat, std::max<uint64_t>(numFat, 1) * kFatStride4 * sizeof(float4)));
+  out.bytes += std::max<uint64_t>(numFat, 1) * kFatStride4 * sizeof(float4);
   hipLaunchKernelGGL(k_cell_fill, dim3(nc), dim3(64), 0, s, offsets, numCells, pv2, rng, edges, cellBase,
                      reinterpret_cast<uint32_t *>(out.binHdr), planesF, meta,
                      reinterpret_cast<const float *>(keys), out.fat);

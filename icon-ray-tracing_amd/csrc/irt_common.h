@@ -366,6 +366,9 @@ IRT_HD uint32_t sph_hash(float r) {
 //           meta = numLayers | (height[1..numLayers] non-decreasing) << 31
 //   [4]     coarse keys {height[7], height[15], height[23], height[31]}
 constexpr int kFat4 = 5;
+// Stride of the fat entries in float4: one 128-B line each (an 80-B entry at 80-B stride
+// straddles two lines half the time; the line is fetched whole either way)
+constexpr int kFatStride4 = 8;
 // Per-record height/value blocks (the render record without its planes/keys), kBlk4
 // float4 = 256 B: block b (4 float4) = {height[8b..8b+3]}, {height[8b+4..8b+7]},
 // {value[8b-1..8b+2]}, {value[8b+3..8b+6]} (value[-1] := 0).

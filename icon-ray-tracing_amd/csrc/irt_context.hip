@@ -1108,7 +1108,7 @@ extern "C" int irt_debug_context_array(const irt_context *c, int which, void *ds
   size_t n = 0;
   switch (which) {
     case IRT_DEBUG_ARRAY_BIN_HDR: src = c->d_binHdr; n = (size_t)6 * c->G * c->G * kBinHdrWords * 4; break;
-    case IRT_DEBUG_ARRAY_FAT: src = c->d_fat; n = c->binEntries * kFat4 * 16; break;
+    case IRT_DEBUG_ARRAY_FAT: src = c->d_fat; n = c->binEntries * kFatStride4 * 16; break;
     case IRT_DEBUG_ARRAY_BLOCKS: src = c->d_blocks; n = (size_t)c->n * kBlk4 * 16; break;
     case IRT_DEBUG_ARRAY_SPH_R: src = c->d_sphR; n = (size_t)c->numSph * 4; break;
     case IRT_DEBUG_ARRAY_SPH_OFF: src = c->d_sphOff; n = c->numSph ? ((size_t)c->numSph + 1) * 4 : 4; break;

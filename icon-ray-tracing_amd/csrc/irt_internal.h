@@ -35,7 +35,7 @@ struct HostScene {
   std::vector<uint32_t> entrySub; // ... and each entry's sub-cell mask
   // the product locator (irt_build.h)
   std::vector<uint32_t> binHdr;   // 6*G*G * kBinHdrWords
-  std::vector<float> fat;         // binEntries * kFat4 * 4
+  std::vector<float> fat;         // binEntries * kFatStride4 * 4
   size_t binEntries = 0;
   // zero-thickness records (spheres): distinct radii, CSR into record indices (ascending),
   // and a hash bitmap of the radii (irt_common.h sph_hash) the kernel keeps in LDS

@@ -136,7 +136,7 @@ struct Tracer {
         j = m ? j + (uint32_t)__builtin_ctz(m) : (uint32_t)kMaskCand;
       }
       if (j >= n) break;
-      const float4 *F = A.fat + (size_t)(q + j) * kFat4;
+      const float4 *F = A.fat + (size_t)(q + j) * kFatStride4;
       const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3], ak = F[4];
       if (__float_as_uint(am.z) >= limit) return false;
       if (pass_fat(a0, a1, a2, am, px, py, pz, r)) {

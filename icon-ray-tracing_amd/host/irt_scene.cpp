@@ -258,7 +258,7 @@ int build_bins(HostScene &S, int threads) {
     return IRT_E_INVALID;
   }
   S.binEntries = total;
-  S.fat.assign(total * kFat4 * 4, 0.f);
+  S.fat.assign(total * kFatStride4 * 4, 0.f);
   // pass 2: the fat entries, bin by bin
   parallel_ranges(numGridCells, threads, [&](int, size_t b, size_t e) {
     for (size_t cell = b; cell < e; ++cell) {
@@ -274,7 +274,7 @@ int build_bins(HostScene &S, int threads) {
           const uint32_t rec = S.entryRec[q];
           if (!in_bin(S.rng[2 * (size_t)rec], S.rng[2 * (size_t)rec + 1], lo, hi)) continue;
           fat_entry(rec, S.planes.data(), S.rng.data(), S.meta.data(), S.keys.data(),
-                    &S.fat[at++ * kFat4 * 4]);
+                    &S.fat[at++ * kFatStride4 * 4]);
         }
       }
     }
@@ -349,7 +349,7 @@ int locate_bins_host(const HostScene &s, float px, float py, float pz, float &va
         j += (uint32_t)__builtin_ctz(m);
         if (beg + j >= end) break;
       }
-      const float *F = &s.fat[(size_t)(beg + j) * kFat4 * 4];
+      const float *F = &s.fat[(size_t)(beg + j) * kFatStride4 * 4];
       if (hit && f2u(F[14]) >= best) break;  // the second bin: only lower records
       if (tested) ++*tested;
       float v;
