@@ -63,6 +63,25 @@ IRT_HD uint32_t lcg_seed(uint32_t v0, uint32_t v1) {
 IRT_HD uint32_t lcg_next(uint32_t s) { return 1664525u * s + 1013904223u; }
 IRT_HD float lcg_float(uint32_t s) { return (float)(s & 0x00FFFFFFu) / (float)0x01000000; }
 
+// n LCG steps at once: state_n = mul * state + add (mod 2^32), composed from the one-step
+// map by binary powers (the maps commute).  The wave-cooperative Woodcock loop
+// (irt_render.hip) evaluates sample k of a ray from the state 2k+1 (its step draw) and 2k+2
+// (its acceptance draw) draws ahead; it tabulates n < kLcgJumps in LDS.
+constexpr int kLcgJumps = 130;
+IRT_HD void lcg_jump(uint32_t n, uint32_t &mul, uint32_t &add) {
+  uint32_t m = 1u, c = 0u, bm = 1664525u, bc = 1013904223u;
+  for (; n; n >>= 1) {
+    if (n & 1u) {
+      c = bm * c + bc;
+      m = bm * m;
+    }
+    bc = bm * bc + bc;
+    bm = bm * bm;
+  }
+  mul = m;
+  add = c;
+}
+
 // ---------------------------------------------------------------------------------
 // glibc 2.35 flt-32 asinf / atanf / atan2f (fdlibm lineage: Sun Microsystems 1993,
 // float conversion by Ian Lance Taylor, Cygnus; asinf polynomial by Naohiko Shimizu).

@@ -30,6 +30,8 @@ enum : int {
                       // the default kernels
   OPT_GRID = 8192,    // GRID_ACCEL_MODE traversal (render_grid); likewise
   OPT_STATS = 32768,  // per-wave statistics into counters[5..9] (measurement only)
+  OPT_SERIAL = 65536, // one lane per ray through the Woodcock loop (render_pixel), for A/B:
+                      // the default user-geometry/sphere kernel is render_pixel_coop
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
@@ -75,6 +77,27 @@ __device__ __forceinline__ uint32_t cubemap_cell_fast(float px, float py, float 
   return cubemap_cell_fast(px, py, pz, G, sub);
 }
 
+// Per-wave LDS of the cooperative Woodcock loop (Tracer::woodcock_wave).
+struct CoopWave {
+  float4 req[64];   // the request of the rank-r ray: {t, tmax, q = majorant/unitDistance, majorant}
+  float4 ray[64];   // {dx, dy, dz, RNG state bits}
+  float step[64];   // lane l's Woodcock step log(1 - xi)/q this round
+  uint32_t cnt[64]; // the request is counted (a positive-length leaf)
+};
+
+// t0 - d[0] - d[1] - ... - d[k], subtracted one at a time as woodcockTracking's `t -=`
+// (deviceCode.cu:165) does: the same roundings as k+1 iterations of the serial loop.
+template <int G>
+__device__ __forceinline__ float coop_prefix(float t0, const float *d, int k) {
+  float t = t0;
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const float dj = d[j];
+    t = j <= k ? t - dj : t;
+  }
+  return t;
+}
+
 template <int OPT>
 struct Tracer {
   const RenderArgs &A;
@@ -82,6 +105,30 @@ struct Tracer {
   const uint32_t *s_sph;
   uint32_t *s_cnt;  // [0] launched [1] inBox [2] locate [3] found [4] candidates
   Counts cnt;       // per-lane statistics (OPT_STATS)
+  uint32_t specCand = 0;  // candidate tests of this lane's sample in a cooperative round
+  // the cooperative loop's statistics, per lane (samples taken, their locates / found /
+  // candidate tests), added into s_cnt at the end by flush_coop
+  uint32_t nLocate = 0, nFound = 0, nCand = 0;
+
+  // wave sum of a per-lane count from bit-slice ballots (no LDS, no shuffle chain)
+  __device__ __forceinline__ static uint32_t wave_sum(uint32_t v) {
+    uint32_t sum = 0;
+    for (int b = 0; __ballot(v >> b) != 0ull; ++b) sum += (uint32_t)__popcll(__ballot((v >> b) & 1u)) << b;
+    return sum;
+  }
+  // (per-lane LDS atomics on one address serialise: +17 us per C3 frame measured)
+  __device__ __forceinline__ void flush_coop() {
+    const uint32_t a = wave_sum(nLocate), b = wave_sum(nFound), c = wave_sum(nCand);
+    if (__lane_id() == 0) {
+      if (a) atomicAdd(&s_cnt[2], a);
+      if (b) atomicAdd(&s_cnt[3], b);
+      if (c) atomicAdd(&s_cnt[4], c);
+    }
+  }
+
+  // the cooperative Woodcock loop (woodcock_wave) runs in every user-geometry sphere-accel
+  // kernel but the OPT_SERIAL comparison one
+  static constexpr bool kCoop = (OPT & (OPT_GRID | OPT_WEDGE | OPT_SERIAL)) == 0;
 
   // one wave-aggregated LDS add per event site
   __device__ __forceinline__ void count(int k) {
@@ -109,7 +156,10 @@ struct Tracer {
   // the radial range and the three ccw side planes
   __device__ __forceinline__ bool pass_fat(const float4 &p0, const float4 &p1, const float4 &p2,
                                            const float4 &m, float px, float py, float pz, float r) {
-    count(4);
+    if constexpr (kCoop)
+      ++specCand;  // counted only if the sample is one the reference takes (woodcock_wave)
+    else
+      count(4);
     if (r < m.x || r > m.y) return false;                                 // ICONGrid.h:184
     if (dot3(px, py, pz, p0.x, p0.y, p0.z) - p0.w > 0.f) return false;  // ICONGrid.h:201
     if (dot3(px, py, pz, p1.x, p1.y, p1.z) - p1.w > 0.f) return false;  // 202
@@ -384,6 +434,145 @@ struct Tracer {
     }
     return fminf(t, tmax);
   }
+
+  // woodcockTracking (deviceCode.cu:149-186) for every lane of the wave with `req` set,
+  // evaluated together.  A ray's sample positions depend on nothing but its RNG: sample k
+  // (k = 0, 1, ...) of a ray whose earlier samples were all located and rejected lies at
+  // t - d_0 - ... - d_k with d_j from the state 2j+1 draws ahead, and is accepted against
+  // the state 2k+2 draws ahead.  So each round the wave's R undecided rays get G = 64/R
+  // (a power of two) lanes each; lane k of a group takes sample k of its ray -- independent
+  // gathers in parallel instead of a chain -- and the ray's first event among its G samples
+  // (past tmax / not located / accepted) decides it exactly as the serial loop would; the
+  // samples after the event are discarded.  A not-located sample consumes only its step
+  // draw, so the ray resumes from there next round.  Statistics count only the samples
+  // the reference takes.  Returns in t the woodcockTracking return value.
+  __device__ __forceinline__ void woodcock_wave(bool req, float dx, float dy, float dz, float &t,
+                                                float tmax, uint32_t &st, float majorant,
+                                                bool counted, float4 &sampleOut, CoopWave &W,
+                                                const uint32_t *jmul, const uint32_t *jadd) {
+    const int lane = (int)__lane_id();
+    const uint64_t below = (1ull << lane) - 1ull;
+    const float q = majorant / A.unitDistance;
+    bool active = req && !(majorant <= 0.f);  // majorant <= 0: return at once (161-162)
+    while (true) {
+      const uint64_t am = __ballot(active);
+      if (am == 0ull) break;
+      const int R = __popcll(am);
+      const int lg = R > 32 ? 0 : R > 16 ? 1 : R > 8 ? 2 : R > 4 ? 3 : R > 2 ? 4 : R > 1 ? 5 : 6;
+      const int G = 1 << lg;
+      // solo round (G = 1): every ray on its own lane, nothing exchanged
+      const bool solo = lg == 0;
+      const int rank = __popcll(am & below);
+      int grp, k;
+      bool used, cntd;
+      float4 rq, ry;
+      if (solo) {
+        grp = lane;
+        k = 0;
+        used = active;
+        cntd = counted;
+        rq = make_float4(t, tmax, q, majorant);
+        ry = make_float4(dx, dy, dz, __uint_as_float(st));
+      } else {
+        if (active) {
+          W.req[rank] = make_float4(t, tmax, q, majorant);
+          W.ray[rank] = make_float4(dx, dy, dz, __uint_as_float(st));
+          W.cnt[rank] = counted ? 1u : 0u;
+        }
+        __builtin_amdgcn_wave_barrier();
+        grp = lane >> lg;
+        k = lane & (G - 1);
+        used = grp < R;
+        const int g = used ? grp : 0;
+        rq = W.req[g];
+        ry = W.ray[g];
+        cntd = W.cnt[g] != 0u;
+      }
+      const uint32_t s0 = __float_as_uint(ry.w);
+      const uint32_t sk = solo ? lcg_next(s0) : jmul[2 * k + 1] * s0 + jadd[2 * k + 1];
+      const float dk = woodcock_log(sk, s_logf) / rq.z;
+      float tk;
+      if (solo) {
+        tk = rq.x - dk;
+      } else {
+        W.step[lane] = dk;
+        __builtin_amdgcn_wave_barrier();
+        const float *dg = &W.step[grp << lg];
+        switch (lg) {
+          case 1: tk = coop_prefix<2>(rq.x, dg, k); break;
+          case 2: tk = coop_prefix<4>(rq.x, dg, k); break;
+          case 3: tk = coop_prefix<8>(rq.x, dg, k); break;
+          case 4: tk = coop_prefix<16>(rq.x, dg, k); break;
+          case 5: tk = coop_prefix<32>(rq.x, dg, k); break;
+          default: tk = coop_prefix<64>(rq.x, dg, k); break;
+        }
+      }
+      const bool past = used && tk > rq.y;
+      bool found = false, acc = false;
+      float value = 0.f;
+      if (used && !past) {
+        found = locate(A.org.x + ry.x * tk, A.org.y + ry.y * tk, A.org.z + ry.z * tk, value);
+        if (found) {
+          const float sw = classify_alpha(value);  // postClassify(value).w
+          acc = sw >= lcg_float(lcg_next(sk)) * rq.w;
+        }
+      }
+      const bool ev = used && (past || !found || acc);
+      // the lane's group: its first event, G if none; the samples up to it are taken
+      int first;
+      uint64_t em = 0ull;
+      if (solo) {
+        first = ev ? 0 : 1;
+      } else {
+        em = __ballot(ev);
+        const uint64_t gm = lg == 6 ? ~0ull : (((1ull << G) - 1ull) << (grp << lg));
+        first = (em & gm) ? (int)__builtin_ctzll(em & gm) - (grp << lg) : G;
+      }
+      if (used && k <= first) {
+        if (cntd) {
+          nLocate += past ? 0u : 1u;
+          nFound += found ? 1u : 0u;
+        }
+        nCand += specCand;
+      }
+      specCand = 0u;
+      // the rays' owners take their group's outcome
+      int of;
+      float tsrc, vsrc;
+      bool pastS, accS;
+      if (solo) {
+        of = first;
+        tsrc = tk;
+        vsrc = value;
+        pastS = past;
+        accS = acc;
+      } else {
+        const uint64_t pastM = __ballot(past), accM = __ballot(acc);
+        const int ob = active ? rank << lg : 0;  // < 64 for an owner
+        const uint64_t om = lg == 6 ? ~0ull : (((1ull << G) - 1ull) << ob);
+        of = (active && (em & om)) ? (int)__builtin_ctzll(em & om) - ob : G;
+        const int src = active ? ob + (of < G ? of : G - 1) : lane;
+        tsrc = __shfl(tk, src, 64);
+        vsrc = __shfl(value, src, 64);
+        pastS = (pastM >> src) & 1ull;
+        accS = (accM >> src) & 1ull;
+      }
+      if (active) {
+        if constexpr ((OPT & OPT_STATS) != 0) cnt.steps += of < G ? (uint32_t)of + 1u : (uint32_t)G;
+        t = tsrc;
+        const int n = of == G ? 2 * G : (accS ? 2 * of + 2 : 2 * of + 1);
+        if (solo)
+          st = n == 1 ? sk : lcg_next(sk);  // the draws this round made
+        else
+          st = jmul[n] * st + jadd[n];
+        if (of < G && (pastS || accS)) {
+          active = false;
+          if (accS) sampleOut = post_classify(vsrc);
+        }
+      }
+    }
+    if (req) t = fminf(t, tmax);
+  }
 };
 
 // ------------------------------------------------------------------ per-pixel pieces
@@ -437,8 +626,7 @@ __device__ __forceinline__ void gen_ray(const RenderArgs &A, int accumID, int x,
 // accumulate lerp(vec4f(color,alpha), old, 1/(accumID+1)) and write linear_to_srgb +
 // make_rgba (deviceCode.cu:333-340)
 __device__ __forceinline__ void write_pixel(const RenderArgs &A, size_t outIdx, float cr, float cg,
-                                            float cb, float alpha, const float *s_th) {
-  const float4 old = A.accum[outIdx];
+                                            float cb, float alpha, const float *s_th, float4 old) {
   const float w = 1.f / (float)(A.accumID + 1);
   float4 nv;
   nv.x = w * cr + (1.f - w) * old.x;
@@ -448,6 +636,10 @@ __device__ __forceinline__ void write_pixel(const RenderArgs &A, size_t outIdx, 
   A.accum[outIdx] = nv;
   A.fb[outIdx] = srgb_byte(s_th, nv.x) + (srgb_byte(s_th, nv.y) << 8) +
                  (srgb_byte(s_th, nv.z) << 16) + (make_8bit(nv.w) << 24);
+}
+__device__ __forceinline__ void write_pixel(const RenderArgs &A, size_t outIdx, float cr, float cg,
+                                            float cb, float alpha, const float *s_th) {
+  write_pixel(A, outIdx, cr, cg, cb, alpha, s_th, A.accum[outIdx]);
 }
 
 // The workgroup's event counts (LDS) out to the launch's statistics.  Default: one store of
@@ -690,6 +882,210 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
     write_pixel(A, px.outIdx, cr, cg, cb, alpha, s_th);
 }
 
+// render_pixel restated as a per-lane state machine whose one Woodcock call site is reached
+// by the whole wave together (Tracer::woodcock_wave): each lane runs its ranges and sdda
+// leaves on its own until it needs a woodcockFunc on a leaf (kWait) or is finished
+// (kDone); then the wave tracks every waiting lane's leaf at once, and each lane resumes
+// with the leaf's outcome.  Every lane of the wave calls it (those without a pixel start
+// finished).  Same ranges, leaves, draws and results as render_pixel, step for step.
+template <int OPT>
+__device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
+                                                  const float *s_th, int4 *s_dda, float4 *s_entry,
+                                                  float4 *s_acc, CoopWave &W, const uint32_t *jmul,
+                                                  const uint32_t *jadd, int tid, int accumID,
+                                                  float4 *sampleOut) {
+  enum : int { kRange, kLeaf, kWait, kDone };
+  const bool ae = A.raygen == 1;
+  uint32_t st = 0;
+  float dx = 1.f, dy = 1.f, dz = 1.f;
+  float rlo0 = 0.f, rhi0 = 0.f, rlo1 = __builtin_inff(), rhi1 = -__builtin_inff();
+  int numRanges = 0, phase = kDone;
+  bool inBox = false;
+  if (px.active) {
+    gen_ray(A, accumID, px.x, px.y, st, dx, dy, dz);
+    const Ray ray = {A.org.x, A.org.y, A.org.z, 0.f, dx, dy, dz, 1e10f};
+    float t0, t1;
+    if (box_test(ray, A, t0, t1)) {
+      inBox = true;
+      T.count(1);
+      phase = kRange;
+      // the accum pixel the lerp reads at the end, fetched now straight into LDS (no VGPRs
+      // held through the Woodcock rounds; its latency hides behind them)
+      if (!sampleOut)
+        __builtin_amdgcn_global_load_lds((const void *)(A.accum + px.outIdx),
+                                         (__attribute__((address_space(3))) void *)(s_acc + (tid & ~63)),
+                                         16, 0, 0);
+      rlo0 = t0;
+      rhi0 = t1;
+      numRanges = 1;
+      if (!ae) {  // the shell's sphere ranges, as render_pixel
+        float st1 = 0.f, st2 = 0.f, st3 = 0.f, st4 = 0.f;
+        const bool s1 = intersect_sphere(ray, A.sbHi.x, st1, st4);
+        const bool s2 = intersect_sphere(ray, A.sbLo.x, st2, st3);
+        numRanges = 0;
+        if ((s1 || s2) && !(st4 < t0)) {
+          numRanges = 2;
+          if (s1 && !s2) {
+            rlo0 = st1; rhi0 = st4;
+          } else if (t0 < st2) {
+            rlo0 = st1; rhi0 = st2;
+            rlo1 = st3; rhi1 = st4;
+          } else {
+            rlo0 = st3; rhi0 = st4;
+          }
+        }
+      }
+    } else if (sampleOut) {
+      *sampleOut = make_float4(0.f, 0.f, 0.f, kNoSample);  // deviceCode.cu:294-295
+    }
+  }
+  const float sceneEPS = A.sbLo.x * 1e-6f;
+  int i = 0, iter = 0, cx = 0, cy = 0, cz = 0;
+  float t = 0.f, upper = 0.f, tt1 = 0.f, maj = 0.f;
+  bool lastRange = true, zeroLen = false, hit = false;
+  // after a leaf without a hit: the next leaf of the range, or the next range
+  // (render_pixel's loop tail, ShellAccel.h:201-226)
+  auto next_leaf = [&]() {
+    if (lastRange) {  // every later leaf of the last range is zero-length
+      ++i;
+      phase = kRange;
+      return;
+    }
+    const float tnx = upper, tny = 0.f, tnz = 0.f;
+    int4 dd;
+    if (iter == 0) {
+      const float e2 = upper - sceneEPS;
+      float r2, la2, lo2;
+      to_spherical(A.org.x + dx * e2, A.org.y + dy * e2, A.org.z + dz * e2, r2, la2, lo2);
+      const float4 en = s_entry[tid];
+      const float r1 = en.x, la1 = en.y, lo1 = en.z;
+      const int sx = r1 < r2 ? 1 : -1, sy = la1 < la2 ? 1 : -1, sz = lo1 < lo2 ? 1 : -1;
+      dd.x = (sx > 0 ? 1 : 0) | (sy > 0 ? 2 : 0) | (sz > 0 ? 4 : 0);
+      dd.y = (int)((uint32_t)project_axis(r2, A.sbLo.x, A.sbHi.x, A.dims.x) + (uint32_t)sx);
+      dd.z = (int)((uint32_t)project_axis(la2, A.sbLo.y, A.sbHi.y, A.dims.y) + (uint32_t)sy);
+      dd.w = (int)((uint32_t)project_axis(lo2, A.sbLo.z, A.sbHi.z, A.dims.z) + (uint32_t)sz);
+      s_dda[tid] = dd;
+    } else {
+      dd = s_dda[tid];
+    }
+    const float t_closest = fminf(fminf(tnx, tny), tnz);
+    bool stop = false;
+    if (tnx == t_closest) {
+      cx += (dd.x & 1) ? 1 : -1;
+      stop = cx == dd.y;
+    }
+    if (!stop && tny == t_closest) {
+      cy += (dd.x & 2) ? 1 : -1;
+      stop = cy == dd.z;
+    }
+    if (!stop && tnz == t_closest) {
+      cz += (dd.x & 4) ? 1 : -1;
+      stop = cz == dd.w;
+    }
+    t = t_closest;
+    if (stop || ++iter >= (1 << 22)) {
+      ++i;
+      phase = kRange;
+    } else {
+      phase = kLeaf;
+    }
+  };
+  while (true) {
+    // this lane, on its own: up to its next woodcockFunc, or to the end
+    while (phase == kRange || phase == kLeaf) {
+      if (phase == kRange) {
+        if (i >= numRanges) {
+          phase = kDone;
+          break;
+        }
+        const float lower = i ? rlo1 : rlo0;
+        upper = i ? rhi1 : rhi0;
+        if (upper <= lower) {  // box1f::empty (vecmath.h:981)
+          phase = kDone;
+          break;
+        }
+        lastRange = ae || i == 1 || rhi1 <= rlo1;
+        cx = cy = cz = 0;
+        if (!ae) {  // cellID of the entry point (ShellAccel.h:121-124)
+          const float e1 = lower + sceneEPS;
+          float r1, la1, lo1;
+          to_spherical(A.org.x + dx * e1, A.org.y + dy * e1, A.org.z + dz * e1, r1, la1, lo1);
+          cx = project_axis(r1, A.sbLo.x, A.sbHi.x, A.dims.x);
+          cy = project_axis(la1, A.sbLo.y, A.sbHi.y, A.dims.y);
+          cz = project_axis(lo1, A.sbLo.z, A.sbHi.z, A.dims.z);
+          if (!lastRange) s_entry[tid] = make_float4(r1, la1, lo1, 0.f);
+        }
+        t = lower;
+        iter = 0;
+        phase = kLeaf;
+      }
+      // the leaf [t, tt1] (tnext = {upper, 0, 0}: render_pixel)
+      tt1 = IRT_FLT_MAX;
+      if (ae) {
+        tt1 = upper;
+      } else {
+        if (upper < tt1 && upper >= t) tt1 = upper;
+        if (0.f < tt1 && 0.f >= t) tt1 = 0.f;
+      }
+      zeroLen = tt1 == t;
+      if (zeroLen && lastRange) {
+        ++i;
+        phase = kRange;
+        continue;
+      }
+      if constexpr ((OPT & OPT_STATS) != 0) T.cnt.deg += zeroLen ? 1u : 0u;
+      maj = 1.f;
+      if (!ae) {
+        const uint32_t leaf = (uint32_t)wrap_coord(cz, A.dims.z) * (uint32_t)A.dims.x * (uint32_t)A.dims.y +
+                              (uint32_t)wrap_coord(cy, A.dims.y) * (uint32_t)A.dims.x +
+                              (uint32_t)wrap_coord(cx, A.dims.x);
+        maj = A.maxOp[leaf];
+      }
+      bool fast = false;
+      if (zeroLen) {
+        const float q = maj / A.unitDistance;
+        const uint32_t nx = lcg_next(st);
+        if (!(maj > 0.f)) {
+          fast = true;
+        } else if (q > 0.f && q <= 1e30f && (nx & 0x00FFFFFFu) != 0u) {
+          st = nx;
+          fast = true;
+        }
+      }
+      if (!fast) {
+        phase = kWait;
+        break;
+      }
+      next_leaf();
+    }
+    // the wave, together: woodcockFunc(leafID, t, tt1) of every waiting lane
+    const bool req = phase == kWait;
+    if (__ballot(req) == 0ull) break;
+    float tw = t;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    T.woodcock_wave(req, dx, dy, dz, tw, tt1, st, maj, !zeroLen, s, W, jmul, jadd);
+    if (req) {
+      if (!zeroLen && (ae || (tw > t && tw < tt1))) {
+        // the colour waits in the lane's s_entry slot (free once it is finished)
+        s_entry[tid] = make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
+                                   s.z * A.amb.z * A.ambRad, s.w > 0.f ? 1.f : 0.f);
+        hit = true;
+        phase = kDone;
+      } else {
+        next_leaf();
+      }
+    }
+  }
+  if (!inBox) return;
+  const float4 c = hit ? s_entry[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (sampleOut) {
+    *sampleOut = c;
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
+    write_pixel(A, px.outIdx, c.x, c.y, c.z, c.w, s_th, s_acc[tid]);
+  }
+}
+
 // The raygen over the frame grid: one lane per pixel (see pixel_of).
 template <int OPT>
 __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1) k_render(RenderArgs A) {
@@ -699,7 +1095,13 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   __shared__ uint32_t s_sph[kSphBitWords];
   __shared__ int4 s_dda[256];       // sdda state needed only after a range's first leaf
   __shared__ float4 s_entry[256];
+  __shared__ CoopWave s_coop[4];    // the cooperative Woodcock loop (kCoop kernels)
+  __shared__ float4 s_acc[256];     // kCoop: the accum pixels, prefetched
+  __shared__ uint32_t s_jmul[kLcgJumps], s_jadd[kLcgJumps];
   const int tid = threadIdx.x;
+  if constexpr (Tracer<OPT>::kCoop) {
+    if (tid < kLcgJumps) lcg_jump((uint32_t)tid, s_jmul[tid], s_jadd[tid]);
+  }
   if (A.numSph)
     for (int i = tid; i < kSphBitWords; i += 256) s_sph[i] = A.sphBits[i];
   s_th[tid] = A.srgbTh[tid];
@@ -715,7 +1117,13 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   const uint32_t gid = blk * 256u + (uint32_t)tid;
   const Pixel px = pixel_of(A, gid);
   float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + gid : nullptr;
-  if (px.active) render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, A.accumID + (int)blockIdx.y, slot);
+  if constexpr (Tracer<OPT>::kCoop) {
+    render_pixel_coop<OPT>(A, T, px, s_th, s_dda, s_entry, s_acc, s_coop[tid >> 6], s_jmul, s_jadd, tid,
+                           A.accumID + (int)blockIdx.y, slot);
+    T.flush_coop();
+  }
+  else if (px.active)
+    render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, A.accumID + (int)blockIdx.y, slot);
   if constexpr ((OPT & OPT_STATS) != 0) {
     // Woodcock draws and zero-length sdda leaves: sums, per-wave maxima, draws histogram
     uint32_t ss = T.cnt.steps, sm = T.cnt.steps, ds = T.cnt.deg, dm = T.cnt.deg;
@@ -789,11 +1197,12 @@ __global__ void __launch_bounds__(256) k_accumulate(RenderArgs A) {
 // Variant bits: irt_render.hip OPT_* (bits 8-11: minimum waves per SIMD asked of the
 // register allocator).  OPT_MONO (4096) is kept in the numbering of round 1 (the one-kernel
 // raygen; the setup -> march -> continuation pipeline it distinguished from was removed).
-// All variants give identical results.
+// 70656 = 5120 | OPT_SERIAL: the one-lane-per-ray Woodcock loop, for A/B against the
+// cooperative default.  All variants give identical results.
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(36864) X(70656)
 
 bool render_variant_available(int v) {
 #define IRT_CASE(N) if (v == N) return true;

@@ -31,9 +31,10 @@ ACCEL_GRID = 1         # GRID_ACCEL_MODE (Params.h:34): dda3 over the 256^3 grid
 MODE_USER_GEOM = 0     # Volume::mode (Params.h:29-31): sample() on the cells (default)
 MODE_TRIANGLES = 1     # closest bottom triangle toward the centre (deviceCode.cu:61-76)
 MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
-# compiled variants of the raygen (irt_render.hip OPT_* bits; 4096 = one monolithic
-# kernel instead of the setup -> march -> continuation pipeline); all bit-identical
-BIN_VARIANTS = (4096, 5120, 5376, 36864)
+# compiled variants of the raygen (irt_render.hip OPT_* bits): 4096 no waves-per-SIMD
+# floor, 5120 the default (4 waves/SIMD), 36864 with per-wave statistics, 70656 the
+# one-lane-per-ray Woodcock loop instead of the wave-cooperative one; all bit-identical
+BIN_VARIANTS = (4096, 5120, 36864, 70656)
 
 
 class IrtError(RuntimeError):

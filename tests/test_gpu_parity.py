@@ -404,3 +404,24 @@ def test_comb_transfunc_sample_heavy():
     assert_same_frame(a_gpu, f_gpu, a_ref, f_ref, "comb TF")
     assert st_gpu[0].locateCalls == st_ref[0].locate_calls
     assert st_ref[0].samples_found > 4 * 80 * 80  # sample-heavy indeed
+
+
+@pytest.mark.parametrize("raygen", [0, 1])
+def test_cooperative_woodcock_holes_and_long_chains(raygen):
+    """The wave-cooperative Woodcock loop (irt_render.hip woodcock_wave) at its edges: a
+    lat/lon-filtered scene, so samples fall in holes between cells (not located: the ray
+    resumes from that sample's step draw, inside a group of speculative lanes), under the
+    comb TF (long chains: few rays left per wave, up to 64 lanes on one ray), in both
+    raygens.  Frame, locate and found counts as the oracle's."""
+    cells = irt.filter_cells(irt.synth_grid(2, 3, 60), (-40, 50), (-100, 70))
+    setup = irt.setup_frame(cells, 8, 8)
+    lut = setup.lut.copy()
+    lut[:, 3] = 0.01
+    lut[::50, 3] = 1.0
+    kw = dict(camera=FRAMING, lut=lut, value_range=setup.value_range, raygen=raygen)
+    a_ref, f_ref, st_ref, _ = oracle_frame(cells, 72, 72, **kw)
+    a_gpu, f_gpu, st_gpu, ctx = gpu_frame(cells, 72, 72, **kw)
+    assert_same_frame(a_gpu, f_gpu, a_ref, f_ref, f"coop raygen {raygen}")
+    assert st_gpu[0].locateCalls == st_ref[0].locate_calls
+    assert st_gpu[0].samplesFound == st_ref[0].samples_found
+    assert st_ref[0].locate_calls > st_ref[0].samples_found  # holes were sampled
