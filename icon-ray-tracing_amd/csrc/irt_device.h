@@ -19,7 +19,7 @@ struct Ray {
 
 struct Counts {
   uint32_t inBox, locate, found, cand;
-  uint32_t steps, deg, r1;  // OPT_STATS only: Woodcock draws, zero-length leaves, range-1 rays
+  uint32_t steps, deg, rounds;  // OPT_STATS only: Woodcock draws, zero-length leaves, cooperative rounds
 };
 
 __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {

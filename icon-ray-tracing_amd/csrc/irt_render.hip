@@ -29,7 +29,7 @@ enum : int {
   OPT_WEDGE = 16384,  // CUBQL / TRIANGLE samplers (locate_wedge, locate_tri); kept out of
                       // the default kernels
   OPT_GRID = 8192,    // GRID_ACCEL_MODE traversal (render_grid); likewise
-  OPT_STATS = 32768,  // per-wave statistics into counters[5..9] (measurement only)
+  OPT_STATS = 32768,  // per-wave statistics into counters[5..15] (measurement only)
   OPT_SERIAL = 65536, // one lane per ray through the Woodcock loop (render_pixel), for A/B:
                       // the default user-geometry/sphere kernel is render_pixel_coop
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
@@ -457,6 +457,7 @@ struct Tracer {
     while (true) {
       const uint64_t am = __ballot(active);
       if (am == 0ull) break;
+      if constexpr ((OPT & OPT_STATS) != 0) ++cnt.rounds;
       const int R = __popcll(am);
       const int lg = R > 32 ? 0 : R > 16 ? 1 : R > 8 ? 2 : R > 4 ? 3 : R > 2 ? 4 : R > 1 ? 5 : 6;
       const int G = 1 << lg;
@@ -1144,6 +1145,7 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
       atomicAdd(&A.counters[8], (unsigned long long)dm);
       atomicMax(&A.counters[9], (unsigned long long)sm);
       atomicMax(&A.counters[10], (unsigned long long)dm);
+      atomicAdd(&A.counters[11], (unsigned long long)T.cnt.rounds);  // uniform per wave
       for (int k = 0; k < 4; ++k)
         if (hist[k]) atomicAdd(&A.counters[12 + k], (unsigned long long)hist[k]);
     }

@@ -118,8 +118,13 @@ extern "C" int irt_convert_icon(const irt_convert_opts *o, irt_icon_cell *out, s
   std::vector<double> clon, clat;
   {
     irt_nc::File f;
-    if ((rc = openNc(f, o->hgridFile)) || (rc = readDim(f, o->hgridFile, "cell", cell)) ||
-        (rc = readDoubleVar(f, o->hgridFile, "clon_vertices", cell * 3, clon)) ||
+    if ((rc = openNc(f, o->hgridFile)) || (rc = readDim(f, o->hgridFile, "cell", cell)))
+      return rc;
+    if (cell > (size_t)INT32_MAX) {  // cellID * 3 below, and the record's int fields
+      set_error("irt_convert_icon: %s: cell dimension %zu too large", o->hgridFile, cell);
+      return IRT_E_INVALID;
+    }
+    if ((rc = readDoubleVar(f, o->hgridFile, "clon_vertices", cell * 3, clon)) ||
         (rc = readDoubleVar(f, o->hgridFile, "clat_vertices", cell * 3, clat)))
       return rc;
   }

@@ -81,8 +81,9 @@ void skipAttributes(Cursor &c, int cnt) {
     c.name(cnt);
     const NcType t = (NcType)c.be(4);
     const uint64_t nv = c.be(cnt);
-    const uint64_t bytes = nv * typeSize(t);
-    if (typeSize(t) == 0) {
+    uint64_t bytes = 0;
+    if (typeSize(t) == 0 || __builtin_mul_overflow(nv, (uint64_t)typeSize(t), &bytes) ||
+        bytes > (1ull << 48)) {
       c.ok = false;
       return;
     }
@@ -229,33 +230,47 @@ const Var *File::findVar(const std::string &name) const {
   return nullptr;
 }
 
+// The product of the variable's dimension lengths; kOverflow when it does not fit 64 bits
+// (a crafted header: no caller's expected count can match it).
 uint64_t File::numValues(const Var &v) const {
   uint64_t n = 1;
   for (size_t k = 0; k < v.dimids.size(); ++k) {
-    const uint64_t len = dims_[v.dimids[k]].length;
-    n *= (k == 0 && v.isRecord) ? numrecs_ : len;
+    const uint64_t len = (k == 0 && v.isRecord) ? numrecs_ : dims_[v.dimids[k]].length;
+    if (__builtin_mul_overflow(n, len, &n)) return kOverflow;
   }
   return n;
 }
 
 bool File::readRaw(const Var &v, std::vector<uint8_t> &bytes, std::string &err) const {
-  const size_t ts = typeSize(v.type);
+  const uint64_t ts = typeSize(v.type);
   const uint64_t total = numValues(v);
-  bytes.assign(total * ts, 0);
+  uint64_t size = 0;
   FILE *f = fopen(path_.c_str(), "rb");
   if (!f) {
     err = "cannot open " + path_;
     return false;
   }
+  // every byte the reads below store must fit the buffer, and the buffer the file
+  fseeko(f, 0, SEEK_END);
+  const uint64_t fileBytes = (uint64_t)ftello(f);
+  if (total == kOverflow || __builtin_mul_overflow(total, ts, &size) || size > fileBytes) {
+    fclose(f);
+    err = path_ + ": variable " + v.name + " is larger than the file";
+    return false;
+  }
+  bytes.assign(size, 0);
   bool ok = true;
   if (!v.isRecord) {
     ok = fseeko(f, (off_t)v.begin, SEEK_SET) == 0 &&
          fread(bytes.data(), 1, bytes.size(), f) == bytes.size();
   } else {
     const uint64_t perRec = numrecs_ ? total / numrecs_ * ts : 0;
-    for (uint64_t r = 0; r < numrecs_ && ok; ++r)
-      ok = fseeko(f, (off_t)(v.begin + r * recsize_), SEEK_SET) == 0 &&
-           fread(bytes.data() + r * perRec, 1, perRec, f) == perRec;
+    for (uint64_t r = 0; r < numrecs_ && ok; ++r) {
+      uint64_t at = 0, end = 0;
+      ok = !__builtin_mul_overflow(r, perRec, &at) && !__builtin_add_overflow(at, perRec, &end) &&
+           end <= bytes.size() && fseeko(f, (off_t)(v.begin + r * recsize_), SEEK_SET) == 0 &&
+           fread(bytes.data() + at, 1, perRec, f) == perRec;
+    }
   }
   fclose(f);
   if (!ok) err = path_ + ": short read of variable " + v.name;

@@ -46,6 +46,7 @@ class File {
   const Var *findVar(const std::string &name) const;
 
   // Number of values of a variable (product of its dimension lengths, records included).
+  static constexpr uint64_t kOverflow = ~0ull;  // numValues of a header whose product overflows
   uint64_t numValues(const Var &v) const;
 
   // nc_get_var_double / nc_get_var_int: every value of the variable converted to the

@@ -114,3 +114,41 @@ def test_convert_tool_writes_loadable_ic(tmp_path):
     assert 6.371e6 < info.sphericalBounds.lower.x < info.sphericalBounds.upper.x < 6.45e6
     r = subprocess.run([TOOL, "-hgrid", hg], capture_output=True, text=True)
     assert r.returncode == 1 and "Usage" in r.stderr
+
+
+def _cdf5(path, dims, variables):
+    """A minimal CDF-5 header: dims [(name, length)], variables [(name, [dim index])] of
+    doubles with no data behind them (the reader must not trust the header's sizes)."""
+    import struct
+
+    def name(s):
+        b = s.encode()
+        return struct.pack(">Q", len(b)) + b + bytes((4 - len(b) % 4) % 4)
+
+    out = b"CDF\x05" + struct.pack(">Q", 1)
+    out += struct.pack(">IQ", 0x0A, len(dims))
+    for n, length in dims:
+        out += name(n) + struct.pack(">Q", length)
+    out += struct.pack(">IQ", 0, 0)  # no global attributes
+    out += struct.pack(">IQ", 0x0B, len(variables))
+    for n, ids in variables:
+        out += name(n) + struct.pack(">Q", len(ids)) + b"".join(struct.pack(">Q", i) for i in ids)
+        out += struct.pack(">IQ", 0, 0) + struct.pack(">IQQ", 6, 8, 4096)  # NC_DOUBLE, vsize, begin
+    path.write_bytes(out + bytes(64))
+    return str(path)
+
+
+def test_convert_rejects_crafted_header_sizes(tmp_path):
+    """header dimension products that wrap 64 bits, or claim more bytes than
+    the file holds, fail cleanly instead of sizing a buffer from a wrapped product."""
+    hg, hs, hhl, data = write_icon_set(str(tmp_path), levels=6)
+    verts = [("clon_vertices", [0, 1]), ("clat_vertices", [0, 1])]
+    wrap = _cdf5(tmp_path / "wrap.nc", [("cell", 3), ("nv", (1 << 63) + 1)], verts)
+    with pytest.raises(irt.IrtError, match="expected 9"):
+        irt.convert_icon(wrap, hs, hhl, data)
+    big = _cdf5(tmp_path / "big.nc", [("cell", 1 << 20), ("nv", 3)], verts)
+    with pytest.raises(irt.IrtError, match="larger than the file"):
+        irt.convert_icon(big, hs, hhl, data)
+    huge = _cdf5(tmp_path / "huge.nc", [("cell", 1 << 40), ("nv", 3)], verts)
+    with pytest.raises(irt.IrtError, match="too large"):
+        irt.convert_icon(huge, hs, hhl, data)
