@@ -15,6 +15,7 @@
 #include "irt_build.h"
 #include "irt_internal.h"
 #include "icon_rt_hip_debug.h"
+#include "irt_device.h"
 #include "irt_kernels.h"
 
 using namespace irt;
@@ -1080,6 +1081,43 @@ extern "C" int irt_debug_device_woodcock_log(int device, float *out) {
   (void)hipFree(d);
   if (e != hipSuccess) {
     set_error("irt_debug_device_woodcock_log: %s", hipGetErrorString(e));
+    return IRT_E_HIP;
+  }
+  return IRT_OK;
+}
+
+namespace {
+__global__ void k_debug_srgb(const float *th, const float *x, uint32_t *out, int n) {
+  __shared__ float s_th[256];
+  s_th[threadIdx.x] = th[threadIdx.x];
+  __syncthreads();
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < n) out[j] = srgb_byte(s_th, x[j]);
+}
+}  // namespace
+
+extern "C" int irt_debug_device_srgb(int device, const float *x, uint32_t *out, int n) {
+  if (!x || !out || n < 0) {
+    set_error("irt_debug_device_srgb: bad argument");
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(device));
+  float th[256];
+  srgb_thresholds(th);
+  float *d = nullptr;
+  const size_t m = 256 + 2 * (size_t)n;  // thresholds, x, out
+  IRT_HIP(hipMalloc((void **)&d, m * sizeof(float)));
+  hipError_t e = hipMemcpy(d, th, sizeof(th), hipMemcpyHostToDevice);
+  e = e == hipSuccess ? hipMemcpy(d + 256, x, n * sizeof(float), hipMemcpyHostToDevice) : e;
+  if (e == hipSuccess && n > 0) {
+    hipLaunchKernelGGL(k_debug_srgb, dim3((n + 255) / 256), dim3(256), 0, 0, d, d + 256,
+                       reinterpret_cast<uint32_t *>(d + 256 + n), n);
+    e = hipGetLastError();
+  }
+  e = e == hipSuccess ? hipMemcpy(out, d + 256 + n, n * sizeof(uint32_t), hipMemcpyDeviceToHost) : e;
+  (void)hipFree(d);
+  if (e != hipSuccess) {
+    set_error("irt_debug_device_srgb: %s", hipGetErrorString(e));
     return IRT_E_HIP;
   }
   return IRT_OK;

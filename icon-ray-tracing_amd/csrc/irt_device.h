@@ -78,15 +78,23 @@ __device__ __forceinline__ uint32_t make_8bit(float f) {
 }
 
 // make_8bit(linear_to_srgb(x)) via the host-built monotone thresholds th[1..255] (LDS):
-// the number of thresholds <= x.
+// the number of thresholds <= x.  The hardware log2/exp2 estimate of the expression
+// (dvr_course-common-both.h:29-34, 89-92) is within one byte of it; the thresholds then
+// settle the exact count (two independent LDS reads instead of an 8-step binary search).
 __device__ __forceinline__ uint32_t srgb_byte(const float *th, float x) {
-  uint32_t lo = 0;
-#pragma unroll
-  for (uint32_t step = 128; step > 0; step >>= 1) {
-    const uint32_t probe = lo + step;
-    if (probe <= 255 && th[probe] <= x) lo = probe;
+  const float s = x <= 0.0031308f
+                      ? 12.92f * x
+                      : 1.055f * __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(x) * (1.f / 2.4f)) - 0.055f;
+  int b = (int)fminf(255.f, fmaxf(0.f, s * 256.f));  // NaN -> 0
+  const float up = th[b < 255 ? b + 1 : 255], at = th[b];
+  if (b < 255 && up <= x) {
+    ++b;
+    while (b < 255 && th[b + 1] <= x) ++b;
+  } else if (b > 0 && !(at <= x)) {
+    --b;
+    while (b > 0 && !(th[b] <= x)) --b;
   }
-  return lo;
+  return (uint32_t)b;
 }
 
 }  // namespace irt

@@ -99,6 +99,9 @@ int irt_debug_device_math(int device, const float *a, const float *y, const floa
                           float *out_asinf, float *out_atan2f);
 /* The device logf(1.f - rnd()) for every LCG low-24-bit value j (out: 2^24 floats, index j). */
 int irt_debug_device_woodcock_log(int device, float *out);
+/* The kernels' make_8bit(linear_to_srgb(x[i])) (csrc/irt_device.h srgb_byte) for n host
+ * values on GPU `device`; out: n bytes widened to uint32. */
+int irt_debug_device_srgb(int device, const float *x, uint32_t *out, int n);
 
 #ifdef __cplusplus
 }

@@ -33,7 +33,7 @@ def test_device_woodcock_log_matches_glibc_everywhere():
     dev = np.zeros(1 << 24, np.float32)
     host = np.zeros(1 << 24, np.float32)
     L = irt.lib()
-    assert L.irt_debug_device_woodcock_log(0, dev.ctypes.data) == 0, L.irt_last_error()
+    assert L.irt_debug_device_woodcock_log(0, dev.ctypes.data) == 0, L.L.irt_last_error()
     L.irt_debug_host_woodcock_log(host.ctypes.data)  # glibc logf, evaluated here
     assert np.array_equal(bits(dev), bits(host))
 
@@ -54,7 +54,7 @@ def test_device_math_matches_glibc():
     L.irt_debug_device_math.argtypes = [C.c_int] + [C.c_void_p] * 3 + [C.c_int] + [C.c_void_p] * 2
     rc = L.irt_debug_device_math(0, a.ctypes.data, y.ctypes.data, x.ctypes.data, n,
                                  oa.ctypes.data, ot.ctypes.data)
-    assert rc == 0, L.irt_last_error()
+    assert rc == 0, L.L.irt_last_error()
     libm = C.CDLL("libm.so.6")
     libm.asinf.restype = C.c_float
     libm.asinf.argtypes = [C.c_float]
@@ -425,3 +425,29 @@ def test_cooperative_woodcock_holes_and_long_chains(raygen):
     assert st_gpu[0].locateCalls == st_ref[0].locate_calls
     assert st_gpu[0].samplesFound == st_ref[0].samples_found
     assert st_ref[0].locate_calls > st_ref[0].samples_found  # holes were sampled
+
+
+def test_device_srgb_byte_equals_threshold_count():
+    """csrc/irt_device.h srgb_byte (hardware log2/exp2 estimate, then settled on the host
+    thresholds) == the number of thresholds <= x, which test_host_logic pins to the
+    reference's make_8bit(linear_to_srgb(x)): every threshold and its float neighbours,
+    a dense sweep, random values, specials."""
+    L = irt.lib()
+    L.irt_debug_device_srgb.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+    th = np.zeros(256, np.float32)
+    L.irt_debug_srgb_thresholds(th.ctypes.data)
+    t = th[1:]
+    near = np.concatenate([t, np.nextafter(t, np.float32(-np.inf)), np.nextafter(t, np.float32(np.inf)),
+                           np.nextafter(np.nextafter(t, np.float32(-np.inf)), np.float32(-np.inf))])
+    rng = np.random.default_rng(7)
+    x = np.concatenate([near, np.linspace(-0.05, 1.05, 1 << 20, dtype=np.float32),
+                        rng.random(1 << 20, dtype=np.float32),
+                        rng.random(1 << 16, dtype=np.float32) * np.float32(1e-3),
+                        np.float32([0.0, -0.0, 0.0031308, 1.0, 2.0, -1.0, 1e-30, np.nan, np.inf, -np.inf])])
+    x = x.astype(np.float32)
+    out = np.zeros(x.size, np.uint32)
+    assert L.irt_debug_device_srgb(0, x.ctypes.data, out.ctypes.data, x.size) == 0, L.irt_last_error()
+    want = np.searchsorted(t, x, side="right").astype(np.uint32)
+    want[np.isnan(x)] = 0
+    bad = np.nonzero(out != want)[0]
+    assert bad.size == 0, (x[bad[:5]], out[bad[:5]], want[bad[:5]])
