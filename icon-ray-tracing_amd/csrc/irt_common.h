@@ -371,12 +371,12 @@ IRT_HD int bin_of(float r, float e0, float e1, float e2) {
   return (e0 < r ? 1 : 0) + (e1 < r ? 1 : 0) + (e2 < r ? 1 : 0);
 }
 
-// Zero-thickness records are spheres (host/irt_scene.cpp); a 2^16-bit hash bitmap of
-// their radii says "certainly not a sphere radius" for almost every sample.
-constexpr int kSphBitWords = 2048;
+// Zero-thickness records are spheres (host/irt_scene.cpp); a 2^14-bit hash bitmap of
+// their radii (2 KB of LDS) says "certainly not a sphere radius" for almost every sample.
+constexpr int kSphBitWords = 512;
 IRT_HD uint32_t sph_hash(float r) {
   uint32_t h = f2u(r) * 0x9E3779B1u;
-  return h >> 16;
+  return h >> 18;
 }
 
 // Fat entry: everything one candidate test of sample() reads, kFat4 float4 = 80 B:

@@ -1123,6 +1123,43 @@ extern "C" int irt_debug_device_srgb(int device, const float *x, uint32_t *out, 
   return IRT_OK;
 }
 
+extern "C" int irt_debug_locate(irt_context *c, const float *xyz, int n, int *found, float *value) {
+  if (!c || !xyz || !found || !value || n < 0) {
+    set_error("irt_debug_locate: bad argument");
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(c->device));
+  RenderArgs A;
+  memset(&A, 0, sizeof(A));
+  A.numCells = c->n;
+  A.G = c->G;
+  A.binHdr = c->d_binHdr;
+  A.fat = c->d_fat;
+  A.blocks = c->d_blocks;
+  A.numSph = c->numSph;
+  A.sphR = c->d_sphR;
+  A.sphOff = c->d_sphOff;
+  A.sphRec = c->d_sphRec;
+  A.sphBits = c->d_sphBits;
+  float *d = nullptr;
+  IRT_HIP(hipMalloc((void **)&d, (size_t)std::max(n, 1) * 5 * sizeof(float)));
+  hipError_t e = hipMemcpy(d, xyz, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice);
+  int *dFound = reinterpret_cast<int *>(d + 3 * (size_t)n);
+  float *dValue = d + 4 * (size_t)n;
+  if (e == hipSuccess) {
+    launch_debug_locate(A, d, n, dFound, dValue, 0);
+    e = hipGetLastError();
+  }
+  e = e == hipSuccess ? hipMemcpy(found, dFound, (size_t)n * sizeof(int), hipMemcpyDeviceToHost) : e;
+  e = e == hipSuccess ? hipMemcpy(value, dValue, (size_t)n * sizeof(float), hipMemcpyDeviceToHost) : e;
+  (void)hipFree(d);
+  if (e != hipSuccess) {
+    set_error("irt_debug_locate: %s", hipGetErrorString(e));
+    return IRT_E_HIP;
+  }
+  return IRT_OK;
+}
+
 extern "C" int irt_debug_counters(irt_context *c, unsigned long long *out16) {
   if (!c || !out16) {
     set_error("irt_debug_counters: null argument");

@@ -345,9 +345,9 @@ struct Tracer {
     // bin, so a second pass scans it for a lower record (one scan site, two passes)
     const float eb = __uint_as_float(H0.x ^ (m1 & (H0.x ^ H0.y)) ^ (m2 & (H0.y ^ H0.z)));
     const bool onEdge = b < kMaxEdges && r == eb;
-    uint32_t qb = H0.w + beg, qe = H0.w + end;
     Found f = {0xFFFFFFFFu, 0u, make_float4(0.f, 0.f, 0.f, 0.f)};
     bool hit = false;
+    uint32_t qb = H0.w + beg, qe = H0.w + end;
     for (int pass = 0; pass < 2; ++pass) {
       Found g;
       if (scan_fat(qb, qe, (M >> (8 * (b + pass))) & 0xFFu, f.rec, px, py, pz, r, g)) {
@@ -965,9 +965,9 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       dd.y = (int)((uint32_t)project_axis(r2, A.sbLo.x, A.sbHi.x, A.dims.x) + (uint32_t)sx);
       dd.z = (int)((uint32_t)project_axis(la2, A.sbLo.y, A.sbHi.y, A.dims.y) + (uint32_t)sy);
       dd.w = (int)((uint32_t)project_axis(lo2, A.sbLo.z, A.sbHi.z, A.dims.z) + (uint32_t)sz);
-      s_dda[tid] = dd;
+      s_entry[tid] = __builtin_bit_cast(float4, dd);  // the entry point is not needed again
     } else {
-      dd = s_dda[tid];
+      dd = __builtin_bit_cast(int4, s_entry[tid]);
     }
     const float t_closest = fminf(fminf(tnx, tny), tnz);
     bool stop = false;
@@ -1193,6 +1193,31 @@ __global__ void __launch_bounds__(256) k_accumulate(RenderArgs A) {
   A.accum[px.outIdx] = a;
   A.fb[px.outIdx] = srgb_byte(s_th, a.x) + (srgb_byte(s_th, a.y) << 8) +
                     (srgb_byte(s_th, a.z) << 16) + (make_8bit(a.w) << 24);
+}
+
+// ------------------------------------------------------------------ debug: point location
+// The default kernel's Tracer::locate (sampleVolume over the binned lists) on given points:
+// the device locator pinned point by point (tests/test_gpu_parity.py), e.g. exactly on
+// radial bin edges, which frames almost never hit.
+__global__ void __launch_bounds__(256) k_debug_locate(RenderArgs A, const float *xyz, int n,
+                                                      int *found, float *value) {
+  __shared__ uint32_t s_sph[kSphBitWords];
+  __shared__ uint32_t s_cnt[kCnt];
+  for (int i = threadIdx.x; i < kSphBitWords; i += 256) s_sph[i] = A.numSph ? A.sphBits[i] : 0u;
+  if (threadIdx.x < kCnt) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  Tracer<kDefaultVariant & ~4096> T{A, nullptr, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
+  const int j = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (j < n) {
+    float v = 0.f;
+    found[j] = T.locate(xyz[3 * j], xyz[3 * j + 1], xyz[3 * j + 2], v) ? 1 : 0;
+    value[j] = v;
+  }
+}
+
+void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *found, float *value,
+                         hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_debug_locate, dim3((n + 255) / 256), dim3(256), 0, s, A, xyz, n, found, value);
 }
 
 // ------------------------------------------------------------------ variants / launcher

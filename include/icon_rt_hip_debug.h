@@ -102,6 +102,9 @@ int irt_debug_device_woodcock_log(int device, float *out);
 /* The kernels' make_8bit(linear_to_srgb(x[i])) (csrc/irt_device.h srgb_byte) for n host
  * values on GPU `device`; out: n bytes widened to uint32. */
 int irt_debug_device_srgb(int device, const float *x, uint32_t *out, int n);
+/* The render kernel's point location (sampleVolume over the context's binned lists,
+ * csrc/irt_render.hip Tracer::locate) for n points xyz[3i..3i+2]: found[i] 0/1, value[i]. */
+int irt_debug_locate(irt_context *ctx, const float *xyz, int n, int *found, float *value);
 
 #ifdef __cplusplus
 }

@@ -105,3 +105,43 @@ def terrain_cells(seed=11, bisections=1, levels=70):
         elif i % 4 == 2:
             cells["height"][i][nl] = cells["height"][i][0] - 1.0  # inverted: never hit
     return cells
+
+
+def on_radius(v, r):
+    """A float32 point in direction v whose float32 |p| (sqrtf(x*x+y*y+z*z), as
+    toSpherical computes it) equals r exactly, when one is found nearby."""
+    v = np.asarray(v, np.float64)
+    v = v / np.linalg.norm(v)
+    r = np.float32(r)
+    s = np.float64(r)
+    p = (v * s).astype(np.float32)
+    for _ in range(64):
+        q = np.sqrt(np.float32(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]))
+        if q == r:
+            break
+        s *= 1 + (float(r) - float(q)) / float(r) * 0.999 + (1e-8 if q < r else -1e-8)
+        p = (v * s).astype(np.float32)
+    return p
+
+
+def locator_points(cells, seed, n_random=400, n_cols=80):
+    """Points for point-location checks: random ones in the shell, and per sampled column
+    points exactly on (and one float either side of) every record boundary -- where the
+    per-cell radial bin edges sit -- at the cell centre, on edge midpoints and at a corner
+    (shared triangle edges: the lower record index must win)."""
+    rng = np.random.default_rng(seed)
+    top = cells["height"][np.arange(cells.size), cells["numLayers"]]
+    sbl, sbu = float(cells["height"][:, 0].min()), float(top.max())
+    d = rng.normal(size=(n_random, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    pts = list((d * rng.uniform(sbl - 50, sbu + 50, (n_random, 1))).astype(np.float32))
+    for i in rng.choice(cells.size, min(n_cols, cells.size), replace=False):
+        c = cells[i]
+        lat, lon = c["lat"].astype(np.float64), c["lon"].astype(np.float64)
+        cd = np.stack([np.cos(lat) * np.cos(lon), np.cos(lat) * np.sin(lon), np.sin(lat)], 1)
+        nl = int(c["numLayers"])
+        for hh in (c["height"][0], c["height"][nl], c["height"][nl // 2]):
+            for rr in (hh, np.nextafter(hh, np.float32(np.inf)), np.nextafter(hh, np.float32(0))):
+                for v in (cd.mean(0), cd[0] + cd[1], cd[0]):
+                    pts.append(on_radius(v, rr))
+    return np.array(pts, np.float32)
