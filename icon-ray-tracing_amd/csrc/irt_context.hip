@@ -113,6 +113,8 @@ struct irt_context {
   bool schedOn = true;         // IRT_SCHED=0 disables
   int schedPolicy = 2;         // IRT_SCHED: 1 tiles, 2 bands of tiles (a tile row; default), 3 reversed
   bool schedOrderValid = false;
+  bool schedLastApplied = false;   // the last launch ran in a measured-cost order
+  long long schedApplied = 0;      // launches that did
   long long schedKey[8] = {};
   long long schedSrc = -1;      // launch whose costs the current order came from
   long long schedCopied[kSlots] = {};  // launch index whose costs slot i holds (-1: none)
@@ -450,6 +452,8 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
       A.schedCost = c->d_schedCost;
     }
   }
+  c->schedLastApplied = A.schedOrder != nullptr;
+  c->schedApplied += c->schedLastApplied ? 1 : 0;
   // the 16-counter block (device atomics) is only needed by the statistics variant and the
   // IRT_COUNTERS=atomic mode; it must start zeroed
   const bool block = !c->wgCountsOn || (c->variant & 32768) != 0;
@@ -1157,6 +1161,17 @@ extern "C" int irt_debug_locate(irt_context *c, const float *xyz, int n, int *fo
     set_error("irt_debug_locate: %s", hipGetErrorString(e));
     return IRT_E_HIP;
   }
+  return IRT_OK;
+}
+
+extern "C" int irt_debug_sched(irt_context *c, int *policy, int *lastApplied, long long *applied) {
+  if (!c || !policy || !lastApplied || !applied) {
+    set_error("irt_debug_sched: null argument");
+    return IRT_E_INVALID;
+  }
+  *policy = c->schedOn ? c->schedPolicy : 0;
+  *lastApplied = c->schedLastApplied ? 1 : 0;
+  *applied = c->schedApplied;
   return IRT_OK;
 }
 

@@ -105,6 +105,9 @@ int irt_debug_device_srgb(int device, const float *x, uint32_t *out, int n);
 /* The render kernel's point location (sampleVolume over the context's binned lists,
  * csrc/irt_render.hip Tracer::locate) for n points xyz[3i..3i+2]: found[i] 0/1, value[i]. */
 int irt_debug_locate(irt_context *ctx, const float *xyz, int n, int *found, float *value);
+/* Measured-cost scheduling state: the policy (IRT_SCHED; 0 = off), whether the last launch
+ * ran its workgroups in a measured-cost order, and how many launches have. */
+int irt_debug_sched(irt_context *ctx, int *policy, int *lastApplied, long long *applied);
 
 #ifdef __cplusplus
 }

@@ -351,6 +351,7 @@ def test_measured_cost_scheduling_keeps_frames_identical():
     ctx = irt.Context(cells, 0)
     ctx.set_transfunc(setup.lut, setup.value_range)
     fr = GpuFrame(ctx, W, W)
+    applied = 0
     for k in range(24):
         fr.accum.zero_()
         fr.fb.zero_()
@@ -358,6 +359,55 @@ def test_measured_cost_scheduling_keeps_frames_identical():
         a, f = fr.host()
         assert_same_frame(a, f, a_ref, f_ref, f"launch {k}")
         assert (st.locateCalls, st.samplesFound) == (st_ref[0].locate_calls, st_ref[0].samples_found)
+        applied += _sched_state(ctx)[1]
+    policy, last, total = _sched_state(ctx)
+    assert policy == 2 and last == 1 and total == applied > 0  # the order was in effect
+    ctx.close()
+
+
+def _sched_state(ctx):
+    L = irt.lib()
+    L.irt_debug_sched.argtypes = [C.c_void_p] + [C.c_void_p] * 3
+    p, a, n = C.c_int(), C.c_int(), C.c_longlong()
+    assert L.irt_debug_sched(ctx._h, C.byref(p), C.byref(a), C.byref(n)) == 0
+    return p.value, a.value, n.value
+
+
+def test_measured_cost_scheduling_on_a_rank_tile_subset():
+    """the scheduled path with tileStride > 1 (one rank's interleaved tiles, where
+    the policy-2 band is tilesX/tileStride tiles): repeated launches run in a measured-cost
+    order and every launch's tiles equal the full frame's."""
+    import torch
+    cells = irt.synth_grid(2, 3, 47)
+    W, H = 328, 200  # 6 x 4 tiles, the last column and row ragged
+    setup = irt.setup_frame(cells, W, H, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    dev = "cuda:0"
+    fb = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+    ctx.render(setup.lp, W, H, fb.data_ptr(), acc.data_ptr())
+    torch.cuda.synchronize()
+    full = fb.cpu().numpy()
+    ranks, rank = 3, 1
+    ntot = irt.num_tiles(W, H)
+    maxt = (ntot + ranks - 1) // ranks
+    gathered = torch.zeros(ranks * maxt * 4096, dtype=torch.int32, device=dev)
+    mine = gathered[rank * maxt * 4096:(rank + 1) * maxt * 4096]
+    seen = 0
+    tiles_x = (W + 63) // 64
+    tile = ((np.arange(H) // 64)[:, None] * tiles_x + (np.arange(W) // 64)[None, :]).reshape(-1)
+    sel = tile % ranks == rank  # this rank's pixels
+    for k in range(24):
+        tacc = torch.zeros(maxt * 4096 * 4, dtype=torch.float32, device=dev)
+        mine.zero_()
+        ctx.render_tiles(setup.lp, W, H, rank, ranks, mine.data_ptr(), tacc.data_ptr())
+        seen += _sched_state(ctx)[1]
+        out = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        ctx.unpack_tiles(gathered.data_ptr(), ranks, maxt, W, H, out.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy()[sel], full[sel]), f"launch {k}"
+    assert seen > 0 and _sched_state(ctx)[1] == 1
     ctx.close()
 
 
