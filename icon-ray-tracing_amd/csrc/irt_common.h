@@ -67,14 +67,13 @@ IRT_HD float lcg_float(uint32_t s) { return (float)(s & 0x00FFFFFFu) / (float)0x
 // map by binary powers (the maps commute).  The wave-cooperative Woodcock loop
 // (irt_render.hip) evaluates sample k of a ray from the state 2k+1 (its step draw) and 2k+2
 // (its acceptance draw) draws ahead; it tabulates n < kLcgJumps in LDS.
-constexpr int kLcgJumps = 130;
+constexpr int kLcgJumps = 130;  // < 256 (lcg_jump's 8 bits)
 IRT_HD void lcg_jump(uint32_t n, uint32_t &mul, uint32_t &add) {
   uint32_t m = 1u, c = 0u, bm = 1664525u, bc = 1013904223u;
-  for (; n; n >>= 1) {
-    if (n & 1u) {
-      c = bm * c + bc;
-      m = bm * m;
-    }
+  for (int bit = 0; bit < 8; ++bit) {  // n < 256; selects, no divergent branches
+    const bool on = (n >> bit) & 1u;
+    c = on ? bm * c + bc : c;
+    m = on ? bm * m : m;
     bc = bm * bc + bc;
     bm = bm * bm;
   }

@@ -1100,13 +1100,28 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   __shared__ float4 s_acc[256];     // kCoop: the accum pixels, prefetched
   __shared__ uint32_t s_jmul[kLcgJumps], s_jadd[kLcgJumps];
   const int tid = threadIdx.x;
-  if constexpr (Tracer<OPT>::kCoop) {
-    if (tid < kLcgJumps) lcg_jump((uint32_t)tid, s_jmul[tid], s_jadd[tid]);
+  // the prologue's global loads issued together, one wait (not one round trip each)
+  const float th = A.srgbTh[tid];
+  const LogfTab lt = kLogfTab[tid & 15];
+  uint32_t sph[kSphBitWords / 256];
+  if (A.numSph) {
+#pragma unroll
+    for (int k = 0; k < kSphBitWords / 256; ++k) sph[k] = A.sphBits[tid + 256 * k];
   }
-  if (A.numSph)
-    for (int i = tid; i < kSphBitWords; i += 256) s_sph[i] = A.sphBits[i];
-  s_th[tid] = A.srgbTh[tid];
-  if (tid < 16) s_logf[tid] = kLogfTab[tid];
+  if constexpr (Tracer<OPT>::kCoop) {
+    if (tid < kLcgJumps) {
+      uint32_t m, a;
+      lcg_jump((uint32_t)tid, m, a);
+      s_jmul[tid] = m;
+      s_jadd[tid] = a;
+    }
+  }
+  s_th[tid] = th;
+  if (tid < 16) s_logf[tid] = lt;
+  if (A.numSph) {
+#pragma unroll
+    for (int k = 0; k < kSphBitWords / 256; ++k) s_sph[tid + 256 * k] = sph[k];
+  }
   if (tid < kCnt) s_cnt[tid] = 0;
   __syncthreads();
   Tracer<OPT> T{A, s_logf, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
