@@ -555,15 +555,17 @@ int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_
     set_error("binned locator too large (%llu entries)", (unsigned long long)numFat);
     return IRT_E_INVALID;
   }
+  clk.mark("headers");
   // --- 9. fat entries
   BHIP(hipMalloc((void **)&out.fat, std::max<uint64_t>(numFat, 1) * kFatStride4 * sizeof(float4)));
   out.bytes += std::max<uint64_t>(numFat, 1) * kFatStride4 * sizeof(float4);
+  clk.mark("fat entries allocated");
   hipLaunchKernelGGL(k_cell_fill, dim3(nc), dim3(64), 0, s, offsets, numCells, pv2, rng, edges, cellBase,
                      reinterpret_cast<uint32_t *>(out.binHdr), planesF, meta,
                      reinterpret_cast<const float *>(keys), out.fat);
   BHIP(hipGetLastError());
   BHIP(hipStreamSynchronize(s));
-  clk.mark("headers + fat entries");
+  clk.mark("fat entries");
   out.entries = numPairs;
   out.binEntries = numFat;
   out.bigCells = numBig;

@@ -543,6 +543,92 @@ int irt_create_begin(size_t numCells, int device, irt_context **out) {
   return IRT_OK;
 }
 
+namespace {
+// One chunk of records: validation, glibc corner trig and getBounds, and the record-order
+// folds (volume facts, column count, sphere records), per contiguous slice of records in
+// parallel; the slices' partial folds are combined in slice order, which selects the same
+// elements as one sequential fold (volume_acc_merge).  Then the cells and their trig go to
+// HBM: synchronously from the caller's memory, or, with `trigPinned` (cells already in
+// pinned memory, irt_create_synth), asynchronously on the context stream.
+int append_chunk(irt_context *c, const irt_icon_cell *cells, size_t n, float *trigPinned) {
+  const size_t base = c->received;
+  std::vector<float> trigHeap;
+  float *trig = trigPinned;
+  if (!trig) {
+    trigHeap.resize(n * 12);
+    trig = trigHeap.data();
+  }
+  const int threads = n < 4096 ? 1 : default_threads();
+  const size_t slice = (n + threads - 1) / threads;
+  struct Part {
+    VolumeAcc acc;
+    size_t runs = 0, bad = SIZE_MAX;
+    std::vector<irt_context::Sphere> sph;
+  };
+  std::vector<Part> part(threads);
+  auto work = [&](int t) {
+    Part &P = part[t];
+    volume_acc_init(P.acc);
+    const size_t b = (size_t)t * slice, e = std::min(n, b + slice);
+    for (size_t i = b; i < e; ++i) {
+      const irt_icon_cell &x = cells[i];
+      bool ok = x.numLayers >= 0 && x.numLayers <= 31;
+      for (int k = 0; ok && k < 3; ++k) ok = std::isfinite(x.lat[k]) && std::isfinite(x.lon[k]);
+      for (int j = 0; ok && j <= x.numLayers; ++j) ok = std::isfinite(x.height[j]);
+      if (!ok) {
+        P.bad = i;
+        return;
+      }
+      float *tr = &trig[12 * i];
+      if (i > b && same_corners(x.lat, x.lon, cells[i - 1].lat, cells[i - 1].lon))
+        memcpy(tr, tr - 12, 12 * sizeof(float));  // same column, same corners
+      else
+        corner_trig(x, tr);
+      float lo[3], hi[3];
+      cell_bounds(x, tr, lo, hi);
+      volume_acc_add(P.acc, x, lo, hi);
+      const irt_icon_cell &prev = i ? cells[i - 1] : c->last;
+      if (base + i == 0 || !same_corners(x.lat, x.lon, prev.lat, prev.lon)) ++P.runs;
+      if (x.height[0] == x.height[x.numLayers])  // a sphere record
+        P.sph.push_back({x.height[0], (uint32_t)(base + i), x.numLayers});
+    }
+  };
+  if (threads == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t) ts.emplace_back(work, t);
+    for (auto &t : ts) t.join();
+  }
+  size_t bad = SIZE_MAX;
+  for (const Part &P : part) bad = std::min(bad, P.bad);
+  if (bad != SIZE_MAX) {  // the first bad record, as a sequential check would report
+    const irt_icon_cell &x = cells[bad];
+    if (x.numLayers < 0 || x.numLayers > 31)
+      set_error("cell %zu: numLayers %d outside [0,31] (MAX_LAYERS 32, ICONGrid.h:57)", base + bad, x.numLayers);
+    else
+      set_error("cell %zu: non-finite lat/lon/height", base + bad);
+    return IRT_E_DATA;
+  }
+  for (const Part &P : part) {
+    volume_acc_merge(c->vacc, P.acc);
+    c->numRuns += P.runs;
+    c->sph.insert(c->sph.end(), P.sph.begin(), P.sph.end());
+  }
+  IRT_HIP(hipSetDevice(c->device));
+  if (trigPinned) {
+    IRT_HIP(hipMemcpyAsync(c->d_cells + base, cells, n * sizeof(irt_icon_cell), hipMemcpyHostToDevice, c->stream));
+    IRT_HIP(hipMemcpyAsync(c->d_trig + 3 * base, trig, n * 12 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  } else {
+    IRT_HIP(hipMemcpy(c->d_cells + base, cells, n * sizeof(irt_icon_cell), hipMemcpyHostToDevice));
+    IRT_HIP(hipMemcpy(c->d_trig + 3 * base, trig, n * 12 * sizeof(float), hipMemcpyHostToDevice));
+  }
+  c->last = cells[n - 1];
+  c->received += n;
+  return IRT_OK;
+}
+}  // namespace
+
 int irt_create_append(irt_context *c, const irt_icon_cell *cells, size_t n) {
   if (!c || !c->building || (n && !cells)) {
     set_error("irt_create_append: no context being created, or null cells");
@@ -553,56 +639,7 @@ int irt_create_append(irt_context *c, const irt_icon_cell *cells, size_t n) {
     return IRT_E_INVALID;
   }
   if (n == 0) return IRT_OK;
-  const size_t base = c->received;
-  for (size_t i = 0; i < n; ++i) {
-    if (cells[i].numLayers < 0 || cells[i].numLayers > 31) {
-      set_error("cell %zu: numLayers %d outside [0,31] (MAX_LAYERS 32, ICONGrid.h:57)", base + i,
-                cells[i].numLayers);
-      return IRT_E_DATA;
-    }
-    const irt_icon_cell &x = cells[i];
-    bool finite = true;
-    for (int k = 0; k < 3; ++k) finite = finite && std::isfinite(x.lat[k]) && std::isfinite(x.lon[k]);
-    for (int j = 0; j <= x.numLayers; ++j) finite = finite && std::isfinite(x.height[j]);
-    if (!finite) {
-      set_error("cell %zu: non-finite lat/lon/height", base + i);
-      return IRT_E_DATA;
-    }
-  }
-  // corner trig (host glibc: the only libm values the device build needs) and getBounds,
-  // per record in parallel; then the order-dependent folds in record order
-  std::vector<float> trig(n * 12), bnd(n * 6);
-  {
-    const int threads = n < 4096 ? 1 : default_threads();
-    std::vector<std::thread> ts;
-    const size_t chunk = (n + threads - 1) / threads;
-    for (int t = 0; t < threads; ++t)
-      ts.emplace_back([&, t] {
-        for (size_t i = t * chunk; i < std::min(n, (t + 1) * chunk); ++i) {
-          float *tr = &trig[12 * i];
-          if (i > 0 && same_corners(cells[i].lat, cells[i].lon, cells[i - 1].lat, cells[i - 1].lon) &&
-              i != t * chunk)
-            memcpy(tr, tr - 12, 12 * sizeof(float));  // same column, same corners
-          else
-            corner_trig(cells[i], tr);
-          cell_bounds(cells[i], tr, &bnd[6 * i], &bnd[6 * i + 3]);
-        }
-      });
-    for (auto &t : ts) t.join();
-  }
-  for (size_t i = 0; i < n; ++i) {
-    volume_acc_add(c->vacc, cells[i], &bnd[6 * i], &bnd[6 * i + 3]);
-    const irt_icon_cell &prev = i ? cells[i - 1] : c->last;
-    if (base + i == 0 || !same_corners(cells[i].lat, cells[i].lon, prev.lat, prev.lon)) ++c->numRuns;
-    if (cells[i].height[0] == cells[i].height[cells[i].numLayers])  // a sphere record
-      c->sph.push_back({cells[i].height[0], (uint32_t)(base + i), cells[i].numLayers});
-  }
-  IRT_HIP(hipSetDevice(c->device));
-  IRT_HIP(hipMemcpy(c->d_cells + base, cells, n * sizeof(irt_icon_cell), hipMemcpyHostToDevice));
-  IRT_HIP(hipMemcpy(c->d_trig + 3 * base, trig.data(), n * 12 * sizeof(float), hipMemcpyHostToDevice));
-  c->last = cells[n - 1];
-  c->received += n;
-  return IRT_OK;
+  return append_chunk(c, cells, n, nullptr);
 }
 
 int irt_create_end(irt_context *c) {
@@ -800,11 +837,41 @@ int irt_create_synth(int rootN, int bisections, int levels, float topHeight, flo
     synth_close(gen);
     return rc;
   }
-  std::vector<irt_icon_cell> buf(std::min(n, kChunk));
-  for (size_t at = 0; at < n && !rc; at += buf.size()) {
-    const size_t m = std::min(buf.size(), n - at);
-    synth_fill(gen, at, m, buf.data());
-    rc = irt_create_append(c, buf.data(), m);
+  // two pinned chunk buffers: chunk k+1 is synthesised and prepared while chunk k's
+  // asynchronous upload runs
+  const size_t cap = std::max<size_t>(1, std::min(n, kChunk));
+  irt_icon_cell *cb[2] = {nullptr, nullptr};
+  float *tb[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  for (int k = 0; k < 2 && !rc; ++k) {
+    if (hipHostMalloc((void **)&cb[k], cap * sizeof(irt_icon_cell)) != hipSuccess ||
+        hipHostMalloc((void **)&tb[k], cap * 12 * sizeof(float)) != hipSuccess ||
+        hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) {
+      set_error("irt_create_synth: pinned staging buffers");
+      rc = IRT_E_HIP;
+    }
+  }
+  size_t k = 0;
+  for (size_t at = 0; at < n && !rc; at += cap, ++k) {
+    const int b = (int)(k & 1);
+    if (k >= 2 && hipEventSynchronize(ev[b]) != hipSuccess) {
+      set_error("irt_create_synth: upload failed");
+      rc = IRT_E_HIP;
+      break;
+    }
+    const size_t m = std::min(cap, n - at);
+    synth_fill(gen, at, m, cb[b]);
+    rc = append_chunk(c, cb[b], m, tb[b]);
+    if (!rc && hipEventRecord(ev[b], c->stream) != hipSuccess) rc = IRT_E_HIP;
+  }
+  if (hipStreamSynchronize(c->stream) != hipSuccess && !rc) {
+    set_error("irt_create_synth: upload failed");
+    rc = IRT_E_HIP;
+  }
+  for (int q = 0; q < 2; ++q) {
+    if (cb[q]) (void)hipHostFree(cb[q]);
+    if (tb[q]) (void)hipHostFree(tb[q]);
+    if (ev[q]) (void)hipEventDestroy(ev[q]);
   }
   synth_close(gen);
   if (!rc) rc = irt_create_end(c);

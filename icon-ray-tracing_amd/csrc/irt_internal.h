@@ -67,6 +67,7 @@ void corner_trig(const irt_icon_cell &c, float *t12);
 void cell_bounds(const irt_icon_cell &c, const float *t12, float lo[3], float hi[3]);
 void volume_acc_init(VolumeAcc &a);
 void volume_acc_add(VolumeAcc &a, const irt_icon_cell &c, const float blo[3], const float bhi[3]);
+void volume_acc_merge(VolumeAcc &a, const VolumeAcc &b);  // a's records, then b's
 void volume_acc_finish(const VolumeAcc &a, irt_volume_info &info);
 
 // glibc logf(1 - k/2^24) for k in [0, 2^24): the only arguments woodcockTracking's

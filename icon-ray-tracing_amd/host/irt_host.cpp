@@ -13,6 +13,7 @@
 #include <atomic>
 #include <cfloat>
 #include <mutex>
+#include <sched.h>
 #include <thread>
 #include <vector>
 
@@ -32,12 +33,20 @@ void set_error(const char *fmt, ...) {
 }
 void clear_error() { g_error.clear(); }
 
+// Host worker threads: the CPUs this process may run on (affinity mask), within
+// OMP_NUM_THREADS when set (the GPU box sets it to the job's share) and at most 32.
 int default_threads() {
-  unsigned h = std::thread::hardware_concurrency();
-  if (h == 0) h = 1;
-  // The GPU box exposes many more cores than its share; stay polite.
-  if (h > 32) h = 32;
-  return (int)h;
+  static const int n = [] {
+    int h = (int)std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) h = CPU_COUNT(&set);
+    if (const char *e = getenv("OMP_NUM_THREADS")) {
+      const int v = atoi(e);
+      if (v > 0 && v < h) h = v;
+    }
+    return std::max(1, std::min(h, 32));
+  }();
+  return n;
 }
 
 template <typename F>
@@ -159,6 +168,21 @@ void volume_acc_add(VolumeAcc &a, const irt_icon_cell &c, const float blo[3], co
     a.dhi = fmaxf(a.dhi, c.value[j]);
   }
   ++a.n;
+}
+
+// a's records, then b's: fminf/fmaxf select one of their arguments, ties to the second, so
+// folding per-chunk partials in chunk order selects the element the sequential fold selects
+// (signed zeros included)
+void volume_acc_merge(VolumeAcc &a, const VolumeAcc &b) {
+  for (int k = 0; k < 3; ++k) {
+    a.vlo[k] = fminf(a.vlo[k], b.vlo[k]);
+    a.vhi[k] = fmaxf(a.vhi[k], b.vhi[k]);
+    a.slo[k] = fminf(a.slo[k], b.slo[k]);
+    a.shi[k] = fmaxf(a.shi[k], b.shi[k]);
+  }
+  a.dlo = fminf(a.dlo, b.dlo);
+  a.dhi = fmaxf(a.dhi, b.dhi);
+  a.n += b.n;
 }
 
 void volume_acc_finish(const VolumeAcc &a, irt_volume_info &info) {
