@@ -119,13 +119,14 @@ def test_sample_statistics_are_plausible(scene):
     assert st.candidatesTested / st.samplesFound < 1.5
 
 
-def test_streamed_context_equals_array_context(scene):
+def test_streamed_context_equals_array_context():
     """The streamed creation keeps host memory at one chunk: the scene's HBM arrays match
-    a context created from the full host array (C2 only: the same code path at any size)."""
-    if scene["name"] != "c2":
-        pytest.skip("checked once, at C2")
+    a context created from the full host array (C2; the same code path at any size)."""
     rn, bis, L, _, _ = SCALE["c2"]
+    whole = irt.Context(irt.synth_grid(rn, bis, L), 0)
     streamed = irt.Context.synth(rn, bis, L, 0)
     for name in irt.SCENE_ARRAYS:
-        assert np.array_equal(streamed.array(name), scene["ctx"].array(name)), name
+        assert np.array_equal(streamed.array(name), whole.array(name)), name
+    assert bytes(streamed.info)[:-8] == bytes(whole.info)[:-8]  # all but deviceBytes
     streamed.close()
+    whole.close()
