@@ -126,9 +126,9 @@ struct Tracer {
     }
   }
 
-  // the cooperative Woodcock loop (woodcock_wave) runs in every user-geometry sphere-accel
-  // kernel but the OPT_SERIAL comparison one
-  static constexpr bool kCoop = (OPT & (OPT_GRID | OPT_WEDGE | OPT_SERIAL)) == 0;
+  // the cooperative Woodcock loop (woodcock_wave) runs in every sphere-accel kernel (any
+  // sampler) but the OPT_SERIAL comparison one; the grid accel walks dda3 one lane per ray
+  static constexpr bool kCoop = (OPT & (OPT_GRID | OPT_SERIAL)) == 0;
 
   // one wave-aggregated LDS add per event site
   __device__ __forceinline__ void count(int k) {
@@ -1258,13 +1258,18 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
   constexpr int K = N & ~OPT_MONO;
   // the grid accel or the unstructured samplers: their own instantiations of the raygen
   // (kept out of the default kernel, whose registers they would cost); the wedge kernels
-  // hold a 6-vertex Newton state: no waves-per-SIMD floor
+  // hold a 6-vertex Newton state: no waves-per-SIMD floor.  TRIANGLES runs the cooperative
+  // Woodcock loop (3.4x faster at C2); CUBQL keeps one lane per ray: its Newton solve's
+  // per-lane iteration counts and frequent misses make speculative samples cost more than
+  // they save (1.26x slower measured, profiles/r02b_investigation/).
   constexpr int D = kDefaultVariant & ~OPT_MONO;
-  constexpr int DW = (D & ~0xF00) | OPT_WEDGE;
+  constexpr int DW = (D & ~0xF00) | OPT_WEDGE | (K & OPT_SERIAL);
   const dim3 grid(numBlocks, A.numSamples);
   const bool g = A.accelMode == IRT_ACCEL_GRID;
   if (A.sampler != IRT_MODE_USER_GEOM && g)  // CUBQL or TRIANGLES: the unstructured locator
     hipLaunchKernelGGL(k_render<DW | OPT_GRID>, grid, dim3(256), 0, s, A);
+  else if (A.sampler == IRT_MODE_CUBQL)
+    hipLaunchKernelGGL(k_render<DW | OPT_SERIAL>, grid, dim3(256), 0, s, A);
   else if (A.sampler != IRT_MODE_USER_GEOM)
     hipLaunchKernelGGL(k_render<DW>, grid, dim3(256), 0, s, A);
   else if (g)

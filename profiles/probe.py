@@ -9,7 +9,8 @@ launches).  One JSON line per case.
 A case is `;`-separated; inside a case, `,`-separated KEY=VALUE items: environment
 variables read at context creation (IRT_*), `cam=framing|viewall|away`, `variant=N`,
 `tf=default|zero|dense|comb` (alpha 0: the full sdda walk without a sample; alpha 1: one
-accepted sample per in-shell ray; comb: bench.py's C3s sparse comb).
+accepted sample per in-shell ray; comb: bench.py's C3s sparse comb), `mode=user|tri|cubql`
+(sampler), `accel=sphere|grid`.
 """
 import argparse
 import ctypes as C
@@ -31,7 +32,8 @@ CAMS = {"framing": ((0.0, 0.0, 1.4e7), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0),
 
 
 def parse(case):
-    env, opt = {}, {"cam": "framing", "variant": None, "tf": "default"}
+    env, opt = {}, {"cam": "framing", "variant": None, "tf": "default", "mode": "user",
+                    "accel": "sphere"}
     for item in filter(None, case.split(",")):
         if item == "base":
             continue
@@ -74,6 +76,11 @@ def main():
             else:
                 os.environ[k] = v
         setup = irt.setup_frame(cells, W, W, camera=CAMS[opt["cam"]])
+        setup.lp.mode = {"user": irt.MODE_USER_GEOM, "tri": irt.MODE_TRIANGLES,
+                         "cubql": irt.MODE_CUBQL}[opt["mode"]]
+        setup.lp.accelMode = irt.ACCEL_GRID if opt["accel"] == "grid" else 0
+        if opt["mode"] != "user":
+            ctx.build_wedge_accel(cells)
         lut = setup.lut.copy()
         if opt["tf"] == "zero":
             lut[:, 3] = 0.0
@@ -97,8 +104,8 @@ def main():
         runs.append(dict(env=env, opt=opt, ctx=ctx, setup=setup, out=out, st=st.asdict(),
                          counters=[int(v) for v in cnt], create_s=t_create, k=[], step=[]))
     ref = {}
-    for r in runs:  # identical frames among cases sharing camera and TF
-        key = (r["opt"]["cam"], r["opt"]["tf"])
+    for r in runs:  # identical frames among cases sharing camera, TF, sampler and accel
+        key = (r["opt"]["cam"], r["opt"]["tf"], r["opt"]["mode"], r["opt"]["accel"])
         if key not in ref:
             ref[key] = r["out"]
         r["identical"] = bool(np.array_equal(r["out"][0], ref[key][0]) and
