@@ -210,6 +210,12 @@ def main():
                          "split over the N ranks (strong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--sampler", default="user", choices=["user", "tri", "cubql"],
+                    help="Volume::mode (Params.h:29-31): sample() on the cells (default), "
+                         "TRIANGLE_MODE, CUBQL_MODE wedges")
+    ap.add_argument("--accel", default="sphere", choices=["sphere", "grid"],
+                    help="Volume::accelMode (Params.h:33-34): the spherical shell (sdda, "
+                         "default) or the 256^3 grid (dda3)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path with host-staged collectives "
                          "(ranks may share a GPU); nccl (RCCL) is the measured path")
@@ -244,6 +250,10 @@ def main():
         f"peak host RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.2f} GiB)")
 
     lp = setup.lp
+    lp.mode = {"user": irt.MODE_USER_GEOM, "tri": irt.MODE_TRIANGLES, "cubql": irt.MODE_CUBQL}[args.sampler]
+    lp.accelMode = irt.ACCEL_GRID if args.accel == "grid" else 0
+    if args.sampler != "user":  # buildTriangleAccel / buildCuBQLAccel (hostCode.cu:440-649)
+        ctx.build_wedge_accel(irt.synth_grid(rn, bis, L))
     orbit = None
     if orbit_cfg:  # one orbit frame per step (a new view: accumID 0)
         orbit = [irt.camera_look_at(*orbit_camera(k), W, H) for k in range(ORBIT_FRAMES)]
@@ -370,9 +380,14 @@ def main():
                                     if orbit is not None else
                                     ", framing camera --camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60, "
                                     "one frame per step") +
-                           ", woodcockTrackingWithAccel, " + ("sparse comb TF" if tf == "comb" else "default TF"),
+                           ", woodcockTrackingWithAccel, " + ("sparse comb TF" if tf == "comb" else "default TF") +
+                           ("" if args.sampler == "user" else
+                            {"tri": ", TRIANGLE_MODE sampler", "cubql": ", CUBQL_MODE wedge sampler"}[args.sampler]) +
+                           (", GRID_ACCEL_MODE (dda3 over the 256^3 grid)" if args.accel == "grid" else ""),
                 "records": int(info.numCells), "width": W, "height": H,
                 "transfer_function": tf,
+                "sampler": args.sampler,
+                "accel": args.accel,
                 "parallelism": parallelism,
                 "frames_per_step": frames,
                 "ms_per_frame": round(elapsed / (args.steps * frames) * 1e3, 4),

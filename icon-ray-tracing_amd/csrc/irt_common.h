@@ -436,6 +436,8 @@ IRT_HD float select8(int m, float a0, float a1, float a2, float a3, float b0, fl
 // GRID_ACCEL_MODE (Params.h:34): the 256^3 Cartesian macrocell grid over the volume
 // bounds (hostCode.cu:668-682) and its traversal dda3 (DDA.h:35-136).
 constexpr int kGridDim = 256;  // Grid{nullptr, vec3i(256), volbounds} (hostCode.cu:670)
+constexpr int kGridBlock = 8;  // GRID_ACCEL_MODE empty-space blocks: 32^3 of 8^3 cells, 4 KB of bits
+constexpr int kGridBitWords = (kGridDim / kGridBlock) * (kGridDim / kGridBlock) * (kGridDim / kGridBlock) / 32;
 
 // projectOnGrid (DDA.h:23-31), one axis: clamp(int((V-lo)/(hi-lo)*dims), 0, dims-1)
 IRT_HD int project_on_grid(float v, float lo, float hi, int dim) {

@@ -64,6 +64,7 @@ struct irt_context {
   float *d_maxOp = nullptr;
   float *d_gridVR = nullptr;     // GRID_ACCEL_MODE: Grid::valueRanges, kGridDim^3 box1f
   float *d_gridMaxOp = nullptr;  // Grid::maxOpacities
+  uint32_t *d_gridBits = nullptr;  // its empty-space bitmap (k_grid_bits)
   // CUBQL_MODE wedge locator (irt_build_wedge_accel; irt_internal.h WedgeScene)
   int wG = 0;
   uint32_t *d_wOff = nullptr, *d_wRec = nullptr;
@@ -160,7 +161,7 @@ void free_all(irt_context *c) {
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
-                  c->d_sphBits, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
+                  c->d_sphBits, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_gridBits, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
                   c->d_lut, c->d_counters};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -364,6 +365,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.maxOp = c->d_maxOp;
   A.accelMode = lp->accelMode;
   A.gridMaxOp = c->d_gridMaxOp;
+  A.gridBits = c->d_gridBits;
   A.sampler = lp->mode;
   A.wG = c->wG;
   A.wOff = c->d_wOff;
@@ -735,6 +737,8 @@ int irt_create_end(irt_context *c) {
   const size_t gridMCs = (size_t)kGridDim * kGridDim * kGridDim;
   if ((rc = dalloc(c, &c->d_gridVR, 2 * gridMCs))) return rc;
   if ((rc = dalloc(c, &c->d_gridMaxOp, gridMCs))) return rc;
+  if ((rc = dalloc(c, &c->d_gridBits, (size_t)kGridBitWords))) return rc;
+  IRT_HIP(hipMemsetAsync(c->d_gridBits, 0, kGridBitWords * sizeof(uint32_t), c->stream));
   launch_shell_init(c->d_gridVR, gridMCs, c->stream);  // initGrid(Grid) (hostCode.cu:205-214)
   IRT_HIP(hipMemsetAsync(c->d_gridMaxOp, 0, gridMCs * sizeof(float), c->stream));
   if (numCells) {
@@ -930,6 +934,7 @@ int irt_set_transfunc(irt_context *c, const irt_vec4f *lut, int size, irt_box1f 
                        valueRange.upper, c->d_maxOp, c->stream);
   launch_max_opacities(c->d_gridVR, (size_t)kGridDim * kGridDim * kGridDim, c->d_lut, size,
                        valueRange.lower, valueRange.upper, c->d_gridMaxOp, c->stream);
+  launch_grid_bits(c->d_gridMaxOp, c->d_gridBits, c->stream);
   IRT_HIP(hipGetLastError());
   IRT_HIP(hipStreamSynchronize(c->stream));
   c->tfSet = true;

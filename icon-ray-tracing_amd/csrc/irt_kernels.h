@@ -25,6 +25,7 @@ struct RenderArgs {
   const float *maxOp;    // ShellAccel::maxOpacities
   int accelMode;         // Volume::accelMode (Params.h:33-34): 0 sphere (sdda), 1 grid (dda3)
   const float *gridMaxOp;  // Grid::maxOpacities, kGridDim^3 over bmin..bmax (Params.h:44-49)
+  const uint32_t *gridBits;  // per kGridBlock^3 block: any majorant not <= 0 (k_grid_bits)
   int sampler;           // Volume::mode (Params.h:60): 0 cell sample() scan, 2 CUBQL wedges
   int wG;                // CUBQL_MODE wedge locator (host/irt_scene.cpp build_wedges)
   const uint32_t *wOff, *wRec;
@@ -86,6 +87,7 @@ void launch_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, float3 
                         float *valueRanges, hipStream_t s);
 void launch_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n, float3 lo,
                        float3 hi, float *valueRanges, hipStream_t s);
+void launch_grid_bits(const float *maxOp, uint32_t *bits, hipStream_t s);
 void launch_max_opacities(const float *valueRanges, size_t numMCs, const float4 *lut, int size,
                           float lo, float hi, float *maxOp, hipStream_t s);
 void launch_clear(uint32_t *fb, float4 *accum, size_t n, hipStream_t s);

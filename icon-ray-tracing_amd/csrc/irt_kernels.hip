@@ -285,6 +285,34 @@ void launch_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n,
   (void)hipFreeAsync(big, s);
   (void)hipFreeAsync(numBig, s);
 }
+// GRID_ACCEL_MODE's empty-space bitmap: bit b = block b (kGridBlock^3 cells of the kGridDim^3
+// grid, x fastest) holds a cell whose majorant is not <= 0.  woodcockTracking returns at once
+// on a majorant <= 0 (deviceCode.cu:161-162: no draw, no sample, tw = t0 fails the hit test),
+// so render_grid may step through a block whose bit is clear without reading its majorants.
+__global__ void k_grid_bits(const float *maxOp, uint32_t *bits) {
+  const int b = (int)(blockIdx.x * 256 + threadIdx.x);
+  constexpr int NB = kGridDim / kGridBlock;
+  if (b >= NB * NB * NB) return;
+  const int bx = b % NB, by = (b / NB) % NB, bz = b / (NB * NB);
+  bool any = false;
+  for (int z = 0; z < kGridBlock && !any; ++z)
+    for (int y = 0; y < kGridBlock && !any; ++y)
+      for (int x = 0; x < kGridBlock && !any; ++x) {
+        const size_t i = ((size_t)(bz * kGridBlock + z) * kGridDim + (size_t)(by * kGridBlock + y)) * kGridDim +
+                         (size_t)(bx * kGridBlock + x);
+        any = !(maxOp[i] <= 0.f);
+      }
+  const unsigned long long m = __ballot(any);  // 64 blocks per wave -> two words
+  const int lane = (int)(threadIdx.x & 63);
+  if (lane == 0) bits[b / 32] = (uint32_t)m;
+  if (lane == 32) bits[b / 32] = (uint32_t)(m >> 32);
+}
+
+void launch_grid_bits(const float *maxOp, uint32_t *bits, hipStream_t s) {
+  constexpr int NB = kGridDim / kGridBlock;
+  hipLaunchKernelGGL(k_grid_bits, dim3((NB * NB * NB + 255) / 256), dim3(256), 0, s, maxOp, bits);
+}
+
 void launch_max_opacities(const float *vr, size_t numMCs, const float4 *lut, int size, float lo,
                           float hi, float *maxOp, hipStream_t s) {
   hipLaunchKernelGGL(k_max_opacities, dim3((unsigned)((numMCs + 255) / 256)), dim3(256), 0, s,

@@ -106,6 +106,7 @@ struct Tracer {
   uint32_t *s_cnt;  // [0] launched [1] inBox [2] locate [3] found [4] candidates
   Counts cnt;       // per-lane statistics (OPT_STATS)
   uint32_t specCand = 0;  // candidate tests of this lane's sample in a cooperative round
+  const uint32_t *s_gbits = nullptr;  // OPT_GRID: the grid's empty-space bitmap in LDS
   // the cooperative loop's statistics, per lane (samples taken, their locates / found /
   // candidate tests), added into s_cnt at the end by flush_coop
   uint32_t nLocate = 0, nFound = 0, nCand = 0;
@@ -129,6 +130,9 @@ struct Tracer {
   // the cooperative Woodcock loop (woodcock_wave) runs in every sphere-accel kernel (any
   // sampler) but the OPT_SERIAL comparison one; the grid accel walks dda3 one lane per ray
   static constexpr bool kCoop = (OPT & (OPT_GRID | OPT_SERIAL)) == 0;
+  // the miss mode of woodcock_wave: only where misses come in runs (the unstructured
+  // samplers, the grid accel); user-geometry samples almost always land in a cell
+  static constexpr bool kMiss = (OPT & (OPT_WEDGE | OPT_GRID)) != 0;
 
   // one wave-aggregated LDS add per event site
   __device__ __forceinline__ void count(int k) {
@@ -444,12 +448,16 @@ struct Tracer {
   // gathers in parallel instead of a chain -- and the ray's first event among its G samples
   // (past tmax / not located / accepted) decides it exactly as the serial loop would; the
   // samples after the event are discarded.  A not-located sample consumes only its step
-  // draw, so the ray resumes from there next round.  Statistics count only the samples
+  // draw, so the ray resumes from there next round -- in miss mode: its samples are then
+  // placed as if none were located (sample k from the state k+1 draws ahead) until one is,
+  // which switches back (samples outside every cell come in runs: grid-accel cells and
+  // wedge gaps).  Statistics count only the samples
   // the reference takes.  Returns in t the woodcockTracking return value.
   __device__ __forceinline__ void woodcock_wave(bool req, float dx, float dy, float dz, float &t,
                                                 float tmax, uint32_t &st, float majorant,
-                                                bool counted, float4 &sampleOut, CoopWave &W,
-                                                const uint32_t *jmul, const uint32_t *jadd) {
+                                                bool counted, float4 &sampleOut, bool &miss,
+                                                CoopWave &W, const uint32_t *jmul,
+                                                const uint32_t *jadd) {
     const int lane = (int)__lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
     const float q = majorant / A.unitDistance;
@@ -465,20 +473,21 @@ struct Tracer {
       const bool solo = lg == 0;
       const int rank = __popcll(am & below);
       int grp, k;
-      bool used, cntd;
+      bool used, cntd, mm;
       float4 rq, ry;
       if (solo) {
         grp = lane;
         k = 0;
         used = active;
         cntd = counted;
+        mm = kMiss && miss;
         rq = make_float4(t, tmax, q, majorant);
         ry = make_float4(dx, dy, dz, __uint_as_float(st));
       } else {
         if (active) {
           W.req[rank] = make_float4(t, tmax, q, majorant);
           W.ray[rank] = make_float4(dx, dy, dz, __uint_as_float(st));
-          W.cnt[rank] = counted ? 1u : 0u;
+          W.cnt[rank] = (counted ? 1u : 0u) | (miss ? 2u : 0u);
         }
         __builtin_amdgcn_wave_barrier();
         grp = lane >> lg;
@@ -487,10 +496,15 @@ struct Tracer {
         const int g = used ? grp : 0;
         rq = W.req[g];
         ry = W.ray[g];
-        cntd = W.cnt[g] != 0u;
+        const uint32_t cf = W.cnt[g];
+        cntd = cf & 1u;
+        mm = kMiss && (cf & 2u);
       }
       const uint32_t s0 = __float_as_uint(ry.w);
-      const uint32_t sk = solo ? lcg_next(s0) : jmul[2 * k + 1] * s0 + jadd[2 * k + 1];
+      // sample k's step draw: 2k+1 draws ahead if every earlier sample is located (and
+      // rejected), k+1 if none is (miss mode)
+      const int jk = mm ? k + 1 : 2 * k + 1;
+      const uint32_t sk = solo ? lcg_next(s0) : jmul[jk] * s0 + jadd[jk];
       const float dk = woodcock_log(sk, s_logf) / rq.z;
       float tk;
       if (solo) {
@@ -518,7 +532,8 @@ struct Tracer {
           acc = sw >= lcg_float(lcg_next(sk)) * rq.w;
         }
       }
-      const bool ev = used && (past || !found || acc);
+      // the first sample that breaks the round's assumption, or ends the ray's leaf
+      const bool ev = used && (past || acc || (mm ? found : !found));
       // the lane's group: its first event, G if none; the samples up to it are taken
       int first;
       uint64_t em = 0ull;
@@ -540,15 +555,16 @@ struct Tracer {
       // the rays' owners take their group's outcome
       int of;
       float tsrc, vsrc;
-      bool pastS, accS;
+      bool pastS, accS, foundS;
       if (solo) {
         of = first;
         tsrc = tk;
         vsrc = value;
         pastS = past;
         accS = acc;
+        foundS = found;
       } else {
-        const uint64_t pastM = __ballot(past), accM = __ballot(acc);
+        const uint64_t pastM = __ballot(past), accM = __ballot(acc), foundM = kMiss ? __ballot(found) : 0ull;
         const int ob = active ? rank << lg : 0;  // < 64 for an owner
         const uint64_t om = lg == 6 ? ~0ull : (((1ull << G) - 1ull) << ob);
         of = (active && (em & om)) ? (int)__builtin_ctzll(em & om) - ob : G;
@@ -557,11 +573,14 @@ struct Tracer {
         vsrc = __shfl(value, src, 64);
         pastS = (pastM >> src) & 1ull;
         accS = (accM >> src) & 1ull;
+        foundS = (foundM >> src) & 1ull;
       }
       if (active) {
         if constexpr ((OPT & OPT_STATS) != 0) cnt.steps += of < G ? (uint32_t)of + 1u : (uint32_t)G;
         t = tsrc;
-        const int n = of == G ? 2 * G : (accS ? 2 * of + 2 : 2 * of + 1);
+        // draws taken: two per located sample, one per miss (and the one past tmax)
+        const int n = (kMiss && miss) ? (of == G ? G : (foundS ? of + 2 : of + 1))
+                           : (of == G ? 2 * G : (accS ? 2 * of + 2 : 2 * of + 1));
         if (solo)
           st = n == 1 ? sk : lcg_next(sk);  // the draws this round made
         else
@@ -569,6 +588,8 @@ struct Tracer {
         if (of < G && (pastS || accS)) {
           active = false;
           if (accS) sampleOut = post_classify(vsrc);
+        } else if (kMiss && of < G) {
+          miss = !miss;  // the assumption broke: a miss, or (miss mode) a located sample
         }
       }
     }
@@ -697,15 +718,24 @@ __device__ __forceinline__ void render_grid(const RenderArgs &A, Tracer<OPT> &T,
     const float tmn = fminf(fminf(tnx, tny), tnz);  // reduce_min (vecmath.h:512-514)
     const float tc1 = dda3_min_quirk(tmn, tmax);
     const float w0 = rtmin + tc0, w1 = rtmin + tc1;  // func(leaf, ray_tmin+t0, ray_tmin+t1)
-    const float maj = A.gridMaxOp[(size_t)cz * D * D + (size_t)cy * D + cx];
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float tw = T.woodcock(ray.dx, ray.dy, ray.dz, w0, w1, st, maj, s, !(w0 == w1));
-    if (tw > w0 && tw < w1) {
-      cr = s.x * A.amb.x * A.ambRad;
-      cg = s.y * A.amb.y * A.ambRad;
-      cb = s.z * A.amb.z * A.ambRad;
-      alpha = s.w > 0.f ? 1.f : 0.f;
-      return;
+    // every majorant of this cell's block <= 0 (k_grid_bits): woodcockTracking would return
+    // at once (deviceCode.cu:161-162) -- no draw, no sample, no hit -- so only the walk goes on
+    constexpr int NB = kGridDim / kGridBlock;
+    const bool inGrid = (unsigned)cx < (unsigned)D && (unsigned)cy < (unsigned)D && (unsigned)cz < (unsigned)D;
+    const uint32_t gb = inGrid ? ((uint32_t)(cz / kGridBlock) * NB + (uint32_t)(cy / kGridBlock)) * NB +
+                                     (uint32_t)(cx / kGridBlock)
+                               : 0u;
+    if (!inGrid || ((T.s_gbits[gb >> 5] >> (gb & 31)) & 1u)) {
+      const float maj = A.gridMaxOp[(size_t)cz * D * D + (size_t)cy * D + cx];
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float tw = T.woodcock(ray.dx, ray.dy, ray.dz, w0, w1, st, maj, s, !(w0 == w1));
+      if (tw > w0 && tw < w1) {
+        cr = s.x * A.amb.x * A.ambRad;
+        cg = s.y * A.amb.y * A.ambRad;
+        cb = s.z * A.amb.z * A.ambRad;
+        alpha = s.w > 0.f ? 1.f : 0.f;
+        return;
+      }
     }
     if (tnx == tmn) {
       tnx += dx;
@@ -944,6 +974,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   int i = 0, iter = 0, cx = 0, cy = 0, cz = 0;
   float t = 0.f, upper = 0.f, tt1 = 0.f, maj = 0.f;
   bool lastRange = true, zeroLen = false, hit = false;
+  bool miss = false;  // the cooperative loop's speculation mode, carried from leaf to leaf
   // after a leaf without a hit: the next leaf of the range, or the next range
   // (render_pixel's loop tail, ShellAccel.h:201-226)
   auto next_leaf = [&]() {
@@ -1064,7 +1095,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     if (__ballot(req) == 0ull) break;
     float tw = t;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    T.woodcock_wave(req, dx, dy, dz, tw, tt1, st, maj, !zeroLen, s, W, jmul, jadd);
+    T.woodcock_wave(req, dx, dy, dz, tw, tt1, st, maj, !zeroLen, s, miss, W, jmul, jadd);
     if (req) {
       if (!zeroLen && (ae || (tw > t && tw < tt1))) {
         // the colour waits in the lane's s_entry slot (free once it is finished)
@@ -1123,8 +1154,14 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
     for (int k = 0; k < kSphBitWords / 256; ++k) s_sph[tid + 256 * k] = sph[k];
   }
   if (tid < kCnt) s_cnt[tid] = 0;
+  __shared__ uint32_t s_gbits[(OPT & OPT_GRID) ? kGridBitWords : 1];
+  if constexpr ((OPT & OPT_GRID) != 0) {
+#pragma unroll
+    for (int k = 0; k < kGridBitWords / 256; ++k) s_gbits[tid + 256 * k] = A.gridBits[tid + 256 * k];
+  }
   __syncthreads();
   Tracer<OPT> T{A, s_logf, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
+  T.s_gbits = s_gbits;
   const uint64_t c0 = A.schedCost ? wall_clock64() : 0;
   // grid.y = frame k of a progressive batch (accumID + k), whose colour goes to the sample
   // buffer for k_accumulate; a single frame writes accum/fb directly.  With measured-cost
@@ -1258,18 +1295,15 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
   constexpr int K = N & ~OPT_MONO;
   // the grid accel or the unstructured samplers: their own instantiations of the raygen
   // (kept out of the default kernel, whose registers they would cost); the wedge kernels
-  // hold a 6-vertex Newton state: no waves-per-SIMD floor.  TRIANGLES runs the cooperative
-  // Woodcock loop (3.4x faster at C2); CUBQL keeps one lane per ray: its Newton solve's
-  // per-lane iteration counts and frequent misses make speculative samples cost more than
-  // they save (1.26x slower measured, profiles/r02b_investigation/).
+  // hold a 6-vertex Newton state: no waves-per-SIMD floor.  Both run the cooperative
+  // Woodcock loop with its miss mode (C2: TRIANGLES 3.4x, CUBQL 2.5x faster than one lane per
+  // ray; profiles/r02b_investigation/).
   constexpr int D = kDefaultVariant & ~OPT_MONO;
   constexpr int DW = (D & ~0xF00) | OPT_WEDGE | (K & OPT_SERIAL);
   const dim3 grid(numBlocks, A.numSamples);
   const bool g = A.accelMode == IRT_ACCEL_GRID;
   if (A.sampler != IRT_MODE_USER_GEOM && g)  // CUBQL or TRIANGLES: the unstructured locator
     hipLaunchKernelGGL(k_render<DW | OPT_GRID>, grid, dim3(256), 0, s, A);
-  else if (A.sampler == IRT_MODE_CUBQL)
-    hipLaunchKernelGGL(k_render<DW | OPT_SERIAL>, grid, dim3(256), 0, s, A);
   else if (A.sampler != IRT_MODE_USER_GEOM)
     hipLaunchKernelGGL(k_render<DW>, grid, dim3(256), 0, s, A);
   else if (g)
