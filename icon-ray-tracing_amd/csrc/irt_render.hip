@@ -127,9 +127,9 @@ struct Tracer {
     }
   }
 
-  // the cooperative Woodcock loop (woodcock_wave) runs in every sphere-accel kernel (any
-  // sampler) but the OPT_SERIAL comparison one; the grid accel walks dda3 one lane per ray
-  static constexpr bool kCoop = (OPT & (OPT_GRID | OPT_SERIAL)) == 0;
+  // the cooperative Woodcock loop (woodcock_wave) runs in every kernel (any sampler, either
+  // accelerator) but the OPT_SERIAL comparison one
+  static constexpr bool kCoop = (OPT & OPT_SERIAL) == 0;
   // the miss mode of woodcock_wave: only where misses come in runs (the unstructured
   // samplers, the grid accel); user-geometry samples almost always land in a cell
   static constexpr bool kMiss = (OPT & (OPT_WEDGE | OPT_GRID)) != 0;
@@ -925,13 +925,15 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
                                                   float4 *s_acc, CoopWave &W, const uint32_t *jmul,
                                                   const uint32_t *jadd, int tid, int accumID,
                                                   float4 *sampleOut) {
-  enum : int { kRange, kLeaf, kWait, kDone };
+  enum : int { kRange, kLeaf, kWait, kDone, kGrid, kGridNext };
+  constexpr bool grid = (OPT & OPT_GRID) != 0;
   const bool ae = A.raygen == 1;
   uint32_t st = 0;
   float dx = 1.f, dy = 1.f, dz = 1.f;
   float rlo0 = 0.f, rhi0 = 0.f, rlo1 = __builtin_inff(), rhi1 = -__builtin_inff();
   int numRanges = 0, phase = kDone;
   bool inBox = false;
+  float t0box = 0.f, t1box = 0.f;
   if (px.active) {
     gen_ray(A, accumID, px.x, px.y, st, dx, dy, dz);
     const Ray ray = {A.org.x, A.org.y, A.org.z, 0.f, dx, dy, dz, 1e10f};
@@ -940,6 +942,8 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       inBox = true;
       T.count(1);
       phase = kRange;
+      t0box = t0;
+      t1box = t1;
       // the accum pixel the lerp reads at the end, fetched now straight into LDS (no VGPRs
       // held through the Woodcock rounds; its latency hides behind them)
       if (!sampleOut)
@@ -968,6 +972,39 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       }
     } else if (sampleOut) {
       *sampleOut = make_float4(0.f, 0.f, 0.f, kNoSample);  // deviceCode.cu:294-295
+    }
+  }
+  // GRID_ACCEL_MODE (deviceCode.cu:326-328): dda3 (DDA.h:35-136) over the 256^3 grid as
+  // render_grid walks it, each cell's woodcockFunc one of the wave's cooperative requests
+  int gcx = 0, gcy = 0, gcz = 0, gsteps = 0, gdirs = 0;
+  float gtnx = 0.f, gtny = 0.f, gtnz = 0.f, gdx = 0.f, gdy = 0.f, gdz = 0.f, gtmax = 0.f, grtmin = 0.f,
+        gtc0 = 0.f, gtc1 = 0.f;
+  if constexpr (grid) {
+    if (phase == kRange && !ae) {
+      const float rtmin = t0box, rtmax = t1box;  // the box interval [t0, t1]
+      const int D = kGridDim;
+      const float ox = A.org.x + rtmin * dx, oy = A.org.y + rtmin * dy, oz = A.org.z + rtmin * dz;
+      gtmax = rtmax - rtmin;
+      grtmin = rtmin;
+      const float rx = 1.f / dx, ry = 1.f / dy, rz = 1.f / dz;
+      const float lx = (A.bmin.x - ox) * rx, ly = (A.bmin.y - oy) * ry, lz = (A.bmin.z - oz) * rz;
+      const float hx = (A.bmax.x - ox) * rx, hy = (A.bmax.y - oy) * ry, hz = (A.bmax.z - oz) * rz;
+      float nx = fminf(lx, hx), ny = fminf(ly, hy), nz = fminf(lz, hz);
+      const float fx = fmaxf(lx, hx), fy = fmaxf(ly, hy), fz = fmaxf(lz, hz);
+      if (dx == 0.f) nx = IRT_FLT_MAX;
+      if (dy == 0.f) ny = IRT_FLT_MAX;
+      if (dz == 0.f) nz = IRT_FLT_MAX;
+      gcx = project_on_grid(ox, A.bmin.x, A.bmax.x, D);
+      gcy = project_on_grid(oy, A.bmin.y, A.bmax.y, D);
+      gcz = project_on_grid(oz, A.bmin.z, A.bmax.z, D);
+      gdx = fmaxf(0.f, (fx - nx) / (float)D);
+      gdy = fmaxf(0.f, (fy - ny) / (float)D);
+      gdz = fmaxf(0.f, (fz - nz) / (float)D);
+      gdirs = (dx > 0.f ? 1 : 0) | (dy > 0.f ? 2 : 0) | (dz > 0.f ? 4 : 0);
+      gtnx = dx > 0.f ? nx + (float)(gcx + 1) * gdx : nx + (float)(D - gcx) * gdx;
+      gtny = dy > 0.f ? ny + (float)(gcy + 1) * gdy : ny + (float)(D - gcy) * gdy;
+      gtnz = dz > 0.f ? nz + (float)(gcz + 1) * gdz : nz + (float)(D - gcz) * gdz;
+      phase = kGrid;
     }
   }
   const float sceneEPS = A.sbLo.x * 1e-6f;
@@ -1023,6 +1060,57 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     }
   };
   while (true) {
+    if constexpr (grid) {
+      // this lane's dda3 cells, on its own: up to the next one whose woodcockFunc can act
+      const int D = kGridDim;
+      constexpr int NB = kGridDim / kGridBlock;
+      while (phase == kGrid || phase == kGridNext) {
+        if (phase == kGridNext) {  // the step to the next cell (render_grid)
+          const float tmn = fminf(fminf(gtnx, gtny), gtnz);
+          bool out = false;
+          if (gtnx == tmn) {
+            gtnx += gdx;
+            gcx += (gdirs & 1) ? 1 : -1;
+            out = gcx == ((gdirs & 1) ? D : -1);
+          }
+          if (!out && gtny == tmn) {
+            gtny += gdy;
+            gcy += (gdirs & 2) ? 1 : -1;
+            out = gcy == ((gdirs & 2) ? D : -1);
+          }
+          if (!out && gtnz == tmn) {
+            gtnz += gdz;
+            gcz += (gdirs & 4) ? 1 : -1;
+            out = gcz == ((gdirs & 4) ? D : -1);
+          }
+          gtc0 = gtc1;
+          if (out || ++gsteps >= 4 * D + 16) {
+            phase = kDone;
+            break;
+          }
+          phase = kGrid;
+        }
+        const float tmn = fminf(fminf(gtnx, gtny), gtnz);  // reduce_min (vecmath.h:512-514)
+        gtc1 = dda3_min_quirk(tmn, gtmax);
+        // a cell whose block holds no majorant above 0 (k_grid_bits), or whose own majorant
+        // is <= 0: woodcockTracking returns at once (deviceCode.cu:161-162), nothing to do
+        const bool inGrid = (unsigned)gcx < (unsigned)D && (unsigned)gcy < (unsigned)D && (unsigned)gcz < (unsigned)D;
+        const uint32_t gb = inGrid ? ((uint32_t)(gcz / kGridBlock) * NB + (uint32_t)(gcy / kGridBlock)) * NB +
+                                         (uint32_t)(gcx / kGridBlock)
+                                   : 0u;
+        if (!inGrid || ((T.s_gbits[gb >> 5] >> (gb & 31)) & 1u)) {
+          maj = A.gridMaxOp[(size_t)gcz * D * D + (size_t)gcy * D + gcx];
+          if (!(maj <= 0.f)) {
+            t = grtmin + gtc0;  // woodcockFunc(leaf, ray_tmin + t0, ray_tmin + t1)
+            tt1 = grtmin + gtc1;
+            zeroLen = t == tt1;  // counted = !(w0 == w1)
+            phase = kWait;
+            break;
+          }
+        }
+        phase = kGridNext;
+      }
+    }
     // this lane, on its own: up to its next woodcockFunc, or to the end
     while (phase == kRange || phase == kLeaf) {
       if (phase == kRange) {
@@ -1096,7 +1184,16 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     float tw = t;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     T.woodcock_wave(req, dx, dy, dz, tw, tt1, st, maj, !zeroLen, s, miss, W, jmul, jadd);
-    if (req) {
+    if (grid && req && phase == kWait && !ae) {
+      if (tw > t && tw < tt1) {  // render_grid's hit test (deviceCode.cu:316)
+        s_entry[tid] = make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
+                                   s.z * A.amb.z * A.ambRad, s.w > 0.f ? 1.f : 0.f);
+        hit = true;
+        phase = kDone;
+      } else {
+        phase = kGridNext;
+      }
+    } else if (req) {
       if (!zeroLen && (ae || (tw > t && tw < tt1))) {
         // the colour waits in the lane's s_entry slot (free once it is finished)
         s_entry[tid] = make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
@@ -1307,7 +1404,7 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
   else if (A.sampler != IRT_MODE_USER_GEOM)
     hipLaunchKernelGGL(k_render<DW>, grid, dim3(256), 0, s, A);
   else if (g)
-    hipLaunchKernelGGL(k_render<D | OPT_GRID>, grid, dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_render<D | OPT_GRID | (K & OPT_SERIAL)>, grid, dim3(256), 0, s, A);
   else
     hipLaunchKernelGGL(k_render<K>, grid, dim3(256), 0, s, A);
   // progressive batch: the lerp chain over the frames' samples
