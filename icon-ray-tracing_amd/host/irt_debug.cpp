@@ -20,6 +20,7 @@ extern "C" {
 float irt_debug_asinf(float x) { return glibc_asinf(x); }
 float irt_debug_atan2f(float y, float x) { return glibc_atan2f(y, x); }
 int irt_debug_f2i(float x) { return f2i_x86(x); }
+void irt_debug_lcg_jump(uint32_t n, uint32_t *mul, uint32_t *add) { lcg_jump(n, *mul, *add); }
 
 float irt_debug_logf_entry(uint32_t k) { return logf_table()[k & 0x00FFFFFFu]; }
 

@@ -18,6 +18,9 @@ float irt_debug_asinf(float x);
 float irt_debug_atan2f(float y, float x);
 /* x86 cvttss2si float->int semantics used by the kernels. */
 int irt_debug_f2i(float x);
+/* n LCG steps as one affine map, state_n = mul * state + add (mod 2^32), n < 256: the jump
+ * table of the cooperative Woodcock loop (irt_common.h lcg_jump). */
+void irt_debug_lcg_jump(uint32_t n, uint32_t *mul, uint32_t *add);
 
 /* Host-built tables uploaded to HBM: logf(1 - k/2^24) and the sRGB byte thresholds. */
 float irt_debug_logf_entry(uint32_t k);

@@ -398,3 +398,22 @@ def test_triangle_locator_matches_oracle_and_cell_sampler():
                 same_as_cells += 1
         assert same_as_cells >= 0.8 * 300, same_as_cells  # chord vs sphere bands differ
         L.irt_debug_scene_free(h)
+
+
+def test_lcg_jump_equals_sequential_steps():
+    """The cooperative Woodcock loop places sample k with the LCG state 2k+1 (or k+1) draws
+    ahead through one affine map (irt_common.h lcg_jump); that map must be the n-fold LCG
+    step (dvr_course-common-both.h:41-86) for every n the kernel tabulates, on any state."""
+    L = irt.lib()
+    L.irt_debug_lcg_jump.argtypes = [C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    L.irt_debug_lcg_jump.restype = None
+    rng = np.random.default_rng(3)
+    states = [int(v) for v in rng.integers(0, 2**32, 16)] + [0, 1, 2**32 - 1]
+    for n in range(256):
+        m, a = C.c_uint32(), C.c_uint32()
+        L.irt_debug_lcg_jump(n, C.byref(m), C.byref(a))
+        for s0 in states:
+            s = s0
+            for _ in range(n):
+                s = (1664525 * s + 1013904223) & 0xFFFFFFFF
+            assert (m.value * s0 + a.value) & 0xFFFFFFFF == s, (n, s0)
