@@ -216,6 +216,9 @@ def main():
     ap.add_argument("--accel", default="sphere", choices=["sphere", "grid"],
                     help="Volume::accelMode (Params.h:33-34): the spherical shell (sdda, "
                          "default) or the 256^3 grid (dda3)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="(overhead check) run the multi-rank path -- tile render, RCCL gather, "
+                         "unpack -- even with one rank (under torchrun)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path with host-staged collectives "
                          "(ranks may share a GPU); nccl (RCCL) is the measured path")
@@ -227,8 +230,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = local % max(torch.cuda.device_count(), 1) if world > 1 else 0
-    if world > 1:
+    dist_path = world > 1 or args.force_dist
+    device = local % max(torch.cuda.device_count(), 1) if dist_path else 0
+    json_out = sys.stdout
+    if dist_path:
+        # RCCL (and the runtime under it) may print banners on fd 1: send everything
+        # native to stderr and keep stdout for the one JSON line
+        json_out = os.fdopen(os.dup(1), "w")
+        sys.stdout.flush()
+        os.dup2(2, 1)
         import torch.distributed as dist
         torch.cuda.set_device(device)
         if args.dist_backend == "nccl":
@@ -258,11 +268,17 @@ def main():
     if orbit_cfg:  # one orbit frame per step (a new view: accumID 0)
         orbit = [irt.camera_look_at(*orbit_camera(k), W, H) for k in range(ORBIT_FRAMES)]
     ntiles = irt.num_tiles(W, H)
+    if dist_path:
+        # render on a high-priority stream: its hardware queue comes from another pool than
+        # RCCL's normal-priority stream.  Sharing one queue (measured: torch's default stream
+        # and the gather's stream on the same queue) puts step s's gather in front of step
+        # s+1's unpack and render, ~20 us of barrier latency per step.
+        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=-1))
     stream = torch.cuda.current_stream(device).cuda_stream
     # frames per step: 1 on one GPU or in frame mode; N in progressive mode on N GPUs
     strong = args.mode == "frame"
     frames = 1 if (world == 1 or strong) else world
-    if world == 1:
+    if not dist_path:
         fb = torch.zeros(W * H, dtype=torch.int32, device=dev)
         accum = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
         ctx.clear(fb.data_ptr(), accum.data_ptr(), W * H, stream)
@@ -282,7 +298,7 @@ def main():
             c = orbit[s % ORBIT_FRAMES]
             lp.org, lp.dir_00, lp.dir_du, lp.dir_dv = c.org, c.dir_00, c.dir_du, c.dir_dv
             lp.accumID = 0
-        if world == 1:
+        if not dist_path:
             ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
             return
         b = s % 2
@@ -307,31 +323,32 @@ def main():
 
     for f in range(args.warmup):
         step(f)
-    if world > 1:
+    if dist_path:
         drain()
     st = ctx.stats()
     log(f"[rank {rank}] warmup: last launch kernel {st.kernelMs:.3f} ms, {st.samplesFound} "
         f"samples, {st.candidatesTested} candidates")
     ctx.reset_stats_total()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_path:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k)
-    if world > 1:
+    host_loop = time.perf_counter() - t_start  # host side of the loop (launches only)
+    if dist_path:
         drain()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_path:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     tot, launches = ctx.stats_total()
-    log(f"[rank {rank}] timed {args.steps} steps ({launches} launches) in {elapsed:.3f} s; "
-        f"peak host RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.2f} GiB")
+    log(f"[rank {rank}] timed {args.steps} steps ({launches} launches) in {elapsed:.4f} s "
+        f"(host loop {host_loop:.4f} s); peak host RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.2f} GiB")
     samples, in_box = tot.samplesFound, tot.raysInBox
-    if world > 1:
+    if dist_path:
         rdev = dev if args.dist_backend == "nccl" else "cpu"
         t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -351,7 +368,7 @@ def main():
     achieved = bytes_per_launch / avg_kernel_s if avg_kernel_s > 0 else float("nan")
 
     if rank == 0:
-        if world == 1:
+        if world == 1 and not dist_path:
             parallelism = "single GPU"
         elif strong:
             parallelism = (f"{world} GPUs x 64x64 interleaved tiles of ONE frame per step, RCCL "
@@ -415,8 +432,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cam = orbit_camera(0) if orbit is not None else FRAMING
             out["cpu_baseline"] = cpu_baseline(rn, bis, L, W, H, cam, tf, args.cpu_budget)
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        print(json.dumps(out), file=json_out, flush=True)
+    if dist_path:
         dist.barrier()
         dist.destroy_process_group()
     ctx.close()

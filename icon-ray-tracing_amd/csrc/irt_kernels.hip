@@ -227,17 +227,29 @@ __global__ void k_clear(uint32_t *fb, float4 *accum, size_t n) {
 }
 
 // Scatter rank-major packed tiles into a linear framebuffer (multi-GPU gather epilogue).
+// Four workgroups per tile slot (16 rows each); a lane moves 4 pixels of a row with one
+// 16-byte load and store when the row is 16-byte aligned in the framebuffer (W % 4 == 0)
+// and the 4 pixels are inside the frame, pixel by pixel otherwise (ragged right/bottom edge).
 __global__ void k_unpack(const uint32_t *gathered, int numRanks, int maxTiles, int W, int H,
                          int tilesX, int numTilesTotal, uint32_t *fb) {
-  const int k = blockIdx.x;  // tile slot
+  const int k = blockIdx.x >> 2;  // tile slot
   const int rank = blockIdx.y;
   const int tileId = rank + k * numRanks;
   if (k >= maxTiles || tileId >= numTilesTotal) return;
   const int tx = tileId % tilesX, ty = tileId / tilesX;
-  const uint32_t *src = gathered + ((size_t)rank * maxTiles + k) * 4096;
-  for (int p = threadIdx.x; p < 4096; p += blockDim.x) {
-    const int x = tx * 64 + (p & 63), y = ty * 64 + (p >> 6);
-    if (x < W && y < H) fb[(size_t)x + (size_t)W * y] = src[p];
+  const int ly = (blockIdx.x & 3) * 16 + (threadIdx.x >> 4), lx = (threadIdx.x & 15) * 4;
+  const uint32_t *src = gathered + ((size_t)rank * maxTiles + k) * 4096 + ly * 64 + lx;
+  const int x = tx * 64 + lx, y = ty * 64 + ly;
+  if (y >= H || x >= W) return;
+  uint32_t *dst = fb + (size_t)x + (size_t)W * y;
+  const uint4 v = *reinterpret_cast<const uint4 *>(src);
+  if ((W & 3) == 0 && x + 4 <= W) {
+    *reinterpret_cast<uint4 *>(dst) = v;
+  } else {
+    dst[0] = v.x;
+    if (x + 1 < W) dst[1] = v.y;
+    if (x + 2 < W) dst[2] = v.z;
+    if (x + 3 < W) dst[3] = v.w;
   }
 }
 
@@ -340,7 +352,7 @@ void launch_clear(uint32_t *fb, float4 *accum, size_t n, hipStream_t s) {
 void launch_unpack(const uint32_t *g, int numRanks, int maxTiles, int W, int H, uint32_t *fb,
                    hipStream_t s) {
   const int tilesX = (W + 63) / 64, tilesY = (H + 63) / 64;
-  hipLaunchKernelGGL(k_unpack, dim3(maxTiles, numRanks), dim3(256), 0, s, g, numRanks, maxTiles,
+  hipLaunchKernelGGL(k_unpack, dim3(maxTiles * 4, numRanks), dim3(256), 0, s, g, numRanks, maxTiles,
                      W, H, tilesX, tilesX * tilesY, fb);
 }
 

@@ -160,6 +160,27 @@ def test_tiles_match_full_frame():
         assert np.array_equal(out.cpu().numpy(), full), f"{ranks} ranks"
 
 
+@pytest.mark.parametrize("W,H,ranks", [(203, 71, 3), (130, 64, 1), (64, 200, 5), (1024, 1024, 8)])
+def test_unpack_tiles_equals_host_twin(W, H, ranks):
+    """irt_unpack_tiles (16-byte rows where W % 4 == 0, pixel by pixel on ragged edges) equals
+    irt_dist.unpack_host on random packed tiles; pixels outside the frame are never written."""
+    import torch
+    import irt_dist
+    ctx = irt.Context(irt.synth_grid(2, 1, 4), 0)
+    split = irt_dist.TileSplit(W, H, 0, ranks)
+    rng = np.random.default_rng(W * 7 + H)
+    g = rng.integers(0, 2**32, ranks * split.max_tiles * 4096, dtype=np.uint32)
+    dev = "cuda:0"
+    gathered = torch.from_numpy(g.view(np.int32)).to(dev)
+    out = torch.full((W * H + 64,), -1, dtype=torch.int32, device=dev)  # guard words past the end
+    ctx.unpack_tiles(gathered.data_ptr(), ranks, split.max_tiles, W, H, out.data_ptr())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got[:W * H].reshape(H, W), irt_dist.unpack_host(g, split))
+    assert (got[W * H:] == 0xFFFFFFFF).all()
+    ctx.close()
+
+
 def test_lat_lon_filtered_and_truncated_scenes():
     """--lat-range/--lon-range filter and --num-cells truncation (hostCode.cu:728-758)."""
     cells = irt.synth_grid(2, 2, 20)
