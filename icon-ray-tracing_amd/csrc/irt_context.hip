@@ -112,6 +112,10 @@ struct irt_context {
   long long schedSwitch = 0;    // first launch reading it
   size_t schedCap = 0;
   bool schedOn = true;         // IRT_SCHED=0 disables
+  // cooperative Woodcock loop: a ray's lanes per round <= 2^(coopMaxLg + round) with the
+  // ramp, 2^coopMaxLg without (IRT_COOP_MAXLG, IRT_COOP_RAMP; profiles/r02e_dist/)
+  int coopMaxLg = 0;
+  int coopRamp = 1;
   int schedPolicy = 2;         // IRT_SCHED: 1 tiles, 2 bands of tiles (a tile row; default), 3 reversed
   bool schedOrderValid = false;
   bool schedLastApplied = false;   // the last launch ran in a measured-cost order
@@ -377,6 +381,8 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.opacityScale = c->opScale;
   A.lut = c->d_lut;
   A.lutSize = c->lutSize;
+  A.coopMaxLg = c->coopMaxLg;
+  A.coopRamp = c->coopRamp;
   A.numCells = c->n;
   A.G = c->G;
   A.srgbTh = c->d_srgb;
@@ -727,6 +733,8 @@ int irt_create_end(irt_context *c) {
   memset(c->h_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long));
   if (const char *e = getenv("IRT_COUNTERS")) c->wgCountsOn = strcmp(e, "atomic") != 0;
   if (const char *e = getenv("IRT_TIMING_EVERY")) c->timingEvery = std::max(1, atoi(e));
+  if (const char *e = getenv("IRT_COOP_MAXLG")) c->coopMaxLg = std::min(6, std::max(0, atoi(e)));
+  if (const char *e = getenv("IRT_COOP_RAMP")) c->coopRamp = atoi(e) != 0 ? 1 : 0;
   IRT_HIP(hipHostGetDevicePointer((void **)&c->dh_counters, c->h_counters, 0));
   IRT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long), c->stream));
 

@@ -70,6 +70,11 @@ struct RenderArgs {
   const uint32_t *schedOrder;
   uint32_t *schedCost;
   float4 *sampleBuf;
+  // cooperative Woodcock loop: at most 2^coopMaxLg lanes (samples) per ray in the first
+  // round of a woodcock_wave call, one power of two more per later round with coopRamp
+  // (any setting gives the same frame)
+  int coopMaxLg;
+  int coopRamp;
 };
 
 // Event counts kept per workgroup: [0] launched [1] inBox [2] locate [3] found [4] candidates

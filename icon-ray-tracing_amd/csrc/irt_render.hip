@@ -462,12 +462,17 @@ struct Tracer {
     const uint64_t below = (1ull << lane) - 1ull;
     const float q = majorant / A.unitDistance;
     bool active = req && !(majorant <= 0.f);  // majorant <= 0: return at once (161-162)
-    while (true) {
+    // speculation ramps up: a ray gets at most 2^lgCap lanes this round, and lgCap grows
+    // each round it stays undecided.  Most chains end within a few samples (default TF:
+    // 3 draws), and the lines of samples past the event are wasted gathers; long chains
+    // (sparse TFs) reach whole-wave groups after six rounds.
+    int lgCap = A.coopMaxLg;
+    for (;; lgCap = A.coopRamp ? min(lgCap + 1, 6) : lgCap) {
       const uint64_t am = __ballot(active);
       if (am == 0ull) break;
       if constexpr ((OPT & OPT_STATS) != 0) ++cnt.rounds;
       const int R = __popcll(am);
-      const int lg = R > 32 ? 0 : R > 16 ? 1 : R > 8 ? 2 : R > 4 ? 3 : R > 2 ? 4 : R > 1 ? 5 : 6;
+      const int lg = min(lgCap, R > 32 ? 0 : R > 16 ? 1 : R > 8 ? 2 : R > 4 ? 3 : R > 2 ? 4 : R > 1 ? 5 : 6);
       const int G = 1 << lg;
       // solo round (G = 1): every ray on its own lane, nothing exchanged
       const bool solo = lg == 0;

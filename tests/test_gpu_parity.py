@@ -498,6 +498,27 @@ def test_cooperative_woodcock_holes_and_long_chains(raygen):
     assert st_ref[0].locate_calls > st_ref[0].samples_found  # holes were sampled
 
 
+@pytest.mark.parametrize("maxlg,ramp", [("6", "0"), ("0", "0"), ("3", "0"), ("2", "1")])
+def test_cooperative_group_caps(monkeypatch, maxlg, ramp):
+    """The speculation cap of the cooperative loop (IRT_COOP_MAXLG / IRT_COOP_RAMP; the
+    default ramps from one lane per ray) changes only how many samples a round evaluates:
+    whole-wave groups, solo rounds only, a fixed cap, another ramp -- each the oracle's
+    frame and counts, over holes and long chains."""
+    monkeypatch.setenv("IRT_COOP_MAXLG", maxlg)
+    monkeypatch.setenv("IRT_COOP_RAMP", ramp)
+    cells = irt.filter_cells(irt.synth_grid(2, 3, 60), (-40, 50), (-100, 70))
+    setup = irt.setup_frame(cells, 8, 8)
+    lut = setup.lut.copy()
+    lut[:, 3] = 0.01
+    lut[::50, 3] = 1.0
+    kw = dict(camera=FRAMING, lut=lut, value_range=setup.value_range)
+    a_ref, f_ref, st_ref, _ = oracle_frame(cells, 64, 64, **kw)
+    a_gpu, f_gpu, st_gpu, _ = gpu_frame(cells, 64, 64, **kw)
+    assert_same_frame(a_gpu, f_gpu, a_ref, f_ref, f"maxlg {maxlg} ramp {ramp}")
+    assert st_gpu[0].locateCalls == st_ref[0].locate_calls
+    assert st_gpu[0].samplesFound == st_ref[0].samples_found
+
+
 def test_device_srgb_byte_equals_threshold_count():
     """csrc/irt_device.h srgb_byte (hardware log2/exp2 estimate, then settled on the host
     thresholds) == the number of thresholds <= x, which test_host_logic pins to the
