@@ -111,7 +111,7 @@ struct irt_context {
   int schedBuf = 0;             // the order buffer launches read now
   long long schedSwitch = 0;    // first launch reading it
   size_t schedCap = 0;
-  bool schedOn = true;         // IRT_SCHED=0 disables
+  bool schedOn = false;        // IRT_SCHED=1|2|3 enables (neutral since the ramped loop: profiles/r02e_coop_cap)
   // cooperative Woodcock loop: a ray's lanes per round <= 2^(coopMaxLg + round) with the
   // ramp, 2^coopMaxLg without (IRT_COOP_MAXLG, IRT_COOP_RAMP; profiles/r02e_dist/)
   int coopMaxLg = 0;
@@ -734,7 +734,7 @@ int irt_create_end(irt_context *c) {
   if (const char *e = getenv("IRT_COUNTERS")) c->wgCountsOn = strcmp(e, "atomic") != 0;
   if (const char *e = getenv("IRT_TIMING_EVERY")) c->timingEvery = std::max(1, atoi(e));
   if (const char *e = getenv("IRT_COOP_MAXLG")) c->coopMaxLg = std::min(6, std::max(0, atoi(e)));
-  if (const char *e = getenv("IRT_COOP_RAMP")) c->coopRamp = atoi(e) != 0 ? 1 : 0;
+  if (const char *e = getenv("IRT_COOP_RAMP")) c->coopRamp = std::min(6, std::max(0, atoi(e)));
   IRT_HIP(hipHostGetDevicePointer((void **)&c->dh_counters, c->h_counters, 0));
   IRT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long), c->stream));
 

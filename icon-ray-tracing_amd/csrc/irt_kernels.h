@@ -71,8 +71,8 @@ struct RenderArgs {
   uint32_t *schedCost;
   float4 *sampleBuf;
   // cooperative Woodcock loop: at most 2^coopMaxLg lanes (samples) per ray in the first
-  // round of a woodcock_wave call, one power of two more per later round with coopRamp
-  // (any setting gives the same frame)
+  // round of a woodcock_wave call, coopRamp powers of two more per later round (any
+  // setting gives the same frame)
   int coopMaxLg;
   int coopRamp;
 };

@@ -467,7 +467,7 @@ struct Tracer {
     // 3 draws), and the lines of samples past the event are wasted gathers; long chains
     // (sparse TFs) reach whole-wave groups after six rounds.
     int lgCap = A.coopMaxLg;
-    for (;; lgCap = A.coopRamp ? min(lgCap + 1, 6) : lgCap) {
+    for (;; lgCap = min(lgCap + A.coopRamp, 6)) {
       const uint64_t am = __ballot(active);
       if (am == 0ull) break;
       if constexpr ((OPT & OPT_STATS) != 0) ++cnt.rounds;
@@ -669,18 +669,18 @@ __device__ __forceinline__ void write_pixel(const RenderArgs &A, size_t outIdx, 
   write_pixel(A, outIdx, cr, cg, cb, alpha, s_th, A.accum[outIdx]);
 }
 
-// The workgroup's event counts (LDS) out to the launch's statistics.  Default: one store of
-// the kCnt counts per workgroup into wgCounts, pinned host memory the host sums when asked
-// (irt_context.hip finish_slot): no statistics kernel, and no two workgroups touch the same
-// line.  Without wgCounts: device-scope atomics into the counter block -- 4 096 workgroups
-// x 5 same-line atomics per 1024^2 frame, ~40 us of serialised atomics.
-__device__ __forceinline__ void flush_counters(const RenderArgs &A, uint32_t *s_cnt, int tid) {
-  __syncthreads();
+// The workgroup's event counts (LDS) out to the launch's statistics, by the workgroup's
+// last wave to finish (k_render).  Default: one store of the kCnt counts per workgroup into
+// wgCounts, pinned host memory the host sums when asked (irt_context.hip finish_slot): no
+// statistics kernel, and no two workgroups touch the same line.  Without wgCounts:
+// device-scope atomics into the counter block -- 4 096 workgroups x 5 same-line atomics per
+// 1024^2 frame, ~35 us of serialised atomics.
+__device__ __forceinline__ void flush_counters(const RenderArgs &A, const uint32_t *s_cnt, int lane) {
   if (A.wgCounts) {
     const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-    if (tid < kCnt) A.wgCounts[wg * kCnt + tid] = s_cnt[tid];
-  } else if (tid < 5 && s_cnt[tid]) {
-    atomicAdd(&A.counters[tid], (unsigned long long)s_cnt[tid]);
+    if (lane < kCnt) A.wgCounts[wg * kCnt + lane] = s_cnt[lane];
+  } else if (lane < 5 && s_cnt[lane]) {
+    atomicAdd(&A.counters[lane], (unsigned long long)s_cnt[lane]);
   }
 }
 
@@ -1256,6 +1256,8 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
     for (int k = 0; k < kSphBitWords / 256; ++k) s_sph[tid + 256 * k] = sph[k];
   }
   if (tid < kCnt) s_cnt[tid] = 0;
+  __shared__ uint32_t s_done;  // waves of this workgroup finished (the epilogue)
+  if (tid == 0) s_done = 0;
   __shared__ uint32_t s_gbits[(OPT & OPT_GRID) ? kGridBitWords : 1];
   if constexpr ((OPT & OPT_GRID) != 0) {
 #pragma unroll
@@ -1304,16 +1306,24 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
         if (hist[k]) atomicAdd(&A.counters[12 + k], (unsigned long long)hist[k]);
     }
   }
-  if (A.counters) {
+  if (A.counters || A.schedCost) {
+    const int lane = tid & 63;
     const unsigned long long m = __ballot(px.active);  // rays launched, once per wave
-    if (__lane_id() == 0 && m) atomicAdd(&s_cnt[0], (uint32_t)__popcll(m));
-    flush_counters(A, s_cnt, tid);
-  }
-  if (A.schedCost) {  // this workgroup's duration, for the next launches' order
-    __syncthreads();
-    if (tid == 0) {
-      const uint64_t dt = wall_clock64() - c0;
-      A.schedCost[blk] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
+    if (A.counters && lane == 0 && m) atomicAdd(&s_cnt[0], (uint32_t)__popcll(m));
+    // The last wave of the workgroup to get here writes the workgroup's counts and duration.
+    // No end-of-workgroup barrier: a wave that finishes early frees its slot at once instead
+    // of waiting for the slowest wave of its workgroup.  The acq-rel LDS add orders every
+    // wave's count adds before the last wave's reads.
+    uint32_t prev = 0;
+    if (lane == 0)
+      prev = __hip_atomic_fetch_add(&s_done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    prev = (uint32_t)__shfl((int)prev, 0, 64);
+    if (prev == (blockDim.x >> 6) - 1u) {
+      if (A.counters) flush_counters(A, s_cnt, lane);
+      if (A.schedCost && lane == 0) {  // this workgroup's duration, for the next launches' order
+        const uint64_t dt = wall_clock64() - c0;
+        A.schedCost[blk] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
+      }
     }
   }
 }

@@ -360,11 +360,12 @@ def test_converted_icon_files_render_bit_exact(tmp_path):
         ctx.close()
 
 
-def test_measured_cost_scheduling_keeps_frames_identical():
-    """Repeated launches on one context: after the first few the workgroups run in the
-    measured-cost (longest-first) tile order; every frame must stay bit-identical to the
-    oracle's, counters included."""
+def test_measured_cost_scheduling_keeps_frames_identical(monkeypatch):
+    """Repeated launches on one context with IRT_SCHED=2 (off by default): after the first
+    few the workgroups run in the measured-cost (longest-first) tile order; every frame must
+    stay bit-identical to the oracle's, counters included."""
     from helpers import GpuFrame
+    monkeypatch.setenv("IRT_SCHED", "2")
     cells = irt.synth_grid(2, 3, 47)
     W = 160
     a_ref, f_ref, st_ref, _ = oracle_frame(cells, W, W, camera=FRAMING)
@@ -394,11 +395,12 @@ def _sched_state(ctx):
     return p.value, a.value, n.value
 
 
-def test_measured_cost_scheduling_on_a_rank_tile_subset():
+def test_measured_cost_scheduling_on_a_rank_tile_subset(monkeypatch):
     """the scheduled path with tileStride > 1 (one rank's interleaved tiles, where
     the policy-2 band is tilesX/tileStride tiles): repeated launches run in a measured-cost
     order and every launch's tiles equal the full frame's."""
     import torch
+    monkeypatch.setenv("IRT_SCHED", "2")
     cells = irt.synth_grid(2, 3, 47)
     W, H = 328, 200  # 6 x 4 tiles, the last column and row ragged
     setup = irt.setup_frame(cells, W, H, camera=FRAMING)
