@@ -465,8 +465,10 @@ struct Tracer {
     // speculation ramps up: a ray gets at most 2^lgCap lanes this round, and lgCap grows
     // each round it stays undecided.  Most chains end within a few samples (default TF:
     // 3 draws), and the lines of samples past the event are wasted gathers; long chains
-    // (sparse TFs) reach whole-wave groups after six rounds.
-    int lgCap = A.coopMaxLg;
+    // (sparse TFs) reach whole-wave groups after six rounds.  The miss-mode kernels (wedge
+    // samplers, grid accel) keep whole-wave groups from the start: their misses come in
+    // runs that wide groups cross in one round (2 % faster there, profiles/r02e_coop_cap).
+    int lgCap = kMiss ? 6 : A.coopMaxLg;
     for (;; lgCap = min(lgCap + A.coopRamp, 6)) {
       const uint64_t am = __ballot(active);
       if (am == 0ull) break;
