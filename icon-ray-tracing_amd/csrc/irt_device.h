@@ -20,6 +20,9 @@ struct Ray {
 struct Counts {
   uint32_t inBox, locate, found, cand;
   uint32_t steps, deg, rounds;  // OPT_STATS only: Woodcock draws, zero-length leaves, cooperative rounds
+  // OPT_STATS only, cooperative loop: per round the wave's longest candidate scan (entry
+  // hops), rounds with a locate, and per lane the samples by candidates tested (0,1,2,>=3)
+  uint32_t hops, locRounds, candHist[4];
 };
 
 __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {

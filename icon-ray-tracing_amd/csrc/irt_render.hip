@@ -29,9 +29,13 @@ enum : int {
   OPT_WEDGE = 16384,  // CUBQL / TRIANGLE samplers (locate_wedge, locate_tri); kept out of
                       // the default kernels
   OPT_GRID = 8192,    // GRID_ACCEL_MODE traversal (render_grid); likewise
-  OPT_STATS = 32768,  // per-wave statistics into counters[5..15] (measurement only)
+  OPT_STATS = 32768,  // per-wave statistics into counters[5..15] (measurement only; with the
+                      // cooperative loop [7] entry hops, [8] locate rounds, [12..15] samples by
+                      // candidates tested 0/1/2/>=3)
   OPT_SERIAL = 65536, // one lane per ray through the Woodcock loop (render_pixel), for A/B:
                       // the default user-geometry/sphere kernel is render_pixel_coop
+  OPT_SCAN1 = 131072, // the cooperative loop with each lane's candidate scan on its own
+                      // (locate), for A/B against Tracer::locate_wave
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
@@ -83,6 +87,13 @@ struct CoopWave {
   float4 ray[64];   // {dx, dy, dz, RNG state bits}
   float step[64];   // lane l's Woodcock step log(1 - xi)/q this round
   uint32_t cnt[64]; // the request is counted (a positive-length leaf)
+};
+// Per-wave LDS of Tracer::locate_wave's candidate scan
+struct ScanWave {
+  float4 pt[64];    // lane l's sample {point, r}
+  uint4 lst[64];    // its candidate list {first entry, sub-cell mask, next position, record limit}
+  float4 fck[64];   // the record found: coarse keys
+  uint2 frm[64];    // {record, meta}
 };
 
 // t0 - d[0] - d[1] - ... - d[k], subtracted one at a time as woodcockTracking's `t -=`
@@ -377,6 +388,186 @@ struct Tracer {
     return hit;
   }
 
+  // sampleVolume for every lane of the wave with `want` set (the cooperative loop's locate;
+  // all lanes call it).  The same answer as locate: the first candidate of the sample's bin
+  // and sub-cell, in record order, passing sample().  But the candidate scan is spread over
+  // the wave: every lane first tests its list's first candidate (a quarter of C3's samples
+  // fail it: 916,920 / 270,995 / 30,517 samples take 1 / 2 / >=3 tests), then the wave's
+  // remaining candidates are dealt out one per lane and tested together, so a round waits
+  // for two entry gathers instead of the longest lane's chain (2.96 per round at C3).  The
+  // lowest passing candidate of each list wins, as in the serial scan.  Samples exactly on a
+  // radial bin edge (the two-bin scan) take locate_hdr's serial path.
+  static constexpr bool kWaveScan = kCoop && (OPT & (OPT_WEDGE | OPT_GRID | OPT_SCAN1)) == 0;
+  __device__ __forceinline__ bool pass_entry(const float4 *F, float px, float py, float pz, float r,
+                                             Found &f) {
+    const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3], ak = F[4];
+    f = {__float_as_uint(am.z), __float_as_uint(am.w), ak};
+    if (r < am.x || r > am.y) return false;                               // ICONGrid.h:184
+    if (dot3(px, py, pz, a0.x, a0.y, a0.z) - a0.w > 0.f) return false;  // ICONGrid.h:201
+    if (dot3(px, py, pz, a1.x, a1.y, a1.z) - a1.w > 0.f) return false;  // 202
+    if (dot3(px, py, pz, a2.x, a2.y, a2.z) - a2.w > 0.f) return false;  // 203
+    return true;
+  }
+  // position p of a candidate list {set bits of m8, ascending} ++ {8, 9, ...} -> entry offset
+  __device__ __forceinline__ static uint32_t list_entry(uint32_t m8, uint32_t p) {
+    const uint32_t nm = (uint32_t)__popc(m8);
+    if (p >= nm) return (uint32_t)kMaskCand + (p - nm);
+    for (uint32_t k = 0; k < p; ++k) m8 &= m8 - 1u;
+    return (uint32_t)__builtin_ctz(m8);
+  }
+  __device__ __forceinline__ bool locate_wave(bool want, float px, float py, float pz, float &value,
+                                              CoopWave &CW, ScanWave &W) {
+    want = want && A.numCells != 0;
+    const int lane = (int)__lane_id();
+    // The scan's state lives in the wave's LDS (fewer live VGPRs across it):
+    //   W.pt[l]  the sample {point, r} of lane l
+    //   W.lst[l] its list {first entry, sub-cell mask, next list position, record limit}
+    //   W.fck[l], W.frm[l]  the record found so far: coarse keys, {record, meta}
+    //   W.own[s] the lane whose tasks start at s (W.step, free after the round's prefix)
+    uint32_t *own = reinterpret_cast<uint32_t *>(CW.step);
+    uint32_t c = 0u;
+    bool hit = false, edge = false;
+    if (want) {
+      const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
+      uint32_t sub;
+      const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G, sub);
+      const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
+      const uint4 H0 = Hc[0], H1 = Hc[1];
+      const uint32_t M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
+      const int b = bin_of(r, __uint_as_float(H0.x), __uint_as_float(H0.y), __uint_as_float(H0.z));
+      const uint32_t m1 = b > 0 ? ~0u : 0u, m2 = b > 1 ? ~0u : 0u, m3 = b > 2 ? ~0u : 0u;
+      const uint32_t beg = (m1 & H1.x) + (m2 & (H1.y - H1.x)) + (m3 & (H1.z - H1.y));
+      const uint32_t end = H1.x + (m1 & (H1.y - H1.x)) + (m2 & (H1.z - H1.y)) + (m3 & (H1.w - H1.z));
+      // r exactly on the bin's upper edge: records starting at that edge sit in the next
+      // bin, whose list is scanned in a second pass for a lower record (locate_hdr)
+      const float eb = __uint_as_float(H0.x ^ (m1 & (H0.x ^ H0.y)) ^ (m2 & (H0.y ^ H0.z)));
+      edge = b < kMaxEdges && r == eb;
+      const uint32_t n = end - beg;
+      const uint32_t m8 = (M >> (8 * b)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
+      c = (uint32_t)__popc(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
+      W.pt[lane] = make_float4(px, py, pz, r);
+      W.lst[lane] = make_uint4(H0.w + beg, m8, 0u, 0xFFFFFFFFu);
+    }
+    for (int pass = 0;; ++pass) {
+      // every lane: its list's first candidate
+      uint32_t rem = 0u;
+      if (c > 0u) {
+        const uint4 d = W.lst[lane];
+        Found f;
+        const bool ok = pass_entry(A.fat + (size_t)(d.x + (d.y ? (uint32_t)__builtin_ctz(d.y) : (uint32_t)kMaskCand)) *
+                                               kFatStride4,
+                                   px, py, pz, W.pt[lane].w, f);
+        if (f.rec < d.w) {  // scan_fat stops, uncounted, at the first record >= the limit
+          ++specCand;
+          if (ok) {
+            hit = true;
+            W.fck[lane] = f.ck;
+            W.frm[lane] = make_uint2(f.rec, f.meta);
+          } else {
+            rem = c - 1u;
+            W.lst[lane].z = 1u;
+          }
+        }
+      }
+      bool need = rem > 0u;
+      for (uint64_t nm = __ballot(need); nm != 0ull; nm = __ballot(need)) {
+        // deal the owners' untested candidates out to the lanes: exclusive prefix of rem
+        uint32_t incl = need ? rem : 0u;
+        for (int off = 1; off < 64; off <<= 1) {
+          const uint32_t y = (uint32_t)__shfl_up((int)incl, off, 64);
+          if (lane >= off) incl += y;
+        }
+        const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+        const uint32_t start = incl - (need ? rem : 0u);
+        const bool owns = need && start < 64u;
+        own[lane] = 0xFFFFFFFFu;
+        __builtin_amdgcn_wave_barrier();
+        if (owns) own[start] = (uint32_t)lane;
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t sm = __ballot(own[lane] != 0xFFFFFFFFu);  // bit s: an owner's tasks start at s
+        // lane t: task t - s0 of the owner whose tasks start at the highest s0 <= t
+        const uint32_t t = (uint32_t)lane;
+        const bool task = t < total;
+        const uint32_t s0 = task ? 63u - (uint32_t)__builtin_clzll(sm & (~0ull >> (63u - t))) : 0u;
+        const uint32_t o = own[s0];
+        bool tp = false, tl = false;
+        Found g;
+        if (task) {
+          const float4 po = W.pt[o];
+          const uint4 d = W.lst[o];
+          tp = pass_entry(A.fat + (size_t)(d.x + list_entry(d.y, d.z + (t - s0))) * kFatStride4, po.x, po.y,
+                          po.z, po.w, g);
+          tl = g.rec >= d.w;  // past the limit: the serial scan stops there
+          tp = tp && !tl;
+        }
+        const uint64_t pm = __ballot(tp), lm = __ballot(tl);
+        // the lowest event of each owner's tasks: a passing record (it hands it over) or the limit
+        const uint64_t below = t ? (~0ull >> (64u - t)) : 0ull;  // tasks < t
+        if (tp && ((pm | lm) & below & (~0ull << s0)) == 0ull) {
+          W.fck[o] = g.ck;
+          W.frm[o] = make_uint2(g.rec, g.meta);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (owns) {
+          const uint32_t k = min(rem, 64u - start);  // this owner's tasks in this batch
+          const uint64_t ev = (pm | lm) & ((k >= 64u ? ~0ull : ((1ull << k) - 1ull)) << start);
+          if (ev) {
+            const uint32_t e = (uint32_t)__builtin_ctzll(ev) - start;
+            const bool ps = (pm >> (start + e)) & 1ull;
+            specCand += e + (ps ? 1u : 0u);
+            hit = hit || ps;
+            need = false;
+          } else {
+            specCand += k;
+            rem -= k;
+            W.lst[lane].z += k;
+            need = rem > 0u;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      // the second pass: bin-edge samples, the next bin's list below the record found
+      if (pass == 1 || __ballot(edge) == 0ull) break;
+      c = 0u;
+      if (edge) {
+        const float4 p = W.pt[lane];
+        uint32_t sub;
+        const uint32_t cell = cubemap_cell_fast(p.x, p.y, p.z, A.G, sub);
+        const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
+        const uint4 H0 = Hc[0], H1 = Hc[1];
+        const uint32_t M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
+        const int b = bin_of(p.w, __uint_as_float(H0.x), __uint_as_float(H0.y), __uint_as_float(H0.z)) + 1;
+        const uint32_t m1 = b > 0 ? ~0u : 0u, m2 = b > 1 ? ~0u : 0u, m3 = b > 2 ? ~0u : 0u;
+        const uint32_t beg = (m1 & H1.x) + (m2 & (H1.y - H1.x)) + (m3 & (H1.z - H1.y));
+        const uint32_t end = H1.x + (m1 & (H1.y - H1.x)) + (m2 & (H1.z - H1.y)) + (m3 & (H1.w - H1.z));
+        const uint32_t n = end - beg;
+        const uint32_t m8 = (M >> (8 * b)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
+        c = (uint32_t)__popc(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
+        W.lst[lane] = make_uint4(H0.w + beg, m8, 0u, hit ? W.frm[lane].x : 0xFFFFFFFFu);
+      }
+    }
+    if (!want) return false;
+    const float r = W.pt[lane].w;
+    Found f = {0xFFFFFFFFu, 0u, make_float4(0.f, 0.f, 0.f, 0.f)};
+    if (hit) {
+      const uint2 rm = W.frm[lane];
+      f = {rm.x, rm.y, W.fck[lane]};
+    }
+    if (A.numSph) {
+      const uint32_t h = sph_hash(r);
+      if ((s_sph[h >> 5] >> (h & 31)) & 1u) {
+        float v2;
+        uint32_t rec2;
+        if (sphere_at(r, v2, rec2) && (!hit || rec2 < f.rec)) {
+          value = v2;
+          return true;
+        }
+      }
+    }
+    if (hit) value = record_value(f, r);
+    return hit;
+  }
+
   // postClassify's alpha only (the acceptance test needs nothing else); the colour comes
   // from post_classify on acceptance
   __device__ __forceinline__ float classify_alpha(float v) {
@@ -456,7 +647,7 @@ struct Tracer {
   __device__ __forceinline__ void woodcock_wave(bool req, float dx, float dy, float dz, float &t,
                                                 float tmax, uint32_t &st, float majorant,
                                                 bool counted, float4 &sampleOut, bool &miss,
-                                                CoopWave &W, const uint32_t *jmul,
+                                                CoopWave &W, ScanWave *SW, const uint32_t *jmul,
                                                 const uint32_t *jadd) {
     const int lane = (int)__lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
@@ -532,12 +723,15 @@ struct Tracer {
       const bool past = used && tk > rq.y;
       bool found = false, acc = false;
       float value = 0.f;
-      if (used && !past) {
+      if constexpr (kWaveScan) {
+        found = locate_wave(used && !past, A.org.x + ry.x * tk, A.org.y + ry.y * tk, A.org.z + ry.z * tk,
+                            value, W, *SW);
+      } else if (used && !past) {
         found = locate(A.org.x + ry.x * tk, A.org.y + ry.y * tk, A.org.z + ry.z * tk, value);
-        if (found) {
-          const float sw = classify_alpha(value);  // postClassify(value).w
-          acc = sw >= lcg_float(lcg_next(sk)) * rq.w;
-        }
+      }
+      if (found) {
+        const float sw = classify_alpha(value);  // postClassify(value).w
+        acc = sw >= lcg_float(lcg_next(sk)) * rq.w;
       }
       // the first sample that breaks the round's assumption, or ends the ray's leaf
       const bool ev = used && (past || acc || (mm ? found : !found));
@@ -557,6 +751,14 @@ struct Tracer {
           nFound += found ? 1u : 0u;
         }
         nCand += specCand;
+      }
+      if constexpr ((OPT & OPT_STATS) != 0) {
+        const bool loc = used && !past;
+        uint32_t m = loc ? specCand : 0u;
+        for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+        cnt.hops += m;
+        cnt.locRounds += __ballot(loc) ? 1u : 0u;
+        if (loc) ++cnt.candHist[specCand < 3u ? specCand : 3u];
       }
       specCand = 0u;
       // the rays' owners take their group's outcome
@@ -929,7 +1131,7 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
 template <int OPT>
 __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
                                                   const float *s_th, int4 *s_dda, float4 *s_entry,
-                                                  float4 *s_acc, CoopWave &W, const uint32_t *jmul,
+                                                  float4 *s_acc, CoopWave &W, ScanWave *SW, const uint32_t *jmul,
                                                   const uint32_t *jadd, int tid, int accumID,
                                                   float4 *sampleOut) {
   enum : int { kRange, kLeaf, kWait, kDone, kGrid, kGridNext };
@@ -1190,7 +1392,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     if (__ballot(req) == 0ull) break;
     float tw = t;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    T.woodcock_wave(req, dx, dy, dz, tw, tt1, st, maj, !zeroLen, s, miss, W, jmul, jadd);
+    T.woodcock_wave(req, dx, dy, dz, tw, tt1, st, maj, !zeroLen, s, miss, W, SW, jmul, jadd);
     if (grid && req && phase == kWait && !ae) {
       if (tw > t && tw < tt1) {  // render_grid's hit test (deviceCode.cu:316)
         s_entry[tid] = make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
@@ -1232,6 +1434,7 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   __shared__ int4 s_dda[256];       // sdda state needed only after a range's first leaf
   __shared__ float4 s_entry[256];
   __shared__ CoopWave s_coop[4];    // the cooperative Woodcock loop (kCoop kernels)
+  __shared__ ScanWave s_scan[Tracer<OPT>::kWaveScan ? 4 : 1];  // its wave-wide candidate scan
   __shared__ float4 s_acc[256];     // kCoop: the accum pixels, prefetched
   __shared__ uint32_t s_jmul[kLcgJumps], s_jadd[kLcgJumps];
   const int tid = threadIdx.x;
@@ -1277,7 +1480,8 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   const Pixel px = pixel_of(A, gid);
   float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + gid : nullptr;
   if constexpr (Tracer<OPT>::kCoop) {
-    render_pixel_coop<OPT>(A, T, px, s_th, s_dda, s_entry, s_acc, s_coop[tid >> 6], s_jmul, s_jadd, tid,
+    render_pixel_coop<OPT>(A, T, px, s_th, s_dda, s_entry, s_acc, s_coop[tid >> 6],
+                           &s_scan[Tracer<OPT>::kWaveScan ? tid >> 6 : 0], s_jmul, s_jadd, tid,
                            A.accumID + (int)blockIdx.y, slot);
     T.flush_coop();
   }
@@ -1295,12 +1499,14 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
     const uint32_t d = T.cnt.steps;  // draws histogram: 0, 1-2, 3-5, > 5
     const int bkt = d == 0 ? 0 : (d <= 2 ? 1 : (d <= 5 ? 2 : 3));
     uint32_t hist[4];
-    for (int k = 0; k < 4; ++k) hist[k] = (uint32_t)__popcll(__ballot(px.active && bkt == k));
+    for (int k = 0; k < 4; ++k)
+      hist[k] = T.kCoop ? Tracer<OPT>::wave_sum(T.cnt.candHist[k])
+                        : (uint32_t)__popcll(__ballot(px.active && bkt == k));
     if ((tid & 63) == 0) {
       atomicAdd(&A.counters[5], (unsigned long long)ss);
       atomicAdd(&A.counters[6], (unsigned long long)sm);
-      atomicAdd(&A.counters[7], (unsigned long long)ds);
-      atomicAdd(&A.counters[8], (unsigned long long)dm);
+      atomicAdd(&A.counters[7], (unsigned long long)(T.kCoop ? T.cnt.hops : ds));       // uniform per wave
+      atomicAdd(&A.counters[8], (unsigned long long)(T.kCoop ? T.cnt.locRounds : dm));  // likewise
       atomicMax(&A.counters[9], (unsigned long long)sm);
       atomicMax(&A.counters[10], (unsigned long long)dm);
       atomicAdd(&A.counters[11], (unsigned long long)T.cnt.rounds);  // uniform per wave
@@ -1395,7 +1601,7 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
-#define IRT_VARIANTS(X) X(4096) X(5120) X(36864) X(70656)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(36864) X(70656) X(136192)
 
 bool render_variant_available(int v) {
 #define IRT_CASE(N) if (v == N) return true;

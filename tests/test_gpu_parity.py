@@ -269,7 +269,8 @@ def test_all_render_variants_identical():
         acc.zero_()
         ctx.render(setup.lp, W, W, fb.data_ptr(), acc.data_ptr())
         st = ctx.stats()
-        out = (fb.cpu().numpy().copy(), bits(acc.cpu().numpy()), st.locateCalls, st.samplesFound)
+        out = (fb.cpu().numpy().copy(), bits(acc.cpu().numpy()), st.locateCalls, st.samplesFound,
+               st.candidatesTested)
         if ref is None:
             ref = out
             continue
