@@ -2,13 +2,13 @@
 // this backend's netCDF-classic reader:
 //
 //   convert_icon -hgrid <hg.nc> -hsurf <hs.nc> -hhl [hh.nc*] -data [df.nc*] [-o base]
-//                [--var NAME] [--max-layers N] [--no-ic]
+//                [--var NAME] [--max-layers N] [--no-ic] [--umesh]
 //
 // Same command line as the reference (parseCommandLine, 121-161).  The reference
 // hard-codes convertToIC=false / convertToUMesh=true (22-23) and is normally built
 // without UMesh, so as shipped it writes nothing; this tool writes `<base>.ic` (the file
-// icon_rt loads) unless --no-ic.  --var / --max-layers expose the hard-coded "pres" (308)
-// and maxLayers=5 (24).
+// icon_rt loads) unless --no-ic, and `<base>.umesh` (the UMesh branch, 393-452) with
+// --umesh.  --var / --max-layers expose the hard-coded "pres" (308) and maxLayers=5 (24).
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -22,7 +22,7 @@ int main(int argc, char *argv[]) {
     fprintf(stderr,
             "Convert DWD ICON data (netCDF classic) to the .ic format icon_rt loads.\n"
             "Usage: convert_icon -hgrid <hg.nc> -hsurf <hs.nc> -hhl [hh.nc*] -data [df.nc*]"
-            " [-o base] [--var NAME] [--max-layers N] [--no-ic]\n");
+            " [-o base] [--var NAME] [--max-layers N] [--no-ic] [--umesh]\n");
     return 1;
   }
   enum Mode { Hgrid, Hsurf, Hhl, Data, None };
@@ -30,7 +30,7 @@ int main(int argc, char *argv[]) {
   std::string hgrid, hsurf, outBase = "out", var = "pres";
   std::vector<std::string> hhl, data;
   int maxLayers = 5;
-  bool writeIC = true;
+  bool writeIC = true, writeUMesh = false;
   for (int i = 1; i < argc; ++i) {  // convert_icon.cpp:121-161
     std::string arg = argv[i];
     if (arg[0] != '-') {
@@ -50,6 +50,7 @@ int main(int argc, char *argv[]) {
     else if (arg == "--var" && i + 1 < argc) var = argv[++i];
     else if (arg == "--max-layers" && i + 1 < argc) maxLayers = atoi(argv[++i]);
     else if (arg == "--no-ic") writeIC = false;
+    else if (arg == "--umesh") writeUMesh = true;
   }
   if (hgrid.empty() || hsurf.empty() || hhl.empty()) {
     fprintf(stderr, "Usage: ./convert_icon -hgrid <hg.nc> -hsurf <hs.nc> -hhl [hh.nc*] -data [df.nc*]\n");
@@ -79,6 +80,14 @@ int main(int argc, char *argv[]) {
     }
     printf("wrote %s\n", path.c_str());
   }
-  fprintf(stderr, "Not compiled with support for UMesh files!\n");  // convert_icon.cpp:449-451
+  if (writeUMesh) {
+    const std::string path = outBase + ".umesh";
+    size_t nv = 0, nw = 0;
+    if (irt_convert_icon_umesh(&o, path.c_str(), &nv, &nw)) {
+      fprintf(stderr, "convert_icon: %s\n", irt_last_error());
+      return 1;
+    }
+    printf("%zu\n%zu\nwrote %s\n", nv, nw, path.c_str());  // convert_icon.cpp:444-447
+  }
   return 0;
 }

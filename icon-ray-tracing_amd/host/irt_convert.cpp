@@ -97,14 +97,20 @@ int readField(const char *path, const char *varName, bool isData, size_t cell,
 }
 
 constexpr int LMAX = 32;  // convert_icon.cpp:351
+constexpr uint64_t kUMeshMagic = 0x234235567ull;  // umesh binary files (UMesh::saveTo)
 
 inline int div_up(int a, int b) { return (a + b - 1) / b; }  // 47-49
 
-}  // namespace
+// The netCDF inputs of both outputs (convert_icon.cpp:168-349)
+struct Inputs {
+  size_t cell = 0;
+  std::vector<double> clon, clat, hsurf;
+  std::vector<DataField> hhl, values;
+  int numLayers = 0;  // data files, at most maxLayers (345-349)
+};
 
-extern "C" int irt_convert_icon(const irt_convert_opts *o, irt_icon_cell *out, size_t capacity,
-                                size_t *count) {
-  if (!o || !count || !o->hgridFile || !o->hsurfFile || o->numHhlFiles <= 0 ||
+int load_inputs(const irt_convert_opts *o, Inputs &in) {
+  if (!o || !o->hgridFile || !o->hsurfFile || o->numHhlFiles <= 0 ||
       (o->numHhlFiles && !o->hhlFiles) || o->numDataFiles < 0 ||
       (o->numDataFiles && !o->dataFiles)) {
     set_error("irt_convert_icon: need -hgrid, -hsurf and -hhl files (convert_icon.cpp:176-181)");
@@ -114,8 +120,7 @@ extern "C" int irt_convert_icon(const irt_convert_opts *o, irt_icon_cell *out, s
   const int maxLayers = o->maxLayers > 0 ? o->maxLayers : 5;
   int rc;
   // horizontal grid (187-211)
-  size_t cell = 0;
-  std::vector<double> clon, clat;
+  size_t &cell = in.cell;
   {
     irt_nc::File f;
     if ((rc = openNc(f, o->hgridFile)) || (rc = readDim(f, o->hgridFile, "cell", cell)))
@@ -124,31 +129,47 @@ extern "C" int irt_convert_icon(const irt_convert_opts *o, irt_icon_cell *out, s
       set_error("irt_convert_icon: %s: cell dimension %zu too large", o->hgridFile, cell);
       return IRT_E_INVALID;
     }
-    if ((rc = readDoubleVar(f, o->hgridFile, "clon_vertices", cell * 3, clon)) ||
-        (rc = readDoubleVar(f, o->hgridFile, "clat_vertices", cell * 3, clat)))
+    if ((rc = readDoubleVar(f, o->hgridFile, "clon_vertices", cell * 3, in.clon)) ||
+        (rc = readDoubleVar(f, o->hgridFile, "clat_vertices", cell * 3, in.clat)))
       return rc;
   }
   // HSURF (220-231)
-  std::vector<double> hsurf;
   {
     irt_nc::File f;
-    if ((rc = openNc(f, o->hsurfFile)) || (rc = readDoubleVar(f, o->hsurfFile, "HSURF", cell, hsurf)))
+    if ((rc = openNc(f, o->hsurfFile)) || (rc = readDoubleVar(f, o->hsurfFile, "HSURF", cell, in.hsurf)))
       return rc;
   }
   // HHL and data files, sorted by level index, descending (236-337)
-  std::vector<DataField> hhl(o->numHhlFiles), values(o->numDataFiles);
+  in.hhl.resize(o->numHhlFiles);
+  in.values.resize(o->numDataFiles);
   for (int i = 0; i < o->numHhlFiles; ++i)
-    if ((rc = readField(o->hhlFiles[i], "HHL", false, cell, hhl[i]))) return rc;
+    if ((rc = readField(o->hhlFiles[i], "HHL", false, cell, in.hhl[i]))) return rc;
   for (int i = 0; i < o->numDataFiles; ++i)
-    if ((rc = readField(o->dataFiles[i], varName, true, cell, values[i]))) return rc;
+    if ((rc = readField(o->dataFiles[i], varName, true, cell, in.values[i]))) return rc;
   // std::sort in the reference: equal level indices (malformed input) have no defined
   // order there; stable here
   auto desc = [](const DataField &a, const DataField &b) { return a.height > b.height; };
-  std::stable_sort(hhl.begin(), hhl.end(), desc);
-  std::stable_sort(values.begin(), values.end(), desc);
+  std::stable_sort(in.hhl.begin(), in.hhl.end(), desc);
+  std::stable_sort(in.values.begin(), in.values.end(), desc);
+  in.numLayers = o->numDataFiles;  // 345-349
+  if (in.numLayers > maxLayers) in.numLayers = maxLayers;
+  return IRT_OK;
+}
 
-  int numLayers = o->numDataFiles;  // 345-349
-  if (numLayers > maxLayers) numLayers = maxLayers;
+}  // namespace
+
+extern "C" int irt_convert_icon(const irt_convert_opts *o, irt_icon_cell *out, size_t capacity,
+                                size_t *count) {
+  if (!count) {
+    set_error("irt_convert_icon: null count");
+    return IRT_E_INVALID;
+  }
+  Inputs in;
+  if (int rc = load_inputs(o, in)) return rc;
+  const size_t cell = in.cell;
+  const std::vector<double> &clon = in.clon, &clat = in.clat, &hsurf = in.hsurf;
+  const std::vector<DataField> &hhl = in.hhl, &values = in.values;
+  const int numLayers = in.numLayers;
   // records per column and the layers they consume (362-377)
   const int numRecs = div_up(numLayers, LMAX - 1);
   int used = 0;
@@ -192,5 +213,79 @@ extern "C" int irt_convert_icon(const irt_convert_opts *o, irt_icon_cell *out, s
       c.numLayers = numLayersLocal;
     }
   }
+  return IRT_OK;
+}
+
+// The UMesh branch (convert_icon.cpp:393-452): one wedge per (cell, layer j < numLayers),
+// six vertices of its own (toCartesian with glibc cosf/sinf, 48-57), bottom and top at
+// h1 = R + HSURF*50 for j == 0, else R + (HHL[j] - HSURF)*50, and h2 = R + (HHL[j+1] -
+// HSURF)*50 (double arithmetic, rounded to float); all six vertices carry values[j] (the
+// reference's "TODO: interpolate").  Written in umesh's binary layout (UMesh::saveTo; the
+// umesh library is not part of the reference snapshot): u64 magic, then u64-counted arrays
+// -- vertices (3 f32), per-vertex scalars (f32), triangles, quads, tets, pyramids (empty),
+// wedges (6 i32), hexes (empty).
+extern "C" int irt_convert_icon_umesh(const irt_convert_opts *o, const char *path, size_t *numVertices,
+                                      size_t *numWedges) {
+  if (!path) {
+    set_error("irt_convert_icon_umesh: null path");
+    return IRT_E_INVALID;
+  }
+  Inputs in;
+  if (int rc = load_inputs(o, in)) return rc;
+  const int numLayers = in.numLayers;
+  if (numLayers + 1 > (int)in.hhl.size() || numLayers > (int)in.values.size()) {
+    // the reference reads hhl[j+1] and values[j] unchecked (409-412)
+    set_error("irt_convert_icon_umesh: %d layers need %d HHL and %d data files (have %zu, %zu)",
+              numLayers, numLayers + 1, numLayers, in.hhl.size(), in.values.size());
+    return IRT_E_DATA;
+  }
+  const size_t nw = in.cell * (size_t)numLayers;
+  if (nw * 6 > (size_t)INT32_MAX) {  // UMesh::Wedge holds int indices
+    set_error("irt_convert_icon_umesh: %zu wedges exceed int vertex indices", nw);
+    return IRT_E_INVALID;
+  }
+  std::vector<float> verts(nw * 18), scalars(nw * 6);
+  std::vector<int32_t> wedges(nw * 6);
+  size_t w = 0;
+  for (size_t cellID = 0; cellID < in.cell; ++cellID) {
+    const float lat[3]{(float)in.clat[cellID * 3], (float)in.clat[cellID * 3 + 1], (float)in.clat[cellID * 3 + 2]};
+    const float lon[3]{(float)in.clon[cellID * 3], (float)in.clon[cellID * 3 + 1], (float)in.clon[cellID * 3 + 2]};
+    constexpr float R = 6.371229E6f;
+    constexpr float scale = 50.f;
+    for (int j = 0; j < numLayers; ++j, ++w) {
+      const float h1 = j == 0 ? R + in.hsurf[cellID] * scale
+                              : R + (in.hhl[j].value[cellID] - in.hsurf[cellID]) * scale;
+      const float h2 = R + (in.hhl[j + 1].value[cellID] - in.hsurf[cellID]) * scale;
+      const float v = in.values[j].value[cellID];
+      for (int k = 0; k < 6; ++k) {  // bv1 bv2 bv3 tv1 tv2 tv3
+        const float r = k < 3 ? h1 : h2;
+        float *x = &verts[(6 * w + k) * 3];
+        x[0] = r * cosf(lat[k % 3]) * cosf(lon[k % 3]);
+        x[1] = r * cosf(lat[k % 3]) * sinf(lon[k % 3]);
+        x[2] = r * sinf(lat[k % 3]);
+        scalars[6 * w + k] = v;
+        wedges[6 * w + k] = (int32_t)(6 * w + k);
+      }
+    }
+  }
+  FILE *f = fopen(path, "wb");
+  if (!f) {
+    set_error("irt_convert_icon_umesh: cannot write %s", path);
+    return IRT_E_IO;
+  }
+  const uint64_t magic = kUMeshMagic, zero = 0, nv = nw * 6, nw64 = nw;
+  bool ok = fwrite(&magic, 8, 1, f) == 1;
+  ok = ok && fwrite(&nv, 8, 1, f) == 1 && fwrite(verts.data(), 4, verts.size(), f) == verts.size();
+  ok = ok && fwrite(&nv, 8, 1, f) == 1 && fwrite(scalars.data(), 4, scalars.size(), f) == scalars.size();
+  for (int k = 0; k < 4 && ok; ++k) ok = fwrite(&zero, 8, 1, f) == 1;  // triangles quads tets pyrs
+  ok = ok && fwrite(&nw64, 8, 1, f) == 1 && fwrite(wedges.data(), 4, wedges.size(), f) == wedges.size();
+  ok = ok && fwrite(&zero, 8, 1, f) == 1;  // hexes
+  ok = (fclose(f) == 0) && ok;
+  if (!ok) {
+    set_error("irt_convert_icon_umesh: short write to %s", path);
+    return IRT_E_IO;
+  }
+  if (numVertices) *numVertices = (size_t)nv;
+  if (numWedges) *numWedges = nw;
   return IRT_OK;
 }

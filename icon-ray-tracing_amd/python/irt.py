@@ -141,6 +141,7 @@ def lib() -> C.CDLL:
             "irt_load_ic": [C.c_char_p, C.c_long, P, S, C.POINTER(S)],
             "irt_save_ic": [C.c_char_p, P, S],
             "irt_convert_icon": [C.POINTER(ConvertOpts), P, S, C.POINTER(S)],
+            "irt_convert_icon_umesh": [C.POINTER(ConvertOpts), C.c_char_p, C.POINTER(S), C.POINTER(S)],
             "irt_filter_cells": [P, S, Box1, Box1, C.POINTER(S)],
             "irt_compute_volume_info": [P, S, C.POINTER(VolumeInfo)],
             "irt_default_transfunc": [Box1, P, C.POINTER(Box1)],
@@ -249,6 +250,48 @@ def convert_icon(hgrid: str, hsurf: str, hhl: list, data: list, var: str = "pres
     _check(lib().irt_convert_icon(C.byref(o), _ptr(cells), n.value, C.byref(n)),
            "irt_convert_icon")
     return cells
+
+
+def convert_icon_umesh(hgrid: str, hsurf: str, hhl: list, data: list, path: str,
+                       var: str = "pres", max_layers: int = 5):
+    """convert_icon's UMesh branch (convert_icon.cpp:393-452): writes `path` in umesh's
+    binary layout; returns (vertices, wedges) written."""
+    hp = (C.c_char_p * max(len(hhl), 1))(*[f.encode() for f in hhl])
+    dp = (C.c_char_p * max(len(data), 1))(*[f.encode() for f in data])
+    o = ConvertOpts(hgrid.encode(), hsurf.encode(), hp, len(hhl), dp, len(data), var.encode(),
+                    max_layers)
+    nv, nw = C.c_size_t(), C.c_size_t()
+    _check(lib().irt_convert_icon_umesh(C.byref(o), path.encode(), C.byref(nv), C.byref(nw)),
+           "irt_convert_icon_umesh")
+    return nv.value, nw.value
+
+
+def read_umesh(path: str) -> dict:
+    """The arrays of a .umesh file as irt_convert_icon_umesh writes it (u64-counted)."""
+    raw = open(path, "rb").read()
+    pos = 0
+
+    def u64():
+        nonlocal pos
+        v = int(np.frombuffer(raw, np.uint64, 1, pos)[0])
+        pos += 8
+        return v
+
+    def arr(dtype, width):
+        nonlocal pos
+        n = u64()
+        a = np.frombuffer(raw, dtype, n * width, pos).reshape(n, width) if width > 1 else \
+            np.frombuffer(raw, dtype, n, pos)
+        pos += a.nbytes
+        return a
+
+    out = {"magic": u64(), "vertices": arr(np.float32, 3), "scalars": arr(np.float32, 1)}
+    for name, w in (("triangles", 3), ("quads", 4), ("tets", 4), ("pyrs", 5),
+                    ("wedges", 6), ("hexes", 8)):
+        out[name] = arr(np.int32, w)
+    if pos != len(raw):
+        raise ValueError(f"{path}: {len(raw) - pos} trailing bytes")
+    return out
 
 
 def save_ic(path: str, cells: np.ndarray):

@@ -266,6 +266,16 @@ typedef struct irt_convert_opts {
 int irt_convert_icon(const irt_convert_opts *opts, irt_icon_cell *out, size_t capacity,
                      size_t *count);
 
+/* convert_icon's UMesh output (tools/convert_icon/convert_icon.cpp:393-452, the tool's
+ * default convertToUMesh branch): one wedge per (cell, layer) with six vertices of its own
+ * at R + HSURF*50 / R + (HHL - HSURF)*50, each carrying the layer's value, written to
+ * `path` in umesh's binary layout (u64 magic 0x234235567, then u64-counted arrays:
+ * vertices vec3f, per-vertex f32 scalars, triangles, quads, tets, pyramids, wedges
+ * (6 x i32), hexes).  Needs numLayers+1 HHL files (the reference reads hhl[j+1]).
+ * The counts written go to *numVertices / *numWedges (either may be NULL). */
+int irt_convert_icon_umesh(const irt_convert_opts *opts, const char *path, size_t *numVertices,
+                           size_t *numWedges);
+
 /* Lat/lon filter in degrees (hostCode.cu:736-758); stable, in place; returns the kept
  * count in *count. */
 int irt_filter_cells(irt_icon_cell *cells, size_t n, irt_box1f latRangeDeg,

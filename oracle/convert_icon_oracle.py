@@ -85,3 +85,58 @@ def convert(hgrid, hsurf, hhl_files, data_files, var="pres", max_layers=5) -> np
             vit += 1
         out[i::num_recs] = rec
     return out
+
+
+def _glibc_trig():
+    """cosf/sinf from glibc (the reference tool's toCartesian, convert_icon.cpp:48-57):
+    numpy's float32 cos/sin are not glibc's."""
+    import ctypes
+    m = ctypes.CDLL("libm.so.6")
+    for fn in (m.cosf, m.sinf):
+        fn.restype = ctypes.c_float
+        fn.argtypes = [ctypes.c_float]
+    cosf = np.vectorize(lambda x: np.float32(m.cosf(float(x))), otypes=[np.float32])
+    sinf = np.vectorize(lambda x: np.float32(m.sinf(float(x))), otypes=[np.float32])
+    return cosf, sinf
+
+
+def convert_umesh(hgrid, hsurf, hhl_files, data_files, var="pres", max_layers=5) -> dict:
+    """The UMesh branch (convert_icon.cpp:393-452): per (cell, layer j) six vertices
+    bv1..bv3 at h1, tv1..tv3 at h2, every one carrying values[j]; one wedge of their indices.
+      h1 = (float)(R + hsurf*50)            j == 0   (double: hsurf is double)  (403-404)
+      h1 = (float)(R + (hhl_j - hsurf)*50)  j > 0    (hhl float, promoted)      (404-405)
+      h2 = (float)(R + (hhl_{j+1} - hsurf)*50)                                  (406)
+      x, y, z = (r*cosf(lat))*cosf(lon), (r*cosf(lat))*sinf(lon), r*sinf(lat)   (48-57)"""
+    cell = _dim(hgrid, "cell")
+    clat = _read(hgrid, "clat_vertices").reshape(cell, 3).astype(np.float32)
+    clon = _read(hgrid, "clon_vertices").reshape(cell, 3).astype(np.float32)
+    hs = _read(hsurf, "HSURF")
+    hhl = sorted(((int(np.trunc(_read(p, "height")[0])), _read(p, "HHL").astype(np.float32))
+                  for p in hhl_files), key=lambda t: -t[0])
+    vals = []
+    for p in data_files:
+        h = int(np.trunc(_read(p, "height")[0]))
+        v = _read(p, var)
+        mn = np.fmin.reduce(v, initial=np.finfo(np.float64).max)
+        mx = np.fmax.reduce(v, initial=-np.finfo(np.float64).max)
+        vals.append((h, ((v - mn) / (mx - mn))[:cell].astype(np.float32)))
+    vals.sort(key=lambda t: -t[0])
+    L = min(len(data_files), max_layers)
+    cosf, sinf = _glibc_trig()
+    cl, sl, co, so = cosf(clat), sinf(clat), cosf(clon), sinf(clon)
+    R64, S64 = float(np.float32(6.371229e6)), 50.0
+    verts = np.zeros((cell, L, 6, 3), np.float32)
+    scal = np.zeros((cell, L, 6), np.float32)
+    for j in range(L):
+        h1 = (R64 + hs * S64) if j == 0 else (R64 + (hhl[j][1].astype(np.float64) - hs) * S64)
+        h2 = R64 + (hhl[j + 1][1].astype(np.float64) - hs) * S64
+        for k in range(6):
+            r = (h1 if k < 3 else h2).astype(np.float32)
+            c = k % 3
+            verts[:, j, k, 0] = (r * cl[:, c]) * co[:, c]
+            verts[:, j, k, 1] = (r * cl[:, c]) * so[:, c]
+            verts[:, j, k, 2] = r * sl[:, c]
+            scal[:, j, k] = vals[j][1]
+    n = cell * L
+    return {"vertices": verts.reshape(n * 6, 3), "scalars": scal.reshape(n * 6),
+            "wedges": np.arange(n * 6, dtype=np.int32).reshape(n, 6)}

@@ -106,7 +106,7 @@ def test_convert_tool_writes_loadable_ic(tmp_path):
     r = subprocess.run([TOOL, "-hgrid", hg, "-hsurf", hs, "-hhl", *hhl, "-data", *data,
                         "-o", base, "--max-layers", "12"], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
-    assert "Not compiled with support for UMesh files!" in r.stderr
+    assert not os.path.exists(base + ".umesh")  # the UMesh branch only with --umesh
     cells = irt.load_ic(base + ".ic")
     assert same_records(cells, CO.convert(hg, hs, hhl, data, max_layers=12))
     info = irt.volume_info(cells)
@@ -152,3 +152,44 @@ def test_convert_rejects_crafted_header_sizes(tmp_path):
     huge = _cdf5(tmp_path / "huge.nc", [("cell", 1 << 40), ("nv", 3)], verts)
     with pytest.raises(irt.IrtError, match="too large"):
         irt.convert_icon(huge, hs, hhl, data)
+
+
+@pytest.mark.parametrize("levels,max_layers", [(6, 5), (8, 3), (31, 31)])
+def test_umesh_matches_restatement(tmp_path, levels, max_layers):
+    """The UMesh branch (convert_icon.cpp:393-452) vs the numpy restatement: vertex and
+    scalar bits, wedge indices, the file layout (parity unpinned: umesh is absent)."""
+    hg, hs, hhl, data = write_icon_set(str(tmp_path), levels=levels)
+    out = str(tmp_path / "o.umesh")
+    nv, nw = irt.convert_icon_umesh(hg, hs, hhl, data, out, max_layers=max_layers)
+    got = irt.read_umesh(out)
+    ref = CO.convert_umesh(hg, hs, hhl, data, max_layers=max_layers)
+    assert got["magic"] == 0x234235567
+    assert nw == ref["wedges"].shape[0] and nv == 6 * nw
+    assert np.array_equal(got["vertices"].view(np.uint32), ref["vertices"].view(np.uint32))
+    assert np.array_equal(got["scalars"].view(np.uint32), ref["scalars"].view(np.uint32))
+    assert np.array_equal(got["wedges"], ref["wedges"])
+    for k in ("triangles", "quads", "tets", "pyrs", "hexes"):
+        assert got[k].shape[0] == 0
+    # bottom below top where HHL ascends past the surface layer
+    v = got["vertices"].reshape(nw, 6, 3).astype(np.float64)
+    assert np.all(np.linalg.norm(v[:, 3:], axis=2) > 0)
+
+
+def test_umesh_needs_one_more_hhl_level(tmp_path):
+    """hhl[j+1] for every layer j < numLayers (convert_icon.cpp:406): one HHL file short is
+    an error here, an out-of-bounds read in the reference."""
+    hg, hs, hhl, data = write_icon_set(str(tmp_path), levels=6)
+    with pytest.raises(irt.IrtError):
+        irt.convert_icon_umesh(hg, hs, hhl[:5], data, str(tmp_path / "x.umesh"), max_layers=5)
+
+
+def test_umesh_cli(tmp_path):
+    hg, hs, hhl, data = write_icon_set(str(tmp_path), levels=6)
+    base = str(tmp_path / "cli")
+    r = subprocess.run([TOOL, "-hgrid", hg, "-hsurf", hs, "-hhl", *hhl, "-data", *data, "-o", base,
+                        "--umesh", "--no-ic"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    got = irt.read_umesh(base + ".umesh")
+    ref = CO.convert_umesh(hg, hs, hhl, data)
+    assert np.array_equal(got["vertices"].view(np.uint32), ref["vertices"].view(np.uint32))
+    assert not os.path.exists(base + ".ic")
