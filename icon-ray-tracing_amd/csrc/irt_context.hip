@@ -57,6 +57,9 @@ struct irt_context {
   bool slotBlock[32] = {};      // whether k_stats_out copied the slot's 16-counter block
   bool lastBlock = false;       // ... for the previous launch (which zeroed this slot's)
   bool wgCountsOn = true;       // IRT_COUNTERS=atomic: device-scope atomics instead
+  int countersProbe = 0;        // measurement only: IRT_COUNTERS=off (no counts), =device
+                                // (per-workgroup stores into device memory, never read)
+  uint32_t *d_probeCounts = nullptr;
   float4 *d_samples = nullptr;   // per-frame colours of a progressive batch
   size_t sampleCap = 0;
   float *d_srgb = nullptr;
@@ -424,6 +427,13 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     c->wgCap = numWG;
   }
   A.wgCounts = c->wgCountsOn ? c->dh_wgCounts + (size_t)slot * c->wgCap * kCnt : nullptr;
+  if (c->countersProbe == 1) {
+    A.wgCounts = nullptr;
+    A.counters = nullptr;
+  } else if (c->countersProbe == 2) {
+    if (!c->d_probeCounts) IRT_HIP(hipMalloc((void **)&c->d_probeCounts, c->wgCap * kCnt * sizeof(uint32_t)));
+    A.wgCounts = c->d_probeCounts;
+  }
   A.numSamples = numFrames;
   if (numFrames > 1) {
     const size_t need = lanes * (size_t)numFrames;
@@ -731,7 +741,10 @@ int irt_create_end(irt_context *c) {
     IRT_HIP(hipEventCreate(&c->evDone[i]));
   }
   memset(c->h_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long));
-  if (const char *e = getenv("IRT_COUNTERS")) c->wgCountsOn = strcmp(e, "atomic") != 0;
+  if (const char *e = getenv("IRT_COUNTERS")) {
+    c->wgCountsOn = strcmp(e, "atomic") != 0;
+    c->countersProbe = strcmp(e, "off") == 0 ? 1 : (strcmp(e, "device") == 0 ? 2 : 0);
+  }
   if (const char *e = getenv("IRT_TIMING_EVERY")) c->timingEvery = std::max(1, atoi(e));
   if (const char *e = getenv("IRT_COOP_MAXLG")) c->coopMaxLg = std::min(6, std::max(0, atoi(e)));
   if (const char *e = getenv("IRT_COOP_RAMP")) c->coopRamp = std::min(6, std::max(0, atoi(e)));
@@ -897,6 +910,7 @@ int irt_create_synth(int rootN, int bisections, int levels, float topHeight, flo
 
 void irt_destroy(irt_context *c) {
   if (!c) return;
+  if (c->d_probeCounts) (void)hipFree(c->d_probeCounts);
   free_all(c);
   delete c;
 }
