@@ -415,6 +415,17 @@ struct Tracer {
     for (uint32_t k = 0; k < p; ++k) m8 &= m8 - 1u;
     return (uint32_t)__builtin_ctz(m8);
   }
+  // inclusive prefix sum over the wave's 64 lanes in six DPP adds (row shifts within rows of
+  // 16, then the row broadcasts), no LDS round trips
+  __device__ __forceinline__ static uint32_t wave_incl_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+  }
   __device__ __forceinline__ bool locate_wave(bool want, float px, float py, float pz, float &value,
                                               CoopWave &CW, ScanWave &W) {
     want = want && A.numCells != 0;
@@ -426,6 +437,8 @@ struct Tracer {
     //   W.own[s] the lane whose tasks start at s (W.step, free after the round's prefix)
     uint32_t *own = reinterpret_cast<uint32_t *>(CW.step);
     uint32_t c = 0u;
+    uint32_t fe = 0u, flim = 0xFFFFFFFFu;  // the pass's first candidate entry, record limit
+    float fr = 0.f;                        // the sample's r
     bool hit = false, edge = false;
     if (want) {
       const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
@@ -447,17 +460,16 @@ struct Tracer {
       c = (uint32_t)__popc(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
       W.pt[lane] = make_float4(px, py, pz, r);
       W.lst[lane] = make_uint4(H0.w + beg, m8, 0u, 0xFFFFFFFFu);
+      fe = H0.w + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
+      fr = r;
     }
     for (int pass = 0;; ++pass) {
       // every lane: its list's first candidate
       uint32_t rem = 0u;
-      if (c > 0u) {
-        const uint4 d = W.lst[lane];
+      if (c > 0u) {  // (from registers: no LDS round trip before the gather)
         Found f;
-        const bool ok = pass_entry(A.fat + (size_t)(d.x + (d.y ? (uint32_t)__builtin_ctz(d.y) : (uint32_t)kMaskCand)) *
-                                               kFatStride4,
-                                   px, py, pz, W.pt[lane].w, f);
-        if (f.rec < d.w) {  // scan_fat stops, uncounted, at the first record >= the limit
+        const bool ok = pass_entry(A.fat + (size_t)fe * kFatStride4, px, py, pz, fr, f);
+        if (f.rec < flim) {  // scan_fat stops, uncounted, at the first record >= the limit
           ++specCand;
           if (ok) {
             hit = true;
@@ -472,12 +484,8 @@ struct Tracer {
       bool need = rem > 0u;
       for (uint64_t nm = __ballot(need); nm != 0ull; nm = __ballot(need)) {
         // deal the owners' untested candidates out to the lanes: exclusive prefix of rem
-        uint32_t incl = need ? rem : 0u;
-        for (int off = 1; off < 64; off <<= 1) {
-          const uint32_t y = (uint32_t)__shfl_up((int)incl, off, 64);
-          if (lane >= off) incl += y;
-        }
-        const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+        const uint32_t incl = wave_incl_sum(need ? rem : 0u);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint32_t start = incl - (need ? rem : 0u);
         const bool owns = need && start < 64u;
         own[lane] = 0xFFFFFFFFu;
@@ -543,7 +551,9 @@ struct Tracer {
         const uint32_t n = end - beg;
         const uint32_t m8 = (M >> (8 * b)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
         c = (uint32_t)__popc(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
-        W.lst[lane] = make_uint4(H0.w + beg, m8, 0u, hit ? W.frm[lane].x : 0xFFFFFFFFu);
+        flim = hit ? W.frm[lane].x : 0xFFFFFFFFu;
+        W.lst[lane] = make_uint4(H0.w + beg, m8, 0u, flim);
+        fe = H0.w + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
       }
     }
     if (!want) return false;
