@@ -474,7 +474,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   c->schedApplied += c->schedLastApplied ? 1 : 0;
   // the 16-counter block (device atomics) is only needed by the statistics variant and the
   // IRT_COUNTERS=atomic mode; it must start zeroed
-  const bool block = !c->wgCountsOn || (c->variant & 32768) != 0;
+  const bool block = !c->wgCountsOn || (c->variant & (32768 | 524288)) != 0;  // statistics, timing
   if (block && !c->lastBlock) IRT_HIP(hipMemsetAsync(A.counters, 0, 16 * sizeof(unsigned long long), s));
   if (c->launches > 0 && s != c->lastStream) {
     // this slot may have been zeroed by the previous launch's k_stats_out on another stream

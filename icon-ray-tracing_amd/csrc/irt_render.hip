@@ -36,6 +36,8 @@ enum : int {
                       // the default user-geometry/sphere kernel is render_pixel_coop
   OPT_SCAN1 = 131072, // the cooperative loop with each lane's candidate scan on its own
                       // (locate), for A/B against Tracer::locate_wave
+  OPT_TIMING = 524288,  // measurement only: per-wave shader-clock time by region into
+                        // counters[5..15] (Tracer::tmark)
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
@@ -121,6 +123,16 @@ struct Tracer {
   // the cooperative loop's statistics, per lane (samples taken, their locates / found /
   // candidate tests), added into s_cnt at the end by flush_coop
   uint32_t nLocate = 0, nFound = 0, nCand = 0;
+  // OPT_TIMING: shader clocks per region (wave-uniform), kTimeRegions of them
+  static constexpr int kTimeRegions = 9;
+  uint64_t tLast = 0, tAcc[kTimeRegions] = {};
+  __device__ __forceinline__ void tmark(int region) {
+    if constexpr ((OPT & OPT_TIMING) != 0) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      tAcc[region] += now - tLast;
+      tLast = now;
+    }
+  }
 
   // wave sum of a per-lane count from bit-slice ballots (no LDS, no shuffle chain)
   __device__ __forceinline__ static uint32_t wave_sum(uint32_t v) {
@@ -481,6 +493,7 @@ struct Tracer {
           }
         }
       }
+      tmark(3);  // header, first candidate
       bool need = rem > 0u;
       for (uint64_t nm = __ballot(need); nm != 0ull; nm = __ballot(need)) {
         // deal the owners' untested candidates out to the lanes: exclusive prefix of rem
@@ -534,6 +547,7 @@ struct Tracer {
         }
         __builtin_amdgcn_wave_barrier();
       }
+      tmark(4);  // the dealt-out candidates
       // the second pass: bin-edge samples, the next bin's list below the record found
       if (pass == 1 || __ballot(edge) == 0ull) break;
       c = 0u;
@@ -670,6 +684,7 @@ struct Tracer {
     // samplers, grid accel) keep whole-wave groups from the start: their misses come in
     // runs that wide groups cross in one round (2 % faster there, profiles/r02e_coop_cap).
     int lgCap = kMiss ? 6 : A.coopMaxLg;
+    tmark(6);  // between woodcockFunc calls (sdda leaves, ranges)
     for (;; lgCap = min(lgCap + A.coopRamp, 6)) {
       const uint64_t am = __ballot(active);
       if (am == 0ull) break;
@@ -733,12 +748,14 @@ struct Tracer {
       const bool past = used && tk > rq.y;
       bool found = false, acc = false;
       float value = 0.f;
+      tmark(2);  // round start: exchange, jumps, logf, prefix
       if constexpr (kWaveScan) {
         found = locate_wave(used && !past, A.org.x + ry.x * tk, A.org.y + ry.y * tk, A.org.z + ry.z * tk,
                             value, W, *SW);
       } else if (used && !past) {
         found = locate(A.org.x + ry.x * tk, A.org.y + ry.y * tk, A.org.z + ry.z * tk, value);
       }
+      tmark(5);  // locate's tail: sphere, getValue
       if (found) {
         const float sw = classify_alpha(value);  // postClassify(value).w
         acc = sw >= lcg_float(lcg_next(sk)) * rq.w;
@@ -813,6 +830,7 @@ struct Tracer {
       }
     }
     if (req) t = fminf(t, tmax);
+    tmark(7);  // the rounds' classify, LUT, ballots, outcomes
   }
 };
 
@@ -1231,6 +1249,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   float t = 0.f, upper = 0.f, tt1 = 0.f, maj = 0.f;
   bool lastRange = true, zeroLen = false, hit = false;
   bool miss = false;  // the cooperative loop's speculation mode, carried from leaf to leaf
+  bool first = true;  // OPT_TIMING
   // after a leaf without a hit: the next leaf of the range, or the next range
   // (render_pixel's loop tail, ShellAccel.h:201-226)
   auto next_leaf = [&]() {
@@ -1402,6 +1421,12 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     if (__ballot(req) == 0ull) break;
     float tw = t;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr ((OPT & OPT_TIMING) != 0) {
+      if (first) {
+        T.tmark(1);  // ray setup up to the first woodcockFunc
+        first = false;
+      }
+    }
     T.woodcock_wave(req, dx, dy, dz, tw, tt1, st, maj, !zeroLen, s, miss, W, SW, jmul, jadd);
     if (grid && req && phase == kWait && !ae) {
       if (tw > t && tw < tt1) {  // render_grid's hit test (deviceCode.cu:316)
@@ -1448,6 +1473,8 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   __shared__ float4 s_acc[256];     // kCoop: the accum pixels, prefetched
   __shared__ uint32_t s_jmul[kLcgJumps], s_jadd[kLcgJumps];
   const int tid = threadIdx.x;
+  uint64_t tStart = 0;
+  if constexpr ((OPT & OPT_TIMING) != 0) tStart = __builtin_amdgcn_s_memtime();
   // the prologue's global loads issued together, one wait (not one round trip each)
   const float th = A.srgbTh[tid];
   const LogfTab lt = kLogfTab[tid & 15];
@@ -1481,6 +1508,10 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   __syncthreads();
   Tracer<OPT> T{A, s_logf, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
   T.s_gbits = s_gbits;
+  if constexpr ((OPT & OPT_TIMING) != 0) {
+    T.tLast = tStart;
+    T.tmark(0);  // prologue
+  }
   const uint64_t c0 = A.schedCost ? wall_clock64() : 0;
   // grid.y = frame k of a progressive batch (accumID + k), whose colour goes to the sample
   // buffer for k_accumulate; a single frame writes accum/fb directly.  With measured-cost
@@ -1497,6 +1528,15 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   }
   else if (px.active)
     render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, A.accumID + (int)blockIdx.y, slot);
+  if constexpr ((OPT & OPT_TIMING) != 0) {
+    T.tmark(8);  // after the last woodcockFunc: pixel write, epilogue
+    if ((tid & 63) == 0) {
+      for (int k = 0; k < Tracer<OPT>::kTimeRegions; ++k)
+        atomicAdd(&A.counters[5 + k], (unsigned long long)T.tAcc[k]);
+      atomicAdd(&A.counters[14], (unsigned long long)(__builtin_amdgcn_s_memtime() - tStart));
+      atomicAdd(&A.counters[15], 1ull);
+    }
+  }
   if constexpr ((OPT & OPT_STATS) != 0) {
     // Woodcock draws and zero-length sdda leaves: sums, per-wave maxima, draws histogram
     uint32_t ss = T.cnt.steps, sm = T.cnt.steps, ds = T.cnt.deg, dm = T.cnt.deg;
@@ -1611,7 +1651,7 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
-#define IRT_VARIANTS(X) X(4096) X(5120) X(36864) X(70656) X(136192)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(36864) X(70656) X(136192) X(529408)
 
 bool render_variant_available(int v) {
 #define IRT_CASE(N) if (v == N) return true;

@@ -34,8 +34,9 @@ MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
 # compiled variants of the raygen (irt_render.hip OPT_* bits): 4096 no waves-per-SIMD
 # floor, 5120 the default (4 waves/SIMD), 36864 with per-wave statistics, 70656 the
 # one-lane-per-ray Woodcock loop instead of the wave-cooperative one, 136192 the cooperative
-# loop with per-lane candidate scans (no wave-wide scan); all bit-identical
-BIN_VARIANTS = (4096, 5120, 36864, 70656, 136192)
+# loop with per-lane candidate scans (no wave-wide scan), 529408 with per-region shader-clock
+# timing (profiles/probe.py); all bit-identical
+BIN_VARIANTS = (4096, 5120, 36864, 70656, 136192, 529408)
 
 
 class IrtError(RuntimeError):
