@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "irt_device.h"
 
 namespace irt {
@@ -111,8 +113,15 @@ __device__ __forceinline__ float coop_prefix(float t0, const float *d, int k) {
   return t;
 }
 
+// OPT_TIMING's per-wave region clocks (Tracer::tmark); empty in every other kernel
+struct TimeAccOff {};
+struct TimeAccOn {
+  static constexpr int kTimeRegions = 9;
+  uint64_t tLast = 0, tAcc[kTimeRegions] = {};
+};
+
 template <int OPT>
-struct Tracer {
+struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOff> {
   const RenderArgs &A;
   const LogfTab *s_logf;
   const uint32_t *s_sph;
@@ -123,14 +132,12 @@ struct Tracer {
   // the cooperative loop's statistics, per lane (samples taken, their locates / found /
   // candidate tests), added into s_cnt at the end by flush_coop
   uint32_t nLocate = 0, nFound = 0, nCand = 0;
-  // OPT_TIMING: shader clocks per region (wave-uniform), kTimeRegions of them
-  static constexpr int kTimeRegions = 9;
-  uint64_t tLast = 0, tAcc[kTimeRegions] = {};
+  // OPT_TIMING: shader clocks per region (wave-uniform), in the TimeAcc base
   __device__ __forceinline__ void tmark(int region) {
     if constexpr ((OPT & OPT_TIMING) != 0) {
       const uint64_t now = __builtin_amdgcn_s_memtime();
-      tAcc[region] += now - tLast;
-      tLast = now;
+      this->tAcc[region] += now - this->tLast;
+      this->tLast = now;
     }
   }
 
@@ -1506,7 +1513,7 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
     for (int k = 0; k < kGridBitWords / 256; ++k) s_gbits[tid + 256 * k] = A.gridBits[tid + 256 * k];
   }
   __syncthreads();
-  Tracer<OPT> T{A, s_logf, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
+  Tracer<OPT> T{{}, A, s_logf, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
   T.s_gbits = s_gbits;
   if constexpr ((OPT & OPT_TIMING) != 0) {
     T.tLast = tStart;
@@ -1531,7 +1538,7 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   if constexpr ((OPT & OPT_TIMING) != 0) {
     T.tmark(8);  // after the last woodcockFunc: pixel write, epilogue
     if ((tid & 63) == 0) {
-      for (int k = 0; k < Tracer<OPT>::kTimeRegions; ++k)
+      for (int k = 0; k < TimeAccOn::kTimeRegions; ++k)
         atomicAdd(&A.counters[5 + k], (unsigned long long)T.tAcc[k]);
       atomicAdd(&A.counters[14], (unsigned long long)(__builtin_amdgcn_s_memtime() - tStart));
       atomicAdd(&A.counters[15], 1ull);
@@ -1628,7 +1635,7 @@ __global__ void __launch_bounds__(256) k_debug_locate(RenderArgs A, const float 
   for (int i = threadIdx.x; i < kSphBitWords; i += 256) s_sph[i] = A.numSph ? A.sphBits[i] : 0u;
   if (threadIdx.x < kCnt) s_cnt[threadIdx.x] = 0;
   __syncthreads();
-  Tracer<kDefaultVariant & ~4096> T{A, nullptr, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
+  Tracer<kDefaultVariant & ~4096> T{{}, A, nullptr, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
   const int j = (int)(blockIdx.x * 256 + threadIdx.x);
   if (j < n) {
     float v = 0.f;
