@@ -141,13 +141,21 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     }
   }
 
-  // wave sum of a per-lane count from bit-slice ballots (no LDS, no shuffle chain)
+  // wave sum of a per-lane count: the DPP prefix sum's last lane (wave_incl_sum)
   __device__ __forceinline__ static uint32_t wave_sum(uint32_t v) {
-    uint32_t sum = 0;
-    for (int b = 0; __ballot(v >> b) != 0ull; ++b) sum += (uint32_t)__popcll(__ballot((v >> b) & 1u)) << b;
-    return sum;
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(v), 63);
   }
-  // (per-lane LDS atomics on one address serialise: +17 us per C3 frame measured)
+  // inclusive prefix sum over the wave's 64 lanes in six DPP adds (row shifts within rows of
+  // 16, then the row broadcasts), no LDS round trips
+  __device__ __forceinline__ static uint32_t wave_incl_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+  }
   __device__ __forceinline__ void flush_coop() {
     const uint32_t a = wave_sum(nLocate), b = wave_sum(nFound), c = wave_sum(nCand);
     if (__lane_id() == 0) {
@@ -433,17 +441,6 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     if (p >= nm) return (uint32_t)kMaskCand + (p - nm);
     for (uint32_t k = 0; k < p; ++k) m8 &= m8 - 1u;
     return (uint32_t)__builtin_ctz(m8);
-  }
-  // inclusive prefix sum over the wave's 64 lanes in six DPP adds (row shifts within rows of
-  // 16, then the row broadcasts), no LDS round trips
-  __device__ __forceinline__ static uint32_t wave_incl_sum(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return v;
   }
   __device__ __forceinline__ bool locate_wave(bool want, float px, float py, float pz, float &value,
                                               CoopWave &CW, ScanWave &W) {
