@@ -96,8 +96,6 @@ struct CoopWave {
 struct ScanWave {
   float4 pt[64];    // lane l's sample {point, r}
   uint4 lst[64];    // its candidate list {first entry, sub-cell mask, next position, record limit}
-  float4 fck[64];   // the record found: coarse keys
-  uint2 frm[64];    // {record, meta}
 };
 
 // t0 - d[0] - d[1] - ... - d[k], subtracted one at a time as woodcockTracking's `t -=`
@@ -449,9 +447,12 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     // The scan's state lives in the wave's LDS (fewer live VGPRs across it):
     //   W.pt[l]  the sample {point, r} of lane l
     //   W.lst[l] its list {first entry, sub-cell mask, next list position, record limit}
-    //   W.fck[l], W.frm[l]  the record found so far: coarse keys, {record, meta}
+    //   fck[l], frm[l]  the record found so far: coarse keys, {record, meta} (in the round's
+    //            request slots CW.req / CW.ray, free once the round has read them)
     //   W.own[s] the lane whose tasks start at s (W.step, free after the round's prefix)
     uint32_t *own = reinterpret_cast<uint32_t *>(CW.step);
+    float4 *fck = CW.req;
+    uint2 *frm = reinterpret_cast<uint2 *>(CW.ray);
     uint32_t c = 0u;
     uint32_t fe = 0u, flim = 0xFFFFFFFFu;  // the pass's first candidate entry, record limit
     float fr = 0.f;                        // the sample's r
@@ -489,8 +490,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
           ++specCand;
           if (ok) {
             hit = true;
-            W.fck[lane] = f.ck;
-            W.frm[lane] = make_uint2(f.rec, f.meta);
+            fck[lane] = f.ck;
+            frm[lane] = make_uint2(f.rec, f.meta);
           } else {
             rem = c - 1u;
             W.lst[lane].z = 1u;
@@ -529,8 +530,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         // the lowest event of each owner's tasks: a passing record (it hands it over) or the limit
         const uint64_t below = t ? (~0ull >> (64u - t)) : 0ull;  // tasks < t
         if (tp && ((pm | lm) & below & (~0ull << s0)) == 0ull) {
-          W.fck[o] = g.ck;
-          W.frm[o] = make_uint2(g.rec, g.meta);
+          fck[o] = g.ck;
+          frm[o] = make_uint2(g.rec, g.meta);
         }
         __builtin_amdgcn_wave_barrier();
         if (owns) {
@@ -569,7 +570,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         const uint32_t n = end - beg;
         const uint32_t m8 = (M >> (8 * b)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
         c = (uint32_t)__popc(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
-        flim = hit ? W.frm[lane].x : 0xFFFFFFFFu;
+        flim = hit ? frm[lane].x : 0xFFFFFFFFu;
         W.lst[lane] = make_uint4(H0.w + beg, m8, 0u, flim);
         fe = H0.w + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
       }
@@ -578,8 +579,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     const float r = W.pt[lane].w;
     Found f = {0xFFFFFFFFu, 0u, make_float4(0.f, 0.f, 0.f, 0.f)};
     if (hit) {
-      const uint2 rm = W.frm[lane];
-      f = {rm.x, rm.y, W.fck[lane]};
+      const uint2 rm = frm[lane];
+      f = {rm.x, rm.y, fck[lane]};
     }
     if (A.numSph) {
       const uint32_t h = sph_hash(r);
