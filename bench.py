@@ -294,7 +294,9 @@ def main():
         fg = irt_dist.FrameGather(split, dev, buffers=2, stage_cpu=args.dist_backend == "gloo")
         tiles_acc = torch.zeros(maxt * 4096 * 4, dtype=torch.float32, device=dev)
         fb = torch.zeros(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
-    inflight = {}
+    pipe = None
+    if dist_path:
+        pipe = irt_dist.FramePipeline(ctx, fg, fb)
 
     def step(s):
         lp.accumID = s * frames
@@ -305,25 +307,15 @@ def main():
         if not dist_path:
             ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
             return
-        b = s % 2
-        if b in inflight:  # the gather that last read this buffer must be done
-            finish(inflight.pop(b), b)
         if strong:
-            ctx.render_tiles(lp, W, H, rank, world, fg.bufs[b].data_ptr(), tiles_acc.data_ptr(),
-                             stream)
+            pipe.step(s, lambda buf: ctx.render_tiles(lp, W, H, rank, world, buf.data_ptr(),
+                                                      tiles_acc.data_ptr(), stream))
         else:
-            ctx.render_tiles_accumulate(lp, W, H, rank, world, frames, fg.bufs[b].data_ptr(),
-                                        tiles_acc.data_ptr(), stream)
-        inflight[b] = (s, fg.gather_async(b))  # RCCL gather of this step's frame, overlapped
+            pipe.step(s, lambda buf: ctx.render_tiles_accumulate(
+                lp, W, H, rank, world, frames, buf.data_ptr(), tiles_acc.data_ptr(), stream))
 
-    def finish(pending, b):
-        g = fg.finish(pending[1], b)
-        if rank == 0:
-            ctx.unpack_tiles(g.data_ptr(), world, maxt, W, H, fb.data_ptr(), stream)
-
-    def drain():  # oldest gather first: rank 0's framebuffer ends with the newest frame
-        for b in sorted(inflight, key=lambda k: inflight[k][0]):
-            finish(inflight.pop(b), b)
+    def drain():
+        pipe.drain()
 
     for f in range(args.warmup):
         step(f)

@@ -113,3 +113,63 @@ class FrameGather:
         """Collective: every rank calls it after rendering into self.tiles.  On rank 0
         returns the rank-major gathered tensor, elsewhere None."""
         return self.finish(self.gather_async(0), 0)
+
+
+class FramePipeline:
+    """The multi-rank step loop bench.py runs (and tests/test_gpu_distributed.py checks):
+    two frames in flight through a double-buffered FrameGather.  Step s renders into packed
+    buffer b = s % 2 on the current (render) stream and starts the RCCL gather of that
+    buffer; the gather of step s-2 (same buffer) is finished first.  On rank 0 the gather is
+    issued from a side stream, which also runs the unpack of the frame received two steps
+    earlier: the render stream never waits behind an unpack or a cross-stream event of its
+    own (it only waits, for buffer reuse, on the gather that read the buffer it renders
+    into), so the unpack (~5 us of a ~0.1 ms C3 step) overlaps the next render."""
+
+    def __init__(self, ctx, fg: FrameGather, fb, side_stream: bool = True):
+        import torch
+        self.torch, self.ctx, self.fg, self.fb = torch, ctx, fg, fb
+        self.split = fg.split
+        self.inflight = {}
+        self.rank0 = self.split.rank == 0
+        self.side = torch.cuda.Stream() if (side_stream and self.rank0) else None
+
+    def _unpack(self, g, stream):
+        sp = self.split
+        self.ctx.unpack_tiles(g.data_ptr(), sp.world, sp.max_tiles, sp.width, sp.height,
+                              self.fb.data_ptr(), stream)
+
+    def _finish(self, b):
+        torch = self.torch
+        _, work = self.inflight.pop(b)
+        if self.side is None:
+            g = self.fg.finish(work, b)  # the current stream waits for the gather
+            if self.rank0:
+                self._unpack(g, torch.cuda.current_stream().cuda_stream)
+            return
+        work.wait()  # the render stream: the send buffer it renders into next is free
+        with torch.cuda.stream(self.side):  # the side stream: the received frame is complete
+            g = self.fg.finish(work, b)
+            self._unpack(g, self.side.cuda_stream)
+
+    def step(self, s: int, render):
+        """render(buf): this rank's tiles of step s into the packed buffer `buf`."""
+        torch = self.torch
+        b = s % 2
+        if b in self.inflight:
+            self._finish(b)
+        render(self.fg.bufs[b])
+        if self.side is None:
+            work = self.fg.gather_async(b)
+        else:  # ordered after this render and after the unpack that last read gathered[b]
+            self.side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.side):
+                work = self.fg.gather_async(b)
+        self.inflight[b] = (s, work)
+
+    def drain(self):
+        """Finish every gather in flight, oldest first: rank 0's framebuffer ends with the
+        newest frame."""
+        for b in sorted(self.inflight, key=lambda k: self.inflight[k][0]):
+            self._finish(b)
+        if self.side is not None:
+            self.torch.cuda.current_stream().wait_stream(self.side)

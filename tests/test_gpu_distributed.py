@@ -2,7 +2,8 @@
 host-staged collectives, both ranks on cuda:0) render their interleaved 64x64 tiles
 through irt_render_tiles / irt_render_tiles_accumulate on torch's default stream, gather
 them to rank 0 with irt_dist.FrameGather (two frames in flight, rank-major receive
-buffers), and rank 0 unpacks them with irt_unpack_tiles -- bench.py's two multi-GPU modes:
+buffers), and rank 0 unpacks them with irt_unpack_tiles on a side stream
+(irt_dist.FramePipeline, the loop bench.py runs) -- bench.py's two multi-GPU modes:
   * frame       one frame per step split over the ranks (strong scaling),
   * progressive N progressive frames per step, each rank rendering its tiles of all N
                 (weak scaling).
@@ -51,26 +52,16 @@ def _worker(rank, world, port, mode, out_path):
     acc = torch.zeros(split.max_tiles * 4096 * 4, dtype=torch.float32, device="cuda:0")
     fb = torch.zeros(W * H, dtype=torch.int32, device="cuda:0")
     frames = 1 if mode == "frame" else world
-    inflight = {}
-
-    def finish(b):
-        g = fg.finish(inflight.pop(b)[1], b)
-        if rank == 0:  # NULL stream: ordered after the default-stream copy of the gather
-            ctx.unpack_tiles(g.data_ptr(), world, split.max_tiles, W, H, fb.data_ptr())
-
+    pipe = irt_dist.FramePipeline(ctx, fg, fb)  # bench.py's loop: rank 0 unpacks on a side stream
     for s in range(STEPS):
-        b = s % 2
-        if b in inflight:
-            finish(b)
         lp.accumID = s * frames
         if mode == "frame":
-            ctx.render_tiles(lp, W, H, rank, world, fg.bufs[b].data_ptr(), acc.data_ptr())
+            pipe.step(s, lambda buf: ctx.render_tiles(lp, W, H, rank, world, buf.data_ptr(),
+                                                      acc.data_ptr()))
         else:
-            ctx.render_tiles_accumulate(lp, W, H, rank, world, frames, fg.bufs[b].data_ptr(),
-                                        acc.data_ptr())
-        inflight[b] = (s, fg.gather_async(b))
-    for b in sorted(inflight, key=lambda k: inflight[k][0]):  # oldest first
-        finish(b)
+            pipe.step(s, lambda buf: ctx.render_tiles_accumulate(lp, W, H, rank, world, frames,
+                                                                 buf.data_ptr(), acc.data_ptr()))
+    pipe.drain()
     if rank == 0:
         torch.cuda.synchronize()
         np.save(out_path, fb.cpu().numpy())
