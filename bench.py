@@ -291,7 +291,7 @@ def main():
         split = irt_dist.TileSplit(W, H, rank, world)
         assert split.num_tiles == ntiles
         maxt = split.max_tiles
-        fg = irt_dist.FrameGather(split, dev, buffers=2, stage_cpu=args.dist_backend == "gloo")
+        fg = irt_dist.FrameGather(split, dev, buffers=8, stage_cpu=args.dist_backend == "gloo")
         tiles_acc = torch.zeros(maxt * 4096 * 4, dtype=torch.float32, device=dev)
         fb = torch.zeros(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
     pipe = None

@@ -116,60 +116,74 @@ class FrameGather:
 
 
 class FramePipeline:
-    """The multi-rank step loop bench.py runs (and tests/test_gpu_distributed.py checks):
-    two frames in flight through a double-buffered FrameGather.  Step s renders into packed
-    buffer b = s % 2 on the current (render) stream and starts the RCCL gather of that
-    buffer; the gather of step s-2 (same buffer) is finished first.  On rank 0 the gather is
-    issued from a side stream, which also runs the unpack of the frame received two steps
-    earlier: the render stream never waits behind an unpack or a cross-stream event of its
-    own (it only waits, for buffer reuse, on the gather that read the buffer it renders
-    into), so the unpack (~5 us of a ~0.1 ms C3 step) overlaps the next render."""
+    """The multi-rank step loop bench.py runs (and tests/test_gpu_distributed.py checks).
+    Step s renders this rank's tiles into packed buffer b = s mod 2K on the current (render)
+    stream and starts the RCCL gather of that buffer; K = `batch`.
+      * Buffer reuse: the render into b must follow the gather that read b 2K steps earlier.
+        Gathers of one process group run in order on one collective stream, so the render
+        stream waits once per K steps, on the newest gather of the previous half-cycle,
+        instead of once per step: each cross-queue wait costs the render stream ~20 us of
+        idle time per step (profiles/r02j_dist/), more than the unpack it used to carry.
+      * Rank 0 issues its gathers from a side stream, which also waits for each received
+        frame and unpacks it into the framebuffer (in step order: the framebuffer ends with
+        the newest frame), overlapping the renders; the next gather into a receive buffer
+        follows that buffer's unpack on the same stream."""
 
-    def __init__(self, ctx, fg: FrameGather, fb, side_stream: bool = True):
+    def __init__(self, ctx, fg: FrameGather, fb, batch: int = 4):
         import torch
         self.torch, self.ctx, self.fg, self.fb = torch, ctx, fg, fb
         self.split = fg.split
-        self.inflight = {}
+        self.k = max(1, batch)
+        assert len(fg.bufs) == 2 * self.k, "FrameGather needs buffers = 2 * batch"
+        self.works = {}    # step -> pending gather
+        self.pending = []  # rank 0: steps gathered, not yet unpacked (oldest first)
         self.rank0 = self.split.rank == 0
-        self.side = torch.cuda.Stream() if (side_stream and self.rank0) else None
+        self.side = torch.cuda.Stream() if self.rank0 else None
+        self.host_staged = fg.stage_cpu
 
-    def _unpack(self, g, stream):
-        sp = self.split
-        self.ctx.unpack_tiles(g.data_ptr(), sp.world, sp.max_tiles, sp.width, sp.height,
-                              self.fb.data_ptr(), stream)
-
-    def _finish(self, b):
-        torch = self.torch
-        _, work = self.inflight.pop(b)
-        if self.side is None:
-            g = self.fg.finish(work, b)  # the current stream waits for the gather
-            if self.rank0:
-                self._unpack(g, torch.cuda.current_stream().cuda_stream)
-            return
-        work.wait()  # the render stream: the send buffer it renders into next is free
-        with torch.cuda.stream(self.side):  # the side stream: the received frame is complete
-            g = self.fg.finish(work, b)
-            self._unpack(g, self.side.cuda_stream)
+    def _unpack_upto(self, last):
+        """Rank 0, side stream: wait for and unpack the frames of steps <= last."""
+        torch, sp = self.torch, self.split
+        while self.pending and self.pending[0] <= last:
+            t = self.pending.pop(0)
+            b = t % len(self.fg.bufs)
+            with torch.cuda.stream(self.side):
+                g = self.fg.finish(self.works[t], b)
+                self.ctx.unpack_tiles(g.data_ptr(), sp.world, sp.max_tiles, sp.width, sp.height,
+                                      self.fb.data_ptr(), self.side.cuda_stream)
 
     def step(self, s: int, render):
         """render(buf): this rank's tiles of step s into the packed buffer `buf`."""
         torch = self.torch
-        b = s % 2
-        if b in self.inflight:
-            self._finish(b)
+        nb = len(self.fg.bufs)
+        b = s % nb
+        if b % self.k == 0:  # buffers b .. b+K-1 were last read by the gathers s-2K .. s-K-1
+            newest = s - self.k - 1
+            for t in [t for t in self.works if t <= newest]:
+                if t == newest or self.host_staged:
+                    self.works[t].wait()  # the render stream (in-order collectives: one wait)
+                if not self.rank0:
+                    del self.works[t]
+        if self.rank0:
+            self._unpack_upto(s - 2)
+            for t in [t for t in self.works if t <= s - 2 * self.k]:
+                del self.works[t]
         render(self.fg.bufs[b])
-        if self.side is None:
-            work = self.fg.gather_async(b)
-        else:  # ordered after this render and after the unpack that last read gathered[b]
+        if self.rank0:  # ordered after this render and after earlier unpacks of gathered[b]
             self.side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self.side):
-                work = self.fg.gather_async(b)
-        self.inflight[b] = (s, work)
+                self.works[s] = self.fg.gather_async(b)
+            self.pending.append(s)
+        else:
+            self.works[s] = self.fg.gather_async(b)
 
     def drain(self):
-        """Finish every gather in flight, oldest first: rank 0's framebuffer ends with the
-        newest frame."""
-        for b in sorted(self.inflight, key=lambda k: self.inflight[k][0]):
-            self._finish(b)
-        if self.side is not None:
-            self.torch.cuda.current_stream().wait_stream(self.side)
+        """Finish every gather in flight and unpack the frames still pending, oldest first."""
+        torch = self.torch
+        last = max(self.works) if self.works else -1
+        if self.rank0:
+            self._unpack_upto(last)
+            torch.cuda.current_stream().wait_stream(self.side)
+        for t in sorted(self.works):
+            self.works[t].wait()
+        self.works.clear()

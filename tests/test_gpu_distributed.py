@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 GRID = (2, 3, 47)
 W, H = 200, 136  # ragged: partial tiles on the right and bottom
-STEPS = 3
+STEPS = 11  # past two reuse cycles of the 8 packed buffers (FramePipeline batch 4)
 
 
 def _free_port():
@@ -48,7 +48,7 @@ def _worker(rank, world, port, mode, out_path):
     ctx.set_transfunc(setup.lut, setup.value_range)
     lp = setup.lp
     split = irt_dist.TileSplit(W, H, rank, world)
-    fg = irt_dist.FrameGather(split, "cuda:0", buffers=2, stage_cpu=True)
+    fg = irt_dist.FrameGather(split, "cuda:0", buffers=8, stage_cpu=True)
     acc = torch.zeros(split.max_tiles * 4096 * 4, dtype=torch.float32, device="cuda:0")
     fb = torch.zeros(W * H, dtype=torch.int32, device="cuda:0")
     frames = 1 if mode == "frame" else world
