@@ -1221,7 +1221,7 @@ extern "C" int irt_debug_device_srgb(int device, const float *x, uint32_t *out, 
   return IRT_OK;
 }
 
-extern "C" int irt_debug_locate(irt_context *c, const float *xyz, int n, int *found, float *value) {
+static int debug_locate(irt_context *c, const float *xyz, int n, int *found, float *value, bool wave) {
   if (!c || !xyz || !found || !value || n < 0) {
     set_error("irt_debug_locate: bad argument");
     return IRT_E_INVALID;
@@ -1245,7 +1245,7 @@ extern "C" int irt_debug_locate(irt_context *c, const float *xyz, int n, int *fo
   int *dFound = reinterpret_cast<int *>(d + 3 * (size_t)n);
   float *dValue = d + 4 * (size_t)n;
   if (e == hipSuccess) {
-    launch_debug_locate(A, d, n, dFound, dValue, 0);
+    launch_debug_locate(A, d, n, dFound, dValue, 0, wave);
     e = hipGetLastError();
   }
   e = e == hipSuccess ? hipMemcpy(found, dFound, (size_t)n * sizeof(int), hipMemcpyDeviceToHost) : e;
@@ -1256,6 +1256,14 @@ extern "C" int irt_debug_locate(irt_context *c, const float *xyz, int n, int *fo
     return IRT_E_HIP;
   }
   return IRT_OK;
+}
+
+extern "C" int irt_debug_locate(irt_context *c, const float *xyz, int n, int *found, float *value) {
+  return debug_locate(c, xyz, n, found, value, false);
+}
+
+extern "C" int irt_debug_locate_wave(irt_context *c, const float *xyz, int n, int *found, float *value) {
+  return debug_locate(c, xyz, n, found, value, true);
 }
 
 extern "C" int irt_debug_sched(irt_context *c, int *policy, int *lastApplied, long long *applied) {

@@ -86,7 +86,7 @@ constexpr int kDefaultVariant = 5120;  // one kernel per frame, 4 waves/SIMD: fa
 bool render_variant_available(int variant);
 void launch_render(const RenderArgs &A, int numBlocks, hipStream_t s, int variant);
 void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *found, float *value,
-                         hipStream_t s);
+                         hipStream_t s, bool wave);
 void launch_shell_init(float *valueRanges, size_t numMCs, hipStream_t s);
 void launch_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, float3 lo, float3 hi,
                         float *valueRanges, hipStream_t s);

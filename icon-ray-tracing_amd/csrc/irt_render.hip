@@ -1642,9 +1642,43 @@ __global__ void __launch_bounds__(256) k_debug_locate(RenderArgs A, const float 
   }
 }
 
+// The same points through the cooperative kernel's wave-wide candidate scan
+// (Tracer::locate_wave; every lane of a wave calls it, lanes past n with want = false):
+// pins its dealt-out candidates and its second pass on radial bin edges to the serial path.
+__global__ void __launch_bounds__(256) k_debug_locate_wave(RenderArgs A, const float *xyz, int n,
+                                                           int *found, float *value) {
+  __shared__ uint32_t s_sph[kSphBitWords];
+  __shared__ uint32_t s_cnt[kCnt];
+  __shared__ CoopWave s_coop[4];
+  __shared__ ScanWave s_scan[4];
+  for (int i = threadIdx.x; i < kSphBitWords; i += 256) s_sph[i] = A.numSph ? A.sphBits[i] : 0u;
+  if (threadIdx.x < kCnt) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  Tracer<kDefaultVariant & ~4096> T{{}, A, nullptr, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
+  static_assert(Tracer<kDefaultVariant & ~4096>::kWaveScan, "the default kernel scans wave-wide");
+  const int j = (int)(blockIdx.x * 256 + threadIdx.x);
+  const bool want = j < n;
+  float x = 0.f, y = 0.f, z = 0.f;
+  if (want) {
+    x = xyz[3 * j];
+    y = xyz[3 * j + 1];
+    z = xyz[3 * j + 2];
+  }
+  float v = 0.f;
+  const bool f = T.locate_wave(want, x, y, z, v, s_coop[threadIdx.x >> 6], s_scan[threadIdx.x >> 6]);
+  if (want) {
+    found[j] = f ? 1 : 0;
+    value[j] = v;
+  }
+}
+
 void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *found, float *value,
-                         hipStream_t s) {
-  if (n > 0) hipLaunchKernelGGL(k_debug_locate, dim3((n + 255) / 256), dim3(256), 0, s, A, xyz, n, found, value);
+                         hipStream_t s, bool wave) {
+  if (n <= 0) return;
+  if (wave)
+    hipLaunchKernelGGL(k_debug_locate_wave, dim3((n + 255) / 256), dim3(256), 0, s, A, xyz, n, found, value);
+  else
+    hipLaunchKernelGGL(k_debug_locate, dim3((n + 255) / 256), dim3(256), 0, s, A, xyz, n, found, value);
 }
 
 // ------------------------------------------------------------------ variants / launcher

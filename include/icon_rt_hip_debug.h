@@ -108,6 +108,10 @@ int irt_debug_device_srgb(int device, const float *x, uint32_t *out, int n);
 /* The render kernel's point location (sampleVolume over the context's binned lists,
  * csrc/irt_render.hip Tracer::locate) for n points xyz[3i..3i+2]: found[i] 0/1, value[i]. */
 int irt_debug_locate(irt_context *ctx, const float *xyz, int n, int *found, float *value);
+/* The same through the cooperative kernel's wave-wide candidate scan (Tracer::locate_wave):
+ * the first candidates tested per lane, the rest dealt out over the wave, the second pass
+ * for points exactly on a radial bin edge.  Must equal irt_debug_locate point for point. */
+int irt_debug_locate_wave(irt_context *ctx, const float *xyz, int n, int *found, float *value);
 /* Measured-cost scheduling state: the policy (IRT_SCHED; 0 = off), whether the last launch
  * ran its workgroups in a measured-cost order, and how many launches have. */
 int irt_debug_sched(irt_context *ctx, int *policy, int *lastApplied, long long *applied);

@@ -548,13 +548,17 @@ def test_device_srgb_byte_equals_threshold_count():
     assert bad.size == 0, (x[bad[:5]], out[bad[:5]], want[bad[:5]])
 
 
+@pytest.mark.parametrize("entry", ["irt_debug_locate", "irt_debug_locate_wave"])
 @pytest.mark.parametrize("scene", ["r2b03_l90", "terrain", "filtered"])
-def test_device_locator_matches_host_restatement(scene):
-    """The kernel's point location (Tracer::locate through irt_debug_locate) == the host
-    restatement of the binned lists (which tests/test_host_logic.py pins to the reference's
-    brute-force first hit), point for point: found flag and value bits, including points
-    exactly on record boundaries = radial bin edges (the second-bin pass), their float
-    neighbours, shared triangle edges and zero-thickness records."""
+def test_device_locator_matches_host_restatement(scene, entry):
+    """The kernel's point location == the host restatement of the binned lists (which
+    tests/test_host_logic.py pins to the reference's brute-force first hit), point for
+    point: found flag and value bits, including points exactly on record boundaries =
+    radial bin edges (the second-bin pass), their float neighbours, shared triangle edges
+    and zero-thickness records.  Two device paths: Tracer::locate (one lane per point,
+    irt_debug_locate) and the cooperative kernel's wave-wide scan Tracer::locate_wave
+    (irt_debug_locate_wave: dealt-out candidates and the bin-edge pass, many of them in
+    one wave here)."""
     from helpers import locator_points, terrain_cells
     cells = {"r2b03_l90": lambda: irt.synth_grid(2, 3, 90),
              "terrain": lambda: terrain_cells(11),
@@ -563,11 +567,12 @@ def test_device_locator_matches_host_restatement(scene):
     ctx = irt.Context(cells, 0)
     D = irt.DebugScene(cells)
     L = irt.lib()
-    L.irt_debug_locate.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    fn = getattr(L, entry)
+    fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
     found = np.zeros(len(pts), np.int32)
     value = np.zeros(len(pts), np.float32)
-    assert L.irt_debug_locate(ctx._h, pts.ctypes.data, len(pts), found.ctypes.data,
-                              value.ctypes.data) == 0, L.irt_last_error()
+    assert fn(ctx._h, pts.ctypes.data, len(pts), found.ctypes.data, value.ctypes.data) == 0, \
+        L.irt_last_error()
     n_hit = 0
     for k, p in enumerate(pts):
         hb, vb, _, _ = D.locate_binned(p)
