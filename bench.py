@@ -288,7 +288,10 @@ def main():
         ctx.clear(fb.data_ptr(), accum.data_ptr(), W * H, stream)
     else:
         import irt_dist
-        split = irt_dist.TileSplit(W, H, rank, world)
+        # the cost-balanced deal (irt_deal_tiles) for the first camera: the orbit keeps the
+        # globe centred at the same size, so one deal serves every step
+        split = irt_dist.TileSplit.dealt(W, H, rank, world, orbit[0] if orbit else setup.lp, info,
+                                         frames)
         assert split.num_tiles == ntiles
         maxt = split.max_tiles
         fg = irt_dist.FrameGather(split, dev, buffers=8, stage_cpu=args.dist_backend == "gloo")
@@ -307,12 +310,8 @@ def main():
         if not dist_path:
             ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
             return
-        if strong:
-            pipe.step(s, lambda buf: ctx.render_tiles(lp, W, H, rank, world, buf.data_ptr(),
-                                                      tiles_acc.data_ptr(), stream))
-        else:
-            pipe.step(s, lambda buf: ctx.render_tiles_accumulate(
-                lp, W, H, rank, world, frames, buf.data_ptr(), tiles_acc.data_ptr(), stream))
+        pipe.step(s, lambda buf: split.render(ctx, lp, frames, buf.data_ptr(),
+                                              tiles_acc.data_ptr(), stream))
 
     def drain():
         pipe.drain()
@@ -367,10 +366,10 @@ def main():
         if world == 1 and not dist_path:
             parallelism = "single GPU"
         elif strong:
-            parallelism = (f"{world} GPUs x 64x64 interleaved tiles of ONE frame per step, RCCL "
+            parallelism = (f"{world} GPUs x 64x64 cost-balanced tiles of ONE frame per step, RCCL "
                            f"gather of the RGBA8 tiles to rank 0 overlapped with the next step")
         else:
-            parallelism = (f"{world} GPUs x 64x64 interleaved frame tiles, {frames} progressive "
+            parallelism = (f"{world} GPUs x 64x64 cost-balanced frame tiles, {frames} progressive "
                            f"frames per step in one launch per rank, RCCL gather of the final "
                            f"RGBA8 tiles to rank 0 overlapped with the next step")
         out = {

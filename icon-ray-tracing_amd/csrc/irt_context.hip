@@ -143,6 +143,14 @@ struct irt_context {
     int32_t nl;
   };
   std::vector<Sphere> sph;  // zero-thickness records
+  // device copies of the explicit tile lists / tables of irt_render_tile_list and
+  // irt_unpack_tile_table, keyed by content (a multi-GPU deal is fixed for a run: uploaded
+  // once, never rewritten while a launch may read it)
+  struct TileTable {
+    std::vector<int32_t> ids;
+    int32_t *dev;
+  };
+  std::vector<TileTable> tileTables;
 };
 
 namespace {
@@ -183,7 +191,40 @@ void free_all(irt_context *c) {
     if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
     if (c->evDone[i]) (void)hipEventDestroy(c->evDone[i]);
   }
+  for (auto &t : c->tileTables) (void)hipFree(t.dev);
+  c->tileTables.clear();
   if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+// The device copy of a tile list / table (see irt_context::tileTables): found by content, or
+// uploaded (synchronously: a new allocation no launch in flight can be reading).  Entries
+// must be in [lo, total).
+int tile_table(irt_context *c, const int32_t *ids, size_t n, int lo, int total, const int32_t **out) {
+  for (size_t k = 0; k < n; ++k)
+    if (ids[k] < lo || ids[k] >= total) {
+      set_error("tile id %d at %zu outside [%d, %d)", ids[k], k, lo, total);
+      return IRT_E_INVALID;
+    }
+  for (auto &t : c->tileTables)
+    if (t.ids.size() == n && std::equal(t.ids.begin(), t.ids.end(), ids)) {
+      *out = t.dev;
+      return IRT_OK;
+    }
+  if (c->tileTables.size() >= 64) {  // a camera per step would re-deal every frame: bounded
+    IRT_HIP(hipDeviceSynchronize());
+    for (auto &t : c->tileTables) (void)hipFree(t.dev);
+    c->tileTables.clear();
+  }
+  int32_t *d = nullptr;
+  IRT_HIP(hipMalloc((void **)&d, std::max<size_t>(n, 1) * sizeof(int32_t)));
+  if (hipMemcpy(d, ids, n * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    set_error("tile table upload failed");
+    return IRT_E_HIP;
+  }
+  c->tileTables.push_back({std::vector<int32_t>(ids, ids + n), d});
+  *out = d;
+  return IRT_OK;
 }
 
 int finish_slot(irt_context *c, int i) {
@@ -315,9 +356,10 @@ int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int t
 
 int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int packed,
                 int tileBegin, int tileStride, uint32_t *fb, irt_vec4f *accum, int *numTilesOut,
-                void *stream, int numFrames = 1) {
+                void *stream, int numFrames = 1, const int32_t *tileList = nullptr,
+                int listCount = 0) {
   if (!c || !lp || W <= 0 || H <= 0 || !fb || !accum || tileStride <= 0 || tileBegin < 0 ||
-      numFrames < 1 || numFrames > 65535) {
+      numFrames < 1 || numFrames > 65535 || listCount < 0 || (listCount > 0 && !tileList)) {
     set_error("irt_render: bad argument");
     return IRT_E_INVALID;
   }
@@ -350,6 +392,14 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   const int tilesX = (W + 63) / 64, tilesY = (H + 63) / 64;
   const int total = tilesX * tilesY;
   int numTiles = tileBegin < total ? (total - tileBegin + tileStride - 1) / tileStride : 0;
+  const int32_t *dList = nullptr;
+  if (tileList) {  // irt_render_tile_list
+    numTiles = listCount;
+    if (listCount > 0) {
+      int rc = tile_table(c, tileList, (size_t)listCount, 0, total, &dList);
+      if (rc) return rc;
+    }
+  }
   if (numTilesOut) *numTilesOut = numTiles;
 
   RenderArgs A;
@@ -398,6 +448,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.tileStride = tileStride;
   A.numTiles = numTiles;
   A.tilesX = tilesX;
+  A.tileList = dList;
   A.counters = c->d_counters + 16 * (c->launches % irt_context::kSlots);
   A.binHdr = c->d_binHdr;
   A.fat = c->d_fat;
@@ -455,7 +506,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.schedCost = nullptr;
   const int numBlocks = numTiles * 16;
   bool copyCosts = false;
-  if (c->schedOn && numFrames == 1 && numBlocks > 0) {
+  if (c->schedOn && numFrames == 1 && numBlocks > 0 && !dList) {
     int rc = sched_prepare(c, numBlocks, W, H, packed, tileBegin, tileStride, numTiles, lp, s);
     if (rc) return rc;
     A.schedOrder = c->schedOrderValid ? c->d_schedOrder + (size_t)c->schedBuf * c->schedCap : nullptr;
@@ -1005,6 +1056,35 @@ int irt_unpack_tiles(irt_context *c, const uint32_t *g, int numRanks, int maxTil
   }
   IRT_HIP(hipSetDevice(c->device));
   if (maxTiles > 0) launch_unpack(g, numRanks, maxTiles, W, H, fb, (hipStream_t)stream);
+  IRT_HIP(hipGetLastError());
+  return IRT_OK;
+}
+
+int irt_render_tile_list(irt_context *c, const irt_launch_params *lp, int W, int H,
+                         const int32_t *tiles, int numTiles, int numFrames, uint32_t *fb,
+                         irt_vec4f *accum, void *stream) {
+  if (numTiles < 0 || (numTiles > 0 && !tiles)) {
+    set_error("irt_render_tile_list: bad tile list");
+    return IRT_E_INVALID;
+  }
+  static const int32_t none = 0;
+  return render_impl(c, lp, W, H, 1, 0, 1, fb, accum, nullptr, stream, numFrames,
+                     numTiles > 0 ? tiles : &none, numTiles);
+}
+
+int irt_unpack_tile_table(irt_context *c, const uint32_t *g, int numRanks, int maxTiles,
+                          const int32_t *table, int W, int H, uint32_t *fb, void *stream) {
+  if (!c || !g || !fb || !table || numRanks <= 0 || maxTiles < 0 || W <= 0 || H <= 0) {
+    set_error("irt_unpack_tile_table: bad argument");
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(c->device));
+  if (maxTiles == 0) return IRT_OK;
+  const int total = irt_num_tiles(W, H);
+  const int32_t *d = nullptr;
+  int rc = tile_table(c, table, (size_t)numRanks * (size_t)maxTiles, -1, total, &d);
+  if (rc) return rc;
+  launch_unpack(g, numRanks, maxTiles, W, H, fb, (hipStream_t)stream, d);
   IRT_HIP(hipGetLastError());
   return IRT_OK;
 }

@@ -46,6 +46,7 @@ struct RenderArgs {
   float4 *accum;
   int packed;            // 0: linear x + W*y; 1: packed 64x64 tiles
   int tileBegin, tileStride, numTiles, tilesX;
+  const int32_t *tileList;  // explicit tile ids (irt_render_tile_list); null: tileBegin + k*tileStride
   unsigned long long *counters;  // [0] launched [1] inBox [2] locate [3] found [4] candidates
   // The binned locator (irt_common.h): per cube-map cell a 32-B header, fat entries,
   // per-record height/value blocks.
@@ -111,6 +112,6 @@ struct DeviceScene {
 int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_t n, size_t numRuns,
                        int G, hipStream_t s, DeviceScene &out);
 void launch_unpack(const uint32_t *gathered, int numRanks, int maxTiles, int W, int H,
-                   uint32_t *fb, hipStream_t s);
+                   uint32_t *fb, hipStream_t s, const int32_t *table = nullptr);
 
 }  // namespace irt

@@ -230,12 +230,15 @@ __global__ void k_clear(uint32_t *fb, float4 *accum, size_t n) {
 // Four workgroups per tile slot (16 rows each); a lane moves 4 pixels of a row with one
 // 16-byte load and store when the row is 16-byte aligned in the framebuffer (W % 4 == 0)
 // and the 4 pixels are inside the frame, pixel by pixel otherwise (ragged right/bottom edge).
+// Slot k of rank r holds tile r + k*numRanks, or table[r*maxTiles + k] (irt_deal_tiles; -1
+// marks an empty slot).
 __global__ void k_unpack(const uint32_t *gathered, int numRanks, int maxTiles, int W, int H,
-                         int tilesX, int numTilesTotal, uint32_t *fb) {
+                         int tilesX, int numTilesTotal, uint32_t *fb, const int32_t *table) {
   const int k = blockIdx.x >> 2;  // tile slot
   const int rank = blockIdx.y;
-  const int tileId = rank + k * numRanks;
-  if (k >= maxTiles || tileId >= numTilesTotal) return;
+  if (k >= maxTiles) return;
+  const int tileId = table ? table[(size_t)rank * maxTiles + k] : rank + k * numRanks;
+  if (tileId < 0 || tileId >= numTilesTotal) return;
   const int tx = tileId % tilesX, ty = tileId / tilesX;
   const int ly = (blockIdx.x & 3) * 16 + (threadIdx.x >> 4), lx = (threadIdx.x & 15) * 4;
   const uint32_t *src = gathered + ((size_t)rank * maxTiles + k) * 4096 + ly * 64 + lx;
@@ -350,10 +353,10 @@ void launch_clear(uint32_t *fb, float4 *accum, size_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_clear, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, fb, accum, n);
 }
 void launch_unpack(const uint32_t *g, int numRanks, int maxTiles, int W, int H, uint32_t *fb,
-                   hipStream_t s) {
+                   hipStream_t s, const int32_t *table) {
   const int tilesX = (W + 63) / 64, tilesY = (H + 63) / 64;
   hipLaunchKernelGGL(k_unpack, dim3(maxTiles * 4, numRanks), dim3(256), 0, s, g, numRanks, maxTiles,
-                     W, H, tilesX, tilesX * tilesY, fb);
+                     W, H, tilesX, tilesX * tilesY, fb, table);
 }
 
 }  // namespace irt

@@ -841,7 +841,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
 
 // ------------------------------------------------------------------ per-pixel pieces
 // The frame grid: 256-thread workgroup b, thread t -> gid = 256 b + t.  Workgroup b covers
-// 16x16 pixels of tile k = b / 16 of this launch (frame tile tileBegin + k*tileStride),
+// 16x16 pixels of tile k = b / 16 of this launch (frame tile tileBegin + k*tileStride, or
+// tileList[k]),
 // wave w an 8x8 packet, lane l one pixel.
 struct Pixel {
   int x, y;
@@ -854,7 +855,7 @@ __device__ __forceinline__ Pixel pixel_of(const RenderArgs &A, uint32_t gid) {
   const int wave = tid >> 6, lane = tid & 63;
   const int lx = ((sub & 3) << 4) | ((wave & 1) << 3) | (lane & 7);
   const int ly = ((sub >> 2) << 4) | ((wave >> 1) << 3) | (lane >> 3);
-  const int tileId = A.tileBegin + k * A.tileStride;
+  const int tileId = !A.tileList ? A.tileBegin + k * A.tileStride : (k < A.numTiles ? A.tileList[k] : 0);
   const int tx = tileId % A.tilesX, ty = tileId / A.tilesX;
   Pixel p;
   p.x = tx * 64 + lx;

@@ -452,4 +452,98 @@ int irt_num_tiles(int width, int height) {
   return ((width + 63) / 64) * ((height + 63) / 64);
 }
 
+// Estimated render cost of one 64x64 tile: rays (no jitter) through every 8th pixel of it,
+// in double.  Per ray: 1 (generation + boxTest), +1 inside the box, +8 reaching the shell (the
+// Woodcock rounds: ~5x a ray that misses, profiles/r02b_investigation/), + the chord through
+// the shell in units of its thickness, capped at 8 (limb rays sample longer).
+static double tile_cost(const irt_launch_params &lp, const irt_volume_info &info, int W, int H,
+                        int tx, int ty) {
+  const double ox = lp.org.x, oy = lp.org.y, oz = lp.org.z;
+  const double R0 = info.sphericalBounds.lower.x, R1 = info.sphericalBounds.upper.x;
+  const double thick = R1 > R0 ? R1 - R0 : 1.0;
+  double cost = 0.0;
+  for (int sy = 0; sy < 8; ++sy)
+    for (int sx = 0; sx < 8; ++sx) {
+      const int px = tx * 64 + 8 * sx + 4, py = ty * 64 + 8 * sy + 4;
+      if (px >= W || py >= H) continue;
+      double d[3] = {lp.dir_00.x + (px + 0.5) * lp.dir_du.x + (py + 0.5) * lp.dir_dv.x,
+                     lp.dir_00.y + (px + 0.5) * lp.dir_du.y + (py + 0.5) * lp.dir_dv.y,
+                     lp.dir_00.z + (px + 0.5) * lp.dir_du.z + (py + 0.5) * lp.dir_dv.z};
+      const double l = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+      cost += 1.0;
+      if (!(l > 0)) continue;
+      for (double &v : d) v /= l;
+      // slab test against the volume bounds
+      const double o[3] = {ox, oy, oz};
+      const double lo[3] = {info.bounds.lower.x, info.bounds.lower.y, info.bounds.lower.z};
+      const double hi[3] = {info.bounds.upper.x, info.bounds.upper.y, info.bounds.upper.z};
+      double t0 = 0.0, t1 = 1e30;
+      for (int a = 0; a < 3; ++a) {
+        if (d[a] == 0.0) {
+          if (o[a] < lo[a] || o[a] > hi[a]) t1 = -1.0;
+          continue;
+        }
+        double u = (lo[a] - o[a]) / d[a], v = (hi[a] - o[a]) / d[a];
+        if (u > v) std::swap(u, v);
+        t0 = std::max(t0, u);
+        t1 = std::min(t1, v);
+      }
+      if (!(t0 < t1)) continue;
+      cost += 1.0;
+      const double b = ox * d[0] + oy * d[1] + oz * d[2], oo = ox * ox + oy * oy + oz * oz;
+      const double disc1 = b * b - (oo - R1 * R1);
+      if (disc1 < 0) continue;
+      const double e1 = -b - sqrt(disc1), x1 = -b + sqrt(disc1);
+      if (x1 < 0) continue;
+      const double disc0 = b * b - (oo - R0 * R0);
+      const double stop = disc0 >= 0 && -b - sqrt(disc0) > 0 ? -b - sqrt(disc0) : x1;
+      const double chord = std::max(0.0, stop - std::max(e1, 0.0));
+      cost += 8.0 + std::min(chord / thick, 8.0);
+    }
+  return cost;
+}
+
+int irt_deal_tiles(const irt_launch_params *lp, const irt_volume_info *info, int W, int H,
+                   int N, float rank0Extra, int32_t *table, size_t capacity,
+                   int *maxTilesPerRank) {
+  if (!lp || !info || !maxTilesPerRank || W <= 0 || H <= 0 || N <= 0 || !(rank0Extra >= 0.f) ||
+      !(rank0Extra < 1.f)) {
+    set_error("irt_deal_tiles: bad argument");
+    return IRT_E_INVALID;
+  }
+  const int tilesX = (W + 63) / 64, tilesY = (H + 63) / 64, T = tilesX * tilesY;
+  std::vector<std::pair<double, int>> order(T);
+  double total = 0.0;
+  for (int t = 0; t < T; ++t) {
+    const double c = tile_cost(*lp, *info, W, H, t % tilesX, t / tilesX);
+    order[t] = {-c, t};
+    total += c;
+  }
+  std::sort(order.begin(), order.end());  // heaviest first, ties by tile id
+  // longest-processing-time first: each tile to the least-loaded rank (ties: lowest rank);
+  // rank 0 starts with the unpack's share
+  std::vector<double> load(N, 0.0);
+  load[0] = (double)rank0Extra * total;
+  std::vector<std::vector<int32_t>> rows(N);
+  for (int i = 0; i < T; ++i) {
+    int r = 0;
+    for (int q = 1; q < N; ++q)
+      if (load[q] < load[r]) r = q;
+    load[r] += -order[i].first;
+    rows[r].push_back(order[i].second);
+  }
+  int maxT = 0;
+  for (auto &row : rows) maxT = std::max(maxT, (int)row.size());
+  *maxTilesPerRank = maxT;
+  if (!table) return IRT_OK;  // size query
+  if (capacity < (size_t)N * (size_t)maxT) {
+    set_error("irt_deal_tiles: capacity %zu < %d ranks x %d tiles", capacity, N, maxT);
+    return IRT_E_INVALID;
+  }
+  for (int r = 0; r < N; ++r)
+    for (int k = 0; k < maxT; ++k)
+      table[(size_t)r * maxT + k] = k < (int)rows[r].size() ? rows[r][k] : -1;
+  return IRT_OK;
+}
+
 }  // extern "C"

@@ -131,6 +131,10 @@ def lib() -> C.CDLL:
             "irt_render_tiles_accumulate": [P, C.POINTER(LaunchParams), I, I, I, I, I, P, P,
                                             C.POINTER(C.c_int), P],
             "irt_unpack_tiles": [P, P, I, I, I, I, P, P],
+            "irt_deal_tiles": [C.POINTER(LaunchParams), C.POINTER(VolumeInfo), I, I, I, F, P, S,
+                               C.POINTER(C.c_int)],
+            "irt_render_tile_list": [P, C.POINTER(LaunchParams), I, I, P, I, I, P, P, P],
+            "irt_unpack_tile_table": [P, P, I, I, P, I, I, P, P],
             "irt_get_render_stats": [P, C.POINTER(RenderStats)],
             "irt_get_render_stats_total": [P, C.POINTER(RenderStats), C.POINTER(C.c_longlong)],
             "irt_reset_render_stats_total": [P],
@@ -351,6 +355,20 @@ def num_tiles(w: int, h: int) -> int:
     return lib().irt_num_tiles(w, h)
 
 
+def deal_tiles(lp: LaunchParams, info: VolumeInfo, w: int, h: int, ranks: int,
+               rank0_extra: float = 0.0) -> np.ndarray:
+    """irt_deal_tiles: the cost-balanced deal of the frame's 64x64 tiles over `ranks` ranks,
+    (ranks, max_tiles) int32, row r = rank r's tiles in render order, -1 padding; rank 0
+    carries rank0_extra x a frame's cost besides its tiles."""
+    m = C.c_int()
+    _check(lib().irt_deal_tiles(C.byref(lp), C.byref(info), w, h, ranks, rank0_extra, None, 0,
+                                C.byref(m)), "irt_deal_tiles")
+    table = np.full((ranks, m.value), -1, np.int32)
+    _check(lib().irt_deal_tiles(C.byref(lp), C.byref(info), w, h, ranks, rank0_extra,
+                                _ptr(table), table.size, C.byref(m)), "irt_deal_tiles")
+    return table
+
+
 @dataclass
 class FrameSetup:
     """What icon_rt's main() derives before the first launch (hostCode.cu:736-958)."""
@@ -518,6 +536,23 @@ class Context:
                                                  C.c_void_p(accum_ptr), C.byref(n),
                                                  C.c_void_p(stream)), "irt_render_tiles_accumulate")
         return n.value
+
+    def render_tile_list(self, lp: LaunchParams, width: int, height: int, tiles, num_frames: int,
+                         fb_tiles_ptr: int, accum_tiles_ptr: int, stream: int = 0):
+        """irt_render_tile_list: the listed tiles (row-major ids), packed in list order."""
+        t = np.ascontiguousarray(tiles, dtype=np.int32)
+        _check(lib().irt_render_tile_list(self._h, C.byref(lp), width, height, _ptr(t), t.size,
+                                          num_frames, C.c_void_p(fb_tiles_ptr),
+                                          C.c_void_p(accum_tiles_ptr), C.c_void_p(stream)),
+               "irt_render_tile_list")
+
+    def unpack_tile_table(self, gathered_ptr: int, table: np.ndarray, width: int, height: int,
+                          fb_ptr: int, stream: int = 0):
+        """irt_unpack_tile_table: rank-major packed tiles whose ids are table[rank, k]."""
+        t = np.ascontiguousarray(table, dtype=np.int32)
+        _check(lib().irt_unpack_tile_table(self._h, C.c_void_p(gathered_ptr), t.shape[0], t.shape[1],
+                                           _ptr(t), width, height, C.c_void_p(fb_ptr),
+                                           C.c_void_p(stream)), "irt_unpack_tile_table")
 
     def unpack_tiles(self, gathered_ptr: int, num_ranks: int, max_tiles: int, width: int,
                      height: int, fb_ptr: int, stream: int = 0):

@@ -2,10 +2,13 @@
 
 The reference is single-device; its CPU path already cuts a frame into 64x64 tiles pulled
 by a thread pool (common/for_each.h:70-85, common/thread_pool.h:146-161).  Here the same
-tiles are dealt round-robin to N ranks (tile t -> rank t mod N, which balances the globe in
-the middle of the frame), every rank renders its tiles into a packed buffer
-(irt_render_tiles), and rank 0 gathers the RGBA8 tiles over RCCL (torch.distributed,
-backend "nccl") and scatters them into the framebuffer (irt_unpack_tiles).  Pixel seeds
+tiles are dealt to N ranks by estimated cost (irt_deal_tiles: tiles sorted by the cost of
+their rays through the shell, dealt serpentine, so every rank's share costs about the same;
+the plain round-robin t -> rank t mod N hands whole tile COLUMNS to each rank when N divides
+the tile row, ~1.6x cost spread over a centred globe), every rank renders its tiles into a
+packed buffer (irt_render_tile_list), and rank 0 gathers the RGBA8 tiles over RCCL
+(torch.distributed, backend "nccl") and scatters them into the framebuffer
+(irt_unpack_tile_table).  Pixel seeds
 depend only on (accumID, W, H, x, y) (deviceCode.cu:288-289), so the assembled frame is
 bit-identical to a single-GPU launch.  The accumulation buffer stays sharded: each rank
 keeps the accum of its own tiles across frames (progressive rendering needs no exchange).
@@ -18,14 +21,33 @@ import numpy as np
 
 TILE = 64
 TILE_PIX = TILE * TILE
+# irt_unpack_tile_table of a whole frame against one frame's render on one GPU: ~4.5 us vs
+# 0.104 ms at C3, ~8.5 us vs 0.33 ms at C4 (profiles/r03b_dist/): rank 0's extra work per
+# step, as a fraction of a frame's render cost
+UNPACK_COST = 0.04
 
 
-@dataclass(frozen=True)
+@dataclass(frozen=True, eq=False)
 class TileSplit:
+    """Which 64x64 tiles each rank renders.  `table` (world, max_tiles) from irt_deal_tiles
+    (row r = rank r's tiles in render order, -1 padding); None: round-robin t mod world."""
     width: int
     height: int
     rank: int
     world: int
+    table: np.ndarray | None = None
+
+    @classmethod
+    def dealt(cls, width: int, height: int, rank: int, world: int, lp, info,
+              frames: int = 1) -> "TileSplit":
+        """The cost-balanced deal for the camera lp over the volume `info` (every rank
+        computes the same table: a deterministic function of its inputs).  With more than
+        one rank, rank 0 also unpacks the gathered frame once per step of `frames` frames:
+        UNPACK_COST of one frame's render cost, taken off its tiles."""
+        import irt
+        extra = UNPACK_COST / max(1, frames) if world > 1 else 0.0
+        return cls(width, height, rank, world,
+                   irt.deal_tiles(lp, info, width, height, world, extra))
 
     @property
     def tiles_x(self) -> int:
@@ -37,11 +59,37 @@ class TileSplit:
 
     @property
     def max_tiles(self) -> int:
+        if self.table is not None:
+            return int(self.table.shape[1])
         return (self.num_tiles + self.world - 1) // self.world
 
     def tiles(self, rank: int | None = None) -> list[int]:
         r = self.rank if rank is None else rank
+        if self.table is not None:
+            return [int(t) for t in self.table[r] if t >= 0]
         return list(range(r, self.num_tiles, self.world))
+
+    def render(self, ctx, lp, frames: int, buf_ptr: int, acc_ptr: int, stream: int = 0):
+        """This rank's tiles of `frames` progressive frames (accumID = lp.accumID ...) into
+        the packed buffer buf_ptr (accum tiles acc_ptr)."""
+        if self.table is not None:
+            ctx.render_tile_list(lp, self.width, self.height, self.tiles(), frames, buf_ptr,
+                                 acc_ptr, stream)
+        elif frames == 1:
+            ctx.render_tiles(lp, self.width, self.height, self.rank, self.world, buf_ptr,
+                             acc_ptr, stream)
+        else:
+            ctx.render_tiles_accumulate(lp, self.width, self.height, self.rank, self.world,
+                                        frames, buf_ptr, acc_ptr, stream)
+
+    def unpack(self, ctx, gathered_ptr: int, fb_ptr: int, stream: int = 0):
+        """Rank 0: every rank's packed tiles (gathered rank-major) into the framebuffer."""
+        if self.table is not None:
+            ctx.unpack_tile_table(gathered_ptr, self.table, self.width, self.height, fb_ptr,
+                                  stream)
+        else:
+            ctx.unpack_tiles(gathered_ptr, self.world, self.max_tiles, self.width, self.height,
+                             fb_ptr, stream)
 
     def tile_pixels(self, tile: int) -> np.ndarray:
         """(x, y) of the in-frame pixels of a tile, in packed (ly*64 + lx) order, with -1
@@ -149,8 +197,12 @@ class FramePipeline:
             b = t % len(self.fg.bufs)
             with torch.cuda.stream(self.side):
                 g = self.fg.finish(self.works[t], b)
-                self.ctx.unpack_tiles(g.data_ptr(), sp.world, sp.max_tiles, sp.width, sp.height,
-                                      self.fb.data_ptr(), self.side.cuda_stream)
+                sp.unpack(self.ctx, g.data_ptr(), self.fb.data_ptr(), self.side.cuda_stream)
+
+    def _wait_reuse(self, t):
+        """The render stream waits for the gather of step t (it read the buffers about to
+        be rendered into again)."""
+        self.works[t].wait()
 
     def step(self, s: int, render):
         """render(buf): this rank's tiles of step s into the packed buffer `buf`."""
@@ -161,7 +213,7 @@ class FramePipeline:
             newest = s - self.k - 1
             for t in [t for t in self.works if t <= newest]:
                 if t == newest or self.host_staged:
-                    self.works[t].wait()  # the render stream (in-order collectives: one wait)
+                    self._wait_reuse(t)  # the render stream (in-order collectives: one wait)
                 if not self.rank0:
                     del self.works[t]
         if self.rank0:

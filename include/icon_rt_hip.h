@@ -192,6 +192,36 @@ int irt_render_tiles_accumulate(irt_context *ctx, const irt_launch_params *lp, i
 int irt_unpack_tiles(irt_context *ctx, const uint32_t *d_gathered, int numRanks,
                      int maxTilesPerRank, int width, int height, uint32_t *d_fb, void *stream);
 
+/* Cost-balanced multi-GPU deal of a width x height launch's 64x64 tiles (no GPU needed;
+ * the reference's CPU path hands the same tiles to a thread pool dynamically,
+ * common/thread_pool.h:146-161, for_each.h:70-85).  Each tile's cost is estimated from the
+ * camera (lp) and the shell radii (info->sphericalBounds): rays through an 8x8 subset of
+ * its pixels, weighted by whether they reach the box and the shell and by their chord
+ * through the shell.  Tiles go, heaviest first (ties by id), to the least-loaded rank
+ * (longest-processing-time first; ties to the lowest rank); rank 0 starts loaded with
+ * rank0Extra x the frame's total estimated cost (in [0, 1): the work rank 0 does beyond its
+ * tiles, e.g. the framebuffer unpack per rendered frame).  Deterministic: every rank
+ * computes the same table.  table: numRanks x maxTilesPerRank, rank-major, row r = rank r's
+ * tiles in render order (heaviest first), -1 padding; table == NULL returns only
+ * *maxTilesPerRank (the longest row). */
+int irt_deal_tiles(const irt_launch_params *lp, const irt_volume_info *info, int width,
+                   int height, int numRanks, float rank0Extra, int32_t *table, size_t capacity,
+                   int *maxTilesPerRank);
+
+/* irt_render_tiles / irt_render_tiles_accumulate over an explicit tile list (host array of
+ * row-major tile ids, e.g. one row of irt_deal_tiles' table without its -1 padding):
+ * list entry k is packed at d_fb_tiles[k*4096 ...].  numFrames >= 1 consecutive progressive
+ * frames as irt_render_tiles_accumulate.  Every pixel is bit-identical to irt_render's. */
+int irt_render_tile_list(irt_context *ctx, const irt_launch_params *lp, int width, int height,
+                         const int32_t *tiles, int numTiles, int numFrames,
+                         uint32_t *d_fb_tiles, irt_vec4f *d_accum_tiles, void *stream);
+
+/* Scatter packed tiles gathered rank-major (d_gathered[rank][maxTilesPerRank][4096]) whose
+ * tile ids are the host table[rank * maxTilesPerRank + k] (irt_deal_tiles; -1: empty). */
+int irt_unpack_tile_table(irt_context *ctx, const uint32_t *d_gathered, int numRanks,
+                          int maxTilesPerRank, const int32_t *table, int width, int height,
+                          uint32_t *d_fb, void *stream);
+
 /* Statistics of the most recent launch (waits for it).  Launches never wait for earlier
  * ones' statistics: counters are read back through a ring, so frames queue back to back
  * like the reference's GPU path (owlLaunch2D is asynchronous, pipeline.cu:1064). */

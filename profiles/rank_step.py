@@ -1,16 +1,19 @@
 #!/usr/bin/env python3
-"""One rank's share of an N-GPU bench step, on one GPU, without the collective.
+"""Every rank's share of an N-GPU bench step, timed on one GPU, without the collective.
 
-bench.py on N GPUs: each rank renders its interleaved 64x64 tiles
-(irt_render_tiles_accumulate: N progressive frames per step in --mode progressive, one
-frame in --mode frame), RCCL gathers the packed tiles, and rank 0 unpacks them.  This
-script times rank 0's GPU work per step for N = 1, 2, 4, 8 (render, plus the unpack of a
-gathered buffer of the right size) back to back on one stream, and the single-GPU path for
-reference.  It projects the step time the driver's multi-GPU runs can reach, apart from the
-exchange itself.
+bench.py on N GPUs: each rank renders its 64x64 tiles (N progressive frames per step in
+--mode progressive, one frame in --mode frame) into a packed buffer, RCCL gathers the packed
+tiles and rank 0 unpacks them.  The step time of the job is the SLOWEST rank's, so this
+script times the share of EVERY rank r = 0..N-1 (render; with N > 1 rank 0 also the unpack
+of a gathered buffer of the right size), back to back on one stream, for both deals:
+  * "mod":   tile t -> rank t mod N (rounds 1-2; whole tile columns per rank when N divides
+             the tile row),
+  * "dealt": irt_deal_tiles' cost-balanced deal (round 3, bench.py's: longest-processing-
+             time first on an estimate of each tile's cost, rank 0 lighter by the unpack).
+It prints one JSON line per (deal, mode, N) with the per-rank times, max/mean, and the
+projected whole-job rate from the max rank (the exchange itself left out).
 
-    python profiles/rank_step.py [--config c3] [--steps 100]
-Prints one JSON line per (mode, N).
+    python profiles/rank_step.py [--config c3] [--steps 50]
 """
 import argparse
 import json
@@ -31,13 +34,17 @@ import irt_dist  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--ranks", default="1,2,4,8")
+    ap.add_argument("--modes", default="progressive,frame")
+    ap.add_argument("--deals", default="mod,dealt")
     args = ap.parse_args()
-    rn, bis, L, W, H, tf, _, _ = bench.CONFIGS[args.config]
+    rn, bis, L, W, H, tf, orbit, _ = bench.CONFIGS[args.config]
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
     ctx = irt.Context.synth(rn, bis, L, 0)
-    setup = irt.setup_frame(None, W, H, camera=bench.FRAMING, info=ctx.info)
+    cam = bench.orbit_camera(0) if orbit else bench.FRAMING
+    setup = irt.setup_frame(None, W, H, camera=cam, info=ctx.info)
     ctx.set_transfunc(bench.make_lut(tf, setup.lut), setup.value_range)
     lp = setup.lp
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -58,33 +65,40 @@ def main():
         lp.accumID = s
         ctx.render(lp, W, H, fb.data_ptr(), acc.data_ptr(), stream)
 
-    ms = timed(single)
-    print(json.dumps({"config": args.config, "mode": "single", "n": 1, "ms_per_step": round(ms, 4),
-                      "mray_s": round(W * H / ms / 1e3, 1)}), flush=True)
-    for mode in ("progressive", "frame"):
-        for n in (1, 2, 4, 8):
-            split = irt_dist.TileSplit(W, H, 0, n)
-            maxt = split.max_tiles
-            tiles = torch.zeros(maxt * 4096, dtype=torch.int32, device=dev)
-            tacc = torch.zeros(maxt * 4096 * 4, dtype=torch.float32, device=dev)
-            gathered = torch.zeros(n * maxt * 4096, dtype=torch.int32, device=dev)
-            frames = 1 if mode == "frame" else n
+    ms1 = timed(single)
+    print(json.dumps({"config": args.config, "mode": "single", "n": 1, "ms_per_step": round(ms1, 4),
+                      "mray_s": round(W * H / ms1 / 1e3, 1)}), flush=True)
+    for deal in args.deals.split(","):
+        for mode in args.modes.split(","):
+            for n in (int(v) for v in args.ranks.split(",")):
+                frames = 1 if mode == "frame" else n
+                steps = []
+                for r in range(n):
+                    split = (irt_dist.TileSplit.dealt(W, H, r, n, lp, ctx.info, frames) if deal == "dealt"
+                             else irt_dist.TileSplit(W, H, r, n))
+                    maxt = split.max_tiles
+                    tiles = torch.zeros(maxt * 4096, dtype=torch.int32, device=dev)
+                    tacc = torch.zeros(maxt * 4096 * 4, dtype=torch.float32, device=dev)
+                    gathered = torch.zeros(n * maxt * 4096, dtype=torch.int32, device=dev)
 
-            def step(s):
-                lp.accumID = s * frames
-                if frames == 1:
-                    ctx.render_tiles(lp, W, H, 0, n, tiles.data_ptr(), tacc.data_ptr(), stream)
-                else:
-                    ctx.render_tiles_accumulate(lp, W, H, 0, n, frames, tiles.data_ptr(),
-                                                tacc.data_ptr(), stream)
-                ctx.unpack_tiles(gathered.data_ptr(), n, maxt, W, H, fb.data_ptr(), stream)
+                    def step(s, split=split, tiles=tiles, tacc=tacc, gathered=gathered, r=r):
+                        lp.accumID = s * frames
+                        split.render(ctx, lp, frames, tiles.data_ptr(), tacc.data_ptr(), stream)
+                        if r == 0 and n > 1:
+                            split.unpack(ctx, gathered.data_ptr(), fb.data_ptr(), stream)
 
-            ms = timed(step)
-            print(json.dumps({"config": args.config, "mode": mode, "n": n,
-                              "ms_per_step": round(ms, 4),
-                              # all ranks' rays per step: W*H*frames (frames = n or 1)
-                              "projected_mray_s": round(W * H * frames / ms / 1e3, 1)}),
-                  flush=True)
+                    steps.append(step)
+                # the ranks timed in turn, three passes; each rank's fastest pass (the box's
+                # run-to-run noise is ~3 %, more than the imbalance being measured)
+                per_rank = [min(v) for v in zip(*[[timed(f) for f in steps] for _ in range(3)])]
+                mx, mean = max(per_rank), sum(per_rank) / n
+                print(json.dumps({"config": args.config, "deal": deal, "mode": mode, "n": n,
+                                  "ms_per_rank": [round(v, 4) for v in per_rank],
+                                  "max_over_mean": round(mx / mean, 4),
+                                  "ms_per_step_max": round(mx, 4),
+                                  # all ranks' rays per step: W*H*frames, over the slowest rank
+                                  "projected_mray_s": round(W * H * frames / mx / 1e3, 1),
+                                  "speedup_vs_single": round(ms1 * frames / mx, 3)}), flush=True)
     ctx.close()
 
 

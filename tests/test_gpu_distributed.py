@@ -1,8 +1,9 @@
 """The multi-GPU frame split with the HIP renderer: world-size-2 processes (gloo,
-host-staged collectives, both ranks on cuda:0) render their interleaved 64x64 tiles
-through irt_render_tiles / irt_render_tiles_accumulate on torch's default stream, gather
-them to rank 0 with irt_dist.FrameGather (two frames in flight, rank-major receive
-buffers), and rank 0 unpacks them with irt_unpack_tiles on a side stream
+host-staged collectives, both ranks on cuda:0) render their 64x64 tiles -- the
+cost-balanced deal (irt_deal_tiles, irt_render_tile_list) or round-robin (irt_render_tiles /
+irt_render_tiles_accumulate) -- on torch's default stream, gather them to rank 0 with
+irt_dist.FrameGather (two frames in flight, rank-major receive buffers), and rank 0 unpacks
+them (irt_unpack_tile_table / irt_unpack_tiles) on a side stream
 (irt_dist.FramePipeline, the loop bench.py runs) -- bench.py's two multi-GPU modes:
   * frame       one frame per step split over the ranks (strong scaling),
   * progressive N progressive frames per step, each rank rendering its tiles of all N
@@ -31,7 +32,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, mode, out_path):
+def _worker(rank, world, port, mode, out_path, deal):
     sys.path[:0] = [os.path.join(HERE, "..", "icon-ray-tracing_amd", "python"), HERE]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
@@ -47,7 +48,8 @@ def _worker(rank, world, port, mode, out_path):
     setup = irt.setup_frame(None, W, H, camera=FRAMING, info=ctx.info)
     ctx.set_transfunc(setup.lut, setup.value_range)
     lp = setup.lp
-    split = irt_dist.TileSplit(W, H, rank, world)
+    split = (irt_dist.TileSplit.dealt(W, H, rank, world, lp, ctx.info) if deal == "dealt"
+             else irt_dist.TileSplit(W, H, rank, world))
     fg = irt_dist.FrameGather(split, "cuda:0", buffers=8, stage_cpu=True)
     acc = torch.zeros(split.max_tiles * 4096 * 4, dtype=torch.float32, device="cuda:0")
     fb = torch.zeros(W * H, dtype=torch.int32, device="cuda:0")
@@ -55,12 +57,7 @@ def _worker(rank, world, port, mode, out_path):
     pipe = irt_dist.FramePipeline(ctx, fg, fb)  # bench.py's loop: rank 0 unpacks on a side stream
     for s in range(STEPS):
         lp.accumID = s * frames
-        if mode == "frame":
-            pipe.step(s, lambda buf: ctx.render_tiles(lp, W, H, rank, world, buf.data_ptr(),
-                                                      acc.data_ptr()))
-        else:
-            pipe.step(s, lambda buf: ctx.render_tiles_accumulate(lp, W, H, rank, world, frames,
-                                                                 buf.data_ptr(), acc.data_ptr()))
+        pipe.step(s, lambda buf: split.render(ctx, lp, frames, buf.data_ptr(), acc.data_ptr()))
     pipe.drain()
     if rank == 0:
         torch.cuda.synchronize()
@@ -70,8 +67,9 @@ def _worker(rank, world, port, mode, out_path):
     ctx.close()
 
 
+@pytest.mark.parametrize("deal", ["dealt", "mod"])
 @pytest.mark.parametrize("mode", ["frame", "progressive"])
-def test_two_rank_hip_frame_split(tmp_path, mode):
+def test_two_rank_hip_frame_split(tmp_path, mode, deal):
     import torch
     import torch.multiprocessing as mp
 
@@ -80,7 +78,7 @@ def test_two_rank_hip_frame_split(tmp_path, mode):
 
     world = 2
     out = str(tmp_path / "frame.npy")
-    mp.start_processes(_worker, args=(world, _free_port(), mode, out), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _free_port(), mode, out, deal), nprocs=world, join=True,
                        start_method="spawn")
     ctx = irt.Context.synth(*GRID, 0)
     setup = irt.setup_frame(None, W, H, camera=FRAMING, info=ctx.info)

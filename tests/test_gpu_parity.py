@@ -160,6 +160,86 @@ def test_tiles_match_full_frame():
         assert np.array_equal(out.cpu().numpy(), full), f"{ranks} ranks"
 
 
+def test_dealt_tile_lists_match_full_frame():
+    """The cost-balanced deal (irt_deal_tiles -> irt_render_tile_list, packed in list order ->
+    irt_unpack_tile_table) reproduces the full launch bit for bit, single frames and
+    progressive batches, ragged frames, 1..8 ranks (8 > tiles: empty ranks)."""
+    import torch
+    import irt_dist
+    cells = irt.synth_grid(2, 2, 90)
+    W, H = 200, 136  # 4 x 3 tiles, ragged on both edges
+    setup = irt.setup_frame(cells, W, H, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    lp = setup.lp
+    dev = "cuda:0"
+    for k in (1, 3):
+        fb = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        acc = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+        if k == 1:
+            ctx.render(lp, W, H, fb.data_ptr(), acc.data_ptr())
+        else:
+            ctx.render_accumulate(lp, W, H, k, fb.data_ptr(), acc.data_ptr())
+        torch.cuda.synchronize()
+        full = fb.cpu().numpy()
+        for ranks in (1, 2, 3, 8, 16):
+            splits = [irt_dist.TileSplit.dealt(W, H, r, ranks, lp, ctx.info) for r in range(ranks)]
+            maxt = splits[0].max_tiles
+            gathered = torch.zeros(ranks * maxt * 4096, dtype=torch.int32, device=dev)
+            for r, sp in enumerate(splits):
+                tacc = torch.zeros(maxt * 4096 * 4, dtype=torch.float32, device=dev)
+                sp.render(ctx, lp, k, gathered[r * maxt * 4096:].data_ptr(), tacc.data_ptr())
+                if sp.tiles():  # the launch's rays: this rank's in-frame pixels, k frames
+                    assert ctx.stats().raysLaunched == k * sum(
+                        int((sp.tile_pixels(t)[:, 0] >= 0).sum()) for t in sp.tiles())
+            out = torch.zeros(W * H, dtype=torch.int32, device=dev)
+            splits[0].unpack(ctx, gathered.data_ptr(), out.data_ptr())
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy(), full), f"{ranks} ranks, {k} frames"
+    # bad tile ids are rejected before any launch
+    with pytest.raises(irt.IrtError, match="tile id"):
+        ctx.render_tile_list(lp, W, H, [0, 12], 1, fb.data_ptr(), acc.data_ptr())
+    with pytest.raises(irt.IrtError, match="tile id"):
+        ctx.unpack_tile_table(fb.data_ptr(), np.array([[0, -2]], np.int32), W, H, out.data_ptr())
+    ctx.close()
+
+
+@pytest.mark.parametrize("W,H,ranks", [(203, 71, 3), (1024, 1024, 8), (64, 200, 5)])
+def test_unpack_tile_table_equals_host_twin(W, H, ranks):
+    """irt_unpack_tile_table scatters slot k of rank r to tile table[r, k] (a random
+    permutation dealt into rows with -1 padding) exactly as irt_dist.unpack_host does."""
+    import torch
+    import irt_dist
+    ctx = irt.Context(irt.synth_grid(2, 1, 4), 0)
+    T = irt.num_tiles(W, H)
+    maxt = -(-T // ranks)
+    rng = np.random.default_rng(W + 3 * H)
+    table = np.full(ranks * maxt, -1, np.int32)
+    slots = rng.permutation(ranks * maxt)[:T]
+    table[slots] = rng.permutation(T)
+    table = table.reshape(ranks, maxt)
+    split = irt_dist.TileSplit(W, H, 0, ranks, table)
+    g = rng.integers(0, 2**32, ranks * maxt * 4096, dtype=np.uint32)
+    gathered = torch.from_numpy(g.view(np.int32)).to("cuda:0")
+    out = torch.full((W * H + 64,), -1, dtype=torch.int32, device="cuda:0")
+    split.unpack(ctx, gathered.data_ptr(), out.data_ptr())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    # the host twin reads rank r's tiles in table order, skipping -1 slots: compact the rows
+    compact = np.zeros_like(g).reshape(ranks, maxt, 4096)
+    for r in range(ranks):
+        keep = np.nonzero(table[r] >= 0)[0]
+        compact[r, :len(keep)] = g.reshape(ranks, maxt, 4096)[r, keep]
+    ctable = np.full_like(table, -1)
+    for r in range(ranks):
+        row = table[r][table[r] >= 0]
+        ctable[r, :len(row)] = row
+    assert np.array_equal(got[:W * H].reshape(H, W),
+                          irt_dist.unpack_host(compact.ravel(), irt_dist.TileSplit(W, H, 0, ranks, ctable)))
+    assert (got[W * H:] == 0xFFFFFFFF).all()
+    ctx.close()
+
+
 @pytest.mark.parametrize("W,H,ranks", [(203, 71, 3), (130, 64, 1), (64, 200, 5), (1024, 1024, 8)])
 def test_unpack_tiles_equals_host_twin(W, H, ranks):
     """irt_unpack_tiles (16-byte rows where W % 4 == 0, pixel by pixel on ragged edges) equals

@@ -129,19 +129,22 @@ def test_frame_is_deterministic(scene):
     assert st.samplesFound == scene["stats"].samplesFound
 
 
-def test_eight_way_tile_split_is_bit_identical(scene):
+@pytest.mark.parametrize("deal", ["dealt", "mod"])
+def test_eight_way_tile_split_is_bit_identical(scene, deal):
     import torch
+    import irt_dist
     W, ctx, lp = scene["W"], scene["ctx"], scene["setup"].lp
     ranks = 8
-    ntot = irt.num_tiles(W, W)
-    maxt = (ntot + ranks - 1) // ranks
+    splits = [irt_dist.TileSplit.dealt(W, W, r, ranks, lp, ctx.info) if deal == "dealt"
+              else irt_dist.TileSplit(W, W, r, ranks) for r in range(ranks)]
+    maxt = splits[0].max_tiles
     gathered = torch.zeros(ranks * maxt * 4096, dtype=torch.int32, device="cuda:0")
-    for r in range(ranks):
+    for r, sp in enumerate(splits):
         acc = torch.zeros(maxt * 4096 * 4, dtype=torch.float32, device="cuda:0")
         view = gathered[r * maxt * 4096:(r + 1) * maxt * 4096]
-        ctx.render_tiles(lp, W, W, r, ranks, view.data_ptr(), acc.data_ptr())
+        sp.render(ctx, lp, 1, view.data_ptr(), acc.data_ptr())
     out = torch.zeros(W * W, dtype=torch.int32, device="cuda:0")
-    ctx.unpack_tiles(gathered.data_ptr(), ranks, maxt, W, W, out.data_ptr())
+    splits[0].unpack(ctx, gathered.data_ptr(), out.data_ptr())
     torch.cuda.synchronize()
     f = out.cpu().numpy().view(np.uint32).reshape(W, W)
     assert np.array_equal(f, scene["fb"])
