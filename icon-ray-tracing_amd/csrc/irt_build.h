@@ -103,8 +103,7 @@ IRT_HD bool tri_box_overlap(const double tx[3], const double ty[3], double bx0, 
 // Per record the kernel-side arrays (all indexed by record i):
 //   planes[3 i + k]  float4 side plane k (n.xyz, w) of sample()     ICONGrid.h:187-203
 //   rng[i]           {height[0], height[numLayers]}                  ICONGrid.h:184
-//   meta[i]          numLayers | (height[1..numLayers] non-decreasing) << 31
-//   keys[i]          {height[7], height[15], height[23], height[31]} (coarse findHeight keys)
+//   meta[i]          numLayers, coarse flag, quantised coarse findHeight keys (record_meta)
 //   blocks[16 i ..]  the height/value block (irt_common.h kBlk4)
 // trig[3 i + k] = {cosf lat, sinf lat, cosf lon, sinf lon} of corner k, from the host's
 // glibc -- so toCartesian (ICONGrid.h:44-54) here rounds exactly as the reference's.
@@ -146,12 +145,21 @@ IRT_HD float eval_plane(const float *p, float px, float py, float pz) {
   return (px * p[0] + py * p[1] + pz * p[2]) - p[3];
 }
 
-// meta word: numLayers | (height[1..numLayers] non-decreasing) << 31
+// meta word (irt_common.h): numLayers, the coarse flag, the quantised coarse keys
 IRT_HD uint32_t record_meta(const float *height, int nl) {
-  bool sorted = true;
-  for (int j = 2; j <= nl; ++j)
-    if (!(height[j - 1] <= height[j])) sorted = false;
-  return (uint32_t)nl | (sorted ? 0x80000000u : 0u);
+  // non-decreasing in float_key order (which implies float order; a -0/+0 pair in the wrong
+  // order takes the literal path)
+  bool coarse = true;
+  for (int j = 1; j <= nl; ++j)
+    if (!(float_key(height[j - 1]) <= float_key(height[j]))) coarse = false;
+  uint32_t m = (uint32_t)nl;
+  if (coarse) {
+    m |= kMetaCoarse;
+    const uint32_t k0 = float_key(height[0]), S = meta_quantum(k0, float_key(height[nl]));
+    for (int j = 0; j < 3 && 8 * j + 7 <= nl; ++j)
+      m |= ((float_key(height[8 * j + 7]) - k0) / S) << (6 + 8 * j);
+  }
+  return m;
 }
 
 // The height/value block (kBlk4 float4): block b = {height[8b..8b+3]}, {height[8b+4..8b+7]},
@@ -296,11 +304,6 @@ IRT_HD bool in_bin(float h0, float hN, float lo, float hi) {
   return (h0 < hi && hN > lo) || (h0 == hN && h0 == hi);
 }
 
-// Total order on floats (the sort key of the candidate heights): -0 before +0.
-IRT_HD uint32_t float_key(float v) {
-  const uint32_t b = f2u(v);
-  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-}
 
 // Expected number of list entries a radius drawn uniformly from [rmin, rmax] meets, for
 // the given edges: sum over bins of (bin length within [rmin, rmax]) * count.
@@ -443,13 +446,12 @@ IRT_HD uint32_t cell_header(const E &en, int n, const float *edges, int ne, uint
 
 // One fat entry (kFat4 float4, irt_common.h) of record i.
 IRT_HD void fat_entry(uint32_t i, const float *planes, const float *rng, const uint32_t *meta,
-                      const float *keys, float *F) {
+                      float *F) {
   for (int k = 0; k < 12; ++k) F[k] = planes[12 * (size_t)i + k];
   F[12] = rng[2 * (size_t)i];
   F[13] = rng[2 * (size_t)i + 1];
   F[14] = u2f(i);
   F[15] = u2f(meta[i]);
-  for (int k = 0; k < 4; ++k) F[16 + k] = keys[4 * (size_t)i + k];
 }
 
 }  // namespace irt

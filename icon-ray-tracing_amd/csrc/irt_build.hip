@@ -6,7 +6,7 @@
 //
 // Stages (every count and order deterministic, so the arrays are byte-identical to the
 // host restatement, host/irt_scene.cpp):
-//   1. k_prep        per record: planes, radial range, meta, coarse keys, block; column
+//   1. k_prep        per record: planes, radial range, meta (quantised keys), block; column
 //                    starts (records with different corners than their predecessor)
 //   2. scan          run (column) index of every record, the run start list
 //   3. k_run_count   per run: its kind (irt_build.h run_kind) and, for triangles, the
@@ -55,7 +55,7 @@ inline unsigned grid_for(size_t n, int block = 256) {
 
 // ---------------------------------------------------------------- 1. per record
 __global__ void k_prep(const irt_icon_cell *cells, const float4 *trig, size_t n, float4 *planes,
-                       float2 *rng, uint32_t *meta, float4 *keys, float4 *blocks, uint32_t *runFlag) {
+                       float2 *rng, uint32_t *meta, float4 *blocks, uint32_t *runFlag) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
     const irt_icon_cell &c = cells[i];
@@ -71,7 +71,6 @@ __global__ void k_prep(const irt_icon_cell *cells, const float4 *trig, size_t n,
     for (int k = 0; k < 3; ++k) planes[3 * i + k] = make_float4(pl[4 * k], pl[4 * k + 1], pl[4 * k + 2], pl[4 * k + 3]);
     rng[i] = make_float2(h0, hN);
     meta[i] = record_meta(c.height, nl);
-    keys[i] = make_float4(c.height[7], c.height[15], c.height[23], c.height[31]);
     float blk[64];
     record_block(c.height, c.value, blk);
     for (int k = 0; k < 16; ++k)
@@ -257,8 +256,7 @@ __global__ void k_cell_header(const uint32_t *offsets, uint32_t numCells, const 
 
 __global__ void k_cell_fill(const uint32_t *offsets, uint32_t numCells, const unsigned long long *vals,
                             const float2 *rng, const float4 *edges, const uint64_t *cellBase,
-                            uint32_t *hdr, const float *planes, const uint32_t *meta,
-                            const float *keys, float4 *fat) {
+                            uint32_t *hdr, const float *planes, const uint32_t *meta, float4 *fat) {
   for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < numCells; c += gridDim.x * blockDim.x) {
     const uint32_t q0 = offsets[c], n = offsets[c + 1] - q0;
     const uint64_t base = cellBase[c];
@@ -273,8 +271,8 @@ __global__ void k_cell_fill(const uint32_t *offsets, uint32_t numCells, const un
         const uint32_t rec = (uint32_t)vals[q0 + q];
         const float2 h = rng[rec];
         if (!in_bin(h.x, h.y, lo, hi)) continue;
-        float F[20];
-        fat_entry(rec, planes, reinterpret_cast<const float *>(rng), meta, keys, F);
+        float F[4 * kFat4];
+        fat_entry(rec, planes, reinterpret_cast<const float *>(rng), meta, F);
         float4 *o = fat + (size_t)(at++) * kFatStride4;
         for (int j = 0; j < kFat4; ++j) o[j] = make_float4(F[4 * j], F[4 * j + 1], F[4 * j + 2], F[4 * j + 3]);
         for (int j = kFat4; j < kFatStride4; ++j) o[j] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -373,19 +371,20 @@ int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_
   clk.s = s;
   const unsigned nb = grid_for(n);
   // --- 1. per record
-  float4 *planes, *keys;
+  float4 *planes;
   float2 *rng;
   uint32_t *meta, *runFlag, *runOf1, *runStart;
   BHIP(S.alloc(&planes, 3 * n));
   BHIP(S.alloc(&rng, n));
-  BHIP(S.alloc(&meta, n));
-  BHIP(S.alloc(&keys, n));
+  BHIP(hipMalloc((void **)&out.meta, std::max<size_t>(n, 1) * sizeof(uint32_t)));
+  out.bytes += std::max<size_t>(n, 1) * sizeof(uint32_t);
+  meta = out.meta;
   BHIP(hipMalloc((void **)&out.blocks, std::max<size_t>(n, 1) * kBlk4 * sizeof(float4)));
   out.bytes += std::max<size_t>(n, 1) * kBlk4 * sizeof(float4);
   BHIP(S.alloc(&runFlag, n));
   BHIP(S.alloc(&runOf1, n));
   BHIP(S.alloc(&runStart, numRuns + 1));
-  if (n) hipLaunchKernelGGL(k_prep, dim3(nb), dim3(256), 0, s, d_cells, d_trig, n, planes, rng, meta, keys, out.blocks, runFlag);
+  if (n) hipLaunchKernelGGL(k_prep, dim3(nb), dim3(256), 0, s, d_cells, d_trig, n, planes, rng, meta, out.blocks, runFlag);
   BHIP(hipGetLastError());
   clk.mark("per-record prep");
   // --- 2. runs
@@ -561,8 +560,7 @@ int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_
   out.bytes += std::max<uint64_t>(numFat, 1) * kFatStride4 * sizeof(float4);
   clk.mark("fat entries allocated");
   hipLaunchKernelGGL(k_cell_fill, dim3(nc), dim3(64), 0, s, offsets, numCells, pv2, rng, edges, cellBase,
-                     reinterpret_cast<uint32_t *>(out.binHdr), planesF, meta,
-                     reinterpret_cast<const float *>(keys), out.fat);
+                     reinterpret_cast<uint32_t *>(out.binHdr), planesF, meta, out.fat);
   BHIP(hipGetLastError());
   BHIP(hipStreamSynchronize(s));
   clk.mark("fat entries");

@@ -378,21 +378,67 @@ IRT_HD uint32_t sph_hash(float r) {
   return h >> 18;
 }
 
-// Fat entry: everything one candidate test of sample() reads, kFat4 float4 = 80 B:
+// Fat entry: everything one candidate test of sample() reads, kFat4 float4 = 64 B, packed
+// two to a 128-B line (a cell's bin lists are contiguous, so a list's next candidate usually
+// shares its first's line):
 //   [0..2]  the record's three side planes (n.xyz, w)              ICONGrid.h:197-203
 //   [3]     {height[0], height[numLayers], record index, meta}     ICONGrid.h:184
-//           meta = numLayers | (height[1..numLayers] non-decreasing) << 31
-//   [4]     coarse keys {height[7], height[15], height[23], height[31]}
-constexpr int kFat4 = 5;
-// Stride of the fat entries in float4: one 128-B line each (an 80-B entry at 80-B stride
-// straddles two lines half the time; the line is fetched whole either way)
-constexpr int kFatStride4 = 8;
+//           meta: see record_meta (irt_build.h) and record_path below
+constexpr int kFat4 = 4;
+constexpr int kFatStride4 = 4;
 // Per-record height/value blocks (the render record without its planes/keys), kBlk4
 // float4 = 256 B: block b (4 float4) = {height[8b..8b+3]}, {height[8b+4..8b+7]},
 // {value[8b-1..8b+2]}, {value[8b+3..8b+6]} (value[-1] := 0).
 constexpr int kBlk4 = 16;
 IRT_HD int blk_height_pos(int j) { return 16 * (j >> 3) + (j & 7); }
 IRT_HD int blk_value_pos(int c) { return 16 * ((c + 1) >> 3) + 8 + ((c + 1) & 7); }
+
+// Total order on floats (sort keys, quantised heights): -0 before +0.
+IRT_HD uint32_t float_key(float v) {
+  const uint32_t b = f2u(v);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+// The meta word of a record (its fat entry's last word; irt_build.h record_meta):
+//   bits 0-4   numLayers
+//   bit 5      coarse: height[1..numLayers] non-decreasing and height[0] <= height[1], so
+//              findHeight's 8-height block follows from the keys height[7], height[15],
+//              height[23] (irt_common.h rec_coarse_block; height[31] never counts)
+//   bits 6-29  q_j, j = 0,1,2: float_key(height[8j+7]) - float_key(height[0]), in units of
+//              meta_quantum, floored (8 bits each): key j lies in [q_j S, q_j S + S - 1]
+//              above height[0]'s key
+constexpr uint32_t kMetaCoarse = 32u;
+IRT_HD uint32_t meta_quantum(uint32_t k0, uint32_t kN) { return ((kN - k0) >> 8) + 1u; }
+// rec_coarse_block from the quantised keys, for r in [h0, hN] (the radial test passed):
+// exact wherever r's key is more than one unit outside every key's interval (one unit: the
+// -0/+0 pair, equal as floats, sits one key apart); -1 when r is that close to a key
+// (about 1 % of samples): the exact keys decide (record_value).
+IRT_HD int rec_coarse_block_q(uint32_t meta, float h0, float hN, float r) {
+  const int nl = (int)(meta & 31u);
+  const uint32_t k0 = float_key(h0), S = meta_quantum(k0, float_key(hN));
+  const uint32_t d = float_key(r) - k0;
+  int b = 0;
+  bool amb = false;
+  for (int j = 0; j < 3; ++j) {
+    if (8 * j + 7 > nl) break;
+    const uint32_t lo = ((meta >> (6 + 8 * j)) & 255u) * S, hi = lo + (S - 1u);
+    if (d > hi + 1u)
+      ++b;  // r > key: !(r <= key) counts
+    else if (d + 1u >= lo)
+      amb = true;
+  }
+  return amb ? -1 : b;
+}
+// The getValue path of a record found at radius r (the kernel's Found::path): bits 0-4
+// numLayers; bit 7: one 64-B block (coarse records), bits 5-6 its index b; bit 8: b must be
+// settled on the exact keys first; neither: the literal findHeight over the blocks.
+constexpr uint32_t kPathBlock = 128u, kPathExactKeys = 256u;
+IRT_HD uint32_t record_path(uint32_t meta, float h0, float hN, float r) {
+  const uint32_t nl = meta & 31u;
+  if (!(meta & kMetaCoarse)) return nl;
+  const int b = rec_coarse_block_q(meta, h0, hN, r);
+  return nl | kPathBlock | (b < 0 ? kPathExactKeys : ((uint32_t)b << 5));
+}
 
 // findHeight for non-decreasing height[1..nl], from the record layout in two gathers.
 // lower_bound's answer is #{ j in [1,nl] : !(hpos <= height[j]) } (a monotone predicate on

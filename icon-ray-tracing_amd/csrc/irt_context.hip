@@ -60,11 +60,16 @@ struct irt_context {
   int countersProbe = 0;        // measurement only: IRT_COUNTERS=off (no counts), =device
                                 // (per-workgroup stores into device memory, never read)
   uint32_t *d_probeCounts = nullptr;
+  size_t probeCap = 0;          // workgroups d_probeCounts holds
   float4 *d_samples = nullptr;   // per-frame colours of a progressive batch
   size_t sampleCap = 0;
   float *d_srgb = nullptr;
   float *d_valueRanges = nullptr;
   float *d_maxOp = nullptr;
+  // GRID_ACCEL_MODE's 256^3 grid, built on first use (ensure_grid): 201 MB and ~0.16 s at C5
+  // that a sphere-mode run never needs
+  bool gridBuilt = false;
+  uint32_t *d_meta = nullptr;    // per record numLayers (+ quantised keys), for the grid build
   float *d_gridVR = nullptr;     // GRID_ACCEL_MODE: Grid::valueRanges, kGridDim^3 box1f
   float *d_gridMaxOp = nullptr;  // Grid::maxOpacities
   uint32_t *d_gridBits = nullptr;  // its empty-space bitmap (k_grid_bits)
@@ -133,7 +138,7 @@ struct irt_context {
   bool building = false;
   size_t expected = 0, received = 0;
   irt_icon_cell *d_cells = nullptr;  // freed once the scene is built
-  float4 *d_trig = nullptr;
+  float4 *d_trig = nullptr;          // corner trig: kept for the lazy grid build
   VolumeAcc vacc{};
   size_t numRuns = 0;
   irt_icon_cell last{};
@@ -177,7 +182,7 @@ void free_all(irt_context *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
                   c->d_sphBits, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_gridBits, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
-                  c->d_lut, c->d_counters};
+                  c->d_lut, c->d_counters, c->d_meta};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->d_cells) (void)hipFree(c->d_cells);
@@ -354,6 +359,38 @@ int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int t
   return IRT_OK;
 }
 
+// buildICONGrid (hostCode.cu:668-682: initGrid + buildGrid_ICON over volbounds) on first
+// use of GRID_ACCEL_MODE (a render with IRT_ACCEL_GRID, irt_get_grid), from the scene's
+// blocks, meta words and corner trig, then the grid's majorants for the current transfer
+// function.  The reference builds it in main() whatever the accel mode (hostCode.cu:875);
+// the grid is the same whenever it is built.
+int ensure_grid(irt_context *c) {
+  if (c->gridBuilt) return IRT_OK;
+  const size_t gridMCs = (size_t)kGridDim * kGridDim * kGridDim;
+  int rc;
+  if (!c->d_gridVR && (rc = dalloc(c, &c->d_gridVR, 2 * gridMCs))) return rc;
+  if (!c->d_gridMaxOp && (rc = dalloc(c, &c->d_gridMaxOp, gridMCs))) return rc;
+  if (!c->d_gridBits && (rc = dalloc(c, &c->d_gridBits, (size_t)kGridBitWords))) return rc;
+  IRT_HIP(hipMemsetAsync(c->d_gridBits, 0, kGridBitWords * sizeof(uint32_t), c->stream));
+  launch_shell_init(c->d_gridVR, gridMCs, c->stream);  // initGrid(Grid) (hostCode.cu:205-214)
+  IRT_HIP(hipMemsetAsync(c->d_gridMaxOp, 0, gridMCs * sizeof(float), c->stream));
+  if (c->n) {
+    const irt_box3f &vb = c->info.bounds;
+    launch_grid_build(c->d_blocks, c->d_meta, c->d_trig, c->n, make_float3(vb.lower.x, vb.lower.y, vb.lower.z),
+                      make_float3(vb.upper.x, vb.upper.y, vb.upper.z), c->d_gridVR, c->stream);
+  }
+  if (c->tfSet) {
+    launch_max_opacities(c->d_gridVR, gridMCs, c->d_lut, c->lutSize, c->tfLo, c->tfHi, c->d_gridMaxOp,
+                         c->stream);
+    launch_grid_bits(c->d_gridMaxOp, c->d_gridBits, c->stream);
+  }
+  IRT_HIP(hipGetLastError());
+  IRT_HIP(hipStreamSynchronize(c->stream));
+  c->gridBuilt = true;
+  c->info.deviceBytes = c->bytes;
+  return IRT_OK;
+}
+
 int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int packed,
                 int tileBegin, int tileStride, uint32_t *fb, irt_vec4f *accum, int *numTilesOut,
                 void *stream, int numFrames = 1, const int32_t *tileList = nullptr,
@@ -386,6 +423,10 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     return IRT_E_INVALID;
   }
   IRT_HIP(hipSetDevice(c->device));
+  if (lp->accelMode == IRT_ACCEL_GRID) {
+    int rc = ensure_grid(c);
+    if (rc) return rc;
+  }
   // NULL is the null stream itself (ordered with the caller's blocking streams), never the
   // context's private non-blocking stream
   hipStream_t s = (hipStream_t)stream;
@@ -473,16 +514,36 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     if (c->h_wgCounts) IRT_HIP(hipHostFree(c->h_wgCounts));
     c->h_wgCounts = c->dh_wgCounts = nullptr;
     c->wgCap = 0;
-    IRT_HIP(hipHostMalloc((void **)&c->h_wgCounts, numWG * irt_context::kSlots * kCnt * sizeof(uint32_t)));
-    IRT_HIP(hipHostGetDevicePointer((void **)&c->dh_wgCounts, c->h_wgCounts, 0));
-    c->wgCap = numWG;
+    // kSlots x 1 KiB of pinned memory per workgroup and frame: a huge progressive batch may
+    // not get it -- then the counters go through the device-atomic block from here on
+    // (IRT_COUNTERS=atomic), which needs no per-workgroup memory
+    if (hipHostMalloc((void **)&c->h_wgCounts, numWG * irt_context::kSlots * kCnt * sizeof(uint32_t)) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void **)&c->dh_wgCounts, c->h_wgCounts, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      if (c->h_wgCounts) (void)hipHostFree(c->h_wgCounts);
+      c->h_wgCounts = c->dh_wgCounts = nullptr;
+      c->wgCountsOn = false;
+    } else {
+      c->wgCap = numWG;
+    }
   }
   A.wgCounts = c->wgCountsOn ? c->dh_wgCounts + (size_t)slot * c->wgCap * kCnt : nullptr;
+  const bool statsVariant = (c->variant & (32768 | 524288)) != 0;  // statistics, timing
   if (c->countersProbe == 1) {
+    // measurement only: no counts -- except that the statistics and timing variants add into
+    // the counter block unconditionally, so it stays
     A.wgCounts = nullptr;
-    A.counters = nullptr;
+    if (!statsVariant) A.counters = nullptr;
   } else if (c->countersProbe == 2) {
-    if (!c->d_probeCounts) IRT_HIP(hipMalloc((void **)&c->d_probeCounts, c->wgCap * kCnt * sizeof(uint32_t)));
+    if (numWG > c->probeCap) {  // per-workgroup stores into device memory: one slot per workgroup
+      IRT_HIP(hipStreamSynchronize(s));
+      if (c->d_probeCounts) IRT_HIP(hipFree(c->d_probeCounts));
+      c->d_probeCounts = nullptr;
+      c->probeCap = 0;
+      IRT_HIP(hipMalloc((void **)&c->d_probeCounts, numWG * kCnt * sizeof(uint32_t)));
+      c->probeCap = numWG;
+    }
     A.wgCounts = c->d_probeCounts;
   }
   A.numSamples = numFrames;
@@ -525,7 +586,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   c->schedApplied += c->schedLastApplied ? 1 : 0;
   // the 16-counter block (device atomics) is only needed by the statistics variant and the
   // IRT_COUNTERS=atomic mode; it must start zeroed
-  const bool block = !c->wgCountsOn || (c->variant & (32768 | 524288)) != 0;  // statistics, timing
+  const bool block = A.counters && (!c->wgCountsOn || statsVariant);
   if (block && !c->lastBlock) IRT_HIP(hipMemsetAsync(A.counters, 0, 16 * sizeof(unsigned long long), s));
   if (c->launches > 0 && s != c->lastStream) {
     // this slot may have been zeroed by the previous launch's k_stats_out on another stream
@@ -546,7 +607,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   }
   c->slotBlock[slot] = block;
   c->lastBlock = block;
-  c->slotWG[slot] = (c->wgCountsOn && numTiles > 0) ? numWG : 0;
+  c->slotWG[slot] = (c->wgCountsOn && c->countersProbe == 0 && numTiles > 0) ? numWG : 0;
   c->schedCopied[slot] = -1;
   if (copyCosts) {
     c->schedCopied[slot] = c->launches;
@@ -738,6 +799,7 @@ int irt_create_end(irt_context *c) {
   DeviceScene D;
   int rc = build_scene_device(c->d_cells, c->d_trig, numCells, c->numRuns, c->G, c->stream, D);
   c->d_blocks = D.blocks;
+  c->d_meta = D.meta;
   c->d_binHdr = D.binHdr;
   c->d_fat = D.fat;
   c->bytes += D.bytes;
@@ -806,30 +868,20 @@ int irt_create_end(irt_context *c) {
   // (hostCode.cu:652-666), majorants zero until a transfer function arrives
   if ((rc = dalloc(c, &c->d_valueRanges, 2 * c->numMCs))) return rc;
   launch_shell_init(c->d_valueRanges, c->numMCs, c->stream);
-  const size_t gridMCs = (size_t)kGridDim * kGridDim * kGridDim;
-  if ((rc = dalloc(c, &c->d_gridVR, 2 * gridMCs))) return rc;
-  if ((rc = dalloc(c, &c->d_gridMaxOp, gridMCs))) return rc;
-  if ((rc = dalloc(c, &c->d_gridBits, (size_t)kGridBitWords))) return rc;
-  IRT_HIP(hipMemsetAsync(c->d_gridBits, 0, kGridBitWords * sizeof(uint32_t), c->stream));
-  launch_shell_init(c->d_gridVR, gridMCs, c->stream);  // initGrid(Grid) (hostCode.cu:205-214)
-  IRT_HIP(hipMemsetAsync(c->d_gridMaxOp, 0, gridMCs * sizeof(float), c->stream));
   if (numCells) {
     const irt_box3f &sb = c->info.sphericalBounds;
     launch_shell_build(c->d_cells, numCells, make_int3(dims[0], dims[1], dims[2]),
                        make_float3(sb.lower.x, sb.lower.y, sb.lower.z),
                        make_float3(sb.upper.x, sb.upper.y, sb.upper.z), c->d_valueRanges, c->stream);
-    // buildICONGrid (hostCode.cu:668-682): initGrid + buildGrid_ICON over volbounds
-    const irt_box3f &vb = c->info.bounds;
-    launch_grid_build(c->d_cells, c->d_trig, numCells, make_float3(vb.lower.x, vb.lower.y, vb.lower.z),
-                      make_float3(vb.upper.x, vb.upper.y, vb.upper.z), c->d_gridVR, c->stream);
   }
   IRT_HIP(hipGetLastError());
   IRT_HIP(hipStreamSynchronize(c->stream));
-  mark("shell + grid builds");
+  mark("shell build");
+  // the records themselves are not needed again: the GRID_ACCEL_MODE grid, if ever asked
+  // for, is built from the blocks, meta words and corner trig (ensure_grid)
   IRT_HIP(hipFree(c->d_cells));
-  IRT_HIP(hipFree(c->d_trig));
   c->d_cells = nullptr;
-  c->d_trig = nullptr;
+  c->bytes += std::max<size_t>(numCells, 1) * 3 * sizeof(float4);  // d_trig, kept
   c->building = false;
   c->info.deviceBytes = c->bytes;
   return IRT_OK;
@@ -1005,9 +1057,11 @@ int irt_set_transfunc(irt_context *c, const irt_vec4f *lut, int size, irt_box1f 
   // ignore opacityScale exactly like the reference kernel (hostCode.cu:362-397)
   launch_max_opacities(c->d_valueRanges, c->numMCs, c->d_lut, size, valueRange.lower,
                        valueRange.upper, c->d_maxOp, c->stream);
-  launch_max_opacities(c->d_gridVR, (size_t)kGridDim * kGridDim * kGridDim, c->d_lut, size,
-                       valueRange.lower, valueRange.upper, c->d_gridMaxOp, c->stream);
-  launch_grid_bits(c->d_gridMaxOp, c->d_gridBits, c->stream);
+  if (c->gridBuilt) {  // GRID_ACCEL_MODE's majorants, once its grid exists (ensure_grid)
+    launch_max_opacities(c->d_gridVR, (size_t)kGridDim * kGridDim * kGridDim, c->d_lut, size,
+                         valueRange.lower, valueRange.upper, c->d_gridMaxOp, c->stream);
+    launch_grid_bits(c->d_gridMaxOp, c->d_gridBits, c->stream);
+  }
   IRT_HIP(hipGetLastError());
   IRT_HIP(hipStreamSynchronize(c->stream));
   c->tfSet = true;
@@ -1170,6 +1224,9 @@ int irt_get_grid(const irt_context *c, float *valueRanges, float *maxOpacities) 
     return IRT_E_INVALID;
   }
   IRT_HIP(hipSetDevice(c->device));
+  // the grid is a cache built on first use: building it changes no observable state
+  int rc = ensure_grid(const_cast<irt_context *>(c));
+  if (rc) return rc;
   IRT_HIP(hipStreamSynchronize(c->stream));
   const size_t n = (size_t)kGridDim * kGridDim * kGridDim;
   if (valueRanges)

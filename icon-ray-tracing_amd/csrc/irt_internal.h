@@ -26,8 +26,7 @@ struct HostScene {
   std::vector<float> trig;        // n * 12: per corner {cosf lat, sinf lat, cosf lon, sinf lon}
   std::vector<float> planes;      // n * 12: the side planes of sample() (ICONGrid.h:197-199)
   std::vector<float> rng;         // n * 2: {height[0], height[numLayers]}
-  std::vector<uint32_t> meta;     // n: numLayers | sorted << 31
-  std::vector<float> keys;        // n * 4: coarse findHeight keys
+  std::vector<uint32_t> meta;     // n: record_meta (numLayers, coarse flag, quantised keys)
   std::vector<float> blocks;      // n * kBlk4 * 4: height/value blocks
   int G = 0;                      // cube-map cells per face edge
   std::vector<uint32_t> offsets;  // 6*G*G + 1 CSR offsets
@@ -48,6 +47,8 @@ int build_bins(HostScene &S, int threads);
 // Cube-map resolution for a scene with numRuns columns (IRT_LOCATOR_SCALE / _G override).
 int locator_resolution(size_t numRuns);
 // Point location over the binned locator, as the kernel does it (host restatement).
+// getValue of record rec at radius r along its record_path (the kernel's record_value)
+float record_value_host(const HostScene &s, uint32_t rec, uint32_t path, float r);
 int locate_bins_host(const HostScene &s, float px, float py, float pz, float &value,
                      uint32_t *record, uint32_t *tested);
 

@@ -91,8 +91,8 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 void launch_shell_init(float *valueRanges, size_t numMCs, hipStream_t s);
 void launch_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, float3 lo, float3 hi,
                         float *valueRanges, hipStream_t s);
-void launch_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n, float3 lo,
-                       float3 hi, float *valueRanges, hipStream_t s);
+void launch_grid_build(const float4 *blocks, const uint32_t *meta, const float4 *trig, size_t n,
+                       float3 lo, float3 hi, float *valueRanges, hipStream_t s);
 void launch_grid_bits(const float *maxOp, uint32_t *bits, hipStream_t s);
 void launch_max_opacities(const float *valueRanges, size_t numMCs, const float4 *lut, int size,
                           float lo, float hi, float *maxOp, hipStream_t s);
@@ -105,6 +105,7 @@ void launch_copy_u32(const uint32_t *src, uint32_t *dst, size_t n, hipStream_t s
 // caller owns blocks / binHdr / fat; on failure it frees whatever is non-null.
 struct DeviceScene {
   float4 *blocks = nullptr;
+  uint32_t *meta = nullptr;  // per record (irt_build.h record_meta), kept for the lazy grid build
   uint4 *binHdr = nullptr;
   float4 *fat = nullptr;
   size_t entries = 0, binEntries = 0, bigCells = 0, bytes = 0;

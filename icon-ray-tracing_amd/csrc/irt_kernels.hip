@@ -38,50 +38,102 @@ __device__ __forceinline__ void atomic_max_f(float *addr, float val) {
 // (getValue(h[i]), getValue(h[i+1])).  The lat/lon projections do not depend on the
 // height and dims.x = 1 makes the radial index 0 (times dims.x-1 = 0), so every layer of
 // a cell hits the same rectangle: rasterising min/max over the layers once is the same
-// min/max.  One workgroup-stride loop per cell row keeps seam cells (spanning all 1024
-// longitudes) from serialising a single lane.
-__global__ void k_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, float3 sbLo,
-                              float3 sbHi, float *valueRanges) {
-  const size_t ci = blockIdx.x;
-  if (ci >= n) return;
-  const irt_icon_cell &c = cells[ci];
-  const int nl = c.numLayers;
-  if (nl <= 0) return;
-  // min/max over the layers with the CAS loops' "store only if strictly smaller/larger"
-  // semantics (NaN never stores; +-inf and IRT_FLT_MAX behave as in the reference)
-  float lo = IRT_FLT_MAX, hi = -IRT_FLT_MAX;
-  for (int i = 0; i < nl; ++i) {
-    const float v0 = c.value[find_height(c.height, nl, c.height[i])];      // getValue(h[i])
-    const float v1 = c.value[find_height(c.height, nl, c.height[i + 1])];  // getValue(h[i+1])
-    if (v0 < lo) lo = v0;
-    if (v1 > hi) hi = v1;
+// min/max.
+//
+// One lane per record (round 2 ran a workgroup per record, whose redundant scalar binary
+// searches took 493 ms at C5).  getValue(h[i]) = value[findHeight(h[i])]: for heights
+// non-decreasing in float_key order (record_meta's coarse records) findHeight(h[i]) is
+// #{j >= 1 : h[j] < h[i]}, which a running index gives (0 for i = 0; i-1, or the previous
+// answer on a repeated height); other records run the literal binary search.  Rectangles
+// wider than kShellSmall macrocells (the antimeridian seam's full rows, polar caps) go to
+// k_shell_rects, a workgroup each.
+constexpr int kShellSmall = 64;
+struct ShellRect {
+  int xlo, ylo, zlo, nx, ny, nz;
+  float lo, hi;
+};
+
+__device__ __forceinline__ void shell_write(const ShellRect &q, long k, int3 dims, float *valueRanges) {
+  const int mx = q.xlo + (int)(k % q.nx);
+  const int my = q.ylo + (int)((k / q.nx) % q.ny);
+  const int mz = q.zlo + (int)(k / ((long)q.nx * q.ny));
+  float *vr = valueRanges + 2 * ((size_t)mz * dims.x * dims.y + (size_t)my * dims.x + mx);
+  atomic_min_f(vr, q.lo);
+  atomic_max_f(vr + 1, q.hi);
+}
+
+__global__ void __launch_bounds__(256) k_shell_build(const irt_icon_cell *cells, size_t n, int3 dims,
+                                                     float3 sbLo, float3 sbHi, float *valueRanges,
+                                                     ShellRect *wide, unsigned long long *numWide,
+                                                     size_t wideCap) {
+  for (size_t ci = blockIdx.x * (size_t)blockDim.x + threadIdx.x; ci < n;
+       ci += (size_t)gridDim.x * blockDim.x) {
+    const irt_icon_cell &c = cells[ci];
+    const int nl = c.numLayers;
+    if (nl <= 0) continue;
+    // min/max over the layers with the CAS loops' "store only if strictly smaller/larger"
+    // semantics (NaN never stores; +-inf and IRT_FLT_MAX behave as in the reference)
+    float lo = IRT_FLT_MAX, hi = -IRT_FLT_MAX;
+    bool sorted = true;
+    for (int j = 1; j <= nl; ++j)
+      if (!(float_key(c.height[j - 1]) <= float_key(c.height[j]))) sorted = false;
+    if (sorted) {
+      int f = 0;  // findHeight(h[i])
+      float hp = c.height[0];
+      for (int i = 0; i < nl; ++i) {
+        const float v0 = c.value[f];  // getValue(h[i])
+        const float h1 = c.height[i + 1];
+        f = h1 == hp ? f : i;  // findHeight(h[i+1])
+        hp = h1;
+        const float v1 = c.value[f];  // getValue(h[i+1])
+        if (v0 < lo) lo = v0;
+        if (v1 > hi) hi = v1;
+      }
+    } else {
+      for (int i = 0; i < nl; ++i) {
+        const float v0 = c.value[find_height(c.height, nl, c.height[i])];      // getValue(h[i])
+        const float v1 = c.value[find_height(c.height, nl, c.height[i + 1])];  // getValue(h[i+1])
+        if (v0 < lo) lo = v0;
+        if (v1 > hi) hi = v1;
+      }
+    }
+    int ylo = 0x7fffffff, yhi = (int)0x80000000u, zlo = 0x7fffffff, zhi = (int)0x80000000u;
+    int xlo = 0x7fffffff, xhi = (int)0x80000000u;
+    for (int k = 0; k < 3; ++k) {
+      const int py = project_axis(c.lat[k], sbLo.y, sbHi.y, dims.y);
+      const int pz = project_axis(c.lon[k], sbLo.z, sbHi.z, dims.z);
+      const int pxb = f2i_x86((c.height[0] - sbLo.x) / (sbHi.x - sbLo.x) * (float)(dims.x - 1));
+      const int pxt = f2i_x86((c.height[nl] - sbLo.x) / (sbHi.x - sbLo.x) * (float)(dims.x - 1));
+      ylo = min(ylo, py); yhi = max(yhi, py);
+      zlo = min(zlo, pz); zhi = max(zhi, pz);
+      xlo = min(xlo, pxb); xhi = max(xhi, pxt);
+    }
+    // Out-of-grid rectangles only arise from degenerate bounds (zero-size or non-finite
+    // sphericalBounds), where the reference writes out of bounds; clamp instead.
+    xlo = max(xlo, 0); ylo = max(ylo, 0); zlo = max(zlo, 0);
+    xhi = min(xhi, dims.x - 1); yhi = min(yhi, dims.y - 1); zhi = min(zhi, dims.z - 1);
+    if (xlo > xhi || ylo > yhi || zlo > zhi) continue;
+    const ShellRect q = {xlo, ylo, zlo, xhi - xlo + 1, yhi - ylo + 1, zhi - zlo + 1, lo, hi};
+    const long total = (long)q.nx * q.ny * q.nz;
+    if (total > kShellSmall && numWide) {
+      const unsigned long long k = atomicAdd(numWide, 1ull);
+      if (k < wideCap) {
+        wide[k] = q;
+        continue;
+      }  // list full: this lane does it
+    }
+    for (long k = 0; k < total; ++k) shell_write(q, k, dims, valueRanges);
   }
-  int ylo = 0x7fffffff, yhi = (int)0x80000000u, zlo = 0x7fffffff, zhi = (int)0x80000000u;
-  int xlo = 0x7fffffff, xhi = (int)0x80000000u;
-  for (int k = 0; k < 3; ++k) {
-    const int py = project_axis(c.lat[k], sbLo.y, sbHi.y, dims.y);
-    const int pz = project_axis(c.lon[k], sbLo.z, sbHi.z, dims.z);
-    const int pxb = f2i_x86((c.height[0] - sbLo.x) / (sbHi.x - sbLo.x) * (float)(dims.x - 1));
-    const int pxt = f2i_x86((c.height[nl] - sbLo.x) / (sbHi.x - sbLo.x) * (float)(dims.x - 1));
-    ylo = min(ylo, py); yhi = max(yhi, py);
-    zlo = min(zlo, pz); zhi = max(zhi, pz);
-    xlo = min(xlo, pxb); xhi = max(xhi, pxt);
-  }
-  // Out-of-grid rectangles only arise from degenerate bounds (zero-size or non-finite
-  // sphericalBounds), where the reference writes out of bounds; clamp instead.
-  xlo = max(xlo, 0); ylo = max(ylo, 0); zlo = max(zlo, 0);
-  xhi = min(xhi, dims.x - 1); yhi = min(yhi, dims.y - 1); zhi = min(zhi, dims.z - 1);
-  if (xlo > xhi || ylo > yhi || zlo > zhi) return;
-  const int nx = xhi - xlo + 1, ny = yhi - ylo + 1, nz = zhi - zlo + 1;
-  const long total = (long)nx * ny * nz;
-  for (long q = threadIdx.x; q < total; q += blockDim.x) {
-    const int mx = xlo + (int)(q % nx);
-    const int my = ylo + (int)((q / nx) % ny);
-    const int mz = zlo + (int)(q / ((long)nx * ny));
-    const size_t id = (size_t)mz * dims.x * dims.y + (size_t)my * dims.x + mx;
-    float *vr = valueRanges + 2 * id;
-    atomic_min_f(vr, lo);
-    atomic_max_f(vr + 1, hi);
+}
+
+// The deferred wide rectangles: one workgroup per rectangle, lanes sharing its macrocells.
+__global__ void __launch_bounds__(256) k_shell_rects(const ShellRect *wide, const unsigned long long *numWide,
+                                                     size_t wideCap, int3 dims, float *valueRanges) {
+  const unsigned long long nw = *numWide < wideCap ? *numWide : wideCap;
+  for (size_t b = blockIdx.x; b < nw; b += gridDim.x) {
+    const ShellRect q = wide[b];
+    const long total = (long)q.nx * q.ny * q.nz;
+    for (long k = threadIdx.x; k < total; k += blockDim.x) shell_write(q, k, dims, valueRanges);
   }
 }
 
@@ -104,13 +156,31 @@ struct GridBox {
 };
 constexpr long kSmallBox = 256;
 
-__global__ void __launch_bounds__(128) k_grid_build(const irt_icon_cell *cells, const float4 *trig,
-                                                    size_t n, int dim, float3 lo, float3 hi,
-                                                    float *valueRanges, GridBox *big,
+// findHeight (ICONGrid.h:117-145) over a record's height/value block (irt_common.h kBlk4)
+__device__ __forceinline__ int find_height_blk(const float *Bf, int nl, float hpos) {
+  int first = 0, count = nl;
+  while (count > 0) {
+    const int step = count / 2, it = first + step;
+    if (!(hpos <= Bf[blk_height_pos(it + 1)])) {
+      first = it + 1;
+      count -= step + 1;
+    } else {
+      count = step;
+    }
+  }
+  return first;
+}
+
+// Built on first use (irt_context.hip ensure_grid), from the scene's per-record blocks,
+// meta words (numLayers) and corner trig -- the records themselves are gone by then.
+__global__ void __launch_bounds__(128) k_grid_build(const float4 *blocks, const uint32_t *meta,
+                                                    const float4 *trig, size_t n, int dim, float3 lo,
+                                                    float3 hi, float *valueRanges, GridBox *big,
                                                     unsigned long long *numBig, size_t bigCap) {
   const size_t ci = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (ci >= n) return;
-  const irt_icon_cell &c = cells[ci];
+  const float *Bf = reinterpret_cast<const float *>(blocks + (size_t)kBlk4 * ci);
+  const int numLayers = (int)(meta[ci] & 31u);
   const float4 t0 = trig[3 * ci], t1 = trig[3 * ci + 1], t2 = trig[3 * ci + 2];
   int3 pLo = make_int3(0, 0, 0), pHi = make_int3(-1, -1, -1);
   float rLo = 0.f, rHi = 0.f;
@@ -132,8 +202,8 @@ __global__ void __launch_bounds__(128) k_grid_build(const irt_icon_cell *cells, 
           atomic_max_f(vr + 1, rHi);
         }
   };
-  for (int i = 0; i < c.numLayers; ++i) {
-    const float hb = c.height[i], ht = c.height[i + 1];
+  for (int i = 0; i < numLayers; ++i) {
+    const float hb = Bf[blk_height_pos(i)], ht = Bf[blk_height_pos(i + 1)];
     const float3 b1 = to_cartesian_trig(hb, t0), b2 = to_cartesian_trig(hb, t1), b3 = to_cartesian_trig(hb, t2);
     float3 v1 = to_cartesian_trig(ht, t0), v2 = to_cartesian_trig(ht, t1), v3 = to_cartesian_trig(ht, t2);
     float3 bl = make_float3(__builtin_inff(), __builtin_inff(), __builtin_inff());
@@ -153,8 +223,8 @@ __global__ void __launch_bounds__(128) k_grid_build(const irt_icon_cell *cells, 
     v3 = make_float3(v3.x + v3.x * off, v3.y + v3.y * off, v3.z + v3.z * off);
     ext(v1); ext(v2); ext(v3);
     // box1f valueRange(INFINITY,-INFINITY).extend(getValue(h[i])).extend(getValue(h[i+1]))
-    const float g0 = c.value[find_height(c.height, c.numLayers, hb)];
-    const float g1 = c.value[find_height(c.height, c.numLayers, ht)];
+    const float g0 = Bf[blk_value_pos(find_height_blk(Bf, numLayers, hb))];
+    const float g1 = Bf[blk_value_pos(find_height_blk(Bf, numLayers, ht))];
     const float vlo = fminf(fminf(__builtin_inff(), g0), g1);
     const float vhi = fmaxf(fmaxf(-__builtin_inff(), g0), g1);
     const int3 a = make_int3(project_on_grid(bl.x, lo.x, hi.x, dim), project_on_grid(bl.y, lo.y, hi.y, dim),
@@ -277,10 +347,27 @@ void launch_shell_init(float *vr, size_t numMCs, hipStream_t s) {
 void launch_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, float3 lo, float3 hi,
                         float *vr, hipStream_t s) {
   if (n == 0) return;
-  hipLaunchKernelGGL(k_shell_build, dim3((unsigned)n), dim3(64), 0, s, cells, n, dims, lo, hi, vr);
+  const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1u << 16);
+  // the wide-rectangle list: sized for the seam and polar columns, capped (overflow stays
+  // in-lane)
+  const size_t cap = std::min<size_t>(n / 8 + 4096, size_t(1) << 22);
+  ShellRect *wide = nullptr;
+  unsigned long long *numWide = nullptr;
+  if (hipMallocAsync((void **)&wide, cap * sizeof(ShellRect), s) != hipSuccess ||
+      hipMallocAsync((void **)&numWide, sizeof(unsigned long long), s) != hipSuccess) {
+    hipLaunchKernelGGL(k_shell_build, dim3(blocks), dim3(256), 0, s, cells, n, dims, lo, hi, vr,
+                       (ShellRect *)nullptr, (unsigned long long *)nullptr, (size_t)0);
+    return;
+  }
+  (void)hipMemsetAsync(numWide, 0, sizeof(unsigned long long), s);
+  hipLaunchKernelGGL(k_shell_build, dim3(blocks), dim3(256), 0, s, cells, n, dims, lo, hi, vr, wide,
+                     numWide, cap);
+  hipLaunchKernelGGL(k_shell_rects, dim3(2048), dim3(256), 0, s, wide, numWide, cap, dims, vr);
+  (void)hipFreeAsync(wide, s);
+  (void)hipFreeAsync(numWide, s);
 }
-void launch_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n, float3 lo,
-                       float3 hi, float *vr, hipStream_t s) {
+void launch_grid_build(const float4 *blocks, const uint32_t *meta, const float4 *trig, size_t n,
+                       float3 lo, float3 hi, float *vr, hipStream_t s) {
   if (n == 0) return;
   // the deferred-box list: sized for a few boxes per cell, capped (overflow stays in-lane)
   const size_t cap = std::min<size_t>(4 * n + 1024, size_t(1) << 22);
@@ -289,13 +376,14 @@ void launch_grid_build(const irt_icon_cell *cells, const float4 *trig, size_t n,
   if (hipMallocAsync((void **)&big, cap * sizeof(GridBox), s) != hipSuccess ||
       hipMallocAsync((void **)&numBig, sizeof(unsigned long long), s) != hipSuccess) {
     // no scratch: every box in-lane
-    hipLaunchKernelGGL(k_grid_build, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, cells, trig,
-                       n, kGridDim, lo, hi, vr, (GridBox *)nullptr, (unsigned long long *)nullptr, (size_t)0);
+    hipLaunchKernelGGL(k_grid_build, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, blocks, meta,
+                       trig, n, kGridDim, lo, hi, vr, (GridBox *)nullptr, (unsigned long long *)nullptr,
+                       (size_t)0);
     return;
   }
   (void)hipMemsetAsync(numBig, 0, sizeof(unsigned long long), s);
-  hipLaunchKernelGGL(k_grid_build, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, cells, trig, n,
-                     kGridDim, lo, hi, vr, big, numBig, cap);
+  hipLaunchKernelGGL(k_grid_build, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, blocks, meta, trig,
+                     n, kGridDim, lo, hi, vr, big, numBig, cap);
   hipLaunchKernelGGL(k_grid_boxes, dim3(2048), dim3(256), 0, s, big, numBig, cap, kGridDim, vr);
   (void)hipFreeAsync(big, s);
   (void)hipFreeAsync(numBig, s);

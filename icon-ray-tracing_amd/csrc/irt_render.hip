@@ -192,7 +192,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     return Bf[blk_value_pos(first)];
   }
 
-  // sample()'s point test (ICONGrid.h:184, 197-203) on one fat entry {p0, p1, p2, m, ck}:
+  // sample()'s point test (ICONGrid.h:184, 197-203) on one fat entry {p0, p1, p2, m}:
   // the radial range and the three ccw side planes
   __device__ __forceinline__ bool pass_fat(const float4 &p0, const float4 &p1, const float4 &p2,
                                            const float4 &m, float px, float py, float pz, float r) {
@@ -207,10 +207,10 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     return true;
   }
 
-  // The record a point test found: index, meta (numLayers | sorted << 31), coarse keys.
+  // The record a point test found: index and its getValue path at the sample's radius
+  // (irt_common.h record_path: numLayers, which 64-B block, or the literal search).
   struct Found {
-    uint32_t rec, meta;
-    float4 ck;
+    uint32_t rec, path;
   };
 
   // First entry of fat entries [q, qe) whose point test passes, among records < limit:
@@ -227,10 +227,10 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       }
       if (j >= n) break;
       const float4 *F = A.fat + (size_t)(q + j) * kFatStride4;
-      const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3], ak = F[4];
+      const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3];
       if (__float_as_uint(am.z) >= limit) return false;
       if (pass_fat(a0, a1, a2, am, px, py, pz, r)) {
-        f = {__float_as_uint(am.z), __float_as_uint(am.w), ak};
+        f = {__float_as_uint(am.z), record_path(__float_as_uint(am.w), am.x, am.y, r)};
         return true;
       }
     }
@@ -238,12 +238,18 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   }
 
   // getValue (ICONGrid.h:147-164) of the found record at radius r: sorted heights take the
-  // coarse key's 64-B height/value block (one gather), others the literal binary search
+  // 64-B height/value block the quantised keys pick (one gather; r within a unit of a key:
+  // the exact keys from the record's lines first), others the literal binary search
   __device__ __forceinline__ float record_value(const Found &f, float r) {
-    const int nl = (int)(f.meta & 0x7fffffffu);
+    const int nl = (int)(f.path & 31u);
     const float4 *B = A.blocks + (size_t)f.rec * kBlk4;
-    if (f.meta >> 31) {
-      const int b = rec_coarse_block(f.ck.x, f.ck.y, f.ck.z, f.ck.w, nl, r);
+    if (f.path & kPathBlock) {
+      int b = (int)((f.path >> 5) & 3u);
+      if (f.path & kPathExactKeys) {
+        const float *Bf = reinterpret_cast<const float *>(B);
+        b = rec_coarse_block(Bf[blk_height_pos(7)], Bf[blk_height_pos(15)], Bf[blk_height_pos(23)],
+                             __builtin_inff(), nl, r);  // height[31] = hN >= r never counts
+      }
       const float4 *Q = B + 4 * b;
       const float4 h0 = Q[0], h1 = Q[1], v0 = Q[2], v1 = Q[3];
       const int k = rec_block_index(h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, b, nl, r);
@@ -385,7 +391,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     // bin, so a second pass scans it for a lower record (one scan site, two passes)
     const float eb = __uint_as_float(H0.x ^ (m1 & (H0.x ^ H0.y)) ^ (m2 & (H0.y ^ H0.z)));
     const bool onEdge = b < kMaxEdges && r == eb;
-    Found f = {0xFFFFFFFFu, 0u, make_float4(0.f, 0.f, 0.f, 0.f)};
+    Found f = {0xFFFFFFFFu, 0u};
     bool hit = false;
     uint32_t qb = H0.w + beg, qe = H0.w + end;
     for (int pass = 0; pass < 2; ++pass) {
@@ -425,8 +431,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   static constexpr bool kWaveScan = kCoop && (OPT & (OPT_WEDGE | OPT_GRID | OPT_SCAN1)) == 0;
   __device__ __forceinline__ bool pass_entry(const float4 *F, float px, float py, float pz, float r,
                                              Found &f) {
-    const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3], ak = F[4];
-    f = {__float_as_uint(am.z), __float_as_uint(am.w), ak};
+    const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3];
+    f = {__float_as_uint(am.z), record_path(__float_as_uint(am.w), am.x, am.y, r)};
     if (r < am.x || r > am.y) return false;                               // ICONGrid.h:184
     if (dot3(px, py, pz, a0.x, a0.y, a0.z) - a0.w > 0.f) return false;  // ICONGrid.h:201
     if (dot3(px, py, pz, a1.x, a1.y, a1.z) - a1.w > 0.f) return false;  // 202
@@ -447,11 +453,10 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     // The scan's state lives in the wave's LDS (fewer live VGPRs across it):
     //   W.pt[l]  the sample {point, r} of lane l
     //   W.lst[l] its list {first entry, sub-cell mask, next list position, record limit}
-    //   fck[l], frm[l]  the record found so far: coarse keys, {record, meta} (in the round's
-    //            request slots CW.req / CW.ray, free once the round has read them)
+    //   frm[l]   the record found so far: {record, getValue path} (in the round's request
+    //            slots CW.ray, free once the round has read them)
     //   W.own[s] the lane whose tasks start at s (W.step, free after the round's prefix)
     uint32_t *own = reinterpret_cast<uint32_t *>(CW.step);
-    float4 *fck = CW.req;
     uint2 *frm = reinterpret_cast<uint2 *>(CW.ray);
     uint32_t c = 0u;
     uint32_t fe = 0u, flim = 0xFFFFFFFFu;  // the pass's first candidate entry, record limit
@@ -490,8 +495,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
           ++specCand;
           if (ok) {
             hit = true;
-            fck[lane] = f.ck;
-            frm[lane] = make_uint2(f.rec, f.meta);
+            frm[lane] = make_uint2(f.rec, f.path);
           } else {
             rem = c - 1u;
             W.lst[lane].z = 1u;
@@ -529,10 +533,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         const uint64_t pm = __ballot(tp), lm = __ballot(tl);
         // the lowest event of each owner's tasks: a passing record (it hands it over) or the limit
         const uint64_t below = t ? (~0ull >> (64u - t)) : 0ull;  // tasks < t
-        if (tp && ((pm | lm) & below & (~0ull << s0)) == 0ull) {
-          fck[o] = g.ck;
-          frm[o] = make_uint2(g.rec, g.meta);
-        }
+        if (tp && ((pm | lm) & below & (~0ull << s0)) == 0ull) frm[o] = make_uint2(g.rec, g.path);
         __builtin_amdgcn_wave_barrier();
         if (owns) {
           const uint32_t k = min(rem, 64u - start);  // this owner's tasks in this batch
@@ -577,10 +578,10 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     }
     if (!want) return false;
     const float r = W.pt[lane].w;
-    Found f = {0xFFFFFFFFu, 0u, make_float4(0.f, 0.f, 0.f, 0.f)};
+    Found f = {0xFFFFFFFFu, 0u};
     if (hit) {
       const uint2 rm = frm[lane];
-      f = {rm.x, rm.y, fck[lane]};
+      f = {rm.x, rm.y};
     }
     if (A.numSph) {
       const uint32_t h = sph_hash(r);

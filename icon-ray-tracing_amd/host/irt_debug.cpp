@@ -93,28 +93,11 @@ int irt_debug_scene_values(const irt_debug_scene *s, uint32_t rec, float r, floa
   int32_t nl;
   memcpy(&nl, hv + 63, 4);
   out2[0] = hv[32 + find_height(hv, nl, r)];
-  // the kernel's path: coarse keys + one 64-B block for sorted heights, else the literal
-  // binary search over the block (irt_render.hip record_value)
-  const float *B = &s->s.blocks[(size_t)rec * kBlk4 * 4];
-  const float *K = &s->s.keys[4 * (size_t)rec];
-  if (s->s.meta[rec] >> 31) {
-    const int b = rec_coarse_block(K[0], K[1], K[2], K[3], nl, r);
-    const float *Q = B + 16 * b;
-    const int m = rec_block_index(Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], Q[6], b, nl, r);
-    out2[1] = select8(m, Q[8], Q[9], Q[10], Q[11], Q[12], Q[13], Q[14], Q[15]);
-  } else {
-    int first = 0, count = nl;
-    while (count > 0) {
-      const int stp = count / 2, it = first + stp;
-      if (!(r <= B[blk_height_pos(it + 1)])) {
-        first = it + 1;
-        count -= stp + 1;
-      } else {
-        count = stp;
-      }
-    }
-    out2[1] = B[blk_value_pos(first)];
-  }
+  // the kernel's path (irt_render.hip record_value): the quantised coarse keys pick one
+  // 64-B block for sorted heights (exact keys near a key), else the literal binary search
+  out2[1] = record_value_host(s->s, rec,
+                              record_path(s->s.meta[rec], s->s.rng[2 * (size_t)rec],
+                                          s->s.rng[2 * (size_t)rec + 1], r), r);
   return IRT_OK;
 }
 

@@ -89,13 +89,12 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads)
   S.n = n;
   compute_volume_info(cells, n, S.info);
 
-  // --- per record: glibc corner trig, planes, radial range, meta, keys, blocks
+  // --- per record: glibc corner trig, planes, radial range, meta, blocks
   S.hv.assign(n * kHV, 0.f);
   S.trig.resize(n * 12);
   S.planes.resize(n * 12);
   S.rng.resize(n * 2);
   S.meta.resize(n);
-  S.keys.resize(n * 4);
   S.blocks.resize(n * (size_t)kBlk4 * 4);
   parallel_ranges(n, threads, [&](int, size_t b, size_t e) {
     for (size_t i = b; i < e; ++i) {
@@ -112,10 +111,6 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads)
       S.rng[2 * i] = h0;
       S.rng[2 * i + 1] = hN;
       S.meta[i] = record_meta(c.height, c.numLayers);
-      S.keys[4 * i + 0] = c.height[7];
-      S.keys[4 * i + 1] = c.height[15];
-      S.keys[4 * i + 2] = c.height[23];
-      S.keys[4 * i + 3] = c.height[31];
       record_block(c.height, c.value, &S.blocks[i * (size_t)kBlk4 * 4]);
       float *hv = &S.hv[i * kHV];
       memcpy(hv, c.height, 32 * sizeof(float));
@@ -277,8 +272,7 @@ int build_bins(HostScene &S, int threads) {
         for (uint32_t q = S.offsets[cell]; q < S.offsets[cell + 1]; ++q) {
           const uint32_t rec = S.entryRec[q];
           if (!in_bin(S.rng[2 * (size_t)rec], S.rng[2 * (size_t)rec + 1], lo, hi)) continue;
-          fat_entry(rec, S.planes.data(), S.rng.data(), S.meta.data(), S.keys.data(),
-                    &S.fat[at++ * kFatStride4 * 4]);
+          fat_entry(rec, S.planes.data(), S.rng.data(), S.meta.data(), &S.fat[at++ * kFatStride4 * 4]);
         }
       }
     }
@@ -293,11 +287,23 @@ bool test_fat(const HostScene &s, const float *F, float px, float py, float pz, 
   if (r < F[12] || r > F[13]) return false;  // ICONGrid.h:184
   for (int k = 0; k < 3; ++k)
     if (eval_plane(F + 4 * k, px, py, pz) > 0.f) return false;  // ICONGrid.h:201-203
-  const uint32_t rec = f2u(F[14]), meta = f2u(F[15]);
-  const int nl = (int)(meta & 0x7fffffffu);
+  const uint32_t rec = f2u(F[14]);
+  value = record_value_host(s, rec, record_path(f2u(F[15]), F[12], F[13], r), r);
+  return true;
+}
+}  // namespace
+
+// getValue of record rec at radius r along its path (irt_common.h record_path), as the
+// kernel's record_value reads it from the blocks
+float record_value_host(const HostScene &s, uint32_t rec, uint32_t path, float r) {
+  const int nl = (int)(path & 31u);
   const float *B = &s.blocks[(size_t)rec * kBlk4 * 4];
-  if (meta >> 31) {
-    const int b = rec_coarse_block(F[16], F[17], F[18], F[19], nl, r);
+  float value;
+  if (path & kPathBlock) {
+    int b = (int)((path >> 5) & 3u);
+    if (path & kPathExactKeys)
+      b = rec_coarse_block(B[blk_height_pos(7)], B[blk_height_pos(15)], B[blk_height_pos(23)], INFINITY,
+                           nl, r);
     const float *Q = B + 16 * b;
     const int m = rec_block_index(Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], Q[6], b, nl, r);
     value = select8(m, Q[8], Q[9], Q[10], Q[11], Q[12], Q[13], Q[14], Q[15]);
@@ -314,8 +320,10 @@ bool test_fat(const HostScene &s, const float *F, float px, float py, float pz, 
     }
     value = B[blk_value_pos(first)];
   }
-  return true;
+  return value;
 }
+
+namespace {
 // getValue (ICONGrid.h:147-164) of a zero-thickness record: literal findHeight
 float sphere_value(const HostScene &s, uint32_t rec, float r) {
   const float *hv = &s.hv[(size_t)rec * kHV];

@@ -16,7 +16,8 @@ from dataclasses import dataclass
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libicon_rt_hip.so")
+# IRT_LIB_PATH: another build of the same library (profiles/ A/B runs only)
+LIB_PATH = os.environ.get("IRT_LIB_PATH") or os.path.join(PKG_DIR, "libicon_rt_hip.so")
 
 # icon_rt::ICONCell (icon_rt/ICONGrid.h:59-76), 284 bytes, the `.ic` record
 CELL_DTYPE = np.dtype(

@@ -250,7 +250,10 @@ int irt_build_wedge_accel(irt_context *ctx, const irt_icon_cell *cells, size_t n
  * every cell's bottom triangle toCartesian(height[0], lat, lon) is listed too. */
 
 /* Download the GRID_ACCEL_MODE grid (256^3 macrocells over the volume bounds,
- * hostCode.cu:668-682; index x + 256*(y + 256*z)), same conventions as irt_get_shell. */
+ * hostCode.cu:668-682; index x + 256*(y + 256*z)), same conventions as irt_get_shell.
+ * The grid (201 MB) is built on first use -- this call or the first IRT_ACCEL_GRID render --
+ * not at irt_create as the reference's main() does (hostCode.cu:875): same grid, no cost to
+ * sphere-mode runs. */
 int irt_get_grid(const irt_context *ctx, float *valueRanges, float *maxOpacities);
 
 /* Download the shell accelerator (for checking): valueRanges as 2 floats per

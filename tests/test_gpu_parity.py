@@ -515,6 +515,58 @@ def test_measured_cost_scheduling_on_a_rank_tile_subset(monkeypatch):
     ctx.close()
 
 
+@pytest.mark.parametrize("mode", ["device", "off"])
+def test_counter_probe_modes_survive_growing_launches(monkeypatch, mode):
+    """the IRT_COUNTERS=device probe buffer grows with the launch (a frame with
+    more workgroups than the first), and IRT_COUNTERS=off keeps the counter block the
+    statistics variant adds into.  Frames stay bit-identical to the default context's."""
+    from helpers import GpuFrame
+    cells = irt.synth_grid(2, 2, 47)
+    ref = {}
+    for W in (64, 200):
+        setup = irt.setup_frame(cells, W, W, camera=FRAMING)
+        ctx = irt.Context(cells, 0)
+        ctx.set_transfunc(setup.lut, setup.value_range)
+        fr = GpuFrame(ctx, W, W)
+        fr.render(setup.lp)
+        ref[W] = fr.host()
+        ctx.close()
+    monkeypatch.setenv("IRT_COUNTERS", mode)
+    ctx = irt.Context(cells, 0)
+    L = irt.lib()
+    L.irt_debug_set_variant.argtypes = [C.c_void_p, C.c_int]
+    for variant in ((0, 36864) if mode == "off" else (0,)):  # 36864: the statistics variant
+        if variant:
+            assert L.irt_debug_set_variant(ctx._h, variant) == 0
+        for W in (64, 200):  # 16 then 64 workgroups
+            setup = irt.setup_frame(cells, W, W, camera=FRAMING)
+            ctx.set_transfunc(setup.lut, setup.value_range)
+            fr = GpuFrame(ctx, W, W)
+            fr.render(setup.lp)
+            a, f = fr.host()
+            assert_same_frame(a, f, *ref[W], f"IRT_COUNTERS={mode} variant {variant} W={W}")
+    ctx.close()
+
+
+def test_grid_is_built_on_first_use():
+    """GRID_ACCEL_MODE's 256^3 grid is built lazily (ensure_grid): a sphere-mode context holds
+    no grid; the first grid render or irt_get_grid builds it from the scene's blocks, and a
+    transfer function set before or after gives the same majorants as the oracle's."""
+    cells = irt.synth_grid(2, 2, 31)
+    setup = irt.setup_frame(cells, 8, 8)
+    S = oracle_frame(cells, 8, 8)[3]
+    S.build_grid()
+    ctx = irt.Context(cells, 0)
+    before = ctx.info.deviceBytes
+    ctx.set_transfunc(setup.lut, setup.value_range)  # before the grid exists
+    vr, mo = ctx.grid()
+    assert np.array_equal(vr, S.grid_vr) and np.array_equal(bits(mo), bits(S.grid_max_op))
+    info = irt.VolumeInfo()
+    assert irt.lib().irt_get_volume_info(ctx._h, C.byref(info)) == 0
+    assert info.deviceBytes - before >= 256 ** 3 * 12  # the grid arrived with its first use
+    ctx.close()
+
+
 def test_null_stream_is_ordered_with_torch_default_stream():
     """irt_render with stream NULL runs on HIP's null stream, ordered with torch's default
     stream: a zero_() of the buffers enqueued just before must land before the kernel reads
