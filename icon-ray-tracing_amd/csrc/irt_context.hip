@@ -124,6 +124,7 @@ struct irt_context {
   // ramp, 2^coopMaxLg without (IRT_COOP_MAXLG, IRT_COOP_RAMP; profiles/r02e_dist/)
   int coopMaxLg = 0;
   int coopRamp = 1;
+  int probeExit = 0;           // IRT_PROBE_EXIT (measurement only, RenderArgs::probeExit)
   int schedPolicy = 2;         // IRT_SCHED: 1 tiles, 2 bands of tiles (a tile row; default), 3 reversed
   bool schedOrderValid = false;
   bool schedLastApplied = false;   // the last launch ran in a measured-cost order
@@ -477,6 +478,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.lutSize = c->lutSize;
   A.coopMaxLg = c->coopMaxLg;
   A.coopRamp = c->coopRamp;
+  A.probeExit = c->probeExit;
   A.numCells = c->n;
   A.G = c->G;
   A.srgbTh = c->d_srgb;
@@ -861,6 +863,7 @@ int irt_create_end(irt_context *c) {
   if (const char *e = getenv("IRT_TIMING_EVERY")) c->timingEvery = std::max(1, atoi(e));
   if (const char *e = getenv("IRT_COOP_MAXLG")) c->coopMaxLg = std::min(6, std::max(0, atoi(e)));
   if (const char *e = getenv("IRT_COOP_RAMP")) c->coopRamp = std::min(6, std::max(0, atoi(e)));
+  if (const char *e = getenv("IRT_PROBE_EXIT")) c->probeExit = atoi(e);
   IRT_HIP(hipHostGetDevicePointer((void **)&c->dh_counters, c->h_counters, 0));
   IRT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long), c->stream));
 

@@ -76,6 +76,9 @@ struct RenderArgs {
   // setting gives the same frame)
   int coopMaxLg;
   int coopRamp;
+  // measurement only (IRT_PROBE_EXIT, profiles/): 1 = every workgroup returns at once,
+  // 2 = after the prologue, 3 = after ray generation and boxTest (no pixel written)
+  int probeExit;
 };
 
 // Event counts kept per workgroup: [0] launched [1] inBox [2] locate [3] found [4] candidates

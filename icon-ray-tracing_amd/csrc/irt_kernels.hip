@@ -40,8 +40,8 @@ __device__ __forceinline__ void atomic_max_f(float *addr, float val) {
 // a cell hits the same rectangle: rasterising min/max over the layers once is the same
 // min/max.
 //
-// One lane per record (round 2 ran a workgroup per record, whose redundant scalar binary
-// searches took 493 ms at C5).  getValue(h[i]) = value[findHeight(h[i])]: for heights
+// One lane per record, the records staged through LDS (round 2 ran a workgroup per record,
+// whose redundant scalar binary searches took 493 ms at C5).  getValue(h[i]) = value[findHeight(h[i])]: for heights
 // non-decreasing in float_key order (record_meta's coarse records) findHeight(h[i]) is
 // #{j >= 1 : h[j] < h[i]}, which a running index gives (0 for i = 0; i-1, or the previous
 // answer on a repeated height); other records run the literal binary search.  Rectangles
@@ -66,9 +66,21 @@ __global__ void __launch_bounds__(256) k_shell_build(const irt_icon_cell *cells,
                                                      float3 sbLo, float3 sbHi, float *valueRanges,
                                                      ShellRect *wide, unsigned long long *numWide,
                                                      size_t wideCap) {
-  for (size_t ci = blockIdx.x * (size_t)blockDim.x + threadIdx.x; ci < n;
-       ci += (size_t)gridDim.x * blockDim.x) {
-    const irt_icon_cell &c = cells[ci];
+  // 256 records (72,704 B, 16-B aligned) staged through LDS with coalesced 16-B loads: a
+  // lane reading its own 284-B record straight from HBM would touch a different line with
+  // every load instruction of the wave
+  constexpr int kRecs = 256, kVec = kRecs * (int)sizeof(irt_icon_cell) / 16;
+  static_assert(kRecs * sizeof(irt_icon_cell) % 16 == 0, "record batches are float4 aligned");
+  __shared__ float4 s_rec[kVec];
+  for (size_t b0 = (size_t)blockIdx.x * kRecs; b0 < n; b0 += (size_t)gridDim.x * kRecs) {
+    const size_t nb = n - b0 < (size_t)kRecs ? n - b0 : (size_t)kRecs;
+    const int nv = (int)((nb * sizeof(irt_icon_cell) + 15) / 16);
+    const float4 *src = reinterpret_cast<const float4 *>(cells + b0);
+    __syncthreads();  // the previous batch is done with s_rec
+    for (int v = threadIdx.x; v < nv; v += blockDim.x) s_rec[v] = src[v];
+    __syncthreads();
+    if (threadIdx.x >= nb) continue;
+    const irt_icon_cell &c = reinterpret_cast<const irt_icon_cell *>(s_rec)[threadIdx.x];
     const int nl = c.numLayers;
     if (nl <= 0) continue;
     // min/max over the layers with the CAS loops' "store only if strictly smaller/larger"
@@ -347,7 +359,7 @@ void launch_shell_init(float *vr, size_t numMCs, hipStream_t s) {
 void launch_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, float3 lo, float3 hi,
                         float *vr, hipStream_t s) {
   if (n == 0) return;
-  const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1u << 16);
+  const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 4096);
   // the wide-rectangle list: sized for the seam and polar columns, capped (overflow stays
   // in-lane)
   const size_t cap = std::min<size_t>(n / 8 + 4096, size_t(1) << 22);

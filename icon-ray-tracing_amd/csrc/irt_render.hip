@@ -1182,7 +1182,12 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     gen_ray(A, accumID, px.x, px.y, st, dx, dy, dz);
     const Ray ray = {A.org.x, A.org.y, A.org.z, 0.f, dx, dy, dz, 1e10f};
     float t0, t1;
-    if (box_test(ray, A, t0, t1)) {
+    const bool boxHit = box_test(ray, A, t0, t1);
+    if (A.probeExit == 3) {  // measurement only: ray generation and boxTest, nothing written
+      if (boxHit && t0 == -1.2345f) A.fb[0] = 0u;  // keeps the work live
+      return;
+    }
+    if (boxHit) {
       inBox = true;
       T.count(1);
       phase = kRange;
@@ -1480,6 +1485,7 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   __shared__ float4 s_acc[256];     // kCoop: the accum pixels, prefetched
   __shared__ uint32_t s_jmul[kLcgJumps], s_jadd[kLcgJumps];
   const int tid = threadIdx.x;
+  if (A.probeExit == 1) return;  // measurement only
   uint64_t tStart = 0;
   if constexpr ((OPT & OPT_TIMING) != 0) tStart = __builtin_amdgcn_s_memtime();
   // the prologue's global loads issued together, one wait (not one round trip each)
@@ -1513,6 +1519,7 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
     for (int k = 0; k < kGridBitWords / 256; ++k) s_gbits[tid + 256 * k] = A.gridBits[tid + 256 * k];
   }
   __syncthreads();
+  if (A.probeExit == 2) return;  // measurement only
   Tracer<OPT> T{{}, A, s_logf, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
   T.s_gbits = s_gbits;
   if constexpr ((OPT & OPT_TIMING) != 0) {
