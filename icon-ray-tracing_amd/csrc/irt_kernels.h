@@ -77,7 +77,8 @@ struct RenderArgs {
   int coopMaxLg;
   int coopRamp;
   // measurement only (IRT_PROBE_EXIT, profiles/): 1 = every workgroup returns at once,
-  // 2 = after the prologue, 3 = after ray generation and boxTest (no pixel written)
+  // 2 = after the prologue, 3 = after ray generation and boxTest (no pixel written), 4 = at
+  // the first woodcockFunc, 5 = after it
   int probeExit;
 };
 

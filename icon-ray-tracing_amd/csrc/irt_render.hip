@@ -1431,6 +1431,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     // the wave, together: woodcockFunc(leafID, t, tt1) of every waiting lane
     const bool req = phase == kWait;
     if (__ballot(req) == 0ull) break;
+    if (A.probeExit == 4) break;  // measurement only: ray setup up to the first woodcockFunc
     float tw = t;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     if constexpr ((OPT & OPT_TIMING) != 0) {
@@ -1440,6 +1441,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       }
     }
     T.woodcock_wave(req, dx, dy, dz, tw, tt1, st, maj, !zeroLen, s, miss, W, SW, jmul, jadd);
+    if (A.probeExit == 5) break;  // measurement only: the first woodcockFunc of every lane
     if (grid && req && phase == kWait && !ae) {
       if (tw > t && tw < tt1) {  // render_grid's hit test (deviceCode.cu:316)
         s_entry[tid] = make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
