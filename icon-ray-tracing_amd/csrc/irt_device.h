@@ -61,8 +61,11 @@ __device__ __forceinline__ int project_axis(float s, float lo, float hi, int dim
   return f2i_x86((s - lo) / (hi - lo) * (float)(dim - 1));
 }
 
-// normalizeGridCoord (ShellAccel.h:71-80): the while-loops compute c mod d in [0,d).
+// normalizeGridCoord (ShellAccel.h:71-80): the while-loops compute c mod d in [0,d).  A
+// coordinate already inside the grid (almost every leaf) skips the integer division, ~25
+// VALU instructions per axis on gfx950 (no hardware integer divide).
 __device__ __forceinline__ int wrap_coord(int c, int d) {
+  if ((unsigned)c < (unsigned)d) return c;
   const int m = c % d;
   return m < 0 ? m + d : m;
 }
