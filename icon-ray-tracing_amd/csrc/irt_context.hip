@@ -473,6 +473,14 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.wTrig = c->d_wTrig;
   A.tfLo = c->tfLo;
   A.tfHi = c->tfHi;
+  {
+    const float tfSize = c->tfHi - c->tfLo;  // float, as the reference subtracts
+    A.invTf = 1.0 / (double)tfSize;
+    const float sz[3] = {I.sphericalBounds.upper.x - I.sphericalBounds.lower.x,
+                         I.sphericalBounds.upper.y - I.sphericalBounds.lower.y,
+                         I.sphericalBounds.upper.z - I.sphericalBounds.lower.z};
+    for (int k = 0; k < 3; ++k) A.invSb[k] = 1.0 / (double)sz[k];
+  }
   A.opacityScale = c->opScale;
   A.lut = c->d_lut;
   A.lutSize = c->lutSize;

@@ -61,6 +61,20 @@ __device__ __forceinline__ int project_axis(float s, float lo, float hi, int dim
   return f2i_x86((s - lo) / (hi - lo) * (float)(dim - 1));
 }
 
+// a / b, correctly rounded, for a divisor b fixed per launch, given invB = 1 / (double)b:
+// one double product rounded to float.  The product is within 2^-52 (relative) of a/b,
+// while a quotient of two floats that is not itself a float midpoint lies at least ~2^-49
+// (relative) from every midpoint between floats -- and is never exactly one -- so both round
+// to the same float.  b = 0, inf, NaN give 0/0 = NaN, a/0 = +-inf, a/inf = +-0 either way.
+// Replaces the ~10-instruction correctly rounded f32 division sequence.
+__device__ __forceinline__ float div_uniform(float a, double invB) {
+  return (float)((double)a * invB);
+}
+// project_axis with the per-launch 1 / (double)(hi - lo)
+__device__ __forceinline__ int project_axis_inv(float s, float lo, double invSize, int dim) {
+  return f2i_x86(div_uniform(s - lo, invSize) * (float)(dim - 1));
+}
+
 // normalizeGridCoord (ShellAccel.h:71-80): the while-loops compute c mod d in [0,d).  A
 // coordinate already inside the grid (almost every leaf) skips the integer division, ~25
 // VALU instructions per axis on gfx950 (no hardware integer divide).

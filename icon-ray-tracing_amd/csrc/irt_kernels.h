@@ -33,6 +33,10 @@ struct RenderArgs {
   const float4 *wTrig;   // per record: 3 corners {cosf lat, sinf lat, cosf lon, sinf lon}
   // transfer function (Params.h:77-82)
   float tfLo, tfHi, opacityScale;
+  // 1 / (double)(tfHi - tfLo) and 1 / (double)(sbHi - sbLo) per axis (the float differences):
+  // quotients by these per-launch divisors as one double product (div_uniform, irt_device.h)
+  double invTf;
+  double invSb[3];
   const float4 *lut;
   int lutSize;
   // locator

@@ -601,7 +601,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // postClassify's alpha only (the acceptance test needs nothing else); the colour comes
   // from post_classify on acceptance
   __device__ __forceinline__ float classify_alpha(float v) {
-    v = (v - A.tfLo) / (A.tfHi - A.tfLo);
+    v = div_uniform(v - A.tfLo, A.invTf);  // (v - tfLo) / (tfHi - tfLo), correctly rounded
     const int size = A.lutSize;
     const int idx = f2i_x86(v * (float)size);
     const float frac = (v * (float)size) - (float)idx;
@@ -614,7 +614,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
 
   // postClassify (deviceCode.cu:127-135): weights reversed, opacityScale on 2nd term only
   __device__ __forceinline__ float4 post_classify(float v) {
-    v = (v - A.tfLo) / (A.tfHi - A.tfLo);
+    v = div_uniform(v - A.tfLo, A.invTf);  // (v - tfLo) / (tfHi - tfLo), correctly rounded
     const int size = A.lutSize;
     const int idx = f2i_x86(v * (float)size);
     const float frac = (v * (float)size) - (float)idx;
@@ -1280,9 +1280,9 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       const float r1 = en.x, la1 = en.y, lo1 = en.z;
       const int sx = r1 < r2 ? 1 : -1, sy = la1 < la2 ? 1 : -1, sz = lo1 < lo2 ? 1 : -1;
       dd.x = (sx > 0 ? 1 : 0) | (sy > 0 ? 2 : 0) | (sz > 0 ? 4 : 0);
-      dd.y = (int)((uint32_t)project_axis(r2, A.sbLo.x, A.sbHi.x, A.dims.x) + (uint32_t)sx);
-      dd.z = (int)((uint32_t)project_axis(la2, A.sbLo.y, A.sbHi.y, A.dims.y) + (uint32_t)sy);
-      dd.w = (int)((uint32_t)project_axis(lo2, A.sbLo.z, A.sbHi.z, A.dims.z) + (uint32_t)sz);
+      dd.y = (int)((uint32_t)project_axis_inv(r2, A.sbLo.x, A.invSb[0], A.dims.x) + (uint32_t)sx);
+      dd.z = (int)((uint32_t)project_axis_inv(la2, A.sbLo.y, A.invSb[1], A.dims.y) + (uint32_t)sy);
+      dd.w = (int)((uint32_t)project_axis_inv(lo2, A.sbLo.z, A.invSb[2], A.dims.z) + (uint32_t)sz);
       s_entry[tid] = __builtin_bit_cast(float4, dd);  // the entry point is not needed again
     } else {
       dd = __builtin_bit_cast(int4, s_entry[tid]);
@@ -1380,9 +1380,9 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
           const float e1 = lower + sceneEPS;
           float r1, la1, lo1;
           to_spherical(A.org.x + dx * e1, A.org.y + dy * e1, A.org.z + dz * e1, r1, la1, lo1);
-          cx = project_axis(r1, A.sbLo.x, A.sbHi.x, A.dims.x);
-          cy = project_axis(la1, A.sbLo.y, A.sbHi.y, A.dims.y);
-          cz = project_axis(lo1, A.sbLo.z, A.sbHi.z, A.dims.z);
+          cx = project_axis_inv(r1, A.sbLo.x, A.invSb[0], A.dims.x);
+          cy = project_axis_inv(la1, A.sbLo.y, A.invSb[1], A.dims.y);
+          cz = project_axis_inv(lo1, A.sbLo.z, A.invSb[2], A.dims.z);
           if (!lastRange) s_entry[tid] = make_float4(r1, la1, lo1, 0.f);
         }
         t = lower;

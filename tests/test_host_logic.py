@@ -417,3 +417,28 @@ def test_lcg_jump_equals_sequential_steps():
             for _ in range(n):
                 s = (1664525 * s + 1013904223) & 0xFFFFFFFF
             assert (m.value * s0 + a.value) & 0xFFFFFFFF == s, (n, s0)
+
+
+def test_division_by_a_launch_constant_as_one_double_product():
+    """irt_device.h div_uniform: a / b correctly rounded to float equals the float rounding of
+    (double)a * (1 / (double)b) -- the kernel's form for the per-launch divisors (transfer
+    function and shell-grid scale).  Random operands over many binades, the kernel's
+    operand ranges, and special values."""
+    rng = np.random.default_rng(7)
+    n = 4_000_000
+    a = (rng.uniform(-1, 1, n) * 2.0 ** rng.integers(-60, 60, n)).astype(np.float32)
+    b = (rng.uniform(0.5, 1, n) * 2.0 ** rng.integers(-60, 60, n)).astype(np.float32)
+    b[::3] = -b[::3]
+    # the kernel's cases: (value - tfLo) / (tfHi - tfLo) and (lat - lo) / (hi - lo)
+    a2 = (rng.uniform(-0.1, 1.1, n).astype(np.float32) - np.float32(0.0123))
+    b2 = np.full(n, np.float32(np.float32(0.987) - np.float32(0.0123)), np.float32)
+    a3 = (rng.uniform(-1.6, 1.6, n).astype(np.float32) - np.float32(-1.5707964))
+    b3 = np.full(n, np.float32(np.float32(1.5707964) - np.float32(-1.5707964)), np.float32)
+    sp = np.float32([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, 3.0, 1e-30, 7e30])
+    a4, b4 = np.meshgrid(sp, sp)
+    with np.errstate(all="ignore"):
+        for x, y in ((a, b), (a2, b2), (a3, b3), (a4.ravel(), b4.ravel())):
+            ref = x / y  # float32 IEEE division
+            got = (x.astype(np.float64) * (1.0 / y.astype(np.float64))).astype(np.float32)
+            same = (ref.view(np.uint32) == got.view(np.uint32)) | (np.isnan(ref) & np.isnan(got))
+            assert same.all(), (x[~same][:4], y[~same][:4])
