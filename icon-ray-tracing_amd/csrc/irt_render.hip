@@ -100,13 +100,39 @@ struct ScanWave {
 
 // t0 - d[0] - d[1] - ... - d[k], subtracted one at a time as woodcockTracking's `t -=`
 // (deviceCode.cu:165) does: the same roundings as k+1 iterations of the serial loop.
+typedef float fvec2 __attribute__((ext_vector_type(2)));
+typedef float fvec4 __attribute__((ext_vector_type(4)));
+// 16-byte LDS slots read and written as one ds_read_b128 / ds_write_b128: HIP's float4 and
+// uint4 copy member-wise in IR, and with the IR load/store vectorizer off for this file
+// (Makefile RENDER_FLAGS) they would split into b32 pairs.
+template <class T>
+__device__ __forceinline__ T lds_ld16(const T *p) {
+  static_assert(sizeof(T) == 16, "16-byte slot");
+  return __builtin_bit_cast(T, *reinterpret_cast<const fvec4 *>(p));
+}
+template <class T>
+__device__ __forceinline__ void lds_st16(T *p, T v) {
+  static_assert(sizeof(T) == 16, "16-byte slot");
+  *reinterpret_cast<fvec4 *>(p) = __builtin_bit_cast(fvec4, v);
+}
+// The group's steps are read as explicit 4- / 2-float LDS vectors (the group base is a
+// multiple of G floats), independent of the IR load/store vectorizer (off for this file).
 template <int G>
 __device__ __forceinline__ float coop_prefix(float t0, const float *d, int k) {
   float t = t0;
+  if constexpr (G == 2) {
+    const fvec2 v = *static_cast<const fvec2 *>(__builtin_assume_aligned(d, 8));
+    t = t - v.x;
+    t = k >= 1 ? t - v.y : t;
+  } else {
 #pragma unroll
-  for (int j = 0; j < G; ++j) {
-    const float dj = d[j];
-    t = j <= k ? t - dj : t;
+    for (int c = 0; c < G / 4; ++c) {
+      const fvec4 v = static_cast<const fvec4 *>(__builtin_assume_aligned(d, 16))[c];
+      t = 4 * c <= k ? t - v.x : t;
+      t = 4 * c + 1 <= k ? t - v.y : t;
+      t = 4 * c + 2 <= k ? t - v.z : t;
+      t = 4 * c + 3 <= k ? t - v.w : t;
+    }
   }
   return t;
 }
@@ -480,8 +506,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       const uint32_t n = end - beg;
       const uint32_t m8 = (M >> (8 * b)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
       c = (uint32_t)__popc(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
-      W.pt[lane] = make_float4(px, py, pz, r);
-      W.lst[lane] = make_uint4(H0.w + beg, m8, 0u, 0xFFFFFFFFu);
+      lds_st16(&W.pt[lane], make_float4(px, py, pz, r));
+      lds_st16(&W.lst[lane], make_uint4(H0.w + beg, m8, 0u, 0xFFFFFFFFu));
       fe = H0.w + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
       fr = r;
     }
@@ -523,8 +549,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         bool tp = false, tl = false;
         Found g;
         if (task) {
-          const float4 po = W.pt[o];
-          const uint4 d = W.lst[o];
+          const float4 po = lds_ld16(&W.pt[o]);
+          const uint4 d = lds_ld16(&W.lst[o]);
           tp = pass_entry(A.fat + (size_t)(d.x + list_entry(d.y, d.z + (t - s0))) * kFatStride4, po.x, po.y,
                           po.z, po.w, g);
           tl = g.rec >= d.w;  // past the limit: the serial scan stops there
@@ -558,7 +584,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       if (pass == 1 || __ballot(edge) == 0ull) break;
       c = 0u;
       if (edge) {
-        const float4 p = W.pt[lane];
+        const float4 p = lds_ld16(&W.pt[lane]);
         uint32_t sub;
         const uint32_t cell = cubemap_cell_fast(p.x, p.y, p.z, A.G, sub);
         const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
@@ -572,7 +598,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         const uint32_t m8 = (M >> (8 * b)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
         c = (uint32_t)__popc(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
         flim = hit ? frm[lane].x : 0xFFFFFFFFu;
-        W.lst[lane] = make_uint4(H0.w + beg, m8, 0u, flim);
+        lds_st16(&W.lst[lane], make_uint4(H0.w + beg, m8, 0u, flim));
         fe = H0.w + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
       }
     }
@@ -714,8 +740,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         ry = make_float4(dx, dy, dz, __uint_as_float(st));
       } else {
         if (active) {
-          W.req[rank] = make_float4(t, tmax, q, majorant);
-          W.ray[rank] = make_float4(dx, dy, dz, __uint_as_float(st));
+          lds_st16(&W.req[rank], make_float4(t, tmax, q, majorant));
+          lds_st16(&W.ray[rank], make_float4(dx, dy, dz, __uint_as_float(st)));
           W.cnt[rank] = (counted ? 1u : 0u) | (miss ? 2u : 0u);
         }
         __builtin_amdgcn_wave_barrier();
@@ -723,8 +749,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         k = lane & (G - 1);
         used = grp < R;
         const int g = used ? grp : 0;
-        rq = W.req[g];
-        ry = W.ray[g];
+        rq = lds_ld16(&W.req[g]);
+        ry = lds_ld16(&W.ray[g]);
         const uint32_t cf = W.cnt[g];
         cntd = cf & 1u;
         mm = kMiss && (cf & 2u);
@@ -1061,7 +1087,7 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
       cx = project_axis(r1, A.sbLo.x, A.sbHi.x, A.dims.x);
       cy = project_axis(la1, A.sbLo.y, A.sbHi.y, A.dims.y);
       cz = project_axis(lo1, A.sbLo.z, A.sbHi.z, A.dims.z);
-      if (!lastRange) s_entry[tid] = make_float4(r1, la1, lo1, 0.f);  // for step (125-127)
+      if (!lastRange) lds_st16(&s_entry[tid], make_float4(r1, la1, lo1, 0.f));  // for step (125-127)
     }
     // The lat/lon "planes" (ShellAccel.h:147-160, 183-200) are built from
     // toCartesian(vec3f(0.f, ...)) -- radius 0 -- so N = 0, w = 0 and every evalPlane(...)
@@ -1124,7 +1150,7 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
         const float e2 = upper - sceneEPS;
         float r2, la2, lo2;
         to_spherical(ray.ox + ray.dx * e2, ray.oy + ray.dy * e2, ray.oz + ray.dz * e2, r2, la2, lo2);
-        const float4 en = s_entry[tid];
+        const float4 en = lds_ld16(&s_entry[tid]);
         const float r1 = en.x, la1 = en.y, lo1 = en.z;
         const int sx = r1 < r2 ? 1 : -1, sy = la1 < la2 ? 1 : -1, sz = lo1 < lo2 ? 1 : -1;
         dd.x = (sx > 0 ? 1 : 0) | (sy > 0 ? 2 : 0) | (sz > 0 ? 4 : 0);
@@ -1276,16 +1302,16 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       const float e2 = upper - sceneEPS;
       float r2, la2, lo2;
       to_spherical(A.org.x + dx * e2, A.org.y + dy * e2, A.org.z + dz * e2, r2, la2, lo2);
-      const float4 en = s_entry[tid];
+      const float4 en = lds_ld16(&s_entry[tid]);
       const float r1 = en.x, la1 = en.y, lo1 = en.z;
       const int sx = r1 < r2 ? 1 : -1, sy = la1 < la2 ? 1 : -1, sz = lo1 < lo2 ? 1 : -1;
       dd.x = (sx > 0 ? 1 : 0) | (sy > 0 ? 2 : 0) | (sz > 0 ? 4 : 0);
       dd.y = (int)((uint32_t)project_axis_inv(r2, A.sbLo.x, A.invSb[0], A.dims.x) + (uint32_t)sx);
       dd.z = (int)((uint32_t)project_axis_inv(la2, A.sbLo.y, A.invSb[1], A.dims.y) + (uint32_t)sy);
       dd.w = (int)((uint32_t)project_axis_inv(lo2, A.sbLo.z, A.invSb[2], A.dims.z) + (uint32_t)sz);
-      s_entry[tid] = __builtin_bit_cast(float4, dd);  // the entry point is not needed again
+      lds_st16(&s_entry[tid], __builtin_bit_cast(float4, dd));  // the entry point is not needed again
     } else {
-      dd = __builtin_bit_cast(int4, s_entry[tid]);
+      dd = __builtin_bit_cast(int4, lds_ld16(&s_entry[tid]));
     }
     const float t_closest = fminf(fminf(tnx, tny), tnz);
     bool stop = false;
@@ -1383,7 +1409,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
           cx = project_axis_inv(r1, A.sbLo.x, A.invSb[0], A.dims.x);
           cy = project_axis_inv(la1, A.sbLo.y, A.invSb[1], A.dims.y);
           cz = project_axis_inv(lo1, A.sbLo.z, A.invSb[2], A.dims.z);
-          if (!lastRange) s_entry[tid] = make_float4(r1, la1, lo1, 0.f);
+          if (!lastRange) lds_st16(&s_entry[tid], make_float4(r1, la1, lo1, 0.f));
         }
         t = lower;
         iter = 0;
@@ -1444,8 +1470,8 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     if (A.probeExit == 5) break;  // measurement only: the first woodcockFunc of every lane
     if (grid && req && phase == kWait && !ae) {
       if (tw > t && tw < tt1) {  // render_grid's hit test (deviceCode.cu:316)
-        s_entry[tid] = make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
-                                   s.z * A.amb.z * A.ambRad, s.w > 0.f ? 1.f : 0.f);
+        lds_st16(&s_entry[tid], make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
+                                   s.z * A.amb.z * A.ambRad, s.w > 0.f ? 1.f : 0.f));
         hit = true;
         phase = kDone;
       } else {
@@ -1454,8 +1480,8 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     } else if (req) {
       if (!zeroLen && (ae || (tw > t && tw < tt1))) {
         // the colour waits in the lane's s_entry slot (free once it is finished)
-        s_entry[tid] = make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
-                                   s.z * A.amb.z * A.ambRad, s.w > 0.f ? 1.f : 0.f);
+        lds_st16(&s_entry[tid], make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
+                                   s.z * A.amb.z * A.ambRad, s.w > 0.f ? 1.f : 0.f));
         hit = true;
         phase = kDone;
       } else {
@@ -1464,12 +1490,12 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     }
   }
   if (!inBox) return;
-  const float4 c = hit ? s_entry[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 c = hit ? lds_ld16(&s_entry[tid]) : make_float4(0.f, 0.f, 0.f, 0.f);
   if (sampleOut) {
     *sampleOut = c;
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
-    write_pixel(A, px.outIdx, c.x, c.y, c.z, c.w, s_th, s_acc[tid]);
+    write_pixel(A, px.outIdx, c.x, c.y, c.z, c.w, s_th, lds_ld16(&s_acc[tid]));
   }
 }
 
