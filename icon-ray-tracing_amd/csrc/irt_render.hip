@@ -1723,11 +1723,12 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 // register allocator).  OPT_MONO (4096) is kept in the numbering of round 1 (the one-kernel
 // raygen; the setup -> march -> continuation pipeline it distinguished from was removed).
 // 70656 = 5120 | OPT_SERIAL: the one-lane-per-ray Woodcock loop, for A/B against the
-// cooperative default.  All variants give identical results.
+// cooperative default.  5376: the default with a 5-waves-per-SIMD floor (96 VGPRs, 19
+// spilled; C3s 4 % faster, C3 2 % slower: profiles/r03q_args_waves/), for A/B.  All variants give identical results.
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
-#define IRT_VARIANTS(X) X(4096) X(5120) X(36864) X(70656) X(136192) X(529408)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408)
 
 bool render_variant_available(int v) {
 #define IRT_CASE(N) if (v == N) return true;

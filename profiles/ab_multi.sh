@@ -1,16 +1,23 @@
 #!/bin/bash
-# profiles/ab_multi.sh OUT "CONFIGS" LIB... : bench.py with each library (IRT_LIB_PATH)
-# interleaved round-robin, three rounds, on one box; OUT/<lib-basename>_<cfg>.jsonl.
+# profiles/ab_multi.sh OUT "CONFIGS" LIB[@VAR=VAL[@VAR=VAL]]... : bench.py with each library
+# (IRT_LIB_PATH) and its environment overrides, round-robin, three rounds, on one box;
+# OUT/<lib-basename>[_<VAL>...]_<cfg>.jsonl.
 set -o pipefail
 OUT=${1:?out}; CONFIGS=${2:?configs}; shift 2
 mkdir -p "$OUT"
 for cfg in $CONFIGS; do
   steps=200; [ "$cfg" = c5 ] && steps=60; [ "$cfg" = c3s ] && steps=40; [ "$cfg" = c4 ] && steps=80
   for round in 1 2 3; do
-    for lib in "$@"; do
+    for spec in "$@"; do
+      IFS=@ read -r lib envs <<< "$spec"
       n=$(basename "$lib" .so)
-      IRT_LIB_PATH="$lib" timeout -k 10 240 python3 bench.py --config $cfg --steps $steps --warmup 5 \
-        --no-cpu-baseline >> "$OUT/${n}_$cfg.jsonl" 2>> "$OUT/${n}_$cfg.err" || exit 1
+      vars=()
+      if [ -n "$envs" ]; then
+        IFS=@ read -r -a kv <<< "$envs"
+        for a in "${kv[@]}"; do vars+=("$a"); n="${n}_${a#*=}"; done
+      fi
+      env IRT_LIB_PATH="$lib" "${vars[@]}" timeout -k 10 240 python3 bench.py --config $cfg --steps $steps \
+        --warmup 5 --no-cpu-baseline >> "$OUT/${n}_$cfg.jsonl" 2>> "$OUT/${n}_$cfg.err" || exit 1
     done
   done
 done
