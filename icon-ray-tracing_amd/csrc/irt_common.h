@@ -80,6 +80,30 @@ IRT_HD void lcg_jump(uint32_t n, uint32_t &mul, uint32_t &add) {
   mul = m;
   add = c;
 }
+// lcg_jump for n < kLcgJumps, tabulated at compile time as {mul, add} pairs: the kernels
+// copy it into LDS with one load per lane instead of running lcg_jump's eight rounds of
+// 32-bit multiplies (quarter-rate on the SIMD) in every workgroup's prologue.
+struct LcgJumpTab {
+  uint32_t ma[kLcgJumps][2];
+};
+constexpr LcgJumpTab make_lcg_jump_tab() {
+  LcgJumpTab t{};
+  for (int n = 0; n < kLcgJumps; ++n) {
+    uint32_t m = 1u, c = 0u, bm = 1664525u, bc = 1013904223u;
+    for (int bit = 0; bit < 8; ++bit) {
+      if ((n >> bit) & 1) {
+        c = bm * c + bc;
+        m = bm * m;
+      }
+      bc = bm * bc + bc;
+      bm = bm * bm;
+    }
+    t.ma[n][0] = m;
+    t.ma[n][1] = c;
+  }
+  return t;
+}
+constexpr LcgJumpTab kLcgJumpTab = make_lcg_jump_tab();
 
 // ---------------------------------------------------------------------------------
 // glibc 2.35 flt-32 asinf / atanf / atan2f (fdlibm lineage: Sun Microsystems 1993,
@@ -145,30 +169,20 @@ IRT_HD float glibc_atanf(float x) {
     if (ix > 0x7f800000) return x + x;
     return hx > 0 ? atanhi3 + atanlo3 : -atanhi3 - atanlo3;
   }
-  if (ix < 0x3ee00000) {
-    if (ix < 0x31000000) {
-      if (huge + x > one) return x;
-    }
-    id = -1;
-  } else {
-    x = __builtin_fabsf(x);
-    if (ix < 0x3f980000) {
-      if (ix < 0x3f300000) {
-        id = 0;
-        x = (2.0f * x - one) / (2.0f + x);
-      } else {
-        id = 1;
-        x = (x - one) / (x + one);
-      }
-    } else {
-      if (ix < 0x401c0000) {
-        id = 2;
-        x = (x - 1.5f) / (one + 1.5f * x);
-      } else {
-        id = 3;
-        x = -1.0f / x;
-      }
-    }
+  if (ix < 0x31000000) {
+    if (huge + x > one) return x;
+  }
+  // the argument reduction of the four intervals -- (2x-1)/(2+x), (x-1)/(x+1),
+  // (x-1.5)/(1+1.5x), -1/x on |x| -- as ONE division of selected operands, each operand
+  // the same expression as fdlibm's (so the same roundings); below 7/16 x is kept, as x/1.
+  // Lanes of a wave in different intervals then share one division instead of running
+  // up to four divergent ones.
+  {
+    const float xa = __builtin_fabsf(x);
+    id = ix < 0x3ee00000 ? -1 : ix < 0x3f300000 ? 0 : ix < 0x3f980000 ? 1 : ix < 0x401c0000 ? 2 : 3;
+    const float num = id < 0 ? x : id == 0 ? 2.0f * xa - one : id == 1 ? xa - one : id == 2 ? xa - 1.5f : -1.0f;
+    const float den = id < 0 ? one : id == 0 ? 2.0f + xa : id == 1 ? xa + one : id == 2 ? one + 1.5f * xa : xa;
+    x = num / den;
   }
   z = x * x;
   w = z * z;
@@ -189,7 +203,9 @@ IRT_HD float glibc_atan2f(float y, float x) {
   const int32_t hx = (int32_t)f2u(x), ix = hx & 0x7fffffff;
   const int32_t hy = (int32_t)f2u(y), iy = hy & 0x7fffffff;
   if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
-  if (hx == 0x3f800000) return glibc_atanf(y);
+  // (fdlibm's x == 1.0 shortcut, atanf(y), is left out: the general path below gives the same
+  // float for x = 1 -- atanf is odd bit for bit, y/1 == y, and for |y| > 2^60 both round to
+  // 0x3fc90fdb -- and a second inlined atanf costs the kernel code size)
   const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
   if (iy == 0) {
     switch (m) {

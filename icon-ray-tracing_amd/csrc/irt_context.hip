@@ -88,6 +88,10 @@ struct irt_context {
   // reused or its statistics are asked for.  The last finished launch is `stats`; every
   // finished launch also adds into `total`.
   static constexpr int kSlots = 32;
+  // launches with more workgroups (x frames) than this count through the device-atomic block
+  // (the per-workgroup ring would need 1 KiB of pinned memory per workgroup: 256 MiB here)
+  static constexpr size_t kWgCountsMax = size_t(1) << 18;
+  size_t wgCountsMax = kWgCountsMax;  // IRT_WG_COUNTS_MAX overrides (tests)
   unsigned long long *d_counters = nullptr;  // kSlots x 16
   unsigned long long *h_counters = nullptr;  // pinned, kSlots x 16
   unsigned long long *dh_counters = nullptr; // h_counters as the device sees it
@@ -451,6 +455,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.du = make_float3(lp->dir_du.x, lp->dir_du.y, lp->dir_du.z);
   A.dv = make_float3(lp->dir_dv.x, lp->dir_dv.y, lp->dir_dv.z);
   A.accumID = lp->accumID;
+  A.accumW = 1.f / (float)(lp->accumID + 1);  // the lerp weight (deviceCode.cu:333), per launch
   A.amb = make_float3(lp->ambientColor.x, lp->ambientColor.y, lp->ambientColor.z);
   A.ambRad = lp->ambientRadiance;
   A.unitDistance = lp->unitDistance;
@@ -517,7 +522,11 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   }
   const size_t lanes = (size_t)numTiles * 4096;
   const size_t numWG = (size_t)numTiles * 16 * (size_t)numFrames;
-  if (c->wgCountsOn && numWG > c->wgCap) {
+  // Per-workgroup counts need kSlots x 32 B of pinned host memory per workgroup and frame
+  // (1 KiB): a launch past kWgCountsMax workgroups (a large progressive batch) counts through
+  // the device-atomic block instead, for that launch only.
+  const bool useWG = c->wgCountsOn && numWG <= c->wgCountsMax;
+  if (useWG && numWG > c->wgCap) {
     // every slot's launch must be retired before the ring is reallocated
     int rc = finish_stats(c);
     if (rc) return rc;
@@ -538,7 +547,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
       c->wgCap = numWG;
     }
   }
-  A.wgCounts = c->wgCountsOn ? c->dh_wgCounts + (size_t)slot * c->wgCap * kCnt : nullptr;
+  A.wgCounts = useWG && c->wgCountsOn ? c->dh_wgCounts + (size_t)slot * c->wgCap * kCnt : nullptr;
   const bool statsVariant = (c->variant & (32768 | 524288)) != 0;  // statistics, timing
   if (c->countersProbe == 1) {
     // measurement only: no counts -- except that the statistics and timing variants add into
@@ -596,7 +605,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   c->schedApplied += c->schedLastApplied ? 1 : 0;
   // the 16-counter block (device atomics) is only needed by the statistics variant and the
   // IRT_COUNTERS=atomic mode; it must start zeroed
-  const bool block = A.counters && (!c->wgCountsOn || statsVariant);
+  const bool block = A.counters && (!A.wgCounts || statsVariant);
   if (block && !c->lastBlock) IRT_HIP(hipMemsetAsync(A.counters, 0, 16 * sizeof(unsigned long long), s));
   if (c->launches > 0 && s != c->lastStream) {
     // this slot may have been zeroed by the previous launch's k_stats_out on another stream
@@ -617,7 +626,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   }
   c->slotBlock[slot] = block;
   c->lastBlock = block;
-  c->slotWG[slot] = (c->wgCountsOn && c->countersProbe == 0 && numTiles > 0) ? numWG : 0;
+  c->slotWG[slot] = (A.wgCounts && c->countersProbe == 0 && numTiles > 0) ? numWG : 0;
   c->schedCopied[slot] = -1;
   if (copyCosts) {
     c->schedCopied[slot] = c->launches;
@@ -869,6 +878,7 @@ int irt_create_end(irt_context *c) {
     c->countersProbe = strcmp(e, "off") == 0 ? 1 : (strcmp(e, "device") == 0 ? 2 : 0);
   }
   if (const char *e = getenv("IRT_TIMING_EVERY")) c->timingEvery = std::max(1, atoi(e));
+  if (const char *e = getenv("IRT_WG_COUNTS_MAX")) c->wgCountsMax = (size_t)std::max(0LL, atoll(e));
   if (const char *e = getenv("IRT_COOP_MAXLG")) c->coopMaxLg = std::min(6, std::max(0, atoi(e)));
   if (const char *e = getenv("IRT_COOP_RAMP")) c->coopRamp = std::min(6, std::max(0, atoi(e)));
   if (const char *e = getenv("IRT_PROBE_EXIT")) c->probeExit = atoi(e);

@@ -29,10 +29,44 @@ __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, fl
   return ax * bx + ay * by + az * bz;  // vecmath.h:536-538 order
 }
 
-// boxTest (vecmath.h:1926-1937)
+// Correctly rounded a / b for per-lane divisors through a double reciprocal, cheaper than the
+// f32 division sequence (v_div_scale x2, v_rcp, five fmas, v_div_fmas, v_div_fixup) when
+// one divisor serves several quotients.  r = the hardware estimate of 1/b (v_rcp_f32, within
+// 1 ulp: |e| <= 2^-22 for e = 1 - b r) refined once cubically, r (1 + e + e^2), by double
+// fmas: relative error e^3 plus three roundings, below 2^-52.  Then (double)a * r is within
+// 2^-51 (relative) of a/b, while a quotient of two floats that is not itself representable
+// lies at least 2^-49 from every rounding boundary of the float grid (a - b m, for a boundary
+// m, is a nonzero multiple of 2^min(ea, eb+em): the same argument as div_uniform), so the
+// double product rounds to the float a / b rounds to -- overflow to inf and float subnormal
+// results included.  Valid for 2^-100 <= |b| <= 2^100 (no zero, inf, NaN or subnormal
+// divisor, no double overflow); recip_ok(b) tests that and callers divide otherwise.
+// tests/test_host_logic.py checks the identity with estimates perturbed by up to 2 ulps.
+__device__ __forceinline__ bool recip_ok(float b) {
+  const float ab = __builtin_fabsf(b);
+  return ab >= 0x1p-100f && ab <= 0x1p100f;
+}
+__device__ __forceinline__ double recip_d(float b) {
+  const double r0 = (double)__builtin_amdgcn_rcpf(b);
+  const double e = __builtin_fma(-(double)b, r0, 1.0);
+  return __builtin_fma(r0, __builtin_fma(e, e, e), r0);
+}
+__device__ __forceinline__ float div_recip(float a, double r) { return (float)((double)a * r); }
+
+// boxTest (vecmath.h:1926-1937); the six quotients through one reciprocal per axis
 __device__ __forceinline__ bool box_test(const Ray &r, const RenderArgs &A, float &t0, float &t1) {
-  const float lx = (A.bmin.x - r.ox) / r.dx, ly = (A.bmin.y - r.oy) / r.dy, lz = (A.bmin.z - r.oz) / r.dz;
-  const float hx = (A.bmax.x - r.ox) / r.dx, hy = (A.bmax.y - r.oy) / r.dy, hz = (A.bmax.z - r.oz) / r.dz;
+  float lx, ly, lz, hx, hy, hz;
+  if (recip_ok(r.dx) && recip_ok(r.dy) && recip_ok(r.dz)) {
+    const double rx = recip_d(r.dx), ry = recip_d(r.dy), rz = recip_d(r.dz);
+    lx = div_recip(A.bmin.x - r.ox, rx);
+    ly = div_recip(A.bmin.y - r.oy, ry);
+    lz = div_recip(A.bmin.z - r.oz, rz);
+    hx = div_recip(A.bmax.x - r.ox, rx);
+    hy = div_recip(A.bmax.y - r.oy, ry);
+    hz = div_recip(A.bmax.z - r.oz, rz);
+  } else {
+    lx = (A.bmin.x - r.ox) / r.dx, ly = (A.bmin.y - r.oy) / r.dy, lz = (A.bmin.z - r.oz) / r.dz;
+    hx = (A.bmax.x - r.ox) / r.dx, hy = (A.bmax.y - r.oy) / r.dy, hz = (A.bmax.z - r.oz) / r.dz;
+  }
   const float nx = fminf(lx, hx), ny = fminf(ly, hy), nz = fminf(lz, hz);
   const float fx = fmaxf(lx, hx), fy = fmaxf(ly, hy), fz = fmaxf(lz, hz);
   t0 = fmaxf(r.tmin, fmaxf(fmaxf(nx, ny), nz));
@@ -54,6 +88,38 @@ __device__ __forceinline__ bool intersect_sphere(const Ray &r, float radius, flo
   tnear = fminf(t1, t2);
   tfar = fmaxf(t1, t2);
   return true;
+}
+// The raygen's two intersectSphere calls on one ray (the shell's outer and inner sphere,
+// ShellAccel.h:94-95): the same expressions, A = dot(dir, dir) shared, each quotient through
+// recip_d when its divisor allows.
+__device__ __forceinline__ void intersect_spheres(const Ray &r, float radiusA, float radiusB, bool &hitA,
+                                                  float &nearA, float &farA, bool &hitB, float &nearB,
+                                                  float &farB) {
+  const float A = dot3(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz);
+  const float B = dot3(r.dx, r.dy, r.dz, r.ox, r.oy, r.oz) * 2.f;
+  const float OO = dot3(r.ox, r.oy, r.oz, r.ox, r.oy, r.oz);
+  const bool okA = recip_ok(A);
+  const double rA = okA ? recip_d(A) : 0.0;
+  auto one = [&](float radius, float &tnear, float &tfar) {
+    const float C = OO - radius * radius;
+    float d = B * B - 4.f * A * C;
+    if (d < 0.f) return false;
+    d = sqrtf(d);
+    const float q = B < 0.f ? -0.5f * (B - d) : -0.5f * (B + d);
+    float t1, t2;
+    if (okA && recip_ok(q)) {
+      t1 = div_recip(q, rA);
+      t2 = div_recip(C, recip_d(q));
+    } else {
+      t1 = q / A;
+      t2 = C / q;
+    }
+    tnear = fminf(t1, t2);
+    tfar = fmaxf(t1, t2);
+    return true;
+  };
+  hitA = one(radiusA, nearA, farA);
+  hitB = one(radiusB, nearB, farB);
 }
 
 // projectToSphericalGrid (ShellAccel.h:57-68), one axis: int((s-lo)/size*(dims-1))

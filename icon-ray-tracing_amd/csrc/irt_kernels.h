@@ -14,6 +14,7 @@ struct RenderArgs {
   // camera / frame (Params.h:100-118)
   float3 org, dir00, du, dv;
   int accumID;
+  float accumW;          // 1.f / (float)(accumID + 1), the single frame's lerp weight
   float3 amb;
   float ambRad;
   float unitDistance;

@@ -40,6 +40,13 @@ enum : int {
                       // (locate), for A/B against Tracer::locate_wave
   OPT_TIMING = 524288,  // measurement only: per-wave shader-clock time by region into
                         // counters[5..15] (Tracer::tmark)
+  OPT_HDRLDS = 1048576, // (A/B) the wave-wide scan's cube-map cell headers staged through LDS:
+                        // each distinct header line of the wave's samples loaded once,
+                        // cooperatively, then read from LDS (Tracer::stage_headers)
+  OPT_LEAN = 2097152,   // (A/B) less LDS per workgroup (31.0 -> 24 KB), so that more workgroups
+                        // fit a CU while finished waves wait for their workgroup's last one:
+                        // the sRGB thresholds and the sphere hash read from global memory
+                        // (L1/L2), the accum pixel loaded at the end instead of prefetched
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
@@ -97,6 +104,12 @@ struct ScanWave {
   float4 pt[64];    // lane l's sample {point, r}
   uint4 lst[64];    // its candidate list {first entry, sub-cell mask, next position, record limit}
 };
+// OPT_HDRLDS: up to kHdrStage distinct header lines of a wave's samples, staged in LDS
+constexpr int kHdrStage = 8;
+struct HdrStage {
+  uint32_t cell[kHdrStage];
+  uint32_t w[kHdrStage][kBinHdrWords];
+};
 
 // t0 - d[0] - d[1] - ... - d[k], subtracted one at a time as woodcockTracking's `t -=`
 // (deviceCode.cu:165) does: the same roundings as k+1 iterations of the serial loop.
@@ -109,6 +122,10 @@ template <class T>
 __device__ __forceinline__ T lds_ld16(const T *p) {
   static_assert(sizeof(T) == 16, "16-byte slot");
   return __builtin_bit_cast(T, *reinterpret_cast<const fvec4 *>(p));
+}
+typedef uint32_t uvec2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 lds_ld8(const uint2 *p) {
+  return __builtin_bit_cast(uint2, *reinterpret_cast<const uvec2 *>(p));
 }
 template <class T>
 __device__ __forceinline__ void lds_st16(T *p, T v) {
@@ -472,6 +489,52 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     for (uint32_t k = 0; k < p; ++k) m8 &= m8 - 1u;
     return (uint32_t)__builtin_ctz(m8);
   }
+  // OPT_HDRLDS: the header words 0..7 and word 8+sub of every wanting lane's cube-map cell.
+  // The wave's distinct cells (in lane order, at most kHdrStage) get one 128-B line each,
+  // loaded by 32 lanes together (a dword per lane) and written to LDS; lanes whose cell is
+  // past the kHdrStage-th distinct one load their header directly.
+  HdrStage *s_hdr = nullptr;
+  __device__ __forceinline__ void stage_headers(bool want, uint32_t cell, uint32_t sub, uint4 &H0, uint4 &H1,
+                                                uint32_t &M) {
+    const int lane = (int)__lane_id();
+    HdrStage &S = s_hdr[0];
+    uint64_t todo = __ballot(want);
+    int slot = -1, ns = 0;
+    while (todo != 0ull && ns < kHdrStage) {
+      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cell, (int)__builtin_ctzll(todo));
+      const bool mine = want && cell == c;
+      todo &= ~__ballot(mine);
+      if (mine) slot = ns;
+      if (lane == 0) S.cell[ns] = c;
+      ++ns;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // two lines per pass, every pass's loads issued before the LDS writes
+    uint32_t v[kHdrStage / 2];
+#pragma unroll
+    for (int p = 0; p < kHdrStage / 2; ++p) {
+      const int k = 2 * p + (lane >> 5);
+      v[p] = 0u;
+      if (k < ns) v[p] = reinterpret_cast<const uint32_t *>(A.binHdr)[(size_t)S.cell[k] * kBinHdrWords + (lane & 31)];
+    }
+#pragma unroll
+    for (int p = 0; p < kHdrStage / 2; ++p) {
+      const int k = 2 * p + (lane >> 5);
+      if (k < ns) S.w[k][lane & 31] = v[p];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (slot >= 0) {
+      H0 = lds_ld16(reinterpret_cast<const uint4 *>(&S.w[slot][0]));
+      H1 = lds_ld16(reinterpret_cast<const uint4 *>(&S.w[slot][4]));
+      M = S.w[slot][8 + sub];
+    } else if (want) {
+      const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
+      H0 = Hc[0];
+      H1 = Hc[1];
+      M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
   __device__ __forceinline__ bool locate_wave(bool want, float px, float py, float pz, float &value,
                                               CoopWave &CW, ScanWave &W) {
     want = want && A.numCells != 0;
@@ -488,13 +551,21 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     uint32_t fe = 0u, flim = 0xFFFFFFFFu;  // the pass's first candidate entry, record limit
     float fr = 0.f;                        // the sample's r
     bool hit = false, edge = false;
+    uint4 H0 = make_uint4(0u, 0u, 0u, 0u), H1 = H0;
+    uint32_t M = 0u, cell = 0u, sub = 0u;
+    if constexpr ((OPT & OPT_HDRLDS) != 0) {
+      if (want) cell = cubemap_cell_fast(px, py, pz, A.G, sub);
+      stage_headers(want, cell, sub, H0, H1, M);
+    }
     if (want) {
       const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
-      uint32_t sub;
-      const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G, sub);
-      const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
-      const uint4 H0 = Hc[0], H1 = Hc[1];
-      const uint32_t M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
+      if constexpr ((OPT & OPT_HDRLDS) == 0) {
+        cell = cubemap_cell_fast(px, py, pz, A.G, sub);
+        const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
+        H0 = Hc[0];
+        H1 = Hc[1];
+        M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
+      }
       const int b = bin_of(r, __uint_as_float(H0.x), __uint_as_float(H0.y), __uint_as_float(H0.z));
       const uint32_t m1 = b > 0 ? ~0u : 0u, m2 = b > 1 ? ~0u : 0u, m3 = b > 2 ? ~0u : 0u;
       const uint32_t beg = (m1 & H1.x) + (m2 & (H1.y - H1.x)) + (m3 & (H1.z - H1.y));
@@ -703,8 +774,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   __device__ __forceinline__ void woodcock_wave(bool req, float dx, float dy, float dz, float &t,
                                                 float tmax, uint32_t &st, float majorant,
                                                 bool counted, float4 &sampleOut, bool &miss,
-                                                CoopWave &W, ScanWave *SW, const uint32_t *jmul,
-                                                const uint32_t *jadd) {
+                                                CoopWave &W, ScanWave *SW, const uint2 *jmp) {
     const int lane = (int)__lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
     const float q = majorant / A.unitDistance;
@@ -759,7 +829,13 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       // sample k's step draw: 2k+1 draws ahead if every earlier sample is located (and
       // rejected), k+1 if none is (miss mode)
       const int jk = mm ? k + 1 : 2 * k + 1;
-      const uint32_t sk = solo ? lcg_next(s0) : jmul[jk] * s0 + jadd[jk];
+      uint32_t sk;
+      if (solo) {
+        sk = lcg_next(s0);
+      } else {
+        const uint2 j = lds_ld8(&jmp[jk]);  // {mul, add}: one 8-byte LDS read
+        sk = j.x * s0 + j.y;
+      }
       const float dk = woodcock_log(sk, s_logf) / rq.z;
       float tk;
       if (solo) {
@@ -849,10 +925,12 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         // draws taken: two per located sample, one per miss (and the one past tmax)
         const int n = (kMiss && miss) ? (of == G ? G : (foundS ? of + 2 : of + 1))
                            : (of == G ? 2 * G : (accS ? 2 * of + 2 : 2 * of + 1));
-        if (solo)
+        if (solo) {
           st = n == 1 ? sk : lcg_next(sk);  // the draws this round made
-        else
-          st = jmul[n] * st + jadd[n];
+        } else {
+          const uint2 j = lds_ld8(&jmp[n]);
+          st = j.x * st + j.y;
+        }
         if (of < G && (pastS || accS)) {
           active = false;
           if (accS) sampleOut = post_classify(vsrc);
@@ -870,14 +948,15 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
 // The frame grid: 256-thread workgroup b, thread t -> gid = 256 b + t.  Workgroup b covers
 // 16x16 pixels of tile k = b / 16 of this launch (frame tile tileBegin + k*tileStride, or
 // tileList[k]),
-// wave w an 8x8 packet, lane l one pixel.
+// wave w an 8x8 packet, lane l one pixel.  The block index is passed on its own so that the
+// tile arithmetic (an integer division by tilesX) stays scalar: it is uniform per workgroup.
 struct Pixel {
   int x, y;
   size_t outIdx;
   bool active;
 };
-__device__ __forceinline__ Pixel pixel_of(const RenderArgs &A, uint32_t gid) {
-  const int blk = (int)(gid >> 8), tid = (int)(gid & 255);
+__device__ __forceinline__ Pixel pixel_of(const RenderArgs &A, uint32_t blkU, int tid) {
+  const int blk = (int)__builtin_amdgcn_readfirstlane(blkU);
   const int k = blk >> 4, sub = blk & 15;
   const int wave = tid >> 6, lane = tid & 63;
   const int lx = ((sub & 3) << 4) | ((wave & 1) << 3) | (lane & 7);
@@ -907,9 +986,16 @@ __device__ __forceinline__ void gen_ray(const RenderArgs &A, int accumID, int x,
   dy = (A.dir00.y + a * A.du.y) + b * A.dv.y;
   dz = (A.dir00.z + a * A.du.z) + b * A.dv.z;
   const float len = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
-  dx = dx / len;
-  dy = dy / len;
-  dz = dz / len;
+  if (recip_ok(len)) {  // normalize's three quotients through one reciprocal (irt_device.h)
+    const double r = recip_d(len);
+    dx = div_recip(dx, r);
+    dy = div_recip(dy, r);
+    dz = div_recip(dz, r);
+  } else {
+    dx = dx / len;
+    dy = dy / len;
+    dz = dz / len;
+  }
   if (fabsf(dx) < 1e-5f) dx = 1e-5f;
   if (fabsf(dy) < 1e-5f) dy = 1e-5f;
   if (fabsf(dz) < 1e-5f) dz = 1e-5f;
@@ -919,7 +1005,7 @@ __device__ __forceinline__ void gen_ray(const RenderArgs &A, int accumID, int x,
 // make_rgba (deviceCode.cu:333-340)
 __device__ __forceinline__ void write_pixel(const RenderArgs &A, size_t outIdx, float cr, float cg,
                                             float cb, float alpha, const float *s_th, float4 old) {
-  const float w = 1.f / (float)(A.accumID + 1);
+  const float w = A.accumW;  // 1.f / (float)(accumID + 1), on the host (the same division)
   float4 nv;
   nv.x = w * cr + (1.f - w) * old.x;
   nv.y = w * cg + (1.f - w) * old.y;
@@ -1192,8 +1278,8 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
 template <int OPT>
 __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
                                                   const float *s_th, int4 *s_dda, float4 *s_entry,
-                                                  float4 *s_acc, CoopWave &W, ScanWave *SW, const uint32_t *jmul,
-                                                  const uint32_t *jadd, int tid, int accumID,
+                                                  float4 *s_acc, CoopWave &W, ScanWave *SW, const uint2 *jmp,
+                                                  int tid, int accumID,
                                                   float4 *sampleOut) {
   enum : int { kRange, kLeaf, kWait, kDone, kGrid, kGridNext };
   constexpr bool grid = (OPT & OPT_GRID) != 0;
@@ -1221,7 +1307,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       t1box = t1;
       // the accum pixel the lerp reads at the end, fetched now straight into LDS (no VGPRs
       // held through the Woodcock rounds; its latency hides behind them)
-      if (!sampleOut)
+      if (!sampleOut && (OPT & OPT_LEAN) == 0)
         __builtin_amdgcn_global_load_lds((const void *)(A.accum + px.outIdx),
                                          (__attribute__((address_space(3))) void *)(s_acc + (tid & ~63)),
                                          16, 0, 0);
@@ -1230,8 +1316,8 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       numRanges = 1;
       if (!ae) {  // the shell's sphere ranges, as render_pixel
         float st1 = 0.f, st2 = 0.f, st3 = 0.f, st4 = 0.f;
-        const bool s1 = intersect_sphere(ray, A.sbHi.x, st1, st4);
-        const bool s2 = intersect_sphere(ray, A.sbLo.x, st2, st3);
+        bool s1, s2;
+        intersect_spheres(ray, A.sbHi.x, A.sbLo.x, s1, st1, st4, s2, st2, st3);
         numRanges = 0;
         if ((s1 || s2) && !(st4 < t0)) {
           numRanges = 2;
@@ -1466,7 +1552,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
         first = false;
       }
     }
-    T.woodcock_wave(req, dx, dy, dz, tw, tt1, st, maj, !zeroLen, s, miss, W, SW, jmul, jadd);
+    T.woodcock_wave(req, dx, dy, dz, tw, tt1, st, maj, !zeroLen, s, miss, W, SW, jmp);
     if (A.probeExit == 5) break;  // measurement only: the first woodcockFunc of every lane
     if (grid && req && phase == kWait && !ae) {
       if (tw > t && tw < tt1) {  // render_grid's hit test (deviceCode.cu:316)
@@ -1494,47 +1580,50 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   if (sampleOut) {
     *sampleOut = c;
   } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
-    write_pixel(A, px.outIdx, c.x, c.y, c.z, c.w, s_th, lds_ld16(&s_acc[tid]));
+    if constexpr ((OPT & OPT_LEAN) != 0) {
+      write_pixel(A, px.outIdx, c.x, c.y, c.z, c.w, s_th);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
+      write_pixel(A, px.outIdx, c.x, c.y, c.z, c.w, s_th, lds_ld16(&s_acc[tid]));
+    }
   }
 }
 
 // The raygen over the frame grid: one lane per pixel (see pixel_of).
 template <int OPT>
 __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1) k_render(RenderArgs A) {
-  __shared__ float s_th[256];
+  constexpr bool lean = (OPT & OPT_LEAN) != 0;
+  __shared__ float s_th[lean ? 1 : 256];
   __shared__ uint32_t s_cnt[kCnt];
   __shared__ LogfTab s_logf[16];
-  __shared__ uint32_t s_sph[kSphBitWords];
+  __shared__ uint32_t s_sph[lean ? 1 : kSphBitWords];
   __shared__ int4 s_dda[256];       // sdda state needed only after a range's first leaf
   __shared__ float4 s_entry[256];
   __shared__ CoopWave s_coop[4];    // the cooperative Woodcock loop (kCoop kernels)
   __shared__ ScanWave s_scan[Tracer<OPT>::kWaveScan ? 4 : 1];  // its wave-wide candidate scan
-  __shared__ float4 s_acc[256];     // kCoop: the accum pixels, prefetched
-  __shared__ uint32_t s_jmul[kLcgJumps], s_jadd[kLcgJumps];
+  __shared__ HdrStage s_hdrs[(OPT & OPT_HDRLDS) ? 4 : 1];       // OPT_HDRLDS: staged header lines
+  __shared__ float4 s_acc[lean ? 1 : 256];  // kCoop: the accum pixels, prefetched
+  __shared__ uint2 s_jmp[kLcgJumps];  // lcg_jump's {mul, add} (kLcgJumpTab)
   const int tid = threadIdx.x;
   if (A.probeExit == 1) return;  // measurement only
   uint64_t tStart = 0;
   if constexpr ((OPT & OPT_TIMING) != 0) tStart = __builtin_amdgcn_s_memtime();
   // the prologue's global loads issued together, one wait (not one round trip each)
-  const float th = A.srgbTh[tid];
+  const float th = lean ? 0.f : A.srgbTh[tid];
   const LogfTab lt = kLogfTab[tid & 15];
   uint32_t sph[kSphBitWords / 256];
-  if (A.numSph) {
+  if (!lean && A.numSph) {
 #pragma unroll
     for (int k = 0; k < kSphBitWords / 256; ++k) sph[k] = A.sphBits[tid + 256 * k];
   }
-  if constexpr (Tracer<OPT>::kCoop) {
-    if (tid < kLcgJumps) {
-      uint32_t m, a;
-      lcg_jump((uint32_t)tid, m, a);
-      s_jmul[tid] = m;
-      s_jadd[tid] = a;
-    }
-  }
-  s_th[tid] = th;
+  uint2 jmpv = make_uint2(0u, 0u);
+  if constexpr (Tracer<OPT>::kCoop)
+    if (tid < kLcgJumps) jmpv = make_uint2(kLcgJumpTab.ma[tid][0], kLcgJumpTab.ma[tid][1]);
+  if constexpr (Tracer<OPT>::kCoop)
+    if (tid < kLcgJumps) *reinterpret_cast<uvec2 *>(&s_jmp[tid]) = __builtin_bit_cast(uvec2, jmpv);
+  if constexpr (!lean) s_th[tid] = th;
   if (tid < 16) s_logf[tid] = lt;
-  if (A.numSph) {
+  if (!lean && A.numSph) {
 #pragma unroll
     for (int k = 0; k < kSphBitWords / 256; ++k) s_sph[tid + 256 * k] = sph[k];
   }
@@ -1548,8 +1637,10 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   }
   __syncthreads();
   if (A.probeExit == 2) return;  // measurement only
-  Tracer<OPT> T{{}, A, s_logf, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
+  Tracer<OPT> T{{}, A, s_logf, lean ? A.sphBits : s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
   T.s_gbits = s_gbits;
+  const float *th_p = lean ? A.srgbTh : s_th;
+  T.s_hdr = &s_hdrs[(OPT & OPT_HDRLDS) ? tid >> 6 : 0];
   if constexpr ((OPT & OPT_TIMING) != 0) {
     T.tLast = tStart;
     T.tmark(0);  // prologue
@@ -1560,16 +1651,16 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   // scheduling (irt_context.hip) workgroup b renders block order[b].
   const uint32_t blk = A.schedOrder ? A.schedOrder[blockIdx.x] : blockIdx.x;
   const uint32_t gid = blk * 256u + (uint32_t)tid;
-  const Pixel px = pixel_of(A, gid);
+  const Pixel px = pixel_of(A, blk, tid);
   float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + gid : nullptr;
   if constexpr (Tracer<OPT>::kCoop) {
-    render_pixel_coop<OPT>(A, T, px, s_th, s_dda, s_entry, s_acc, s_coop[tid >> 6],
-                           &s_scan[Tracer<OPT>::kWaveScan ? tid >> 6 : 0], s_jmul, s_jadd, tid,
+    render_pixel_coop<OPT>(A, T, px, th_p, s_dda, s_entry, s_acc, s_coop[tid >> 6],
+                           &s_scan[Tracer<OPT>::kWaveScan ? tid >> 6 : 0], s_jmp, tid,
                            A.accumID + (int)blockIdx.y, slot);
     T.flush_coop();
   }
   else if (px.active)
-    render_pixel<OPT>(A, T, px, s_th, s_dda, s_entry, tid, A.accumID + (int)blockIdx.y, slot);
+    render_pixel<OPT>(A, T, px, th_p, s_dda, s_entry, tid, A.accumID + (int)blockIdx.y, slot);
   if constexpr ((OPT & OPT_TIMING) != 0) {
     T.tmark(8);  // after the last woodcockFunc: pixel write, epilogue
     if ((tid & 63) == 0) {
@@ -1638,7 +1729,7 @@ __global__ void __launch_bounds__(256) k_accumulate(RenderArgs A) {
   s_th[threadIdx.x] = A.srgbTh[threadIdx.x];
   __syncthreads();
   const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
-  const Pixel px = pixel_of(A, gid);
+  const Pixel px = pixel_of(A, blockIdx.x, (int)threadIdx.x);
   if (!px.active) return;
   const size_t lanes = (size_t)gridDim.x * 256u;
   float4 a = A.accum[px.outIdx];
@@ -1724,11 +1815,14 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 // raygen; the setup -> march -> continuation pipeline it distinguished from was removed).
 // 70656 = 5120 | OPT_SERIAL: the one-lane-per-ray Woodcock loop, for A/B against the
 // cooperative default.  5376: the default with a 5-waves-per-SIMD floor (96 VGPRs, 19
-// spilled; C3s 4 % faster, C3 2 % slower: profiles/r03q_args_waves/), for A/B.  All variants give identical results.
+// spilled; C3s 4 % faster, C3 2 % slower: profiles/r03q_args_waves/), for A/B.  1053696 = 5120 |
+// OPT_HDRLDS: the cell headers staged through LDS (profiles/r03s_hdr_lds/).  2102272 = 5120 |
+// OPT_LEAN (24 KB of LDS per workgroup), 2102528 the same at 5 waves/SIMD.  All variants give
+// identical results.
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528)
 
 bool render_variant_available(int v) {
 #define IRT_CASE(N) if (v == N) return true;

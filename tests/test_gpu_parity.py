@@ -715,3 +715,40 @@ def test_device_locator_matches_host_restatement(scene, entry):
     assert n_hit > len(pts) // 3
     ctx.close()
     D.close()
+
+
+def test_counts_past_the_workgroup_ring_cap(monkeypatch):
+    """a launch with more workgroups (x frames) than the per-workgroup count ring
+    allows (IRT_WG_COUNTS_MAX; 2^18 by default) counts through the device-atomic block for that
+    launch only; launches on either side of it keep the ring.  Statistics and frames equal a
+    default context's, launch by launch (single frames and progressive batches)."""
+    import torch
+    cells = irt.synth_grid(2, 2, 47)
+
+    def run():
+        ctx = irt.Context(cells, 0)
+        out = []
+        for W, frames in ((64, 1), (200, 1), (64, 1), (64, 3), (200, 2), (64, 1)):  # 16/64/16/48/128/16 WGs
+            setup = irt.setup_frame(cells, W, W, camera=FRAMING)
+            ctx.set_transfunc(setup.lut, setup.value_range)
+            fb = torch.zeros(W * W, dtype=torch.int32, device="cuda")
+            acc = torch.zeros(W * W * 4, dtype=torch.float32, device="cuda")
+            if frames == 1:
+                ctx.render(setup.lp, W, W, fb.data_ptr(), acc.data_ptr())
+            else:
+                ctx.render_accumulate(setup.lp, W, W, frames, fb.data_ptr(), acc.data_ptr())
+            st = ctx.stats()
+            out.append((fb.cpu().numpy().copy(), bits(acc.cpu().numpy()), st.raysLaunched, st.raysInBox,
+                        st.locateCalls, st.samplesFound, st.candidatesTested))
+        tot = ctx.stats_total()
+        ctx.close()
+        return out, (tot[0].locateCalls, tot[0].samplesFound, tot[1])
+
+    ref, ref_tot = run()
+    assert ref[1][4] > 0 and ref[4][4] > 0
+    monkeypatch.setenv("IRT_WG_COUNTS_MAX", "20")
+    got, got_tot = run()
+    for k, (a, b) in enumerate(zip(ref, got)):
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), k
+        assert a[2:] == b[2:], (k, a[2:], b[2:])
+    assert got_tot == ref_tot

@@ -442,3 +442,112 @@ def test_division_by_a_launch_constant_as_one_double_product():
             got = (x.astype(np.float64) * (1.0 / y.astype(np.float64))).astype(np.float32)
             same = (ref.view(np.uint32) == got.view(np.uint32)) | (np.isnan(ref) & np.isnan(got))
             assert same.all(), (x[~same][:4], y[~same][:4])
+
+
+_RECIP_C = r"""
+#include <math.h>
+#include <stdint.h>
+/* irt_device.h recip_d / div_recip with the hardware estimate of 1/b replaced by the float
+   k ulps away from RN(1/b) (v_rcp_f32 is within 1 ulp); returns the mismatches vs a / b. */
+long check(const float *a, const float *b, long n, int k) {
+  long bad = 0;
+  for (long i = 0; i < n; ++i) {
+    float r0f = 1.0f / b[i];
+    for (int s = 0; s < (k < 0 ? -k : k); ++s) r0f = nextafterf(r0f, k < 0 ? 0.0f : INFINITY);
+    const double r0 = (double)r0f;
+    const double e = fma(-(double)b[i], r0, 1.0);
+    const double r = fma(r0, fma(e, e, e), r0);
+    const float got = (float)((double)a[i] * r);
+    const float ref = a[i] / b[i];
+    if (!(got == ref || (isnan(got) && isnan(ref))) || signbit(got) != signbit(ref)) ++bad;
+  }
+  return bad;
+}
+"""
+
+
+def test_division_through_a_refined_reciprocal(tmp_path):
+    """irt_device.h recip_d / div_recip (gen_ray's normalize, boxTest, intersectSphere): a / b
+    correctly rounded equals (float)((double)a * r) with r the hardware reciprocal estimate
+    refined once cubically in double -- for every estimate within 2 ulps of 1/b, random
+    operands over the divisor range recip_ok admits (2^-100..2^100), the kernel's operand
+    shapes, quotients that overflow or land in the float subnormal range, and signed zeros."""
+    import ctypes
+    import subprocess
+    src = tmp_path / "recip.c"
+    so = tmp_path / "librecip.so"
+    src.write_text(_RECIP_C)
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-fno-fast-math", "-shared", "-fPIC", "-o", str(so),
+                    str(src), "-lm"], check=True)
+    lib = ctypes.CDLL(str(so))
+    lib.check.restype = ctypes.c_long
+    fp = ctypes.POINTER(ctypes.c_float)
+    lib.check.argtypes = [fp, fp, ctypes.c_long, ctypes.c_int]
+    rng = np.random.default_rng(11)
+    n = 1_000_000
+    a = (rng.uniform(-1, 1, n) * 2.0 ** rng.integers(-126, 127, n)).astype(np.float32)
+    b = (rng.uniform(0.5, 1, n) * 2.0 ** rng.integers(-99, 101, n)).astype(np.float32)
+    b[::3] = -b[::3]
+    # the kernel's shapes: direction components / length, box slabs / direction, sphere roots
+    d = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+    ln = np.sqrt((d * d).sum(1, dtype=np.float32)).astype(np.float32)
+    a2, b2 = d[:, 0].copy(), ln
+    a3 = (rng.uniform(-7e6, 7e6, n).astype(np.float32) - np.float32(1.4e7))
+    b3 = np.where(np.abs(d[:, 1]) < 1e-5, np.float32(1e-5), d[:, 1]).astype(np.float32)
+    a4 = rng.uniform(-1e14, 1e14, n).astype(np.float32)
+    b4 = rng.uniform(-2e7, 2e7, n).astype(np.float32)
+    a5 = np.float32([0.0, -0.0, 3.4e38, -3.4e38, 1e-45, 1e-38, 1.0, np.inf, np.nan])
+    b5 = np.float32([1.0, 1.0, 2.0 ** -99, 2.0 ** -99, 2.0 ** 99, 2.0 ** 90, -(2.0 ** -100), 3.0, 3.0])
+    for x, y in ((a, b), (a2, b2), (a3, b3), (a4, b4), (a5, b5)):
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.ascontiguousarray(y, np.float32)
+        for k in (-2, -1, 0, 1, 2):
+            assert lib.check(x.ctypes.data_as(fp), y.ctypes.data_as(fp), x.size, k) == 0, (k, x[:3], y[:3])
+
+
+_ATAN_C = r"""
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+#include "irt_common.h"
+static uint32_t fb(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static float bf(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+/* irt_common.h glibc_atanf over every stride-th float, glibc_atan2f over n xorshift pairs
+   (a quarter with x == 1.0, a quarter of moderate integers): mismatches vs the host glibc */
+extern "C" long check(uint32_t stride, long n) {
+  long bad = 0;
+  for (uint64_t u = 0; u < 0x100000000ull; u += stride) {
+    const float x = bf((uint32_t)u), a = irt::glibc_atanf(x), b = atanf(x);
+    if (fb(a) != fb(b) && !(isnan(a) && isnan(b))) ++bad;
+  }
+  uint64_t s = 88172645463325252ull;
+  for (long i = 0; i < n; ++i) {
+    s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+    float y = bf((uint32_t)s), x = bf((uint32_t)(s >> 32));
+    if (i % 4 == 1) x = 1.0f;
+    if (i % 4 == 2) { y = (float)((int32_t)(s & 0xffffff) - 0x800000) * 1.3f; x = (float)((int32_t)(s >> 40) - 0x800000) * 0.7f; }
+    const float a = irt::glibc_atan2f(y, x), b = atan2f(y, x);
+    if (fb(a) != fb(b) && !(isnan(a) && isnan(b))) ++bad;
+  }
+  return bad;
+}
+"""
+
+
+def test_atanf_reduction_as_one_division_matches_glibc(tmp_path):
+    """irt_common.h glibc_atanf reduces its argument with ONE division of selected operands
+    (fdlibm's four interval formulas as written) and glibc_atan2f drops fdlibm's x == 1
+    shortcut: both still round exactly as the host glibc -- atanf on every 61st float
+    (checked once on all 2^32), atan2f on 4 M pairs including x == 1 (once on 2e8)."""
+    import ctypes
+    import subprocess
+    src = tmp_path / "atan.cpp"
+    so = tmp_path / "libatan.so"
+    src.write_text(_ATAN_C)
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "icon-ray-tracing_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-fno-fast-math", "-shared", "-fPIC", "-I", csrc,
+                    "-o", str(so), str(src), "-lm"], check=True)
+    lib = ctypes.CDLL(str(so))
+    lib.check.restype = ctypes.c_long
+    lib.check.argtypes = [ctypes.c_uint32, ctypes.c_long]
+    assert lib.check(61, 4_000_000) == 0
