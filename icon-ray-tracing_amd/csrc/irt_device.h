@@ -25,6 +25,16 @@ struct Counts {
   uint32_t hops, locRounds, candHist[4];
 };
 
+// A uniform value the compiler must treat as new at this point: the derived values (int ->
+// float conversions, integer-division reciprocals, LDS addresses) are then recomputed where
+// they are used instead of being hoisted out of the raygen's loops and held in VGPRs for the
+// whole kernel -- register pressure is what limits the waves per SIMD.
+__device__ __forceinline__ int opaque_u(int v) {
+  v = __builtin_amdgcn_readfirstlane(v);  // uniform: any lane's copy; keeps it scalar
+  asm volatile("" : "+s"(v));
+  return v;
+}
+__device__ __forceinline__ float opaque_u(float v) { return __builtin_bit_cast(float, opaque_u(__builtin_bit_cast(int, v))); }
 __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
   return ax * bx + ay * by + az * bz;  // vecmath.h:536-538 order
 }
@@ -138,7 +148,7 @@ __device__ __forceinline__ float div_uniform(float a, double invB) {
 }
 // project_axis with the per-launch 1 / (double)(hi - lo)
 __device__ __forceinline__ int project_axis_inv(float s, float lo, double invSize, int dim) {
-  return f2i_x86(div_uniform(s - lo, invSize) * (float)(dim - 1));
+  return f2i_x86(div_uniform(s - lo, invSize) * (float)(opaque_u(dim) - 1));
 }
 
 // normalizeGridCoord (ShellAccel.h:71-80): the while-loops compute c mod d in [0,d).  A
@@ -146,6 +156,8 @@ __device__ __forceinline__ int project_axis_inv(float s, float lo, double invSiz
 // VALU instructions per axis on gfx950 (no hardware integer divide).
 __device__ __forceinline__ int wrap_coord(int c, int d) {
   if ((unsigned)c < (unsigned)d) return c;
+  if (c >= -d && c < 2 * d) return c < 0 ? c + d : c - d;  // one step outside: no division
+  d = opaque_u(d);
   const int m = c % d;
   return m < 0 ? m + d : m;
 }

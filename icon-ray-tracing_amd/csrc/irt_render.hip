@@ -43,6 +43,8 @@ enum : int {
   OPT_HDRLDS = 1048576, // (A/B) the wave-wide scan's cube-map cell headers staged through LDS:
                         // each distinct header line of the wave's samples loaded once,
                         // cooperatively, then read from LDS (Tracer::stage_headers)
+  OPT_DEALALL = 8388608,  // (A/B) the wave-wide scan deals out every candidate, the lists' first
+                          // ones included (Tracer::locate_wave)
   OPT_LEAN = 2097152,   // (A/B) less LDS per workgroup (31.0 -> 24 KB), so that more workgroups
                         // fit a CU while finished waves wait for their workgroup's last one:
                         // the sRGB thresholds and the sphere hash read from global memory
@@ -77,7 +79,7 @@ __device__ __forceinline__ uint32_t cubemap_cell_fast(float px, float py, float 
     den = az;
   }
   const float inv = __builtin_amdgcn_rcpf(den);
-  const int GS = G * kSubCells;
+  const int GS = opaque_u(G) * kSubCells;
   const float fg = 0.5f * (float)GS;
   int i = (int)((num0 * inv + 1.f) * fg);
   int j = (int)((num1 * inv + 1.f) * fg);
@@ -583,9 +585,11 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       fr = r;
     }
     for (int pass = 0;; ++pass) {
-      // every lane: its list's first candidate
-      uint32_t rem = 0u;
-      if (c > 0u) {  // (from registers: no LDS round trip before the gather)
+      // every lane: its list's first candidate (OPT_DEALALL: none -- every candidate of
+      // every lane goes through the deal below, so a round's samples wait for one entry
+      // gather instead of two when the wave's lists hold <= 64 candidates in all)
+      uint32_t rem = (OPT & OPT_DEALALL) != 0 ? c : 0u;
+      if ((OPT & OPT_DEALALL) == 0 && c > 0u) {  // (from registers: no LDS round trip before the gather)
         Found f;
         const bool ok = pass_entry(A.fat + (size_t)fe * kFatStride4, px, py, pz, fr, f);
         if (f.rec < flim) {  // scan_fat stops, uncounted, at the first record >= the limit
@@ -699,7 +703,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // from post_classify on acceptance
   __device__ __forceinline__ float classify_alpha(float v) {
     v = div_uniform(v - A.tfLo, A.invTf);  // (v - tfLo) / (tfHi - tfLo), correctly rounded
-    const int size = A.lutSize;
+    const int size = opaque_u(A.lutSize);
     const int idx = f2i_x86(v * (float)size);
     const float frac = (v * (float)size) - (float)idx;
     const int i1 = idx < 0 ? 0 : (idx > size - 1 ? size - 1 : idx);
@@ -712,7 +716,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // postClassify (deviceCode.cu:127-135): weights reversed, opacityScale on 2nd term only
   __device__ __forceinline__ float4 post_classify(float v) {
     v = div_uniform(v - A.tfLo, A.invTf);  // (v - tfLo) / (tfHi - tfLo), correctly rounded
-    const int size = A.lutSize;
+    const int size = opaque_u(A.lutSize);
     const int idx = f2i_x86(v * (float)size);
     const float frac = (v * (float)size) - (float)idx;
     const int i1 = idx < 0 ? 0 : (idx > size - 1 ? size - 1 : idx);
@@ -1368,7 +1372,9 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       phase = kGrid;
     }
   }
-  const float sceneEPS = A.sbLo.x * 1e-6f;
+  // sceneEPS (ShellAccel.h:121-127), recomputed where it is used (a VALU product the
+  // compiler would otherwise hold in a VGPR through every loop)
+  auto sceneEPS = [&]() { return opaque_u(A.sbLo.x) * 1e-6f; };
   int i = 0, iter = 0, cx = 0, cy = 0, cz = 0;
   float t = 0.f, upper = 0.f, tt1 = 0.f, maj = 0.f;
   bool lastRange = true, zeroLen = false, hit = false;
@@ -1385,7 +1391,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     const float tnx = upper, tny = 0.f, tnz = 0.f;
     int4 dd;
     if (iter == 0) {
-      const float e2 = upper - sceneEPS;
+      const float e2 = upper - sceneEPS();
       float r2, la2, lo2;
       to_spherical(A.org.x + dx * e2, A.org.y + dy * e2, A.org.z + dz * e2, r2, la2, lo2);
       const float4 en = lds_ld16(&s_entry[tid]);
@@ -1489,7 +1495,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
         lastRange = ae || i == 1 || rhi1 <= rlo1;
         cx = cy = cz = 0;
         if (!ae) {  // cellID of the entry point (ShellAccel.h:121-124)
-          const float e1 = lower + sceneEPS;
+          const float e1 = lower + sceneEPS();
           float r1, la1, lo1;
           to_spherical(A.org.x + dx * e1, A.org.y + dy * e1, A.org.z + dz * e1, r1, la1, lo1);
           cx = project_axis_inv(r1, A.sbLo.x, A.invSb[0], A.dims.x);
@@ -1817,12 +1823,12 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 // cooperative default.  5376: the default with a 5-waves-per-SIMD floor (96 VGPRs, 19
 // spilled; C3s 4 % faster, C3 2 % slower: profiles/r03q_args_waves/), for A/B.  1053696 = 5120 |
 // OPT_HDRLDS: the cell headers staged through LDS (profiles/r03s_hdr_lds/).  2102272 = 5120 |
-// OPT_LEAN (24 KB of LDS per workgroup), 2102528 the same at 5 waves/SIMD.  All variants give
-// identical results.
+// OPT_LEAN (24 KB of LDS per workgroup), 2102528 the same at 5 waves/SIMD; 8393728 / 8393984 =
+// 5120 / 5376 | OPT_DEALALL.  All variants give identical results.
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984)
 
 bool render_variant_available(int v) {
 #define IRT_CASE(N) if (v == N) return true;
