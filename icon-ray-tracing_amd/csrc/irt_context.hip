@@ -113,6 +113,7 @@ struct irt_context {
   long long totalLaunches = 0;
   size_t bytes = 0;
   int variant = kDefaultVariant;  // render-kernel variant (irt_render.hip OPT_* bits)
+  bool variantFixed = false;      // IRT_RENDER_VARIANT chose it (no footprint-based choice)
   // Measured-cost workgroup scheduling of the one-kernel raygen: every launch records its
   // workgroups' durations (d_schedCost); now and then a launch copies them back
   // (h_schedCost, pinned, in the stats ring), and once that copy has landed the host
@@ -665,7 +666,10 @@ int irt_create_begin(size_t numCells, int device, irt_context **out) {
   c->device = device;
   if (const char *v = getenv("IRT_RENDER_VARIANT")) {
     const int var = atoi(v);
-    if (render_variant_available(var)) c->variant = var;
+    if (render_variant_available(var)) {
+      c->variant = var;
+      c->variantFixed = true;
+    }
   }
   auto fail = [&](int code) {
     free_all(c);
@@ -905,6 +909,13 @@ int irt_create_end(irt_context *c) {
   c->bytes += std::max<size_t>(numCells, 1) * 3 * sizeof(float4);  // d_trig, kept
   c->building = false;
   c->info.deviceBytes = c->bytes;
+  // Occupancy by footprint (profiles/r03u_waves/): the default's 5 waves/SIMD hide the
+  // gather chains' latency where most lines hit in L2 / Infinity Cache (C3: 2.4 GiB, -1.8 %
+  // against 4 waves); a scene past kWavesBigScene misses so often that the fifth wave only
+  // adds queueing in the memory system, and the 4-wave build is faster (C5: 39 GiB, +1.9 %).
+  constexpr size_t kWavesBigScene = size_t(16) << 30;
+  if (!c->variantFixed && c->variant == kDefaultVariant && c->bytes > kWavesBigScene)
+    c->variant = (kDefaultVariant & ~0xF00) | 0x400;
   return IRT_OK;
 }
 
@@ -1476,6 +1487,8 @@ extern "C" int irt_debug_context_array(const irt_context *c, int which, void *ds
   }
   return IRT_OK;
 }
+
+extern "C" int irt_debug_get_variant(const irt_context *c) { return c ? c->variant : -1; }
 
 extern "C" int irt_debug_set_variant(irt_context *c, int variant) {
   if (!c || !render_variant_available(variant)) {

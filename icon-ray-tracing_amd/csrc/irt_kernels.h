@@ -92,7 +92,9 @@ constexpr int kCnt = 8;
 
 // Render-kernel variants: the bit set of irt_render.hip's OPT_* flags (bits 8-11: minimum
 // waves per SIMD).  All give identical results.
-constexpr int kDefaultVariant = 5120;  // one kernel per frame, 4 waves/SIMD: fastest measured (profiles/)
+// one kernel per frame, 5 waves/SIMD (96 VGPRs; spills only in the prologue/epilogue): against
+// 4 waves C3 -1.8 %, C4 -4.9 %, comb TF -9 %, C5 +1.9 % (profiles/r03u_waves/)
+constexpr int kDefaultVariant = 5376;
 bool render_variant_available(int variant);
 void launch_render(const RenderArgs &A, int numBlocks, hipStream_t s, int variant);
 void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *found, float *value,

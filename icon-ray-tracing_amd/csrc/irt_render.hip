@@ -1283,8 +1283,20 @@ template <int OPT>
 __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
                                                   const float *s_th, int4 *s_dda, float4 *s_entry,
                                                   float4 *s_acc, CoopWave &W, ScanWave *SW, const uint2 *jmp,
-                                                  int tid, int accumID,
-                                                  float4 *sampleOut) {
+                                                  int tid, int accumID, uint32_t blk) {
+  // At 5+ waves/SIMD the pixel's output addresses are recomputed where they are used (from the
+  // workgroup's uniform block index), not held in VGPRs through the rounds: a progressive
+  // batch's sample slot (k_accumulate reads it) and the frame index.  (At 4 waves there is
+  // room for them, and recomputing costs 1 %: profiles/r03u_waves/.)
+  constexpr bool kRecompute = ((OPT >> 8) & 15) >= 5;
+  const bool toSample = A.numSamples > 1;
+  float4 *const slot0 = kRecompute || !toSample
+                            ? nullptr
+                            : A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + (size_t)blk * 256u + (size_t)tid;
+  auto sample_slot = [&]() {
+    if constexpr (!kRecompute) return slot0;
+    return A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + (size_t)opaque_u((int)blk) * 256u + (size_t)tid;
+  };
   enum : int { kRange, kLeaf, kWait, kDone, kGrid, kGridNext };
   constexpr bool grid = (OPT & OPT_GRID) != 0;
   const bool ae = A.raygen == 1;
@@ -1311,7 +1323,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       t1box = t1;
       // the accum pixel the lerp reads at the end, fetched now straight into LDS (no VGPRs
       // held through the Woodcock rounds; its latency hides behind them)
-      if (!sampleOut && (OPT & OPT_LEAN) == 0)
+      if (!toSample && (OPT & OPT_LEAN) == 0)
         __builtin_amdgcn_global_load_lds((const void *)(A.accum + px.outIdx),
                                          (__attribute__((address_space(3))) void *)(s_acc + (tid & ~63)),
                                          16, 0, 0);
@@ -1335,8 +1347,8 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
           }
         }
       }
-    } else if (sampleOut) {
-      *sampleOut = make_float4(0.f, 0.f, 0.f, kNoSample);  // deviceCode.cu:294-295
+    } else if (toSample) {
+      *sample_slot() = make_float4(0.f, 0.f, 0.f, kNoSample);  // deviceCode.cu:294-295
     }
   }
   // GRID_ACCEL_MODE (deviceCode.cu:326-328): dda3 (DDA.h:35-136) over the 256^3 grid as
@@ -1583,14 +1595,15 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   }
   if (!inBox) return;
   const float4 c = hit ? lds_ld16(&s_entry[tid]) : make_float4(0.f, 0.f, 0.f, 0.f);
-  if (sampleOut) {
-    *sampleOut = c;
+  if (toSample) {
+    *sample_slot() = c;
   } else {
+    const size_t outIdx = kRecompute ? pixel_of(A, (uint32_t)opaque_u((int)blk), tid).outIdx : px.outIdx;
     if constexpr ((OPT & OPT_LEAN) != 0) {
-      write_pixel(A, px.outIdx, c.x, c.y, c.z, c.w, s_th);
+      write_pixel(A, outIdx, c.x, c.y, c.z, c.w, s_th);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
-      write_pixel(A, px.outIdx, c.x, c.y, c.z, c.w, s_th, lds_ld16(&s_acc[tid]));
+      write_pixel(A, outIdx, c.x, c.y, c.z, c.w, s_th, lds_ld16(&s_acc[tid]));
     }
   }
 }
@@ -1662,7 +1675,7 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   if constexpr (Tracer<OPT>::kCoop) {
     render_pixel_coop<OPT>(A, T, px, th_p, s_dda, s_entry, s_acc, s_coop[tid >> 6],
                            &s_scan[Tracer<OPT>::kWaveScan ? tid >> 6 : 0], s_jmp, tid,
-                           A.accumID + (int)blockIdx.y, slot);
+                           A.accumID + (int)blockIdx.y, blk);
     T.flush_coop();
   }
   else if (px.active)
@@ -1819,12 +1832,13 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 // Variant bits: irt_render.hip OPT_* (bits 8-11: minimum waves per SIMD asked of the
 // register allocator).  OPT_MONO (4096) is kept in the numbering of round 1 (the one-kernel
 // raygen; the setup -> march -> continuation pipeline it distinguished from was removed).
-// 70656 = 5120 | OPT_SERIAL: the one-lane-per-ray Woodcock loop, for A/B against the
-// cooperative default.  5376: the default with a 5-waves-per-SIMD floor (96 VGPRs, 19
-// spilled; C3s 4 % faster, C3 2 % slower: profiles/r03q_args_waves/), for A/B.  1053696 = 5120 |
-// OPT_HDRLDS: the cell headers staged through LDS (profiles/r03s_hdr_lds/).  2102272 = 5120 |
-// OPT_LEAN (24 KB of LDS per workgroup), 2102528 the same at 5 waves/SIMD; 8393728 / 8393984 =
-// 5120 / 5376 | OPT_DEALALL.  All variants give identical results.
+// 5376 (the default since r03u): 5 waves/SIMD, 96 VGPRs, the few spills in the prologue and
+// epilogue only; 5120: the same kernel at 4 waves/SIMD (117 VGPRs), for A/B.  70656 = 5120 |
+// OPT_SERIAL: the one-lane-per-ray Woodcock loop, for A/B against the cooperative loop.
+// 1053696 = 5120 | OPT_HDRLDS: the cell headers staged through LDS (profiles/r03s_variants/).
+// 2102272 = 5120 | OPT_LEAN (24 KB of LDS per workgroup), 2102528 the same at 5 waves/SIMD;
+// 8393728 / 8393984 = 5120 / 5376 | OPT_DEALALL (profiles/r03t_regs/).  All variants give
+// identical results.
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
@@ -1847,6 +1861,7 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
   // ray; profiles/r02b_investigation/).
   constexpr int D = kDefaultVariant & ~OPT_MONO;
   constexpr int DW = (D & ~0xF00) | OPT_WEDGE | (K & OPT_SERIAL);
+  constexpr int DG = (D & ~0xF00) | 0x400;  // the grid-accel raygen: 4 waves/SIMD as measured in round 2
   const dim3 grid(numBlocks, A.numSamples);
   const bool g = A.accelMode == IRT_ACCEL_GRID;
   if (A.sampler != IRT_MODE_USER_GEOM && g)  // CUBQL or TRIANGLES: the unstructured locator
@@ -1854,7 +1869,7 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
   else if (A.sampler != IRT_MODE_USER_GEOM)
     hipLaunchKernelGGL(k_render<DW>, grid, dim3(256), 0, s, A);
   else if (g)
-    hipLaunchKernelGGL(k_render<D | OPT_GRID | (K & OPT_SERIAL)>, grid, dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_render<DG | OPT_GRID | (K & OPT_SERIAL)>, grid, dim3(256), 0, s, A);
   else
     hipLaunchKernelGGL(k_render<K>, grid, dim3(256), 0, s, A);
   // progressive batch: the lerp chain over the frames' samples

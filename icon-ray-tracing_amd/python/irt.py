@@ -33,10 +33,12 @@ MODE_USER_GEOM = 0     # Volume::mode (Params.h:29-31): sample() on the cells (d
 MODE_TRIANGLES = 1     # closest bottom triangle toward the centre (deviceCode.cu:61-76)
 MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
 # compiled variants of the raygen (irt_render.hip OPT_* bits): 4096 no waves-per-SIMD
-# floor, 5120 the default (4 waves/SIMD), 36864 with per-wave statistics, 70656 the
-# one-lane-per-ray Woodcock loop instead of the wave-cooperative one, 136192 the cooperative
-# loop with per-lane candidate scans (no wave-wide scan), 529408 with per-region shader-clock
-# timing (profiles/probe.py); all bit-identical
+# floor, 5376 the default (5 waves/SIMD), 5120 at 4 waves/SIMD, 36864 with per-wave
+# statistics, 70656 the one-lane-per-ray Woodcock loop instead of the wave-cooperative one,
+# 136192 the cooperative loop with per-lane candidate scans (no wave-wide scan), 529408 with
+# per-region shader-clock timing (profiles/probe.py), 1053696 LDS-staged cell headers,
+# 2102272 / 2102528 less LDS per workgroup, 8393728 / 8393984 every candidate dealt out;
+# all bit-identical
 BIN_VARIANTS = (4096, 5120, 5376, 36864, 70656, 136192, 529408, 1053696, 2102272, 2102528, 8393728, 8393984)
 
 

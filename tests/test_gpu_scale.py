@@ -81,6 +81,21 @@ def scene(request):
     ctx.close()
 
 
+def test_occupancy_follows_the_scene_footprint(scene):
+    """The default raygen runs 5 waves/SIMD; a scene past 16 GiB of HBM (C5: 39 GiB) gets the
+    4-wave build of the same kernel (irt_context.hip, profiles/r03u_waves/).  Either way the
+    frame is the one test_whole_frame_matches_oracle checks."""
+    import ctypes as C
+    L = irt.lib()
+    L.irt_debug_get_variant.argtypes = [C.c_void_p]
+    v, d = L.irt_debug_get_variant(scene["ctx"]._h), L.irt_debug_default_variant()
+    big = scene["ctx"].info.deviceBytes > 16 << 30
+    if os.environ.get("IRT_RENDER_VARIANT"):
+        return
+    assert v == ((d & ~0xF00) | 0x400 if big else d), (scene["name"], v, d)
+    assert big == (scene["name"] == "c5")
+
+
 def test_whole_frame_matches_oracle(scene):
     """Every pixel of the BASELINE-size frame, and its sampleVolume counts, against the
     oracle's direction-voxel locator (fast=2) on all host cores."""
