@@ -351,11 +351,17 @@ def test_all_render_variants_identical():
         st = ctx.stats()
         out = (fb.cpu().numpy().copy(), bits(acc.cpu().numpy()), st.locateCalls, st.samplesFound,
                st.candidatesTested)
+        # and a progressive batch (per-frame sample buffer + k_accumulate) on top of it
+        ctx.render_accumulate(setup.lp, W, W, 3, fb.data_ptr(), acc.data_ptr())
+        st = ctx.stats()
+        out += (fb.cpu().numpy().copy(), bits(acc.cpu().numpy()), st.locateCalls, st.samplesFound)
         if ref is None:
             ref = out
             continue
         assert np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1]), v
-        assert out[2:] == ref[2:], v
+        assert out[2:5] == ref[2:5], v
+        assert np.array_equal(out[5], ref[5]) and np.array_equal(out[6], ref[6]), v
+        assert out[7:] == ref[7:], v
     ctx.close()
 
 
