@@ -522,7 +522,9 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     if (rc) return rc;
   }
   const size_t lanes = (size_t)numTiles * 4096;
-  const size_t numWG = (size_t)numTiles * 16 * (size_t)numFrames;
+  // workgroups of this launch: 16 per 64x64 tile, x4 for the one-wave-workgroup variants
+  // (irt_render.hip OPT_WAVEWG, bit 4194304), per frame
+  const size_t numWG = (size_t)numTiles * 16 * ((c->variant & 4194304) ? 4 : 1) * (size_t)numFrames;
   // Per-workgroup counts need kSlots x 32 B of pinned host memory per workgroup and frame
   // (1 KiB): a launch past kWgCountsMax workgroups (a large progressive batch) counts through
   // the device-atomic block instead, for that launch only.

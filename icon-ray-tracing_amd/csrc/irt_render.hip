@@ -45,6 +45,8 @@ enum : int {
                         // cooperatively, then read from LDS (Tracer::stage_headers)
   OPT_DEALALL = 8388608,  // (A/B) the wave-wide scan deals out every candidate, the lists' first
                           // ones included (Tracer::locate_wave)
+  OPT_WAVEWG = 4194304,   // (A/B, with OPT_LEAN) one wave per workgroup: a wave's LDS is freed as
+                          // soon as it finishes, instead of when its workgroup's last wave does
   OPT_LEAN = 2097152,   // (A/B) less LDS per workgroup (31.0 -> 24 KB), so that more workgroups
                         // fit a CU while finished waves wait for their workgroup's last one:
                         // the sRGB thresholds and the sphere hash read from global memory
@@ -1289,13 +1291,16 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   // batch's sample slot (k_accumulate reads it) and the frame index.  (At 4 waves there is
   // room for them, and recomputing costs 1 %: profiles/r03u_waves/.)
   constexpr bool kRecompute = ((OPT >> 8) & 15) >= 5;
+  // the pixel's thread index within its 256-pixel block (OPT_WAVEWG: four one-wave workgroups
+  // per block; tid is the LDS index within this workgroup)
+  const int ptid = (OPT & OPT_WAVEWG) != 0 ? (int)((blockIdx.x & 3u) * 64u) + tid : tid;
   const bool toSample = A.numSamples > 1;
   float4 *const slot0 = kRecompute || !toSample
                             ? nullptr
-                            : A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + (size_t)blk * 256u + (size_t)tid;
+                            : A.sampleBuf + (size_t)blockIdx.y * gridDim.x * blockDim.x + (size_t)blk * 256u + (size_t)ptid;
   auto sample_slot = [&]() {
     if constexpr (!kRecompute) return slot0;
-    return A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + (size_t)opaque_u((int)blk) * 256u + (size_t)tid;
+    return A.sampleBuf + (size_t)blockIdx.y * gridDim.x * blockDim.x + (size_t)opaque_u((int)blk) * 256u + (size_t)ptid;
   };
   enum : int { kRange, kLeaf, kWait, kDone, kGrid, kGridNext };
   constexpr bool grid = (OPT & OPT_GRID) != 0;
@@ -1598,7 +1603,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   if (toSample) {
     *sample_slot() = c;
   } else {
-    const size_t outIdx = kRecompute ? pixel_of(A, (uint32_t)opaque_u((int)blk), tid).outIdx : px.outIdx;
+    const size_t outIdx = kRecompute ? pixel_of(A, (uint32_t)opaque_u((int)blk), ptid).outIdx : px.outIdx;
     if constexpr ((OPT & OPT_LEAN) != 0) {
       write_pixel(A, outIdx, c.x, c.y, c.z, c.w, s_th);
     } else {
@@ -1610,17 +1615,22 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
 
 // The raygen over the frame grid: one lane per pixel (see pixel_of).
 template <int OPT>
-__global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1) k_render(RenderArgs A) {
+__global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1)
+    k_render(RenderArgs A) {
   constexpr bool lean = (OPT & OPT_LEAN) != 0;
+  constexpr bool wavewg = (OPT & OPT_WAVEWG) != 0;
+  static_assert(!wavewg || (lean && Tracer<OPT>::kCoop), "one-wave workgroups: lean, cooperative kernels");
+  constexpr int kT = wavewg ? 64 : 256;   // threads per workgroup
+  constexpr int kW = kT / 64;            // waves per workgroup
   __shared__ float s_th[lean ? 1 : 256];
   __shared__ uint32_t s_cnt[kCnt];
   __shared__ LogfTab s_logf[16];
   __shared__ uint32_t s_sph[lean ? 1 : kSphBitWords];
-  __shared__ int4 s_dda[256];       // sdda state needed only after a range's first leaf
-  __shared__ float4 s_entry[256];
-  __shared__ CoopWave s_coop[4];    // the cooperative Woodcock loop (kCoop kernels)
-  __shared__ ScanWave s_scan[Tracer<OPT>::kWaveScan ? 4 : 1];  // its wave-wide candidate scan
-  __shared__ HdrStage s_hdrs[(OPT & OPT_HDRLDS) ? 4 : 1];       // OPT_HDRLDS: staged header lines
+  __shared__ int4 s_dda[wavewg ? 1 : 256];  // sdda state needed only after a range's first leaf
+  __shared__ float4 s_entry[kT];
+  __shared__ CoopWave s_coop[kW];   // the cooperative Woodcock loop (kCoop kernels)
+  __shared__ ScanWave s_scan[Tracer<OPT>::kWaveScan ? kW : 1];  // its wave-wide candidate scan
+  __shared__ HdrStage s_hdrs[(OPT & OPT_HDRLDS) ? kW : 1];       // OPT_HDRLDS: staged header lines
   __shared__ float4 s_acc[lean ? 1 : 256];  // kCoop: the accum pixels, prefetched
   __shared__ uint2 s_jmp[kLcgJumps];  // lcg_jump's {mul, add} (kLcgJumpTab)
   const int tid = threadIdx.x;
@@ -1635,11 +1645,18 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
 #pragma unroll
     for (int k = 0; k < kSphBitWords / 256; ++k) sph[k] = A.sphBits[tid + 256 * k];
   }
-  uint2 jmpv = make_uint2(0u, 0u);
-  if constexpr (Tracer<OPT>::kCoop)
-    if (tid < kLcgJumps) jmpv = make_uint2(kLcgJumpTab.ma[tid][0], kLcgJumpTab.ma[tid][1]);
-  if constexpr (Tracer<OPT>::kCoop)
-    if (tid < kLcgJumps) *reinterpret_cast<uvec2 *>(&s_jmp[tid]) = __builtin_bit_cast(uvec2, jmpv);
+  uint2 jmpv[(kLcgJumps + kT - 1) / kT];
+#pragma unroll
+  for (int k = 0; k < (kLcgJumps + kT - 1) / kT; ++k) {
+    const int j = tid + kT * k;
+    jmpv[k] = make_uint2(0u, 0u);
+    if (Tracer<OPT>::kCoop && j < kLcgJumps) jmpv[k] = make_uint2(kLcgJumpTab.ma[j][0], kLcgJumpTab.ma[j][1]);
+  }
+#pragma unroll
+  for (int k = 0; k < (kLcgJumps + kT - 1) / kT; ++k) {
+    const int j = tid + kT * k;
+    if (Tracer<OPT>::kCoop && j < kLcgJumps) *reinterpret_cast<uvec2 *>(&s_jmp[j]) = __builtin_bit_cast(uvec2, jmpv[k]);
+  }
   if constexpr (!lean) s_th[tid] = th;
   if (tid < 16) s_logf[tid] = lt;
   if (!lean && A.numSph) {
@@ -1660,6 +1677,9 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   T.s_gbits = s_gbits;
   const float *th_p = lean ? A.srgbTh : s_th;
   T.s_hdr = &s_hdrs[(OPT & OPT_HDRLDS) ? tid >> 6 : 0];
+  // OPT_WAVEWG: four one-wave workgroups per 256-pixel block, the block's wave blockIdx.x & 3
+  const uint32_t wg = wavewg ? blockIdx.x >> 2 : blockIdx.x;
+  const int ptid = wavewg ? (int)((blockIdx.x & 3u) * 64u) + tid : tid;
   if constexpr ((OPT & OPT_TIMING) != 0) {
     T.tLast = tStart;
     T.tmark(0);  // prologue
@@ -1668,10 +1688,10 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
   // grid.y = frame k of a progressive batch (accumID + k), whose colour goes to the sample
   // buffer for k_accumulate; a single frame writes accum/fb directly.  With measured-cost
   // scheduling (irt_context.hip) workgroup b renders block order[b].
-  const uint32_t blk = A.schedOrder ? A.schedOrder[blockIdx.x] : blockIdx.x;
-  const uint32_t gid = blk * 256u + (uint32_t)tid;
-  const Pixel px = pixel_of(A, blk, tid);
-  float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * 256u + gid : nullptr;
+  const uint32_t blk = A.schedOrder ? A.schedOrder[wg] : wg;
+  const uint32_t gid = blk * 256u + (uint32_t)ptid;
+  const Pixel px = pixel_of(A, blk, ptid);
+  float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * blockDim.x + gid : nullptr;
   if constexpr (Tracer<OPT>::kCoop) {
     render_pixel_coop<OPT>(A, T, px, th_p, s_dda, s_entry, s_acc, s_coop[tid >> 6],
                            &s_scan[Tracer<OPT>::kWaveScan ? tid >> 6 : 0], s_jmp, tid,
@@ -1730,7 +1750,7 @@ __global__ void __launch_bounds__(256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1
     prev = (uint32_t)__shfl((int)prev, 0, 64);
     if (prev == (blockDim.x >> 6) - 1u) {
       if (A.counters) flush_counters(A, s_cnt, lane);
-      if (A.schedCost && lane == 0) {  // this workgroup's duration, for the next launches' order
+      if (A.schedCost && lane == 0 && (!wavewg || (blockIdx.x & 3u) == 0u)) {  // this workgroup's duration, for the next launches' order
         const uint64_t dt = wall_clock64() - c0;
         A.schedCost[blk] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
       }
@@ -1837,12 +1857,12 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 // OPT_SERIAL: the one-lane-per-ray Woodcock loop, for A/B against the cooperative loop.
 // 1053696 = 5120 | OPT_HDRLDS: the cell headers staged through LDS (profiles/r03s_variants/).
 // 2102272 = 5120 | OPT_LEAN (24 KB of LDS per workgroup), 2102528 the same at 5 waves/SIMD;
-// 8393728 / 8393984 = 5120 / 5376 | OPT_DEALALL (profiles/r03t_regs/).  All variants give
-// identical results.
+// 8393728 / 8393984 = 5120 / 5376 | OPT_DEALALL (profiles/r03t_regs/); 6296576 / 6296832 =
+// 2102272 / 2102528 | OPT_WAVEWG (one-wave workgroups).  All variants give identical results.
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832)
 
 bool render_variant_available(int v) {
 #define IRT_CASE(N) if (v == N) return true;
@@ -1870,6 +1890,8 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
     hipLaunchKernelGGL(k_render<DW>, grid, dim3(256), 0, s, A);
   else if (g)
     hipLaunchKernelGGL(k_render<DG | OPT_GRID | (K & OPT_SERIAL)>, grid, dim3(256), 0, s, A);
+  else if ((K & OPT_WAVEWG) != 0)  // four one-wave workgroups per 256-pixel block
+    hipLaunchKernelGGL(k_render<K>, dim3(numBlocks * 4, A.numSamples), dim3(64), 0, s, A);
   else
     hipLaunchKernelGGL(k_render<K>, grid, dim3(256), 0, s, A);
   // progressive batch: the lerp chain over the frames' samples

@@ -37,9 +37,11 @@ MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
 # statistics, 70656 the one-lane-per-ray Woodcock loop instead of the wave-cooperative one,
 # 136192 the cooperative loop with per-lane candidate scans (no wave-wide scan), 529408 with
 # per-region shader-clock timing (profiles/probe.py), 1053696 LDS-staged cell headers,
-# 2102272 / 2102528 less LDS per workgroup, 8393728 / 8393984 every candidate dealt out;
+# 2102272 / 2102528 less LDS per workgroup, 8393728 / 8393984 every candidate dealt out,
+# 6296576 / 6296832 one-wave workgroups;
 # all bit-identical
-BIN_VARIANTS = (4096, 5120, 5376, 36864, 70656, 136192, 529408, 1053696, 2102272, 2102528, 8393728, 8393984)
+BIN_VARIANTS = (4096, 5120, 5376, 36864, 70656, 136192, 529408, 1053696, 2102272, 2102528, 8393728, 8393984,
+                6296576, 6296832)
 
 
 class IrtError(RuntimeError):
