@@ -254,10 +254,11 @@ def main():
     info = ctx.info
     setup = irt.setup_frame(None, W, H, camera=FRAMING, info=info)
     ctx.set_transfunc(make_lut(tf, setup.lut), setup.value_range)
-    # HIP events around every k-th launch (the roofline's kernel duration): k = 8 keeps the
-    # event packets' cost out of the step (every launch timed: +8 us per C3 step); a run of
-    # fewer steps still holds a timed launch
-    ctx.set_timing_interval(max(1, min(8, args.steps)))
+    # HIP events around every k-th launch of the timed region (the roofline's kernel
+    # duration): each timed launch adds ~4.7 us of event packets to its step (every launch
+    # timed: +8 us per C3 step), so k = steps/4 (at most 32; four timed launches per run, one
+    # at least when steps < 4) keeps them to ~1 % of the region
+    ctx.set_timing_interval(max(1, min(32, args.steps // 4)))
     import resource
     log(f"[rank {rank}] context: {info.numCells} records, {info.deviceBytes / 2**30:.2f} GiB HBM, "
         f"locator G={info.locatorFaceRes} entries={info.locatorEntries} ({time.time() - t0:.1f} s, "
