@@ -69,7 +69,7 @@ def _worker(rank, world, port, W, H, out_path, deal):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,deal", [(2, "dealt"), (2, "mod")])
+@pytest.mark.parametrize("world,deal", [(2, "dealt"), (2, "mod"), (4, "dealt")])
 def test_two_rank_gloo_frame_split(tmp_path, world, deal):
     import torch.multiprocessing as mp
 
