@@ -876,7 +876,8 @@ int irt_create_end(irt_context *c) {
   for (int i = 0; i < irt_context::kSlots; ++i) {
     IRT_HIP(hipEventCreate(&c->ev0[i]));
     IRT_HIP(hipEventCreate(&c->ev1[i]));
-    IRT_HIP(hipEventCreate(&c->evDone[i]));
+    // no timestamps: this event only orders the slot's reuse (a timing event's marker costs more)
+    IRT_HIP(hipEventCreateWithFlags(&c->evDone[i], hipEventDisableTiming));
   }
   memset(c->h_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long));
   if (const char *e = getenv("IRT_COUNTERS")) {
