@@ -1307,13 +1307,21 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   // the pixel's thread index within its 256-pixel block (OPT_WAVEWG: four one-wave workgroups
   // per block; tid is the LDS index within this workgroup)
   const int ptid = (OPT & OPT_WAVEWG) != 0 ? (int)((blockIdx.x & 3u) * 64u) + tid : tid;
+  // ... and so is the thread index itself after the rounds: the wave's base (uniform, an SGPR)
+  // plus the lane id, instead of tid and the pixel's in-block coordinates held in scratch
+  // across the rounds (24 B per lane of spill stores and reloads at 5 waves)
+  const int wbase = __builtin_amdgcn_readfirstlane(tid) & ~63;
+  auto tid_late = [&]() { return kRecompute ? (opaque_u(wbase) | (int)__lane_id()) : tid; };
+  auto ptid_late = [&]() {
+    return (OPT & OPT_WAVEWG) != 0 ? (int)((blockIdx.x & 3u) * 64u) + tid_late() : tid_late();
+  };
   const bool toSample = A.numSamples > 1;
   float4 *const slot0 = kRecompute || !toSample
                             ? nullptr
                             : A.sampleBuf + (size_t)blockIdx.y * gridDim.x * blockDim.x + (size_t)blk * 256u + (size_t)ptid;
   auto sample_slot = [&]() {
     if constexpr (!kRecompute) return slot0;
-    return A.sampleBuf + (size_t)blockIdx.y * gridDim.x * blockDim.x + (size_t)opaque_u((int)blk) * 256u + (size_t)ptid;
+    return A.sampleBuf + (size_t)blockIdx.y * gridDim.x * blockDim.x + (size_t)opaque_u((int)blk) * 256u + (size_t)ptid_late();
   };
   enum : int { kRange, kLeaf, kWait, kDone, kGrid, kGridNext };
   constexpr bool grid = (OPT & OPT_GRID) != 0;
@@ -1424,16 +1432,16 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       const float e2 = upper - sceneEPS();
       float r2, la2, lo2;
       to_spherical(A.org.x + dx * e2, A.org.y + dy * e2, A.org.z + dz * e2, r2, la2, lo2);
-      const float4 en = lds_ld16(&s_entry[tid]);
+      const float4 en = lds_ld16(&s_entry[tid_late()]);
       const float r1 = en.x, la1 = en.y, lo1 = en.z;
       const int sx = r1 < r2 ? 1 : -1, sy = la1 < la2 ? 1 : -1, sz = lo1 < lo2 ? 1 : -1;
       dd.x = (sx > 0 ? 1 : 0) | (sy > 0 ? 2 : 0) | (sz > 0 ? 4 : 0);
       dd.y = (int)((uint32_t)project_axis_inv(r2, A.sbLo.x, A.invSb[0], A.dims.x) + (uint32_t)sx);
       dd.z = (int)((uint32_t)project_axis_inv(la2, A.sbLo.y, A.invSb[1], A.dims.y) + (uint32_t)sy);
       dd.w = (int)((uint32_t)project_axis_inv(lo2, A.sbLo.z, A.invSb[2], A.dims.z) + (uint32_t)sz);
-      lds_st16(&s_entry[tid], __builtin_bit_cast(float4, dd));  // the entry point is not needed again
+      lds_st16(&s_entry[tid_late()], __builtin_bit_cast(float4, dd));  // the entry point is not needed again
     } else {
-      dd = __builtin_bit_cast(int4, lds_ld16(&s_entry[tid]));
+      dd = __builtin_bit_cast(int4, lds_ld16(&s_entry[tid_late()]));
     }
     const float t_closest = fminf(fminf(tnx, tny), tnz);
     bool stop = false;
@@ -1531,7 +1539,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
           cx = project_axis_inv(r1, A.sbLo.x, A.invSb[0], A.dims.x);
           cy = project_axis_inv(la1, A.sbLo.y, A.invSb[1], A.dims.y);
           cz = project_axis_inv(lo1, A.sbLo.z, A.invSb[2], A.dims.z);
-          if (!lastRange) lds_st16(&s_entry[tid], make_float4(r1, la1, lo1, 0.f));
+          if (!lastRange) lds_st16(&s_entry[tid_late()], make_float4(r1, la1, lo1, 0.f));
         }
         t = lower;
         iter = 0;
@@ -1592,7 +1600,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     if (A.probeExit == 5) break;  // measurement only: the first woodcockFunc of every lane
     if (grid && req && phase == kWait && !ae) {
       if (tw > t && tw < tt1) {  // render_grid's hit test (deviceCode.cu:316)
-        lds_st16(&s_entry[tid], make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
+        lds_st16(&s_entry[tid_late()], make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
                                    s.z * A.amb.z * A.ambRad, s.w > 0.f ? 1.f : 0.f));
         hit = true;
         phase = kDone;
@@ -1602,7 +1610,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     } else if (req) {
       if (!zeroLen && (ae || (tw > t && tw < tt1))) {
         // the colour waits in the lane's s_entry slot (free once it is finished)
-        lds_st16(&s_entry[tid], make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
+        lds_st16(&s_entry[tid_late()], make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
                                    s.z * A.amb.z * A.ambRad, s.w > 0.f ? 1.f : 0.f));
         hit = true;
         phase = kDone;
@@ -1612,16 +1620,17 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     }
   }
   if (!inBox) return;
-  const float4 c = hit ? lds_ld16(&s_entry[tid]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const int tl = tid_late();
+  const float4 c = hit ? lds_ld16(&s_entry[tl]) : make_float4(0.f, 0.f, 0.f, 0.f);
   if (toSample) {
     *sample_slot() = c;
   } else {
-    const size_t outIdx = kRecompute ? pixel_of(A, (uint32_t)opaque_u((int)blk), ptid).outIdx : px.outIdx;
+    const size_t outIdx = kRecompute ? pixel_of(A, (uint32_t)opaque_u((int)blk), ptid_late()).outIdx : px.outIdx;
     if constexpr ((OPT & OPT_LEAN) != 0) {
       write_pixel(A, outIdx, c.x, c.y, c.z, c.w, s_th);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
-      write_pixel<kRecompute>(A, outIdx, c.x, c.y, c.z, c.w, s_th, lds_ld16(&s_acc[tid]));
+      write_pixel<kRecompute>(A, outIdx, c.x, c.y, c.z, c.w, s_th, lds_ld16(&s_acc[tl]));
     }
   }
 }
@@ -1701,7 +1710,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
   // grid.y = frame k of a progressive batch (accumID + k), whose colour goes to the sample
   // buffer for k_accumulate; a single frame writes accum/fb directly.  With measured-cost
   // scheduling (irt_context.hip) workgroup b renders block order[b].
-  const uint32_t blk = A.schedOrder ? A.schedOrder[wg] : wg;
+  const uint32_t blk = __builtin_amdgcn_readfirstlane(A.schedOrder ? A.schedOrder[wg] : wg);  // uniform: an SGPR
   const uint32_t gid = blk * 256u + (uint32_t)ptid;
   const Pixel px = pixel_of(A, blk, ptid);
   float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * blockDim.x + gid : nullptr;
@@ -1750,7 +1759,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
     }
   }
   if (A.counters || A.schedCost) {
-    const int lane = tid & 63;
+    const int lane = (int)__lane_id();
     const unsigned long long m = __ballot(px.active);  // rays launched, once per wave
     if (A.counters && lane == 0 && m) atomicAdd(&s_cnt[0], (uint32_t)__popcll(m));
     // The last wave of the workgroup to get here writes the workgroup's counts and duration.
