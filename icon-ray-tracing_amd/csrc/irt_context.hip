@@ -113,7 +113,6 @@ struct irt_context {
   long long totalLaunches = 0;
   size_t bytes = 0;
   int variant = kDefaultVariant;  // render-kernel variant (irt_render.hip OPT_* bits)
-  bool variantFixed = false;      // IRT_RENDER_VARIANT chose it (no footprint-based choice)
   // Measured-cost workgroup scheduling of the one-kernel raygen: every launch records its
   // workgroups' durations (d_schedCost); now and then a launch copies them back
   // (h_schedCost, pinned, in the stats ring), and once that copy has landed the host
@@ -670,7 +669,6 @@ int irt_create_begin(size_t numCells, int device, irt_context **out) {
     const int var = atoi(v);
     if (render_variant_available(var)) {
       c->variant = var;
-      c->variantFixed = true;
     }
   }
   auto fail = [&](int code) {
@@ -912,13 +910,9 @@ int irt_create_end(irt_context *c) {
   c->bytes += std::max<size_t>(numCells, 1) * 3 * sizeof(float4);  // d_trig, kept
   c->building = false;
   c->info.deviceBytes = c->bytes;
-  // Occupancy by footprint (profiles/r03u_waves/): the default's 5 waves/SIMD hide the
-  // gather chains' latency where most lines hit in L2 / Infinity Cache (C3: 2.4 GiB, -1.8 %
-  // against 4 waves); a scene past kWavesBigScene misses so often that the fifth wave only
-  // adds queueing in the memory system, and the 4-wave build is faster (C5: 39 GiB, +1.9 %).
-  constexpr size_t kWavesBigScene = size_t(16) << 30;
-  if (!c->variantFixed && c->variant == kDefaultVariant && c->bytes > kWavesBigScene)
-    c->variant = (kDefaultVariant & ~0xF00) | 0x400;
+  // Every scene runs the default 5 waves/SIMD.  (Until the 5-wave kernel lost its scratch
+  // spills, scenes past 16 GiB ran the 4-wave build: C5 was 1.9 % faster at 4 waves then,
+  // and is 2.8 % slower at 4 waves now -- profiles/r03u_waves/, profiles/r03zg_waves/.)
   return IRT_OK;
 }
 

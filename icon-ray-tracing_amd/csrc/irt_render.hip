@@ -1010,9 +1010,9 @@ __device__ __forceinline__ void gen_ray(const RenderArgs &A, int accumID, int x,
 // accumulate lerp(vec4f(color,alpha), old, 1/(accumID+1)) and write linear_to_srgb +
 // make_rgba (deviceCode.cu:333-340).  Stream (nt = true): the pixel's lines are stored with
 // the streaming hint -- nothing in the launch reads them again, so they should not displace
-// locator lines in L2 (5-wave builds: C3 -1.6 %, C4 -4.4 % with the accum prefetch also nt;
-// the 4-wave build for scenes over 16 GiB: C5 +1.7 %, so it keeps plain stores;
-// profiles/r03za_nt/, profiles/r03zb_*).
+// locator lines in L2 (5-wave builds, the default: C3 -1.6 %, C4 -4.4 % with the accum
+// prefetch also nt; the 4-wave A/B build keeps plain stores; profiles/r03za_nt/,
+// profiles/r03zb_*).
 template <bool nt = false>
 __device__ __forceinline__ void write_pixel(const RenderArgs &A, size_t outIdx, float cr, float cg,
                                             float cb, float alpha, const float *s_th, float4 old) {
