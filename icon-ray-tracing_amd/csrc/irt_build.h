@@ -163,11 +163,12 @@ IRT_HD uint32_t record_meta(const float *height, int nl) {
 }
 
 // The height/value block (kBlk4 float4): block b = {height[8b..8b+3]}, {height[8b+4..8b+7]},
-// {value[8b-1..8b+2]}, {value[8b+3..8b+6]} (value[-1] := 0; value[31] never read).
+// {value[8b-1..8b+2]}, {value[8b+3..8b+6]}; value[31] sits in block 0's value[-1] slot
+// (blk_value_pos), which the block path never selects.
 IRT_HD void record_block(const float *height, const float *value, float *out64) {
   for (int j = 0; j < 64; ++j) out64[j] = 0.f;
   for (int j = 0; j < 32; ++j) out64[blk_height_pos(j)] = height[j];
-  for (int c = 0; c < 31; ++c) out64[blk_value_pos(c)] = value[c];
+  for (int c = 0; c < 32; ++c) out64[blk_value_pos(c)] = value[c];
 }
 
 // Two records belong to the same column (one locator run) when their corners are equal bit

@@ -404,10 +404,14 @@ constexpr int kFat4 = 4;
 constexpr int kFatStride4 = 4;
 // Per-record height/value blocks (the render record without its planes/keys), kBlk4
 // float4 = 256 B: block b (4 float4) = {height[8b..8b+3]}, {height[8b+4..8b+7]},
-// {value[8b-1..8b+2]}, {value[8b+3..8b+6]} (value[-1] := 0).
+// {value[8b-1..8b+2]}, {value[8b+3..8b+6]}.  Block 0's value[-1] slot holds value[31]: the
+// block path (rec_block_index) never selects that slot, and findHeight returns 31 only for
+// heights the radial test rules out in the raygen -- but the grid build (k_grid_build) and
+// the wedge scalars take getValue at a record's own heights, where unsorted heights can reach
+// index numLayers = 31 (getValue then reads value[31], as the reference does).
 constexpr int kBlk4 = 16;
 IRT_HD int blk_height_pos(int j) { return 16 * (j >> 3) + (j & 7); }
-IRT_HD int blk_value_pos(int c) { return 16 * ((c + 1) >> 3) + 8 + ((c + 1) & 7); }
+IRT_HD int blk_value_pos(int c) { return 16 * (((c + 1) >> 3) & 3) + 8 + ((c + 1) & 7); }
 
 // Total order on floats (sort keys, quantised heights): -0 before +0.
 IRT_HD uint32_t float_key(float v) {

@@ -523,7 +523,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   const size_t lanes = (size_t)numTiles * 4096;
   // workgroups of this launch: 16 per 64x64 tile, x4 for the one-wave-workgroup variants
   // (irt_render.hip OPT_WAVEWG, bit 4194304), per frame
-  const size_t numWG = (size_t)numTiles * 16 * ((c->variant & 4194304) ? 4 : 1) * (size_t)numFrames;
+  const size_t numWG = (size_t)numTiles * 16 * (size_t)render_wg_per_block(A, c->variant) * (size_t)numFrames;
   // Per-workgroup counts need kSlots x 32 B of pinned host memory per workgroup and frame
   // (1 KiB): a launch past kWgCountsMax workgroups (a large progressive batch) counts through
   // the device-atomic block instead, for that launch only.
@@ -1486,6 +1486,8 @@ extern "C" int irt_debug_context_array(const irt_context *c, int which, void *ds
 }
 
 extern "C" int irt_debug_get_variant(const irt_context *c) { return c ? c->variant : -1; }
+
+extern "C" int irt_debug_variants(int *out, int capacity) { return render_variants(out, capacity); }
 
 extern "C" int irt_debug_set_variant(irt_context *c, int variant) {
   if (!c || !render_variant_available(variant)) {

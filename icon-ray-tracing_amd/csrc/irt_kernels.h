@@ -96,6 +96,10 @@ constexpr int kCnt = 8;
 // 4 waves C3 -1.8 %, C4 -4.9 %, comb TF -9 %, C5 +1.9 % (profiles/r03u_waves/)
 constexpr int kDefaultVariant = 5376;
 bool render_variant_available(int variant);
+int render_variants(int *out, int cap);  // the compiled variants (count; the first cap into out)
+// workgroups per 256-pixel block the launch of `variant` uses for these arguments (4 only for
+// the one-wave-workgroup A/B variants on the user-geometry sphere path)
+int render_wg_per_block(const RenderArgs &A, int variant);
 void launch_render(const RenderArgs &A, int numBlocks, hipStream_t s, int variant);
 void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *found, float *value,
                          hipStream_t s, bool wave);

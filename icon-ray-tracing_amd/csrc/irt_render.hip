@@ -1884,13 +1884,37 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832)
+// The product build instantiates the default and the statistics variant (IRT_COUNTERS,
+// profiles/wave_stats.py); the A/B variants are built only by `make VARIANTS=all`
+// (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
+// tests/test_gpu_parity.py::test_all_render_variants_identical when present).
+#ifdef IRT_ALL_VARIANTS
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784)
+#else
+#define IRT_VARIANTS(X) X(5376) X(36864)
+#endif
+static_assert(kDefaultVariant == 5376, "the product build's variant list names the default");
+
+int render_variants(int *out, int cap) {
+  int n = 0;
+#define IRT_LIST(N) \
+  if (n < cap && out) out[n] = N; \
+  ++n;
+  IRT_VARIANTS(IRT_LIST)
+#undef IRT_LIST
+  return n;
+}
 
 bool render_variant_available(int v) {
 #define IRT_CASE(N) if (v == N) return true;
   IRT_VARIANTS(IRT_CASE)
 #undef IRT_CASE
   return false;
+}
+
+int render_wg_per_block(const RenderArgs &A, int variant) {
+  const bool waveWG = render_variant_available(variant) && (variant & OPT_WAVEWG) != 0;
+  return waveWG && A.sampler == IRT_MODE_USER_GEOM && A.accelMode != IRT_ACCEL_GRID ? 4 : 1;
 }
 
 template <int N>

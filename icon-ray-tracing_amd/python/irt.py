@@ -32,16 +32,24 @@ ACCEL_GRID = 1         # GRID_ACCEL_MODE (Params.h:34): dda3 over the 256^3 grid
 MODE_USER_GEOM = 0     # Volume::mode (Params.h:29-31): sample() on the cells (default)
 MODE_TRIANGLES = 1     # closest bottom triangle toward the centre (deviceCode.cu:61-76)
 MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
-# compiled variants of the raygen (irt_render.hip OPT_* bits): 4096 no waves-per-SIMD
-# floor, 5376 the default (5 waves/SIMD), 5120 at 4 waves/SIMD, 36864 with per-wave
-# statistics, 70656 the one-lane-per-ray Woodcock loop instead of the wave-cooperative one,
-# 136192 the cooperative loop with per-lane candidate scans (no wave-wide scan), 529408 with
-# per-region shader-clock timing (profiles/probe.py), 1053696 LDS-staged cell headers,
-# 2102272 / 2102528 less LDS per workgroup, 8393728 / 8393984 every candidate dealt out,
-# 6296576 / 6296832 one-wave workgroups;
-# all bit-identical
-BIN_VARIANTS = (4096, 5120, 5376, 36864, 70656, 136192, 529408, 1053696, 2102272, 2102528, 8393728, 8393984,
-                6296576, 6296832)
+# The raygen's render variants (irt_render.hip OPT_* bits), all bit-identical: the product
+# library compiles 5376 (the default, 5 waves/SIMD) and 36864 (per-wave statistics);
+# libicon_rt_hip_all.so (`make VARIANTS=all`) adds the A/B variants: 4096 no waves-per-SIMD
+# floor, 5120 at 4 waves/SIMD, 70656 the one-lane-per-ray Woodcock loop, 136192 per-lane
+# candidate scans, 529408 per-region shader-clock timing (profiles/probe.py), 1053696
+# LDS-staged cell headers, 2102272 / 2102528 less LDS per workgroup, 8393728 / 8393984
+# every candidate dealt out, 6296576 / 6296832 one-wave workgroups, 529664 the timing variant
+# at 5 waves/SIMD, 2102784 the lean-LDS build at 6 waves/SIMD.
+ALL_LIB_PATH = os.path.join(PKG_DIR, "libicon_rt_hip_all.so")
+
+
+def compiled_variants() -> tuple:
+    """The render variants the loaded library compiled (irt_debug_variants)."""
+    L = lib()
+    n = L.irt_debug_variants(None, 0)
+    out = (C.c_int * n)()
+    L.irt_debug_variants(out, n)
+    return tuple(out)
 
 
 class IrtError(RuntimeError):

@@ -2,9 +2,10 @@
 
 The reference is single-device; its CPU path already cuts a frame into 64x64 tiles pulled
 by a thread pool (common/for_each.h:70-85, common/thread_pool.h:146-161).  Here the same
-tiles are dealt to N ranks by estimated cost (irt_deal_tiles: tiles sorted by the cost of
-their rays through the shell, dealt serpentine, so every rank's share costs about the same;
-the plain round-robin t -> rank t mod N hands whole tile COLUMNS to each rank when N divides
+tiles are dealt to N ranks by estimated cost (irt_deal_tiles: a longest-processing-time
+greedy deal -- tiles sorted by the estimated cost of their rays through the shell, longest
+first, each given to the least-loaded rank, rank 0 preloaded with its unpack share -- so
+every rank's share costs about the same; the plain round-robin t -> rank t mod N hands whole tile COLUMNS to each rank when N divides
 the tile row, ~1.6x cost spread over a centred globe), every rank renders its tiles into a
 packed buffer (irt_render_tile_list), and rank 0 gathers the RGBA8 tiles over RCCL
 (torch.distributed, backend "nccl") and scatters them into the framebuffer

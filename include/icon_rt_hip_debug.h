@@ -89,9 +89,13 @@ int irt_debug_scene_array(const irt_debug_scene *s, int which, void *dst, size_t
 int irt_debug_set_variant(irt_context *ctx, int variant);
 /* The variant a new context launches (IRT_RENDER_VARIANT overrides it per context). */
 int irt_debug_default_variant(void);
-/* The variant this context launches: the default, or its 4-waves/SIMD build for a scene over
- * 16 GiB of HBM, or what IRT_RENDER_VARIANT / irt_debug_set_variant chose; -1 for NULL. */
+/* The variant this context launches: the default for every scene, unless
+ * IRT_RENDER_VARIANT or irt_debug_set_variant chose another; -1 for NULL. */
 int irt_debug_get_variant(const irt_context *ctx);
+/* The variants this build compiled: returns their count and writes the first `capacity` of
+ * them to `out` (may be NULL).  The product build has the default and the statistics
+ * variant; `make VARIANTS=all` (libicon_rt_hip_all.so) adds the A/B variants. */
+int irt_debug_variants(int *out, int capacity);
 /* The raw per-frame counters of the last render (waits for it): [0] launched [1] in box
  * [2] sampleVolume calls [3] found [4] candidates; with the statistics variant bit also
  * [5] Woodcock draws [6] sum over waves of the per-wave max draws [7] zero-length leaves

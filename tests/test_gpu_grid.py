@@ -42,6 +42,32 @@ def test_grid_build_matches_oracle():
     ctx.close()
 
 
+def test_grid_build_reads_value31_of_unsorted_records():
+    """getValue at a record's own heights (buildGrid_ICON, hostCode.cu:245-250) can reach
+    index numLayers = 31 when the heights are not sorted (findHeight, ICONGrid.h:117-145),
+    and then reads value[31].  Records of 31 layers whose low heights exceed height[31] --
+    the last record among them -- must give the oracle's value ranges and majorants."""
+    cells = irt.synth_grid(2, 2, 62)  # two 31-layer records per column
+    assert (cells["numLayers"] == 31).all()
+    rng = np.random.default_rng(31)
+    pick = np.concatenate([rng.choice(cells.size - 1, 40, replace=False), [cells.size - 1]])
+    for i in pick:
+        h = cells["height"][i].copy()
+        top = h[31]
+        h[:31] = h[:31] + (top - h[0]) * 1.5  # heights 0..30 above height[31]
+        cells["height"][i] = h
+        cells["value"][i, 31] = 1e3 + i  # outside every other value: a wrong slot shows
+    _, _, _, S = oracle_frame(cells, 8, 8, camera=FRAMING, accel_mode=1)
+    setup = irt.setup_frame(cells, 8, 8)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    vr, mo = ctx.grid()
+    assert (S.grid_vr[:, 1] >= 1e3).any()  # value[31] does reach the grid
+    assert np.array_equal(vr, S.grid_vr)
+    assert np.array_equal(bits(mo), bits(S.grid_max_op))
+    ctx.close()
+
+
 GRID_CASES = [
     # (rootN, bisections, levels, W, camera, raygen, accumIDs)
     (1, 0, 4, 96, None, 0, (0,)),      # C1-class, viewAll camera

@@ -7,6 +7,9 @@ seconds; full BASELINE sizes are covered by tests/test_gpu_scale.py through
 size-independent properties.
 """
 import ctypes as C
+import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -330,9 +333,23 @@ def test_terrain_and_degenerate_records_bit_exact():
         assert st_gpu[0].samplesFound == st_ref[0].samples_found
 
 
+@pytest.mark.skipif(not os.path.exists(irt.ALL_LIB_PATH), reason="make VARIANTS=all not built")
+def test_ab_library_variants_identical():
+    """test_all_render_variants_identical on the A/B library (every variant), in a child
+    process: one HIP library per process (IRT_LIB_PATH selects it at load)."""
+    env = dict(os.environ, IRT_LIB_PATH=irt.ALL_LIB_PATH)
+    r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                        f"{__file__}::test_all_render_variants_identical"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "1 passed" in r.stdout
+
+
 def test_all_render_variants_identical():
     """Every compiled variant of the binned raygen (batching, occupancy bounds, LUT in LDS)
-    renders the same frame and counts as the default."""
+    renders the same frame and counts as the default.  The product library compiles the
+    default and the statistics variant; test_ab_library_variants_identical runs this test
+    again on libicon_rt_hip_all.so (`make VARIANTS=all`) with every A/B variant."""
     L = irt.lib()
     L.irt_debug_set_variant.argtypes = [C.c_void_p, C.c_int]
     cells = irt.synth_grid(2, 3, 90)
@@ -344,7 +361,9 @@ def test_all_render_variants_identical():
     fb = torch.zeros(W * W, dtype=torch.int32, device="cuda")
     acc = torch.zeros(W * W * 4, dtype=torch.float32, device="cuda")
     ref = None
-    for v in irt.BIN_VARIANTS:
+    variants = irt.compiled_variants()
+    assert irt.lib().irt_debug_default_variant() in variants
+    for v in variants:
         assert L.irt_debug_set_variant(ctx._h, v) == 0
         acc.zero_()
         ctx.render(setup.lp, W, W, fb.data_ptr(), acc.data_ptr())
