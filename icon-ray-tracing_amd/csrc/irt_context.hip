@@ -129,6 +129,11 @@ struct irt_context {
   int coopMaxLg = 0;
   int coopRamp = 1;
   int probeExit = 0;           // IRT_PROBE_EXIT (measurement only, RenderArgs::probeExit)
+  // persistent launches (RenderArgs::queue, IRT_QUEUE=0|1): every resident wave pulls 8x8
+  // packets from a per-slot counter pair {next, done} (kSlots x 2 u32, zero between launches)
+  bool queueOn = false;
+  uint32_t *d_queue = nullptr;
+  int numCU = 0;
   int schedPolicy = 2;         // IRT_SCHED: 1 tiles, 2 bands of tiles (a tile row; default), 3 reversed
   bool schedOrderValid = false;
   bool schedLastApplied = false;   // the last launch ran in a measured-cost order
@@ -187,7 +192,7 @@ void free_all(irt_context *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
                   c->d_sphBits, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_gridBits, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
-                  c->d_lut, c->d_counters, c->d_meta};
+                  c->d_lut, c->d_counters, c->d_meta, c->d_queue};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->d_cells) (void)hipFree(c->d_cells);
@@ -521,9 +526,19 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     if (rc) return rc;
   }
   const size_t lanes = (size_t)numTiles * 4096;
+  // persistent launch: the cooperative kernels, not for the measurement-only early exits
+  // (every wave must reach the queue's done count)
+  const bool queued = c->queueOn && numTiles > 0 && c->probeExit == 0 && render_queue_ok(A, c->variant);
+  int queueWG = 0;
+  if (queued) {
+    A.queue = c->d_queue + 2 * slot;
+    A.numPackets = (uint32_t)numTiles * 64u * (uint32_t)numFrames;
+    queueWG = render_queue_wgs(A, c->variant, c->numCU, numTiles * 16 * numFrames);
+  }
   // workgroups of this launch: 16 per 64x64 tile, x4 for the one-wave-workgroup variants
-  // (irt_render.hip OPT_WAVEWG, bit 4194304), per frame
-  const size_t numWG = (size_t)numTiles * 16 * (size_t)render_wg_per_block(A, c->variant) * (size_t)numFrames;
+  // (irt_render.hip OPT_WAVEWG, bit 4194304), per frame; a persistent launch's resident ones
+  const size_t numWG = queued ? (size_t)queueWG
+                              : (size_t)numTiles * 16 * (size_t)render_wg_per_block(A, c->variant) * (size_t)numFrames;
   // Per-workgroup counts need kSlots x 32 B of pinned host memory per workgroup and frame
   // (1 KiB): a launch past kWgCountsMax workgroups (a large progressive batch) counts through
   // the device-atomic block instead, for that launch only.
@@ -588,7 +603,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.schedCost = nullptr;
   const int numBlocks = numTiles * 16;
   bool copyCosts = false;
-  if (c->schedOn && numFrames == 1 && numBlocks > 0 && !dList) {
+  if (c->schedOn && numFrames == 1 && numBlocks > 0 && !dList && !queued) {
     int rc = sched_prepare(c, numBlocks, W, H, packed, tileBegin, tileStride, numTiles, lp, s);
     if (rc) return rc;
     A.schedOrder = c->schedOrderValid ? c->d_schedOrder + (size_t)c->schedBuf * c->schedCap : nullptr;
@@ -617,7 +632,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   c->timed[slot] = c->launches % c->timingEvery == 0;
   if (c->timed[slot]) IRT_HIP(hipEventRecord(c->ev0[slot], s));
   if (numTiles > 0) {
-    launch_render(A, numTiles * 16, s, c->variant);
+    launch_render(A, queued ? queueWG : numTiles * 16, s, c->variant);
   }
   IRT_HIP(hipGetLastError());
   if (c->timed[slot]) IRT_HIP(hipEventRecord(c->ev1[slot], s));
@@ -887,6 +902,10 @@ int irt_create_end(irt_context *c) {
   if (const char *e = getenv("IRT_COOP_MAXLG")) c->coopMaxLg = std::min(6, std::max(0, atoi(e)));
   if (const char *e = getenv("IRT_COOP_RAMP")) c->coopRamp = std::min(6, std::max(0, atoi(e)));
   if (const char *e = getenv("IRT_PROBE_EXIT")) c->probeExit = atoi(e);
+  if (const char *e = getenv("IRT_QUEUE")) c->queueOn = atoi(e) != 0;
+  if ((rc = dalloc(c, &c->d_queue, 2 * irt_context::kSlots))) return rc;
+  IRT_HIP(hipMemsetAsync(c->d_queue, 0, 2 * irt_context::kSlots * sizeof(uint32_t), c->stream));
+  IRT_HIP(hipDeviceGetAttribute(&c->numCU, hipDeviceAttributeMultiprocessorCount, c->device));
   IRT_HIP(hipHostGetDevicePointer((void **)&c->dh_counters, c->h_counters, 0));
   IRT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long), c->stream));
 
@@ -1488,6 +1507,17 @@ extern "C" int irt_debug_context_array(const irt_context *c, int which, void *ds
 extern "C" int irt_debug_get_variant(const irt_context *c) { return c ? c->variant : -1; }
 
 extern "C" int irt_debug_variants(int *out, int capacity) { return render_variants(out, capacity); }
+
+extern "C" int irt_debug_set_queue(irt_context *c, int on) {
+  if (!c) {
+    set_error("irt_debug_set_queue: null context");
+    return IRT_E_INVALID;
+  }
+  c->queueOn = on != 0;
+  return IRT_OK;
+}
+
+extern "C" int irt_debug_get_queue(const irt_context *c) { return c ? (c->queueOn ? 1 : 0) : -1; }
 
 extern "C" int irt_debug_set_variant(irt_context *c, int variant) {
   if (!c || !render_variant_available(variant)) {

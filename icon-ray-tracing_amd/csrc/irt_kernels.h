@@ -85,6 +85,12 @@ struct RenderArgs {
   // 2 = after the prologue, 3 = after ray generation and boxTest (no pixel written), 4 = at
   // the first woodcockFunc, 5 = after it
   int probeExit;
+  // persistent launch (the thread pool's queue, common/thread_pool.h:146-161, per wave):
+  // non-null {next, done} pair -- every wave pulls 8x8-pixel packets (packet p: frame
+  // p / (numTiles*64), block (p >> 2) % (numTiles*16), the block's wave p & 3) from `next`
+  // until numPackets; the launch's last wave resets the pair for the next launch
+  uint32_t *queue;
+  uint32_t numPackets;
 };
 
 // Event counts kept per workgroup: [0] launched [1] inBox [2] locate [3] found [4] candidates
@@ -100,6 +106,14 @@ int render_variants(int *out, int cap);  // the compiled variants (count; the fi
 // workgroups per 256-pixel block the launch of `variant` uses for these arguments (4 only for
 // the one-wave-workgroup A/B variants on the user-geometry sphere path)
 int render_wg_per_block(const RenderArgs &A, int variant);
+// whether `variant` can run as a persistent launch (RenderArgs::queue) with these arguments:
+// the cooperative user-geometry sphere-accel kernels with 256-thread workgroups
+bool render_queue_ok(const RenderArgs &A, int variant);
+// workgroups a persistent launch of `variant` runs on a device with numCU compute units:
+// every slot the kernel's occupancy allows (resident at once), at most `numBlocks`
+int render_queue_wgs(const RenderArgs &A, int variant, int numCU, int numBlocks);
+// numBlocks: the frame's 256-pixel blocks (grid launch), or the workgroups of a persistent
+// launch (A.queue, render_queue_wgs)
 void launch_render(const RenderArgs &A, int numBlocks, hipStream_t s, int variant);
 void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *found, float *value,
                          hipStream_t s, bool wave);

@@ -51,6 +51,9 @@ enum : int {
                         // fit a CU while finished waves wait for their workgroup's last one:
                         // the sRGB thresholds and the sphere hash read from global memory
                         // (L1/L2), the accum pixel loaded at the end instead of prefetched
+  OPT_QUEUE = 16777216,  // the persistent launch (RenderArgs::queue): every resident wave pulls
+                        // 8x8-pixel packets from the launch's counter; its own instantiation
+                        // of the default kernel (k_render's grid launch is unchanged)
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
@@ -1298,30 +1301,35 @@ template <int OPT>
 __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
                                                   const float *s_th, int4 *s_dda, float4 *s_entry,
                                                   float4 *s_acc, CoopWave &W, ScanWave *SW, const uint2 *jmp,
-                                                  int tid, int accumID, uint32_t blk) {
+                                                  int tid, int accumID, uint32_t blk, int pwave, int frame) {
   // At 5+ waves/SIMD the pixel's output addresses are recomputed where they are used (from the
   // workgroup's uniform block index), not held in VGPRs through the rounds: a progressive
   // batch's sample slot (k_accumulate reads it) and the frame index.  (At 4 waves there is
   // room for them, and recomputing costs 1 %: profiles/r03u_waves/.)
   constexpr bool kRecompute = ((OPT >> 8) & 15) >= 5;
-  // the pixel's thread index within its 256-pixel block (OPT_WAVEWG: four one-wave workgroups
-  // per block; tid is the LDS index within this workgroup)
-  const int ptid = (OPT & OPT_WAVEWG) != 0 ? (int)((blockIdx.x & 3u) * 64u) + tid : tid;
+  // the pixel's thread index within its 256-pixel block: the packet's wave pwave (uniform) of
+  // the block, and the lane (tid is the LDS index within this workgroup: a persistent launch's
+  // wave renders any packet; OPT_WAVEWG has four one-wave workgroups per block)
+  const int ptid = pwave * 64 + (tid & 63);
   // ... and so is the thread index itself after the rounds: the wave's base (uniform, an SGPR)
   // plus the lane id, instead of tid and the pixel's in-block coordinates held in scratch
   // across the rounds (24 B per lane of spill stores and reloads at 5 waves)
   const int wbase = __builtin_amdgcn_readfirstlane(tid) & ~63;
   auto tid_late = [&]() { return kRecompute ? (opaque_u(wbase) | (int)__lane_id()) : tid; };
   auto ptid_late = [&]() {
-    return (OPT & OPT_WAVEWG) != 0 ? (int)((blockIdx.x & 3u) * 64u) + tid_late() : tid_late();
+    if constexpr (!kRecompute) return ptid;
+    int lane = (int)__lane_id();
+    asm volatile("" : "+v"(lane));  // not CSE'd with the pixel's coordinates at the ray's start
+    return (opaque_u(pwave) << 6) | lane;
   };
   const bool toSample = A.numSamples > 1;
   float4 *const slot0 = kRecompute || !toSample
                             ? nullptr
-                            : A.sampleBuf + (size_t)blockIdx.y * gridDim.x * blockDim.x + (size_t)blk * 256u + (size_t)ptid;
+                            : A.sampleBuf + (size_t)frame * A.numTiles * 4096u + (size_t)blk * 256u + (size_t)ptid;
   auto sample_slot = [&]() {
     if constexpr (!kRecompute) return slot0;
-    return A.sampleBuf + (size_t)blockIdx.y * gridDim.x * blockDim.x + (size_t)opaque_u((int)blk) * 256u + (size_t)ptid_late();
+    return A.sampleBuf + (size_t)opaque_u(frame) * opaque_u(A.numTiles) * 4096u + (size_t)opaque_u((int)blk) * 256u +
+           (size_t)ptid_late();
   };
   enum : int { kRange, kLeaf, kWait, kDone, kGrid, kGridNext };
   constexpr bool grid = (OPT & OPT_GRID) != 0;
@@ -1635,6 +1643,25 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   }
 }
 
+// The persistent launch's packet counter {next, done} (RenderArgs::queue): one wave-wide
+// fetch (lane 0's atomic, read by every lane), and the launch's end -- the last wave to finish
+// resets the pair for the next launch on it (every wave's last fetch precedes its done count).
+__device__ __forceinline__ uint32_t queue_next(uint32_t *q) {
+  uint32_t v = 0u;
+  if (__lane_id() == 0) v = atomicAdd(&q[0], 1u);
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ void queue_done(uint32_t *q) {
+  if (__lane_id() == 0) {
+    __threadfence();
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    if (atomicAdd(&q[1], 1u) == waves - 1u) {
+      __hip_atomic_store(&q[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&q[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // The raygen over the frame grid: one lane per pixel (see pixel_of).
 template <int OPT>
 __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1)
@@ -1711,17 +1738,80 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
   // buffer for k_accumulate; a single frame writes accum/fb directly.  With measured-cost
   // scheduling (irt_context.hip) workgroup b renders block order[b].
   const uint32_t blk = __builtin_amdgcn_readfirstlane(A.schedOrder ? A.schedOrder[wg] : wg);  // uniform: an SGPR
-  const uint32_t gid = blk * 256u + (uint32_t)ptid;
-  const Pixel px = pixel_of(A, blk, ptid);
-  float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * blockDim.x + gid : nullptr;
+  uint32_t launched = 0u;  // rays of this wave's pixels (uniform)
+  bool pxActive = false;   // the one-lane-per-ray kernel's pixel
   if constexpr (Tracer<OPT>::kCoop) {
-    render_pixel_coop<OPT>(A, T, px, th_p, s_dda, s_entry, s_acc, s_coop[tid >> 6],
-                           &s_scan[Tracer<OPT>::kWaveScan ? tid >> 6 : 0], s_jmp, tid,
-                           A.accumID + (int)blockIdx.y, blk);
+    // One call site for both launch forms.  Grid launch: this workgroup's block, once.
+    // Persistent launch (A.queue): the wave pulls packets -- the 8x8-pixel unit a wave renders
+    // -- from the launch's counter until none is left, as the reference's thread pool pulls
+    // 64x64 tiles (common/thread_pool.h:146-161), each wave on its own (no workgroup
+    // barrier: a wave whose packet finishes early takes the next one at once).  Every packet
+    // renders exactly as in the grid launch (same block, wave, frame, seeds).  The next index
+    // is fetched when a packet starts, so its round trip hides behind the packet's work.
+    constexpr bool queued = (OPT & OPT_QUEUE) != 0;
+    static_assert(!queued || (!wavewg && (OPT & (OPT_STATS | OPT_TIMING | OPT_HDRLDS)) == 0),
+                  "persistent launches: 256-thread workgroups, no per-wave statistics");
+    const uint32_t perFrame = (uint32_t)A.numTiles * 64u;  // packets per frame
+    uint32_t p = queued ? queue_next(A.queue) : 0u;
+    bool more = !queued || p < A.numPackets;
+    while (more) {
+      uint32_t pblk = blk, nx = 0u;
+      int pw = wavewg ? (int)(blockIdx.x & 3u) : (tid >> 6), frame = (int)blockIdx.y;
+      if constexpr (queued) {
+        nx = queue_next(A.queue);
+        frame = A.numSamples > 1 ? (int)(p / perFrame) : 0;
+        const uint32_t q = p - (uint32_t)frame * perFrame;
+        pblk = q >> 2;
+        pw = (int)(q & 3u);
+      }
+      pblk = __builtin_amdgcn_readfirstlane(pblk);
+      pw = __builtin_amdgcn_readfirstlane(pw);
+      frame = __builtin_amdgcn_readfirstlane(frame);
+      // the thread index, new to the compiler in every iteration: what derives from it (the
+      // pixel's coordinates, LDS slot addresses) is recomputed per packet, not hoisted out of
+      // the loop and held in VGPRs through it
+      int ltid = tid;
+      if constexpr (queued) {
+        asm volatile("" : "+v"(ltid));
+        // ... and so are the launch's arguments: the kernel-argument segment (RenderArgs is the
+        // kernel's only argument, at offset 0) through a pointer the compiler cannot follow
+        // across iterations.  Every value derived from them (the box's corners relative to
+        // the eye, |eye|^2, cube-map and LUT scales, ...) is then computed per packet as in
+        // the grid launch, instead of once before the loop and held in VGPRs (or scratch)
+        // through every packet.
+        typedef const __attribute__((address_space(4))) RenderArgs *KArgs;
+        KArgs kp = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kp));
+        const RenderArgs &AL = *(const RenderArgs *)kp;
+        Tracer<OPT> TL{{}, AL, s_logf, lean ? AL.sphBits : s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
+        TL.s_gbits = s_gbits;
+        const Pixel ppx = pixel_of(AL, pblk, pw * 64 + (ltid & 63));
+        launched += (uint32_t)__popcll(__ballot(ppx.active));
+        render_pixel_coop<OPT>(AL, TL, ppx, lean ? AL.srgbTh : s_th, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
+                               &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, AL.accumID + frame,
+                               pblk, pw, frame);
+        TL.flush_coop();  // this packet's counts (nothing carried from packet to packet)
+      } else {
+        const Pixel ppx = pixel_of(A, pblk, pw * 64 + (ltid & 63));
+        launched += (uint32_t)__popcll(__ballot(ppx.active));
+        render_pixel_coop<OPT>(A, T, ppx, th_p, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
+                               &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, A.accumID + frame,
+                               pblk, pw, frame);
+      }
+      p = nx;
+      more = queued && p < A.numPackets;
+    }
+    if constexpr (queued) queue_done(A.queue);
     T.flush_coop();
   }
-  else if (px.active)
-    render_pixel<OPT>(A, T, px, th_p, s_dda, s_entry, tid, A.accumID + (int)blockIdx.y, slot);
+  else {
+    const Pixel px = pixel_of(A, blk, ptid);
+    float4 *slot = A.numSamples > 1 ? A.sampleBuf + (size_t)blockIdx.y * gridDim.x * blockDim.x + blk * 256u + ptid
+                                    : nullptr;
+    if (px.active) render_pixel<OPT>(A, T, px, th_p, s_dda, s_entry, tid, A.accumID + (int)blockIdx.y, slot);
+    pxActive = px.active;
+    launched = (uint32_t)__popcll(__ballot(px.active));
+  }
   if constexpr ((OPT & OPT_TIMING) != 0) {
     T.tmark(8);  // after the last woodcockFunc: pixel write, epilogue
     if ((tid & 63) == 0) {
@@ -1745,7 +1835,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
     uint32_t hist[4];
     for (int k = 0; k < 4; ++k)
       hist[k] = T.kCoop ? Tracer<OPT>::wave_sum(T.cnt.candHist[k])
-                        : (uint32_t)__popcll(__ballot(px.active && bkt == k));
+                        : (uint32_t)__popcll(__ballot(pxActive && bkt == k));
     if ((tid & 63) == 0) {
       atomicAdd(&A.counters[5], (unsigned long long)ss);
       atomicAdd(&A.counters[6], (unsigned long long)sm);
@@ -1760,8 +1850,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
   }
   if (A.counters || A.schedCost) {
     const int lane = (int)__lane_id();
-    const unsigned long long m = __ballot(px.active);  // rays launched, once per wave
-    if (A.counters && lane == 0 && m) atomicAdd(&s_cnt[0], (uint32_t)__popcll(m));
+    if (A.counters && lane == 0 && launched) atomicAdd(&s_cnt[0], launched);  // rays launched, once per wave
     // The last wave of the workgroup to get here writes the workgroup's counts and duration.
     // No end-of-workgroup barrier: a wave that finishes early frees its slot at once instead
     // of waiting for the slowest wave of its workgroup.  The acq-rel LDS add orders every
@@ -1917,31 +2006,74 @@ int render_wg_per_block(const RenderArgs &A, int variant) {
   return waveWG && A.sampler == IRT_MODE_USER_GEOM && A.accelMode != IRT_ACCEL_GRID ? 4 : 1;
 }
 
+// variant bits without a persistent form
+constexpr int kNoQueue = OPT_WAVEWG | OPT_SERIAL | OPT_STATS | OPT_TIMING | OPT_HDRLDS;
+bool render_queue_ok(const RenderArgs &A, int variant) {
+  return render_variant_available(variant) && (variant & kNoQueue) == 0 &&
+         A.sampler == IRT_MODE_USER_GEOM && A.accelMode != IRT_ACCEL_GRID;
+}
+
+typedef void (*RenderKernel)(RenderArgs);
+// The kernel a launch of variant N runs for these arguments, and its workgroup size.  The
+// grid accel or the unstructured samplers: their own instantiations of the raygen (kept out
+// of the default kernel, whose registers they would cost); the wedge kernels hold a 6-vertex
+// Newton state: no waves-per-SIMD floor.  Both run the cooperative Woodcock loop with its
+// miss mode (C2: TRIANGLES 3.4x, CUBQL 2.5x faster than one lane per ray;
+// profiles/r02b_investigation/).
 template <int N>
-void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
+RenderKernel kernel_for(const RenderArgs &A, int &threads) {
   constexpr int K = N & ~OPT_MONO;
-  // the grid accel or the unstructured samplers: their own instantiations of the raygen
-  // (kept out of the default kernel, whose registers they would cost); the wedge kernels
-  // hold a 6-vertex Newton state: no waves-per-SIMD floor.  Both run the cooperative
-  // Woodcock loop with its miss mode (C2: TRIANGLES 3.4x, CUBQL 2.5x faster than one lane per
-  // ray; profiles/r02b_investigation/).
   constexpr int D = kDefaultVariant & ~OPT_MONO;
   constexpr int DW = (D & ~0xF00) | OPT_WEDGE | (K & OPT_SERIAL);
   constexpr int DG = (D & ~0xF00) | 0x400;  // the grid-accel raygen: 4 waves/SIMD as measured in round 2
-  const dim3 grid(numBlocks, A.numSamples);
   const bool g = A.accelMode == IRT_ACCEL_GRID;
-  if (A.sampler != IRT_MODE_USER_GEOM && g)  // CUBQL or TRIANGLES: the unstructured locator
-    hipLaunchKernelGGL(k_render<DW | OPT_GRID>, grid, dim3(256), 0, s, A);
-  else if (A.sampler != IRT_MODE_USER_GEOM)
-    hipLaunchKernelGGL(k_render<DW>, grid, dim3(256), 0, s, A);
-  else if (g)
-    hipLaunchKernelGGL(k_render<DG | OPT_GRID | (K & OPT_SERIAL)>, grid, dim3(256), 0, s, A);
-  else if ((K & OPT_WAVEWG) != 0)  // four one-wave workgroups per 256-pixel block
-    hipLaunchKernelGGL(k_render<K>, dim3(numBlocks * 4, A.numSamples), dim3(64), 0, s, A);
-  else
-    hipLaunchKernelGGL(k_render<K>, grid, dim3(256), 0, s, A);
+  threads = 256;
+  if (A.sampler != IRT_MODE_USER_GEOM && g) return k_render<DW | OPT_GRID>;  // CUBQL / TRIANGLES
+  if (A.sampler != IRT_MODE_USER_GEOM) return k_render<DW>;
+  if (g) return k_render<DG | OPT_GRID | (K & OPT_SERIAL)>;
+  if ((K & OPT_WAVEWG) != 0) threads = 64;  // four one-wave workgroups per 256-pixel block
+  if constexpr ((K & kNoQueue) == 0)
+    if (A.queue) return k_render<K | OPT_QUEUE>;
+  return k_render<K>;
+}
+
+template <int N>
+void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
+  int threads = 256;
+  const RenderKernel k = kernel_for<N>(A, threads);
+  if (A.queue) {  // persistent: numBlocks workgroups (render_queue_wgs) pull the packets
+    hipLaunchKernelGGL(k, dim3(numBlocks), dim3(256), 0, s, A);
+    numBlocks = A.numTiles * 16;
+  } else {
+    hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads), A.numSamples), dim3(threads), 0, s, A);
+  }
   // progressive batch: the lerp chain over the frames' samples
   if (A.numSamples > 1) hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);
+}
+
+template <int N>
+int queue_wgs_variant(const RenderArgs &A, int numCU, int numBlocks) {
+  int threads = 256;
+  const RenderKernel k = kernel_for<N>(A, threads);
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, threads, 0) != hipSuccess || occ < 1) {
+    (void)hipGetLastError();
+    occ = 1;
+  }
+  const long long n = (long long)occ * numCU;
+  return (int)(n < numBlocks ? n : numBlocks);
+}
+
+int render_queue_wgs(const RenderArgs &A, int variant, int numCU, int numBlocks) {
+  switch (variant) {
+#define IRT_CASE(N) \
+  case N:           \
+    return queue_wgs_variant<N>(A, numCU, numBlocks);
+    IRT_VARIANTS(IRT_CASE)
+#undef IRT_CASE
+    default:
+      return queue_wgs_variant<kDefaultVariant>(A, numCU, numBlocks);
+  }
 }
 
 void launch_render(const RenderArgs &A, int numBlocks, hipStream_t s, int variant) {

@@ -515,6 +515,18 @@ class Context:
         _check(lib().irt_set_transfunc(self._h, _ptr(lut), lut.shape[0], box1(*value_range),
                                        float(opacity_scale)), "irt_set_transfunc")
 
+    def set_queue(self, on: bool):
+        """Persistent launches (every resident wave pulls 8x8 packets from a per-launch
+        counter) on or off for this context; frames are identical either way."""
+        L = lib()
+        L.irt_debug_set_queue.argtypes = [C.c_void_p, C.c_int]
+        _check(L.irt_debug_set_queue(self._h, 1 if on else 0), "irt_debug_set_queue")
+
+    def queue(self) -> bool:
+        L = lib()
+        L.irt_debug_get_queue.argtypes = [C.c_void_p]
+        return L.irt_debug_get_queue(self._h) == 1
+
     def clear(self, fb_ptr: int, accum_ptr: int, num_pixels: int, stream: int = 0):
         _check(lib().irt_clear_frame(self._h, C.c_void_p(fb_ptr), C.c_void_p(accum_ptr),
                                      num_pixels, C.c_void_p(stream)), "irt_clear_frame")

@@ -96,6 +96,11 @@ int irt_debug_get_variant(const irt_context *ctx);
  * them to `out` (may be NULL).  The product build has the default and the statistics
  * variant; `make VARIANTS=all` (libicon_rt_hip_all.so) adds the A/B variants. */
 int irt_debug_variants(int *out, int capacity);
+/* Persistent launches on or off for this context (IRT_QUEUE sets the default): every
+ * resident wave pulls 8x8-pixel packets from a per-launch counter (RenderArgs::queue) instead
+ * of one workgroup per 16x16 block.  Frames are identical either way.  get: 1/0, -1 for NULL. */
+int irt_debug_set_queue(irt_context *ctx, int on);
+int irt_debug_get_queue(const irt_context *ctx);
 /* The raw per-frame counters of the last render (waits for it): [0] launched [1] in box
  * [2] sampleVolume calls [3] found [4] candidates; with the statistics variant bit also
  * [5] Woodcock draws [6] sum over waves of the per-wave max draws [7] zero-length leaves

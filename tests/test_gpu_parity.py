@@ -777,3 +777,72 @@ def test_counts_past_the_workgroup_ring_cap(monkeypatch):
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), k
         assert a[2:] == b[2:], (k, a[2:], b[2:])
     assert got_tot == ref_tot
+
+
+def test_persistent_launch_identical():
+    """Persistent launches (RenderArgs::queue: every resident wave pulls 8x8-pixel packets
+    from the launch's counter, as the reference's thread pool pulls tiles,
+    common/thread_pool.h:146-161) render every frame, count and progressive batch exactly as
+    the grid launch: single frames at ragged sizes (partial packets), progressive batches,
+    tile lists and strided tile splits, many launches in a row (the counter pair is reset by
+    each launch's last wave), and two streams."""
+    import torch
+    cells = irt.synth_grid(2, 3, 90)
+    S = irt.setup_frame(cells, 8, 8, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(S.lut, S.value_range)
+
+    def run(on, fn):
+        ctx.set_queue(on)
+        return fn()
+
+    def frame(W, H, acc_id=0, frames=1, stream=0):
+        setup = irt.setup_frame(cells, W, H, camera=FRAMING)
+        setup.lp.accumID = acc_id
+        fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+        if frames == 1:
+            ctx.render(setup.lp, W, H, fb.data_ptr(), acc.data_ptr(), stream)
+        else:
+            ctx.render_accumulate(setup.lp, W, H, frames, fb.data_ptr(), acc.data_ptr(), stream)
+        torch.cuda.synchronize()
+        st = ctx.stats()
+        return (fb.cpu().numpy(), bits(acc.cpu().numpy()),
+                (st.raysLaunched, st.raysInBox, st.locateCalls, st.samplesFound, st.candidatesTested))
+
+    def same(a, b, what):
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), what
+        assert a[2] == b[2], (what, a[2], b[2])
+
+    for W, H in ((128, 128), (131, 77), (9, 300), (64, 64)):
+        same(run(True, lambda: frame(W, H)), run(False, lambda: frame(W, H)), f"{W}x{H}")
+    same(run(True, lambda: frame(96, 80, 3, 4)), run(False, lambda: frame(96, 80, 3, 4)), "batch")
+    # many launches back to back through the ring of counter pairs (kSlots = 32)
+    ctx.set_queue(True)
+    first = frame(100, 100)
+    for k in range(40):
+        same(frame(100, 100), first, f"launch {k}")
+    s2 = torch.cuda.Stream()
+    same(frame(100, 100, stream=s2.cuda_stream), first, "side stream")
+    # tile lists (multi-GPU rows) and strided tiles
+    W = H = 200
+    setup = irt.setup_frame(cells, W, H, camera=FRAMING)
+
+    def tiles(on):
+        ctx.set_queue(on)
+        out = []
+        fbt = torch.zeros(16 * 4096, dtype=torch.int32, device="cuda")
+        act = torch.zeros(16 * 4096 * 4, dtype=torch.float32, device="cuda")
+        ctx.render_tile_list(setup.lp, W, H, [15, 2, 7, 0, 9], 2, fbt.data_ptr(), act.data_ptr())
+        torch.cuda.synchronize()
+        out.append((fbt.cpu().numpy(), bits(act.cpu().numpy())))
+        fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+        ctx.render_tiles(setup.lp, W, H, 1, 3, fb.data_ptr(), acc.data_ptr())
+        torch.cuda.synchronize()
+        out.append((fb.cpu().numpy(), bits(acc.cpu().numpy())))
+        return out
+
+    for (a0, a1), (b0, b1) in zip(tiles(True), tiles(False)):
+        assert np.array_equal(a0, b0) and np.array_equal(a1, b1)
+    ctx.close()
