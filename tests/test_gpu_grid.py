@@ -53,8 +53,7 @@ def test_grid_build_reads_value31_of_unsorted_records():
     pick = np.concatenate([rng.choice(cells.size - 1, 40, replace=False), [cells.size - 1]])
     for i in pick:
         h = cells["height"][i].copy()
-        top = h[31]
-        h[:31] = h[:31] + (top - h[0]) * 1.5  # heights 0..30 above height[31]
+        h[0] = h[31] + (h[31] - h[0])  # height[0] above every other: findHeight(height[0]) = 31
         cells["height"][i] = h
         cells["value"][i, 31] = 1e3 + i  # outside every other value: a wrong slot shows
     _, _, _, S = oracle_frame(cells, 8, 8, camera=FRAMING, accel_mode=1)
