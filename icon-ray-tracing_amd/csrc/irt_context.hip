@@ -1340,6 +1340,76 @@ extern "C" int irt_debug_device_math(int device, const float *a, const float *y,
 }
 
 namespace {
+// Exhaustive error bounds of the certified fast lat/lon (irt_device.h kLatErr / kLonErr),
+// as the bit patterns of non-negative doubles (ordered like their values) in out[0..3]:
+//   [0] max |fast_asin(x) - glibc_asinf(x)| over every float x in [-1, 1]
+//   [1] max |fast_atan(q) - atan(q)|, [2] max |glibc_atanf(q) - atan(q)| over every float q in
+//       [0, 2^59] (atan in double)
+//   [3] max |rcp(b) b - 1| of the hardware reciprocal over every float b in [2^-100, 2^100]
+__device__ __forceinline__ void wave_max_out(unsigned long long *out, double v) {
+  unsigned long long b = __double_as_longlong(v);
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(b, off, 64);
+    b = o > b ? o : b;
+  }
+  if (__lane_id() == 0) atomicMax(out, b);
+}
+__global__ void __launch_bounds__(256) k_fast_math_bounds(unsigned long long *out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  double m0 = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;
+  for (uint32_t u = t; u <= 0x3f800000u; u += stride) {
+    const float x = __uint_as_float(u);
+    const double a = fabs((double)fast_asin(x) - (double)glibc_asinf(x));
+    const double b = fabs((double)fast_asin(-x) - (double)glibc_asinf(-x));
+    m0 = fmax(m0, fmax(a, b));
+    if (!(a == a) || !(b == b)) m0 = __longlong_as_double(0x7ff8000000000000ll);
+  }
+  for (uint32_t u = t; u <= 0x5d000000u; u += stride) {
+    const float q = __uint_as_float(u);
+    const double ref = atan((double)q);
+    const double a = fabs((double)fast_atan(q) - ref), b = fabs((double)glibc_atanf(q) - ref);
+    m1 = (a == a) ? fmax(m1, a) : __longlong_as_double(0x7ff8000000000000ll);
+    m2 = (b == b) ? fmax(m2, b) : __longlong_as_double(0x7ff8000000000000ll);
+  }
+  for (uint32_t u = 0x0d800000u + t; u <= 0x71800000u; u += stride) {
+    const float b = __uint_as_float(u);
+    m3 = fmax(m3, fabs((double)__builtin_amdgcn_rcpf(b) * (double)b - 1.0));
+  }
+  wave_max_out(out + 0, m0);
+  wave_max_out(out + 1, m1);
+  wave_max_out(out + 2, m2);
+  wave_max_out(out + 3, m3);
+}
+}  // namespace
+
+extern "C" int irt_debug_fast_math_bounds(int device, double *out4) {
+  if (!out4) {
+    set_error("irt_debug_fast_math_bounds: null argument");
+    return IRT_E_INVALID;
+  }
+  IRT_HIP(hipSetDevice(device));
+  unsigned long long *d = nullptr;
+  IRT_HIP(hipMalloc((void **)&d, 4 * sizeof(unsigned long long)));
+  hipError_t e = hipMemset(d, 0, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_fast_math_bounds, dim3(8192), dim3(256), 0, 0, d);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out4, d, 4 * sizeof(double), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) {
+    set_error("irt_debug_fast_math_bounds: %s", hipGetErrorString(e));
+    return IRT_E_HIP;
+  }
+  return IRT_OK;
+}
+
+extern "C" void irt_debug_fast_spherical_consts(float *out2) {
+  out2[0] = kLatErr;
+  out2[1] = kLonErr;
+}
+
+namespace {
 __global__ void k_debug_wlog(float *out) {
   __shared__ LogfTab t[16];
   if (threadIdx.x < 16) t[threadIdx.x] = kLogfTab[threadIdx.x];

@@ -170,6 +170,85 @@ __device__ __forceinline__ void to_spherical(float x, float y, float z, float &r
   lon = glibc_atan2f(y, x);
 }
 
+// ---------------------------------------------------------------------------------
+// Certified fast toSpherical for the sdda entry/exit cells.  sdda (ShellAccel.h:113-138)
+// uses the lat/lon of a range's entry and exit point only through
+//   * the shell-grid cell int((v - lo)/size * (dims-1)) (projectToSphericalGrid, 57-68), and
+//   * the signs of la2 - la1, lo2 - lo1 (the step direction, 125-127).
+// Both are monotone in v.  So a value known to lie within E of the glibc value certifies the
+// cell when both ends v -+ E project to the same cell, and a sign when |la2 - la1| > 2E (+
+// the rounding of the difference); only when that fails (about 1e-3 of the values) are the
+// glibc-exact asinf / atan2f evaluated.  The fast functions cost ~35 VALU instructions
+// against ~110 for the exact pair (and their branches).
+//
+// The bounds E are proven exhaustively on the device (tests/test_gpu_parity.py
+// test_fast_spherical_bounds, irt_debug_fast_math_bounds):
+//   * asin: x = z / r is computed exactly (as the reference computes it) in both paths, and
+//     |fast_asin(x) - glibc_asinf(x)| is measured over EVERY float x in [-1, 1];
+//   * atan2: |fast_atan(q) - atan(q)| and |glibc_atanf(q) - atan(q)| over every float q in
+//     [0, 2^58] (atan in double), the hardware reciprocal's relative error over every float;
+//     then |fast - glibc atan2f| <= E_fast + E_glibc + |q_fast - y/x| / 2 + |q_glibc - y/x| / 2
+//     (atan's slope q/(1+q^2) <= 1/2 in relative terms) + the four roundings of the
+//     quadrant step pi - (z - pi_lo) (two per evaluation, <= ulp(pi)/2 each).
+// kLatErr / kLonErr include 1.2e-7 for rounding v -+ E itself (ulp(pi)/2).
+constexpr float kLatErr = 1.0e-6f;
+constexpr float kLonErr = 2.0e-6f;
+
+// asin for |x| <= 1 (glibc's polynomial in t, Horner with fmas; no split-pio2 refinement;
+// the hardware square root)
+__device__ __forceinline__ float fast_asin(float x) {
+  const float a = __builtin_fabsf(x);
+  const bool big = a >= 0.5f;
+  const float t = big ? (1.f - a) * 0.5f : a * a;
+  const float s = big ? __builtin_amdgcn_sqrtf(t) : a;
+  const float p = t * __builtin_fmaf(
+                          t, __builtin_fmaf(t, __builtin_fmaf(t, __builtin_fmaf(t, 4.216630880e-2f, 2.417951451e-2f),
+                                                                4.547037598e-2f),
+                                            7.495297643e-2f),
+                          1.666675248e-1f);
+  const float r = __builtin_fmaf(s, p, s);
+  const float v = big ? __builtin_fmaf(-2.f, r, 1.57079637050628662109375f) : r;
+  return __builtin_copysignf(v, x);
+}
+// atan for q >= 0 (Cephes' reduction at tan(pi/8), tan(3pi/8) with the hardware reciprocal,
+// its degree-9 odd polynomial)
+__device__ __forceinline__ float fast_atan(float q) {
+  const bool big = q > 2.414213562373095f, mid = q > 0.4142135623730950f;
+  const float num = big ? -1.f : (mid ? q - 1.f : q);
+  const float den = big ? q : (mid ? q + 1.f : 1.f);
+  const float x = num * __builtin_amdgcn_rcpf(den);
+  const float base = big ? 1.57079637050628662109375f : (mid ? 0.785398185253143310546875f : 0.f);
+  const float z = x * x;
+  const float p = __builtin_fmaf(
+      __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(8.05374449538e-2f, z, -1.38776856032e-1f), z, 1.99777106478e-1f),
+                     z, -3.33329491539e-1f),
+      z * x, x);
+  return base + p;
+}
+// atan2(y, x) for finite, nonzero x, y with |y/x| in [2^-58, 2^58] (false otherwise: glibc's
+// special cases, take the exact path); glibc's quadrant step (glibc_atan2f)
+__device__ __forceinline__ bool fast_atan2(float y, float x, float &lon) {
+  const float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y);
+  const float q = ay * __builtin_amdgcn_rcpf(ax);
+  const bool ok = ax >= 0x1p-100f && ax <= 0x1p100f && ay >= 0x1p-100f && ay <= 0x1p100f && q >= 0x1p-58f &&
+                  q <= 0x1p58f;
+  const float z = fast_atan(q);
+  const float pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+  lon = y < 0.f ? (x < 0.f ? (z - pi_lo) - pi : -z) : (x < 0.f ? pi - (z - pi_lo) : z);
+  return ok;
+}
+// the shell-grid cell of v (project_axis_inv), certified for every value within err of v
+__device__ __forceinline__ bool cell_certified(float v, float err, float lo, double invSize, int dim, int &cell) {
+  const int c0 = project_axis_inv(v - err, lo, invSize, dim), c1 = project_axis_inv(v + err, lo, invSize, dim);
+  cell = c0;
+  return c0 == c1 && v == v;
+}
+// the sign of b - a (a < b) for values within err of a and b, certified
+__device__ __forceinline__ int sign_certified(float a, float b, float err) {
+  const float d = b - a, m = 2.f * err + 2.4e-7f;
+  return d > m ? 1 : (-d > m ? -1 : 0);  // 0: uncertain
+}
+
 // make_8bit (dvr_course-common-both.h:89-92)
 __device__ __forceinline__ uint32_t make_8bit(float f) {
   return (uint32_t)fminf(255.f, fmaxf(0.f, (float)f2i_x86(f * 256.f)));

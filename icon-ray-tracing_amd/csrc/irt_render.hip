@@ -1291,6 +1291,20 @@ __device__ __forceinline__ void render_pixel(const RenderArgs &A, Tracer<OPT> &T
     write_pixel(A, px.outIdx, cr, cg, cb, alpha, s_th);
 }
 
+// toSpherical (ICONGrid.h:36-42) of an sdda entry or exit point with the certified fast
+// lat/lon (irt_device.h): r exactly, lat/lon within kLatErr/kLonErr of glibc's, and the
+// point's shell-grid cells (ShellAccel.h:121-124, 128-130).  Returns false when a cell is
+// not certified (the caller takes the glibc-exact path, to_spherical).
+__device__ __forceinline__ bool spherical_fast(const RenderArgs &A, float x, float y, float z, float &r, float &la,
+                                               float &lo, int &cy, int &cz) {
+  r = sqrtf(dot3(x, y, z, x, y, z));
+  la = fast_asin(z / r);  // z / r rounds as toSpherical's
+  const bool okLon = fast_atan2(y, x, lo);
+  const bool okY = cell_certified(la, kLatErr, A.sbLo.y, A.invSb[1], A.dims.y, cy);
+  const bool okZ = cell_certified(lo, kLonErr, A.sbLo.z, A.invSb[2], A.dims.z, cz);
+  return okY && okZ && okLon;
+}
+
 // render_pixel restated as a per-lane state machine whose one Woodcock call site is reached
 // by the whole wave together (Tracer::woodcock_wave): each lane runs its ranges and sdda
 // leaves on its own until it needs a woodcockFunc on a leaf (kWait) or is finished
@@ -1437,16 +1451,41 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     const float tnx = upper, tny = 0.f, tnz = 0.f;
     int4 dd;
     if (iter == 0) {
+      // exit point, step and stop (ShellAccel.h:125-132): the certified fast lat/lon
+      // (spherical_fast); the entry's (r1, la1, lo1, lower) wait in s_entry
       const float e2 = upper - sceneEPS();
       float r2, la2, lo2;
-      to_spherical(A.org.x + dx * e2, A.org.y + dy * e2, A.org.z + dz * e2, r2, la2, lo2);
+      int cy2, cz2;
+      const bool ok2 = spherical_fast(A, A.org.x + dx * e2, A.org.y + dy * e2, A.org.z + dz * e2, r2, la2, lo2,
+                                      cy2, cz2);
       const float4 en = lds_ld16(&s_entry[tid_late()]);
-      const float r1 = en.x, la1 = en.y, lo1 = en.z;
-      const int sx = r1 < r2 ? 1 : -1, sy = la1 < la2 ? 1 : -1, sz = lo1 < lo2 ? 1 : -1;
+      const float r1 = en.x;
+      const int sx = r1 < r2 ? 1 : -1;
+      int sy = sign_certified(en.y, la2, kLatErr), sz = sign_certified(en.z, lo2, kLonErr);
+      if (!ok2 || sy == 0 || sz == 0) {  // not certified (rare): both points glibc-exact
+        float la1 = 0.f, lo1 = 0.f;
+#pragma nounroll
+        for (int k = 0; k < 2; ++k) {  // the entry, then the exit point (one inlined copy)
+          const float e = k == 0 ? en.w + sceneEPS() : upper - sceneEPS();
+          float rr, la, lo;
+          to_spherical(A.org.x + dx * e, A.org.y + dy * e, A.org.z + dz * e, rr, la, lo);
+          if (k == 0) {
+            la1 = la;
+            lo1 = lo;
+          } else {
+            la2 = la;
+            lo2 = lo;
+          }
+        }
+        sy = la1 < la2 ? 1 : -1;
+        sz = lo1 < lo2 ? 1 : -1;
+        cy2 = project_axis_inv(la2, A.sbLo.y, A.invSb[1], A.dims.y);
+        cz2 = project_axis_inv(lo2, A.sbLo.z, A.invSb[2], A.dims.z);
+      }
       dd.x = (sx > 0 ? 1 : 0) | (sy > 0 ? 2 : 0) | (sz > 0 ? 4 : 0);
       dd.y = (int)((uint32_t)project_axis_inv(r2, A.sbLo.x, A.invSb[0], A.dims.x) + (uint32_t)sx);
-      dd.z = (int)((uint32_t)project_axis_inv(la2, A.sbLo.y, A.invSb[1], A.dims.y) + (uint32_t)sy);
-      dd.w = (int)((uint32_t)project_axis_inv(lo2, A.sbLo.z, A.invSb[2], A.dims.z) + (uint32_t)sz);
+      dd.z = (int)((uint32_t)cy2 + (uint32_t)sy);
+      dd.w = (int)((uint32_t)cz2 + (uint32_t)sz);
       lds_st16(&s_entry[tid_late()], __builtin_bit_cast(float4, dd));  // the entry point is not needed again
     } else {
       dd = __builtin_bit_cast(int4, lds_ld16(&s_entry[tid_late()]));
@@ -1540,14 +1579,18 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
         }
         lastRange = ae || i == 1 || rhi1 <= rlo1;
         cx = cy = cz = 0;
-        if (!ae) {  // cellID of the entry point (ShellAccel.h:121-124)
+        if (!ae) {  // cellID of the entry point (ShellAccel.h:121-124), certified fast lat/lon
           const float e1 = lower + sceneEPS();
+          const float x1 = A.org.x + dx * e1, y1 = A.org.y + dy * e1, z1 = A.org.z + dz * e1;
           float r1, la1, lo1;
-          to_spherical(A.org.x + dx * e1, A.org.y + dy * e1, A.org.z + dz * e1, r1, la1, lo1);
+          if (!spherical_fast(A, x1, y1, z1, r1, la1, lo1, cy, cz)) {  // rare: glibc-exact
+            to_spherical(x1, y1, z1, r1, la1, lo1);
+            cy = project_axis_inv(la1, A.sbLo.y, A.invSb[1], A.dims.y);
+            cz = project_axis_inv(lo1, A.sbLo.z, A.invSb[2], A.dims.z);
+          }
           cx = project_axis_inv(r1, A.sbLo.x, A.invSb[0], A.dims.x);
-          cy = project_axis_inv(la1, A.sbLo.y, A.invSb[1], A.dims.y);
-          cz = project_axis_inv(lo1, A.sbLo.z, A.invSb[2], A.dims.z);
-          if (!lastRange) lds_st16(&s_entry[tid_late()], make_float4(r1, la1, lo1, 0.f));
+          // for the exit's step (sign_certified) and its exact fallback (`lower`)
+          if (!lastRange) lds_st16(&s_entry[tid_late()], make_float4(r1, la1, lo1, lower));
         }
         t = lower;
         iter = 0;

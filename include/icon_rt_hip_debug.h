@@ -112,6 +112,13 @@ int irt_debug_counters(irt_context *ctx, unsigned long long *out16);
  * round exactly like the host glibc. */
 int irt_debug_device_math(int device, const float *a, const float *y, const float *x, int n,
                           float *out_asinf, float *out_atan2f);
+/* Exhaustive device error bounds of the certified fast lat/lon (irt_device.h), into out4:
+ * [0] max |fast_asin(x) - glibc asinf(x)| over every float in [-1, 1]; [1] / [2] max
+ * |fast_atan(q) - atan(q)| / |glibc atanf(q) - atan(q)| over every float q in [0, 2^59];
+ * [3] max relative error of the hardware reciprocal over every float in [2^-100, 2^100]. */
+int irt_debug_fast_math_bounds(int device, double *out4);
+/* The bounds the kernel assumes: out2 = {kLatErr, kLonErr}. */
+void irt_debug_fast_spherical_consts(float *out2);
 /* The device logf(1.f - rnd()) for every LCG low-24-bit value j (out: 2^24 floats, index j). */
 int irt_debug_device_woodcock_log(int device, float *out);
 /* The kernels' make_8bit(linear_to_srgb(x[i])) (csrc/irt_device.h srgb_byte) for n host

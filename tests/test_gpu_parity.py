@@ -73,6 +73,34 @@ def test_device_math_matches_glibc():
     assert np.array_equal(bits(oa[:200000]), bits(ha))
 
 
+def test_fast_spherical_bounds():
+    """The sdda entry/exit cells use fast asin/atan2 certified against glibc's
+    (irt_device.h): a cell or step sign is taken from the fast value only when every value
+    within kLatErr / kLonErr of it gives the same.  This proves those bounds exhaustively on
+    the device: every float asin argument, every float atan argument, every reciprocal."""
+    L = irt.lib()
+    L.irt_debug_fast_math_bounds.argtypes = [C.c_int, C.c_void_p]
+    L.irt_debug_fast_spherical_consts.argtypes = [C.c_void_p]
+    L.irt_debug_fast_spherical_consts.restype = None
+    out = np.zeros(4, np.float64)
+    assert L.irt_debug_fast_math_bounds(0, out.ctypes.data) == 0, L.irt_last_error()
+    e_asin, e_fatan, e_gatan, e_rcp = (float(v) for v in out)
+    assert all(np.isfinite(out)), out
+    consts = np.zeros(2, np.float32)
+    L.irt_debug_fast_spherical_consts(consts.ctypes.data)
+    lat_err, lon_err = (float(v) for v in consts)
+    pad = 2.0 ** -23  # rounding of v -+ E (ulp(pi) / 2 ~ 1.19e-7)
+    # asin: both paths evaluate glibc's argument z / r exactly; the bound is direct
+    assert e_asin + pad <= lat_err, (e_asin, lat_err)
+    # atan2: fast q = |y| rcp(|x|) (relative error <= e_rcp + 2^-24), glibc q = fl(|y/x|)
+    # (2^-24); atan's relative slope q / (1 + q^2) <= 1/2; two quadrant-step roundings per
+    # evaluation (<= ulp(pi/2)/2 + ulp(pi)/2)
+    quad = 2 * (2.0 ** -24 + 2.0 ** -23)
+    e_lon = e_fatan + e_gatan + 0.5005 * (e_rcp + 2.0 ** -24) + 0.5005 * 2.0 ** -24 + quad
+    assert e_lon + pad <= lon_err, (e_fatan, e_gatan, e_rcp, e_lon, lon_err)
+    assert e_rcp <= 2.0 ** -22
+
+
 CASES = [
     # (rootN, bisections, levels, W, camera, raygen)
     (1, 0, 4, 128, None, 0),        # C1-class: 20-face icosahedron, viewAll camera
