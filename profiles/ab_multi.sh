@@ -1,13 +1,13 @@
 #!/bin/bash
 # profiles/ab_multi.sh OUT "CONFIGS" LIB[@VAR=VAL[@VAR=VAL]]... : bench.py with each library
-# (IRT_LIB_PATH) and its environment overrides, round-robin, three rounds, on one box;
+# (IRT_LIB_PATH) and its environment overrides, round-robin, $ROUNDS rounds (default 3), on one box;
 # OUT/<lib-basename>[_<VAL>...]_<cfg>.jsonl.
 set -o pipefail
 OUT=${1:?out}; CONFIGS=${2:?configs}; shift 2
 mkdir -p "$OUT"
 for cfg in $CONFIGS; do
   steps=200; [ "$cfg" = c5 ] && steps=60; [ "$cfg" = c3s ] && steps=40; [ "$cfg" = c4 ] && steps=80
-  for round in 1 2 3; do
+  for round in $(seq 1 ${ROUNDS:-3}); do
     for spec in "$@"; do
       IFS=@ read -r lib envs <<< "$spec"
       n=$(basename "$lib" .so)
