@@ -134,6 +134,8 @@ struct irt_context {
   bool queueOn = false;
   uint32_t *d_queue = nullptr;
   int numCU = 0;
+  int queuePerCU = 0;   // IRT_QUEUE_WGS: workgroups per CU of a persistent launch (0: occupancy)
+  int lastQueueWG = 0;  // workgroups of the last persistent launch (irt_debug_get_queue)
   int schedPolicy = 2;         // IRT_SCHED: 1 tiles, 2 bands of tiles (a tile row; default), 3 reversed
   bool schedOrderValid = false;
   bool schedLastApplied = false;   // the last launch ran in a measured-cost order
@@ -533,7 +535,9 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   if (queued) {
     A.queue = c->d_queue + 2 * slot;
     A.numPackets = (uint32_t)numTiles * 64u * (uint32_t)numFrames;
-    queueWG = render_queue_wgs(A, c->variant, c->numCU, numTiles * 16 * numFrames);
+    queueWG = c->queuePerCU > 0 ? std::min(c->queuePerCU * c->numCU, numTiles * 16 * numFrames)
+                                : render_queue_wgs(A, c->variant, c->numCU, numTiles * 16 * numFrames);
+    c->lastQueueWG = queueWG;
   }
   // workgroups of this launch: 16 per 64x64 tile, x4 for the one-wave-workgroup variants
   // (irt_render.hip OPT_WAVEWG, bit 4194304), per frame; a persistent launch's resident ones
@@ -903,6 +907,7 @@ int irt_create_end(irt_context *c) {
   if (const char *e = getenv("IRT_COOP_RAMP")) c->coopRamp = std::min(6, std::max(0, atoi(e)));
   if (const char *e = getenv("IRT_PROBE_EXIT")) c->probeExit = atoi(e);
   if (const char *e = getenv("IRT_QUEUE")) c->queueOn = atoi(e) != 0;
+  if (const char *e = getenv("IRT_QUEUE_WGS")) c->queuePerCU = std::max(0, atoi(e));
   if ((rc = dalloc(c, &c->d_queue, 2 * irt_context::kSlots))) return rc;
   IRT_HIP(hipMemsetAsync(c->d_queue, 0, 2 * irt_context::kSlots * sizeof(uint32_t), c->stream));
   IRT_HIP(hipDeviceGetAttribute(&c->numCU, hipDeviceAttributeMultiprocessorCount, c->device));
@@ -1588,6 +1593,8 @@ extern "C" int irt_debug_set_queue(irt_context *c, int on) {
 }
 
 extern "C" int irt_debug_get_queue(const irt_context *c) { return c ? (c->queueOn ? 1 : 0) : -1; }
+
+extern "C" int irt_debug_queue_wgs(const irt_context *c) { return c ? c->lastQueueWG : -1; }
 
 extern "C" int irt_debug_set_variant(irt_context *c, int variant) {
   if (!c || !render_variant_available(variant)) {

@@ -101,6 +101,9 @@ int irt_debug_variants(int *out, int capacity);
  * of one workgroup per 16x16 block.  Frames are identical either way.  get: 1/0, -1 for NULL. */
 int irt_debug_set_queue(irt_context *ctx, int on);
 int irt_debug_get_queue(const irt_context *ctx);
+/* Workgroups of this context's last persistent launch (0 if none yet; -1 for NULL):
+ * every CU's resident share by the kernel's occupancy, or IRT_QUEUE_WGS per CU. */
+int irt_debug_queue_wgs(const irt_context *ctx);
 /* The raw per-frame counters of the last render (waits for it): [0] launched [1] in box
  * [2] sampleVolume calls [3] found [4] candidates; with the statistics variant bit also
  * [5] Woodcock draws [6] sum over waves of the per-wave max draws [7] zero-length leaves

@@ -124,7 +124,9 @@ def main():
             r["k"].append(tot.kernelMs / max(n, 1))
     for r in runs:
         k = float(np.median(r["k"]))
-        print(json.dumps({"config": args.config, "env": r["env"], **r["opt"],
+        L.irt_debug_queue_wgs.argtypes = [C.c_void_p]
+        qwg = int(L.irt_debug_queue_wgs(r["ctx"]._h))
+        print(json.dumps({"config": args.config, "env": r["env"], **r["opt"], "queue_wgs": qwg,
                           "identical": r["identical"], "kernel_ms": round(k, 4),
                           "step_ms": round(float(np.median(r["step"])), 4),
                           "mray_s": round(W * W / (k * 1e-3) / 1e6, 1),
