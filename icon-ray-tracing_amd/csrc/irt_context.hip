@@ -924,6 +924,7 @@ int irt_create_end(irt_context *c) {
                        make_float3(sb.lower.x, sb.lower.y, sb.lower.z),
                        make_float3(sb.upper.x, sb.upper.y, sb.upper.z), c->d_valueRanges, c->stream);
   }
+  prewarm_render(c->variant, c->stream);
   IRT_HIP(hipGetLastError());
   IRT_HIP(hipStreamSynchronize(c->stream));
   mark("shell build");

@@ -115,6 +115,9 @@ int render_queue_wgs(const RenderArgs &A, int variant, int numCU, int numBlocks)
 // numBlocks: the frame's 256-pixel blocks (grid launch), or the workgroups of a persistent
 // launch (A.queue, render_queue_wgs)
 void launch_render(const RenderArgs &A, int numBlocks, hipStream_t s, int variant);
+// one empty launch of the variant's raygen kernels (grid and persistent): the runtime's
+// first-launch setup happens at context creation, not in the first frame
+void prewarm_render(int variant, hipStream_t s);
 void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *found, float *value,
                          hipStream_t s, bool wave);
 void launch_shell_init(float *valueRanges, size_t numMCs, hipStream_t s);
