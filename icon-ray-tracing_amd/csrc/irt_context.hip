@@ -130,7 +130,7 @@ struct irt_context {
   int coopRamp = 1;
   int probeExit = 0;           // IRT_PROBE_EXIT (measurement only, RenderArgs::probeExit)
   // persistent launches (RenderArgs::queue, IRT_QUEUE=0|1): every resident wave pulls 8x8
-  // packets from a per-slot counter pair {next, done} (kSlots x 2 u32, zero between launches)
+  // packets from per-slot queue counters (kSlots x kQueueWords u32, zero between launches)
   bool queueOn = false;
   uint32_t *d_queue = nullptr;
   int numCU = 0;
@@ -533,7 +533,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   const bool queued = c->queueOn && numTiles > 0 && c->probeExit == 0 && render_queue_ok(A, c->variant);
   int queueWG = 0;
   if (queued) {
-    A.queue = c->d_queue + 2 * slot;
+    A.queue = c->d_queue + (size_t)kQueueWords * slot;
     A.numPackets = (uint32_t)numTiles * 64u * (uint32_t)numFrames;
     queueWG = c->queuePerCU > 0 ? std::min(c->queuePerCU * c->numCU, numTiles * 16 * numFrames)
                                 : render_queue_wgs(A, c->variant, c->numCU, numTiles * 16 * numFrames);
@@ -908,8 +908,8 @@ int irt_create_end(irt_context *c) {
   if (const char *e = getenv("IRT_PROBE_EXIT")) c->probeExit = atoi(e);
   if (const char *e = getenv("IRT_QUEUE")) c->queueOn = atoi(e) != 0;
   if (const char *e = getenv("IRT_QUEUE_WGS")) c->queuePerCU = std::max(0, atoi(e));
-  if ((rc = dalloc(c, &c->d_queue, 2 * irt_context::kSlots))) return rc;
-  IRT_HIP(hipMemsetAsync(c->d_queue, 0, 2 * irt_context::kSlots * sizeof(uint32_t), c->stream));
+  if ((rc = dalloc(c, &c->d_queue, (size_t)kQueueWords * irt_context::kSlots))) return rc;
+  IRT_HIP(hipMemsetAsync(c->d_queue, 0, (size_t)kQueueWords * irt_context::kSlots * sizeof(uint32_t), c->stream));
   IRT_HIP(hipDeviceGetAttribute(&c->numCU, hipDeviceAttributeMultiprocessorCount, c->device));
   IRT_HIP(hipHostGetDevicePointer((void **)&c->dh_counters, c->h_counters, 0));
   IRT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * irt_context::kSlots * sizeof(unsigned long long), c->stream));

@@ -86,12 +86,16 @@ struct RenderArgs {
   // the first woodcockFunc, 5 = after it
   int probeExit;
   // persistent launch (the thread pool's queue, common/thread_pool.h:146-161, per wave):
-  // non-null {next, done} pair -- every wave pulls 8x8-pixel packets (packet p: frame
-  // p / (numTiles*64), block (p >> 2) % (numTiles*16), the block's wave p & 3) from `next`
-  // until numPackets; the launch's last wave resets the pair for the next launch
+  // non-null: kQueueWords u32 of per-XCD packet counters and a done count -- every wave pulls
+  // 8x8-pixel packets (packet p: block p >> 2 over the launch's frames, the block's wave p & 3)
+  // until none is left; the launch's last wave resets the counters for the next launch
   uint32_t *queue;
   uint32_t numPackets;
 };
+// a persistent launch's queue words (irt_render.hip queue_take): 8 per-XCD counters and the
+// done count, each on its own 128-B line
+constexpr int kQueueLine = 32;
+constexpr int kQueueWords = 9 * kQueueLine;
 
 // Event counts kept per workgroup: [0] launched [1] inBox [2] locate [3] found [4] candidates
 constexpr int kCnt = 8;

@@ -54,6 +54,10 @@ enum : int {
   OPT_QUEUE = 16777216,  // the persistent launch (RenderArgs::queue): every resident wave pulls
                         // 8x8-pixel packets from the launch's counter; its own instantiation
                         // of the default kernel (k_render's grid launch is unchanged)
+  OPT_FASTSPH = 33554432,  // (A/B) the sdda entry/exit cells from the certified fast lat/lon
+                           // (irt_device.h spherical_fast, glibc-exact fallback near cell edges):
+                           // no gain at C3, C5 3 % slower (profiles/r04b/) -- the setup waits on
+                           // the majorant gather, not on asinf/atan2f
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
@@ -1346,6 +1350,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
            (size_t)ptid_late();
   };
   enum : int { kRange, kLeaf, kWait, kDone, kGrid, kGridNext };
+  constexpr bool kFastSph = (OPT & OPT_FASTSPH) != 0;
   constexpr bool grid = (OPT & OPT_GRID) != 0;
   const bool ae = A.raygen == 1;
   uint32_t st = 0;
@@ -1451,18 +1456,30 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     const float tnx = upper, tny = 0.f, tnz = 0.f;
     int4 dd;
     if (iter == 0) {
-      // exit point, step and stop (ShellAccel.h:125-132): the certified fast lat/lon
-      // (spherical_fast); the entry's (r1, la1, lo1, lower) wait in s_entry
+      // exit point, step and stop (ShellAccel.h:125-132); the entry's (r1, la1, lo1, lower)
+      // wait in s_entry.  OPT_FASTSPH: the certified fast lat/lon (spherical_fast).
       const float e2 = upper - sceneEPS();
       float r2, la2, lo2;
-      int cy2, cz2;
-      const bool ok2 = spherical_fast(A, A.org.x + dx * e2, A.org.y + dy * e2, A.org.z + dz * e2, r2, la2, lo2,
-                                      cy2, cz2);
+      int cy2 = 0, cz2 = 0;
+      bool ok2 = false;
+      if constexpr (kFastSph)
+        ok2 = spherical_fast(A, A.org.x + dx * e2, A.org.y + dy * e2, A.org.z + dz * e2, r2, la2, lo2, cy2, cz2);
+      else
+        to_spherical(A.org.x + dx * e2, A.org.y + dy * e2, A.org.z + dz * e2, r2, la2, lo2);
       const float4 en = lds_ld16(&s_entry[tid_late()]);
       const float r1 = en.x;
       const int sx = r1 < r2 ? 1 : -1;
-      int sy = sign_certified(en.y, la2, kLatErr), sz = sign_certified(en.z, lo2, kLonErr);
-      if (!ok2 || sy == 0 || sz == 0) {  // not certified (rare): both points glibc-exact
+      int sy, sz;
+      if constexpr (!kFastSph) {
+        sy = en.y < la2 ? 1 : -1;
+        sz = en.z < lo2 ? 1 : -1;
+        cy2 = project_axis_inv(la2, A.sbLo.y, A.invSb[1], A.dims.y);
+        cz2 = project_axis_inv(lo2, A.sbLo.z, A.invSb[2], A.dims.z);
+      } else {
+        sy = sign_certified(en.y, la2, kLatErr);
+        sz = sign_certified(en.z, lo2, kLonErr);
+      }
+      if (kFastSph && (!ok2 || sy == 0 || sz == 0)) {  // not certified (rare): both points glibc-exact
         float la1 = 0.f, lo1 = 0.f;
 #pragma nounroll
         for (int k = 0; k < 2; ++k) {  // the entry, then the exit point (one inlined copy)
@@ -1579,11 +1596,12 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
         }
         lastRange = ae || i == 1 || rhi1 <= rlo1;
         cx = cy = cz = 0;
-        if (!ae) {  // cellID of the entry point (ShellAccel.h:121-124), certified fast lat/lon
+        if (!ae) {  // cellID of the entry point (ShellAccel.h:121-124)
           const float e1 = lower + sceneEPS();
           const float x1 = A.org.x + dx * e1, y1 = A.org.y + dy * e1, z1 = A.org.z + dz * e1;
           float r1, la1, lo1;
-          if (!spherical_fast(A, x1, y1, z1, r1, la1, lo1, cy, cz)) {  // rare: glibc-exact
+          // OPT_FASTSPH: the certified fast lat/lon, glibc-exact when not certified
+          if (!(kFastSph && spherical_fast(A, x1, y1, z1, r1, la1, lo1, cy, cz))) {
             to_spherical(x1, y1, z1, r1, la1, lo1);
             cy = project_axis_inv(la1, A.sbLo.y, A.invSb[1], A.dims.y);
             cz = project_axis_inv(lo1, A.sbLo.z, A.invSb[2], A.dims.z);
@@ -1686,21 +1704,44 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   }
 }
 
-// The persistent launch's packet counter {next, done} (RenderArgs::queue): one wave-wide
-// fetch (lane 0's atomic, read by every lane), and the launch's end -- the last wave to finish
-// resets the pair for the next launch on it (every wave's last fetch precedes its done count).
-__device__ __forceinline__ uint32_t queue_next(uint32_t *q) {
-  uint32_t v = 0u;
-  if (__lane_id() == 0) v = atomicAdd(&q[0], 1u);
-  return __builtin_amdgcn_readfirstlane(v);
+// The persistent launch's packet queues (RenderArgs::queue, kQueueWords u32 per launch slot):
+// one counter per XCD, each on its own 128-B line, and the launch's done count.  XCD x owns
+// the 16x16 blocks g (over every frame of the launch) with g % 8 == x -- the grid launch's
+// workgroup-to-XCD deal, so each XCD's L2 sees the blocks it would have seen -- and hands out
+// their packets in order; a wave on XCD x takes from queue x, and once that is exhausted from
+// the others in turn (a plain load first, so finished queues cost no read-modify-write).  One
+// counter for the whole launch made every wave's fetch a device-scope atomic on one address:
+// 0.40 ms per C3 frame against 0.09 (profiles/r04b/).  The launch's last wave resets every
+// counter (each wave's last fetch precedes its done count).
+constexpr int kQueueXcds = 8;
+struct QueueCursor {
+  int cur;        // the queue this wave takes from
+  uint32_t dead;  // bit x: queue x is exhausted
+};
+__device__ __forceinline__ uint32_t queue_take(uint32_t *Q, uint32_t numBlocksAll, QueueCursor &c) {
+  while (c.dead != (1u << kQueueXcds) - 1u) {
+    const uint32_t x = (uint32_t)c.cur;
+    // blocks g < numBlocksAll with g % 8 == x, four packets each
+    const uint32_t limit = numBlocksAll > x ? 4u * ((numBlocksAll - x + kQueueXcds - 1) / kQueueXcds) : 0u;
+    uint32_t v = 0xFFFFFFFFu;
+    if (__lane_id() == 0) {
+      uint32_t *q = Q + (size_t)x * kQueueLine;
+      if (__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < limit) v = atomicAdd(q, 1u);
+    }
+    v = __builtin_amdgcn_readfirstlane(v);
+    if (v < limit) return ((v >> 2) * kQueueXcds + x) * 4u + (v & 3u);  // block g's packet v & 3
+    c.dead |= 1u << x;
+    c.cur = (c.cur + 1) & (kQueueXcds - 1);
+  }
+  return 0xFFFFFFFFu;
 }
-__device__ __forceinline__ void queue_done(uint32_t *q) {
+__device__ __forceinline__ void queue_done(uint32_t *Q) {
   if (__lane_id() == 0) {
     __threadfence();
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    if (atomicAdd(&q[1], 1u) == waves - 1u) {
-      __hip_atomic_store(&q[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&q[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (atomicAdd(&Q[kQueueXcds * kQueueLine], 1u) == waves - 1u) {
+      for (int x = 0; x <= kQueueXcds; ++x)
+        __hip_atomic_store(&Q[(size_t)x * kQueueLine], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1794,18 +1835,20 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
     constexpr bool queued = (OPT & OPT_QUEUE) != 0;
     static_assert(!queued || (!wavewg && (OPT & (OPT_STATS | OPT_TIMING | OPT_HDRLDS)) == 0),
                   "persistent launches: 256-thread workgroups, no per-wave statistics");
-    const uint32_t perFrame = (uint32_t)A.numTiles * 64u;  // packets per frame
-    uint32_t p = queued ? queue_next(A.queue) : 0u;
-    bool more = !queued || p < A.numPackets;
+    const uint32_t perFrame = (uint32_t)A.numTiles * 16u;  // blocks per frame
+    const uint32_t blocksAll = perFrame * (uint32_t)A.numSamples;
+    QueueCursor qc = {(int)(blockIdx.x & (kQueueXcds - 1)), 0u};  // workgroup b runs on XCD b % 8
+    uint32_t p = queued ? queue_take(A.queue, blocksAll, qc) : 0u;
+    bool more = !queued || p != 0xFFFFFFFFu;
     while (more) {
       uint32_t pblk = blk, nx = 0u;
       int pw = wavewg ? (int)(blockIdx.x & 3u) : (tid >> 6), frame = (int)blockIdx.y;
       if constexpr (queued) {
-        nx = queue_next(A.queue);
-        frame = A.numSamples > 1 ? (int)(p / perFrame) : 0;
-        const uint32_t q = p - (uint32_t)frame * perFrame;
-        pblk = q >> 2;
-        pw = (int)(q & 3u);
+        nx = queue_take(A.queue, blocksAll, qc);
+        const uint32_t g = p >> 2;  // the packet's block over all frames
+        frame = A.numSamples > 1 ? (int)(g / perFrame) : 0;
+        pblk = g - (uint32_t)frame * perFrame;
+        pw = (int)(p & 3u);
       }
       pblk = __builtin_amdgcn_readfirstlane(pblk);
       pw = __builtin_amdgcn_readfirstlane(pw);
@@ -1842,7 +1885,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
                                pblk, pw, frame);
       }
       p = nx;
-      more = queued && p < A.numPackets;
+      more = queued && p != 0xFFFFFFFFu;
     }
     if constexpr (queued) queue_done(A.queue);
     T.flush_coop();
@@ -2021,7 +2064,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808)
 #else
 #define IRT_VARIANTS(X) X(5376) X(36864)
 #endif

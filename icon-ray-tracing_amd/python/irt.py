@@ -39,7 +39,8 @@ MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
 # candidate scans, 529408 per-region shader-clock timing (profiles/probe.py), 1053696
 # LDS-staged cell headers, 2102272 / 2102528 less LDS per workgroup, 8393728 / 8393984
 # every candidate dealt out, 6296576 / 6296832 one-wave workgroups, 529664 the timing variant
-# at 5 waves/SIMD, 2102784 the lean-LDS build at 6 waves/SIMD.
+# at 5 waves/SIMD, 2102784 the lean-LDS build at 6 waves/SIMD, 33559808 the certified fast
+# lat/lon for the sdda cells (OPT_FASTSPH).
 ALL_LIB_PATH = os.path.join(PKG_DIR, "libicon_rt_hip_all.so")
 
 
