@@ -1,6 +1,6 @@
 #!/bin/bash
 # profiles/pmc_mix.sh OUT LIB... : one rocprofv3 --pmc pass per library (IRT_LIB_PATH) with
-# the SQ instruction-mix counters over a C3 bench run; prints per-wave averages for k_render.
+# the SQ instruction-mix counters over a bench run (C3, or $CONFIG); prints per-wave averages for k_render.
 set -uo pipefail
 OUT=${1:?out}; shift
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -11,7 +11,7 @@ for lib in "$@"; do
   n=$(basename "$lib" .so)
   IRT_LIB_PATH="$ROOT/$lib" timeout -s KILL 120 rocprofv3 --kernel-trace \
     --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU \
-    --output-format csv -d "$ROOT/$OUT/$n" -o run -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline \
+    --output-format csv -d "$ROOT/$OUT/$n" -o run -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --config ${CONFIG:-c3} \
     > "$ROOT/$OUT/$n.json" 2> "$ROOT/$OUT/$n.err" || exit 1
 done
 python3 - "$ROOT/$OUT" <<'PY'

@@ -8,5 +8,15 @@ bash profiles/run_profiles.sh r04d_c3 --config c3 > /dev/null 2>&1 || exit 1
 bash profiles/run_profiles.sh r04d_c3s --config c3s > /dev/null 2>&1 || exit 1
 bash profiles/run_profiles.sh r04d_c5 --config c5 > /dev/null 2>&1 || exit 1
 bash profiles/pmc_mix.sh gpurun_out/r04d/mix $L ab/lib_base.so > gpurun_out/r04d/mix.txt 2>&1 || exit 1
+CONFIG=c3s bash profiles/pmc_mix.sh gpurun_out/r04d/mix_c3s $L > gpurun_out/r04d/mix_c3s.txt 2>&1 || exit 1
 bash profiles/pmc_latency.sh r04d_c3s --config c3s > /dev/null 2>&1 || exit 1
 bash profiles/pmc_latency.sh r04d_c3 --config c3 > /dev/null 2>&1 || exit 1
+# every rank's share of a frame-mode (strong) step on one GPU: grid launch, persistent launch,
+# whole-wave speculation from the first round
+for cfg in c3 c4; do
+  for envs in "" "IRT_QUEUE=1" "IRT_COOP_MAXLG=6"; do
+    n=${envs:-base}; n=${n//=/_}
+    env $envs timeout -k 10 300 python3 profiles/rank_step.py --config $cfg --modes frame --deals dealt \
+      > gpurun_out/r04d/rank_${cfg}_$n.jsonl 2> gpurun_out/r04d/rank_${cfg}_$n.err || exit 1
+  done
+done
