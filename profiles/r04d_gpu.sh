@@ -20,3 +20,9 @@ for cfg in c3 c4; do
       > gpurun_out/r04d/rank_${cfg}_$n.jsonl 2> gpurun_out/r04d/rank_${cfg}_$n.err || exit 1
   done
 done
+# the instruction mix of the launch stopped at successive points (IRT_PROBE_EXIT: 3 after ray
+# generation and boxTest, 4 at the first woodcockFunc, 5 after it), C3 and C3s
+for ex in 3 4 5; do
+  IRT_PROBE_EXIT=$ex bash profiles/pmc_mix.sh gpurun_out/r04d/mix_exit$ex $L > gpurun_out/r04d/mix_exit$ex.txt 2>&1 || exit 1
+  IRT_PROBE_EXIT=$ex CONFIG=c3s bash profiles/pmc_mix.sh gpurun_out/r04d/mix_c3s_exit$ex $L > gpurun_out/r04d/mix_c3s_exit$ex.txt 2>&1 || exit 1
+done
