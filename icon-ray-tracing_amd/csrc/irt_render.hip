@@ -58,6 +58,10 @@ enum : int {
                            // (irt_device.h spherical_fast, glibc-exact fallback near cell edges):
                            // no gain at C3, C5 3 % slower (profiles/r04b/) -- the setup waits on
                            // the majorant gather, not on asinf/atan2f
+  OPT_HDRPF = 67108864,  // (A/B) at each range's entry point, touch its cube-map header line
+                         // (an LDS-DMA load of one word into a dummy LDS slot, issued before the
+                         // entry's toSpherical and waited for with the majorant's gather), so
+                         // that the first Woodcock sample's header read hits the cache
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
@@ -1319,7 +1323,8 @@ template <int OPT>
 __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
                                                   const float *s_th, int4 *s_dda, float4 *s_entry,
                                                   float4 *s_acc, CoopWave &W, ScanWave *SW, const uint2 *jmp,
-                                                  int tid, int accumID, uint32_t blk, int pwave, int frame) {
+                                                  int tid, int accumID, uint32_t blk, int pwave, int frame,
+                                                  uint32_t *s_pf) {
   // At 5+ waves/SIMD the pixel's output addresses are recomputed where they are used (from the
   // workgroup's uniform block index), not held in VGPRs through the rounds: a progressive
   // batch's sample slot (k_accumulate reads it) and the frame index.  (At 4 waves there is
@@ -1599,6 +1604,12 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
         if (!ae) {  // cellID of the entry point (ShellAccel.h:121-124)
           const float e1 = lower + sceneEPS();
           const float x1 = A.org.x + dx * e1, y1 = A.org.y + dy * e1, z1 = A.org.z + dz * e1;
+          if constexpr ((OPT & OPT_HDRPF) != 0) {
+            if (A.numCells != 0)
+              __builtin_amdgcn_global_load_lds(
+                  (const void *)(A.binHdr + (size_t)cubemap_cell_fast(x1, y1, z1, A.G) * (kBinHdrWords / 4)),
+                  (__attribute__((address_space(3))) void *)s_pf, 4, 0, 0);
+          }
           float r1, la1, lo1;
           // OPT_FASTSPH: the certified fast lat/lon, glibc-exact when not certified
           if (!(kFastSph && spherical_fast(A, x1, y1, z1, r1, la1, lo1, cy, cz))) {
@@ -1627,6 +1638,59 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
         ++i;
         phase = kRange;
         continue;
+      }
+      if (!ae && zeroLen && iter >= 1 && upper > 0.f) {
+        // The zero-length leaves after a non-last range's first leaf (see render_pixel): with
+        // upper > 0 the walk steps cy and cz together (tnext = {upper, 0, 0}, t = 0) until one reaches its
+        // stop, and each leaf only reads its majorant and, if positive, consumes one draw
+        // (deviceCode.cu:161-166, the fast path above).  The leaves are known in advance, so
+        // their majorants are gathered kWalk at a time (independent loads, one round trip)
+        // instead of one dependent gather per leaf; the draws are then applied in order, and
+        // a leaf that needs the full woodcockFunc (its draw's low 24 bits zero, or q out of
+        // range) is handed to the single-leaf path below.  Same leaves, draws and state.
+        const int4 dd = __builtin_bit_cast(int4, lds_ld16(&s_entry[tid_late()]));
+        const int sy = (dd.x & 2) ? 1 : -1, sz = (dd.x & 4) ? 1 : -1;
+        const int ky = (dd.z - cy) * sy, kz = (dd.w - cz) * sz;  // leaves left: min(ky, kz)
+        if (ky >= 1 && kz >= 1 && iter + min(ky, kz) < (1 << 22)) {
+          constexpr int kWalk = 8;
+          const int n = min(min(ky, kz), kWalk);
+          const int dimx = opaque_u(A.dims.x), dimy = opaque_u(A.dims.y);
+          const uint32_t wx = (uint32_t)wrap_coord(cx, dimx);
+          float mj[kWalk];
+#pragma unroll
+          for (int j = 0; j < kWalk; ++j) {
+            mj[j] = 0.f;
+            if (j < n) {
+              const uint32_t leaf = (uint32_t)wrap_coord(cz + j * sz, A.dims.z) * (uint32_t)dimx * (uint32_t)dimy +
+                                    (uint32_t)wrap_coord(cy + j * sy, dimy) * (uint32_t)dimx + wx;
+              mj[j] = A.maxOp[leaf];
+            }
+          }
+          int done = n;  // leaves taken by the fast path
+#pragma unroll
+          for (int j = 0; j < kWalk; ++j) {
+            if (j < done) {
+              const float q = mj[j] / A.unitDistance;
+              const uint32_t nx = lcg_next(st);
+              if (!(mj[j] > 0.f)) {
+              } else if (q > 0.f && q <= 1e30f && (nx & 0x00FFFFFFu) != 0u) {
+                st = nx;
+              } else {
+                done = j;  // this leaf needs woodcockFunc: the single-leaf path takes it
+              }
+            }
+          }
+          if constexpr ((OPT & OPT_STATS) != 0) T.cnt.deg += (uint32_t)done;
+          cy += done * sy;
+          cz += done * sz;
+          iter += done;
+          if (done == min(ky, kz)) {  // the walk's stop (render_pixel's loop tail)
+            ++i;
+            phase = kRange;
+            continue;
+          }
+          if (done == n) continue;  // the next batch
+        }
       }
       if constexpr ((OPT & OPT_STATS) != 0) T.cnt.deg += zeroLen ? 1u : 0u;
       maj = 1.f;
@@ -1765,6 +1829,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
   __shared__ ScanWave s_scan[Tracer<OPT>::kWaveScan ? kW : 1];  // its wave-wide candidate scan
   __shared__ HdrStage s_hdrs[(OPT & OPT_HDRLDS) ? kW : 1];       // OPT_HDRLDS: staged header lines
   __shared__ float4 s_acc[lean ? 1 : 256];  // kCoop: the accum pixels, prefetched
+  __shared__ uint32_t s_pf[(OPT & OPT_HDRPF) ? 256 : 1];  // OPT_HDRPF: header touches land here
   __shared__ uint2 s_jmp[kLcgJumps];  // lcg_jump's {mul, add} (kLcgJumpTab)
   const int tid = threadIdx.x;
   if (A.probeExit == 1) return;  // measurement only
@@ -1875,14 +1940,14 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
         launched += (uint32_t)__popcll(__ballot(ppx.active));
         render_pixel_coop<OPT>(AL, TL, ppx, lean ? AL.srgbTh : s_th, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
                                &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, AL.accumID + frame,
-                               pblk, pw, frame);
+                               pblk, pw, frame, s_pf + ((OPT & OPT_HDRPF) ? (ltid & ~63) : 0));
         TL.flush_coop();  // this packet's counts (nothing carried from packet to packet)
       } else {
         const Pixel ppx = pixel_of(A, pblk, pw * 64 + (ltid & 63));
         launched += (uint32_t)__popcll(__ballot(ppx.active));
         render_pixel_coop<OPT>(A, T, ppx, th_p, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
                                &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, A.accumID + frame,
-                               pblk, pw, frame);
+                               pblk, pw, frame, s_pf + ((OPT & OPT_HDRPF) ? (ltid & ~63) : 0));
       }
       p = nx;
       more = queued && p != 0xFFFFFFFFu;
@@ -2064,7 +2129,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(67114240)
 #else
 #define IRT_VARIANTS(X) X(5376) X(36864)
 #endif
