@@ -1773,10 +1773,10 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
 // the 16x16 blocks g (over every frame of the launch) with g % 8 == x -- the grid launch's
 // workgroup-to-XCD deal, so each XCD's L2 sees the blocks it would have seen -- and hands out
 // their packets in order; a wave on XCD x takes from queue x, and once that is exhausted from
-// the others in turn (a plain load first, so finished queues cost no read-modify-write).  One
-// counter for the whole launch made every wave's fetch a device-scope atomic on one address:
-// 0.40 ms per C3 frame against 0.09 (profiles/r04b/).  The launch's last wave resets every
-// counter (each wave's last fetch precedes its done count).
+// the others in turn (a plain load first, so finished queues cost no read-modify-write).  (One
+// counter for the whole launch, with the next fetch issued at each packet's start: 0.40 ms per
+// C3 frame against 0.09, profiles/r04b/.)  The launch's last wave resets every counter (each
+// wave's last fetch precedes its done count).
 constexpr int kQueueXcds = 8;
 struct QueueCursor {
   int cur;        // the queue this wave takes from
@@ -1909,7 +1909,6 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
       uint32_t pblk = blk, nx = 0u;
       int pw = wavewg ? (int)(blockIdx.x & 3u) : (tid >> 6), frame = (int)blockIdx.y;
       if constexpr (queued) {
-        nx = queue_take(A.queue, blocksAll, qc);
         const uint32_t g = p >> 2;  // the packet's block over all frames
         frame = A.numSamples > 1 ? (int)(g / perFrame) : 0;
         pblk = g - (uint32_t)frame * perFrame;
@@ -1949,6 +1948,10 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
                                &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, A.accumID + frame,
                                pblk, pw, frame, s_pf + ((OPT & OPT_HDRPF) ? (ltid & ~63) : 0));
       }
+      // the next packet once this one is done: a fetch issued at the packet's start (to
+      // hide its round trip) made the packet's first gather wait for it as well (vector
+      // memory counts retire in order) -- 0.32 ms per C3 frame against 0.09 (profiles/r04c/)
+      if constexpr (queued) nx = queue_take(A.queue, blocksAll, qc);
       p = nx;
       more = queued && p != 0xFFFFFFFFu;
     }
