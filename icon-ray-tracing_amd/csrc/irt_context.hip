@@ -57,6 +57,7 @@ struct irt_context {
   bool slotBlock[32] = {};      // whether k_stats_out copied the slot's 16-counter block
   bool lastBlock = false;       // ... for the previous launch (which zeroed this slot's)
   bool wgCountsOn = true;       // IRT_COUNTERS=atomic: device-scope atomics instead
+  bool statsOff = false;        // irt_set_statistics(ctx, 0): no counts at all
   int countersProbe = 0;        // measurement only: IRT_COUNTERS=off (no counts), =device
                                 // (per-workgroup stores into device memory, never read)
   uint32_t *d_probeCounts = nullptr;
@@ -106,6 +107,13 @@ struct irt_context {
   hipEvent_t ev0[kSlots] = {}, ev1[kSlots] = {};  // kernel timing
   hipEvent_t evDone[kSlots] = {};                  // counters landed in h_counters
   bool pending[kSlots] = {};
+  // evDone[i] is recorded after launch i only every kDoneEvery-th launch, at a stream switch,
+  // or when asked for (done_event): each marker on the queue costs its launch ~1-2 us, and a
+  // later marker on the same stream completes after launch i as well
+  static constexpr int kDoneEvery = 8;
+  bool evRec[kSlots] = {};
+  hipStream_t slotStream[kSlots] = {};
+  long long slotLaunch[kSlots] = {};
   long long launches = 0;     // slot of launch i: i % kSlots
   irt_render_stats stats{};
   unsigned long long h_last[16] = {};
@@ -244,9 +252,40 @@ int tile_table(irt_context *c, const int32_t *ids, size_t n, int lo, int total, 
   return IRT_OK;
 }
 
+// An event that completes after the launch in slot i (pending): its own marker if recorded,
+// else the first later marker of the same stream, else a marker recorded now on that stream.
+hipEvent_t done_event(irt_context *c, int i) {
+  const long long L = c->slotLaunch[i];
+  for (int k = 0; k < irt_context::kSlots; ++k) {
+    const int j = (i + k) % irt_context::kSlots;
+    if (!c->pending[j] || c->slotLaunch[j] != L + k || c->slotStream[j] != c->slotStream[i]) break;
+    if (c->evRec[j]) return c->evDone[j];
+  }
+  // the newest launch on that stream: mark it now
+  int last = i;
+  for (int k = 1; k < irt_context::kSlots; ++k) {
+    const int j = (i + k) % irt_context::kSlots;
+    if (!c->pending[j] || c->slotLaunch[j] != L + k || c->slotStream[j] != c->slotStream[i]) break;
+    last = j;
+  }
+  if (hipEventRecord(c->evDone[last], c->slotStream[last]) == hipSuccess) {
+    c->evRec[last] = true;
+    return c->evDone[last];
+  }
+  // that stream is gone (destroyed by the caller after its last launch): wait for the device
+  (void)hipGetLastError();
+  (void)hipDeviceSynchronize();
+  return nullptr;
+}
+// waits for the launch in slot i (pending)
+hipError_t wait_slot(irt_context *c, int i) {
+  const hipEvent_t e = done_event(c, i);
+  return e ? hipEventSynchronize(e) : hipSuccess;
+}
+
 int finish_slot(irt_context *c, int i) {
   if (!c->pending[i]) return IRT_OK;
-  IRT_HIP(hipEventSynchronize(c->evDone[i]));
+  IRT_HIP(wait_slot(c, i));
   float ms = 0.f;
   if (c->timed[i]) {
     IRT_HIP(hipEventElapsedTime(&ms, c->ev0[i], c->ev1[i]));
@@ -330,7 +369,7 @@ int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int t
   int bestSlot = -1;
   for (int i = 0; i < irt_context::kSlots; ++i)
     if (c->schedCopied[i] > c->schedSrc && c->schedCopied[i] >= c->schedSwitch &&
-        c->schedCopied[i] > best && hipEventQuery(c->evDone[i]) == hipSuccess) {
+        c->schedCopied[i] > best && (!c->pending[i] || (c->evRec[i] && hipEventQuery(c->evDone[i]) == hipSuccess))) {
       best = c->schedCopied[i];
       bestSlot = i;
     }
@@ -570,7 +609,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   }
   A.wgCounts = useWG && c->wgCountsOn ? c->dh_wgCounts + (size_t)slot * c->wgCap * kCnt : nullptr;
   const bool statsVariant = (c->variant & (32768 | 524288)) != 0;  // statistics, timing
-  if (c->countersProbe == 1) {
+  if (c->countersProbe == 1 || c->statsOff) {
     // measurement only: no counts -- except that the statistics and timing variants add into
     // the counter block unconditionally, so it stays
     A.wgCounts = nullptr;
@@ -630,7 +669,11 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   if (block && !c->lastBlock) IRT_HIP(hipMemsetAsync(A.counters, 0, 16 * sizeof(unsigned long long), s));
   if (c->launches > 0 && s != c->lastStream) {
     // this slot may have been zeroed by the previous launch's k_stats_out on another stream
-    IRT_HIP(hipStreamWaitEvent(s, c->evDone[(c->launches - 1) % irt_context::kSlots], 0));
+    const int prev = (int)((c->launches - 1) % irt_context::kSlots);
+    if (c->pending[prev]) {
+      const hipEvent_t e = done_event(c, prev);
+      if (e) IRT_HIP(hipStreamWaitEvent(s, e, 0));
+    }
   }
   c->lastStream = s;
   c->timed[slot] = c->launches % c->timingEvery == 0;
@@ -647,13 +690,16 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   }
   c->slotBlock[slot] = block;
   c->lastBlock = block;
-  c->slotWG[slot] = (A.wgCounts && c->countersProbe == 0 && numTiles > 0) ? numWG : 0;
+  c->slotWG[slot] = (A.wgCounts && c->countersProbe == 0 && !c->statsOff && numTiles > 0) ? numWG : 0;
   c->schedCopied[slot] = -1;
   if (copyCosts) {
     c->schedCopied[slot] = c->launches;
     c->schedLastCopy = c->launches;
   }
-  IRT_HIP(hipEventRecord(c->evDone[slot], s));
+  c->slotStream[slot] = s;
+  c->slotLaunch[slot] = c->launches;
+  c->evRec[slot] = c->launches % irt_context::kDoneEvery == irt_context::kDoneEvery - 1 || copyCosts;
+  if (c->evRec[slot]) IRT_HIP(hipEventRecord(c->evDone[slot], s));
   c->pending[slot] = true;
   ++c->launches;
   return IRT_OK;
@@ -1090,7 +1136,10 @@ int irt_set_transfunc(irt_context *c, const irt_vec4f *lut, int size, irt_box1f 
   IRT_HIP(hipSetDevice(c->device));
   // frames still in flight on the caller's stream read the LUT and the majorants: the
   // update is serialized after them, as the reference's TF handler is after its launches
-  if (c->launches > 0) IRT_HIP(hipEventSynchronize(c->evDone[(c->launches - 1) % irt_context::kSlots]));
+  if (c->launches > 0) {
+    const int last = (int)((c->launches - 1) % irt_context::kSlots);
+    if (c->pending[last]) IRT_HIP(wait_slot(c, last));
+  }
   if (size > c->lutCap) {
     if (c->d_lut) {
       IRT_HIP(hipStreamSynchronize(c->stream));
@@ -1583,6 +1632,15 @@ extern "C" int irt_debug_context_array(const irt_context *c, int which, void *ds
 extern "C" int irt_debug_get_variant(const irt_context *c) { return c ? c->variant : -1; }
 
 extern "C" int irt_debug_variants(int *out, int capacity) { return render_variants(out, capacity); }
+
+extern "C" int irt_set_statistics(irt_context *c, int on) {
+  if (!c) {
+    set_error("irt_set_statistics: null context");
+    return IRT_E_INVALID;
+  }
+  c->statsOff = on == 0;
+  return IRT_OK;
+}
 
 extern "C" int irt_debug_set_queue(irt_context *c, int on) {
   if (!c) {

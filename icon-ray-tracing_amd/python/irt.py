@@ -516,6 +516,13 @@ class Context:
         _check(lib().irt_set_transfunc(self._h, _ptr(lut), lut.shape[0], box1(*value_range),
                                        float(opacity_scale)), "irt_set_transfunc")
 
+    def set_statistics(self, on: bool):
+        """Per-launch event counts on (default) or off (irt_set_statistics); frames are
+        identical either way, the counts read 0 while off."""
+        L = lib()
+        L.irt_set_statistics.argtypes = [C.c_void_p, C.c_int]
+        _check(L.irt_set_statistics(self._h, 1 if on else 0), "irt_set_statistics")
+
     def set_queue(self, on: bool):
         """Persistent launches (every resident wave pulls 8x8 packets from a per-launch
         counter) on or off for this context; frames are identical either way."""

@@ -236,6 +236,12 @@ int irt_reset_render_stats_total(irt_context *ctx);
  * frame.  irt_render_stats.kernelMs of a launch is that of the most recent timed launch.
  * No counterpart in the reference, which times on the host (pipeline.cu:1062-1073). */
 int irt_set_timing_interval(irt_context *ctx, int every);
+/* The per-launch event counts of irt_render_stats (rays, sampleVolume calls, samples found,
+ * candidates) on (1, the default) or off (0).  Counting costs each launch a store of every
+ * workgroup's counts into pinned host memory -- ~1.5 % of a C3 frame, more of a small
+ * multi-GPU share -- and the reference renders without it; with counting off the counts
+ * read 0 (kernelMs stays).  Frames are identical either way.  No reference counterpart. */
+int irt_set_statistics(irt_context *ctx, int on);
 
 /* buildCuBQLAccel (hostCode.cu:557-649) for IRT_MODE_CUBQL: the wedges of every (cell,
  * layer) -- corners toCartesian(height[h|h+1], lat, lon), scalar

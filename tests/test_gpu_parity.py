@@ -874,3 +874,33 @@ def test_persistent_launch_identical():
     for (a0, a1), (b0, b1) in zip(tiles(True), tiles(False)):
         assert np.array_equal(a0, b0) and np.array_equal(a1, b1)
     ctx.close()
+
+
+def test_statistics_off_renders_the_same_frames():
+    """irt_set_statistics(ctx, 0): no per-workgroup count stores -- the same pixels, the
+    counts read 0; back on, the counts are the oracle's again.  Also many launches in a row
+    with the done markers recorded only every 8th launch (the ring's covering events)."""
+    import torch
+    cells = irt.synth_grid(2, 3, 90)
+    W = 96
+    a_ref, f_ref, st_ref, _ = oracle_frame(cells, W, W, camera=FRAMING)
+    setup = irt.setup_frame(cells, W, W, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    fb = torch.zeros(W * W, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(W * W * 4, dtype=torch.float32, device="cuda")
+    for on in (False, True, False, True):
+        ctx.set_statistics(on)
+        for _ in range(11):  # past a done-marker boundary each time
+            acc.zero_()
+            fb.zero_()
+            ctx.render(setup.lp, W, W, fb.data_ptr(), acc.data_ptr())
+        st = ctx.stats()
+        a = acc.cpu().numpy().reshape(W, W, 4)
+        f = fb.cpu().numpy().reshape(W, W).view(np.uint32)
+        assert_same_frame(a, f, a_ref, f_ref, f"statistics {'on' if on else 'off'}")
+        if on:
+            assert (st.locateCalls, st.samplesFound) == (st_ref[0].locate_calls, st_ref[0].samples_found)
+        else:
+            assert (st.raysLaunched, st.locateCalls, st.samplesFound) == (0, 0, 0)
+    ctx.close()
