@@ -219,6 +219,11 @@ def main():
     ap.add_argument("--force-dist", action="store_true",
                     help="(overhead check) run the multi-rank path -- tile render, RCCL gather, "
                          "unpack -- even with one rank (under torchrun)")
+    ap.add_argument("--stats", default="off", choices=["on", "off"],
+                    help="per-launch event counts (irt_set_statistics) inside the timed loop.  "
+                         "off (default): the product renders without them, as the reference "
+                         "does; the counts the roofline needs come from rendering the same "
+                         "steps again afterwards with counting on (untimed, identical frames)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path with host-staged collectives "
                          "(ranks may share a GPU); nccl (RCCL) is the measured path")
@@ -325,6 +330,7 @@ def main():
     log(f"[rank {rank}] warmup: last launch kernel {st.kernelMs:.3f} ms, {st.samplesFound} "
         f"samples, {st.candidatesTested} candidates")
     ctx.reset_stats_total()
+    ctx.set_statistics(args.stats == "on")
     torch.cuda.synchronize()
     if dist_path:
         dist.barrier()
@@ -340,7 +346,20 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
-    tot, launches = ctx.stats_total()
+    tot, launches = ctx.stats_total()  # kernel time of the timed launches (HIP events)
+    if args.stats == "off":
+        # the event counts of the same steps (same accumIDs and cameras: identical frames and
+        # counts), rendered again with counting on, untimed
+        ctx.reset_stats_total()
+        ctx.set_statistics(True)
+        for k in range(args.steps):
+            step(args.warmup + k)
+        if dist_path:
+            drain()
+        torch.cuda.synchronize()
+        counted, _ = ctx.stats_total()
+        counted.kernelMs = tot.kernelMs
+        tot = counted
     log(f"[rank {rank}] timed {args.steps} steps ({launches} launches) in {elapsed:.4f} s "
         f"(host loop {host_loop:.4f} s); peak host RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.2f} GiB")
     samples, in_box = tot.samplesFound, tot.raysInBox
@@ -408,6 +427,7 @@ def main():
                 "rays_in_box_per_frame": in_box_all / args.steps / frames,
                 "candidates_per_sample": tot.candidatesTested / max(samples, 1),
                 "kernel_ms_rank0": round(avg_kernel_s * 1e3, 4),
+                "statistics_in_timed_loop": args.stats,
                 "bytes_per_launch_rank0": bytes_per_launch,
             },
             "roofline": {
