@@ -58,10 +58,6 @@ enum : int {
                            // (irt_device.h spherical_fast, glibc-exact fallback near cell edges):
                            // no gain at C3, C5 3 % slower (profiles/r04b/) -- the setup waits on
                            // the majorant gather, not on asinf/atan2f
-  OPT_HDRPF = 67108864,  // (A/B) at each range's entry point, touch its cube-map header line
-                         // (an LDS-DMA load of one word into a dummy LDS slot, issued before the
-                         // entry's toSpherical and waited for with the majorant's gather), so
-                         // that the first Woodcock sample's header read hits the cache
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
@@ -1323,8 +1319,7 @@ template <int OPT>
 __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
                                                   const float *s_th, int4 *s_dda, float4 *s_entry,
                                                   float4 *s_acc, CoopWave &W, ScanWave *SW, const uint2 *jmp,
-                                                  int tid, int accumID, uint32_t blk, int pwave, int frame,
-                                                  uint32_t *s_pf) {
+                                                  int tid, int accumID, uint32_t blk, int pwave, int frame) {
   // At 5+ waves/SIMD the pixel's output addresses are recomputed where they are used (from the
   // workgroup's uniform block index), not held in VGPRs through the rounds: a progressive
   // batch's sample slot (k_accumulate reads it) and the frame index.  (At 4 waves there is
@@ -1604,12 +1599,6 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
         if (!ae) {  // cellID of the entry point (ShellAccel.h:121-124)
           const float e1 = lower + sceneEPS();
           const float x1 = A.org.x + dx * e1, y1 = A.org.y + dy * e1, z1 = A.org.z + dz * e1;
-          if constexpr ((OPT & OPT_HDRPF) != 0) {
-            if (A.numCells != 0)
-              __builtin_amdgcn_global_load_lds(
-                  (const void *)(A.binHdr + (size_t)cubemap_cell_fast(x1, y1, z1, A.G) * (kBinHdrWords / 4)),
-                  (__attribute__((address_space(3))) void *)s_pf, 4, 0, 0);
-          }
           float r1, la1, lo1;
           // OPT_FASTSPH: the certified fast lat/lon, glibc-exact when not certified
           if (!(kFastSph && spherical_fast(A, x1, y1, z1, r1, la1, lo1, cy, cz))) {
@@ -1829,7 +1818,6 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
   __shared__ ScanWave s_scan[Tracer<OPT>::kWaveScan ? kW : 1];  // its wave-wide candidate scan
   __shared__ HdrStage s_hdrs[(OPT & OPT_HDRLDS) ? kW : 1];       // OPT_HDRLDS: staged header lines
   __shared__ float4 s_acc[lean ? 1 : 256];  // kCoop: the accum pixels, prefetched
-  __shared__ uint32_t s_pf[(OPT & OPT_HDRPF) ? 256 : 1];  // OPT_HDRPF: header touches land here
   __shared__ uint2 s_jmp[kLcgJumps];  // lcg_jump's {mul, add} (kLcgJumpTab)
   const int tid = threadIdx.x;
   if (A.probeExit == 1) return;  // measurement only
@@ -1939,14 +1927,14 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
         launched += (uint32_t)__popcll(__ballot(ppx.active));
         render_pixel_coop<OPT>(AL, TL, ppx, lean ? AL.srgbTh : s_th, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
                                &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, AL.accumID + frame,
-                               pblk, pw, frame, s_pf + ((OPT & OPT_HDRPF) ? (ltid & ~63) : 0));
+                               pblk, pw, frame);
         TL.flush_coop();  // this packet's counts (nothing carried from packet to packet)
       } else {
         const Pixel ppx = pixel_of(A, pblk, pw * 64 + (ltid & 63));
         launched += (uint32_t)__popcll(__ballot(ppx.active));
         render_pixel_coop<OPT>(A, T, ppx, th_p, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
                                &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, A.accumID + frame,
-                               pblk, pw, frame, s_pf + ((OPT & OPT_HDRPF) ? (ltid & ~63) : 0));
+                               pblk, pw, frame);
       }
       // the next packet once this one is done: a fetch issued at the packet's start (to
       // hide its round trip) made the packet's first gather wait for it as well (vector
@@ -2132,7 +2120,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(67114240)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808)
 #else
 #define IRT_VARIANTS(X) X(5376) X(36864)
 #endif
