@@ -58,6 +58,10 @@ enum : int {
                            // (irt_device.h spherical_fast, glibc-exact fallback near cell edges):
                            // no gain at C3, C5 3 % slower (profiles/r04b/) -- the setup waits on
                            // the majorant gather, not on asinf/atan2f
+  OPT_NEXTHDR = 134217728,  // (A/B) solo rounds after a wave's first: each lane also loads the
+                            // cube-map header line of its ray's next sample (the one taken if
+                            // this sample is located and rejected), in the same batch as this
+                            // sample's header, so that the next round's header read hits L2
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
@@ -547,7 +551,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     __builtin_amdgcn_wave_barrier();
   }
   __device__ __forceinline__ bool locate_wave(bool want, float px, float py, float pz, float &value,
-                                              CoopWave &CW, ScanWave &W) {
+                                              CoopWave &CW, ScanWave &W, const uint32_t *touch = nullptr) {
     want = want && A.numCells != 0;
     const int lane = (int)__lane_id();
     // The scan's state lives in the wave's LDS (fewer live VGPRs across it):
@@ -564,6 +568,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     bool hit = false, edge = false;
     uint4 H0 = make_uint4(0u, 0u, 0u, 0u), H1 = H0;
     uint32_t M = 0u, cell = 0u, sub = 0u;
+    uint32_t tv = 0u;  // OPT_NEXTHDR's loaded word, consumed after the scan
     if constexpr ((OPT & OPT_HDRLDS) != 0) {
       if (want) cell = cubemap_cell_fast(px, py, pz, A.G, sub);
       stage_headers(want, cell, sub, H0, H1, M);
@@ -576,6 +581,12 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         H0 = Hc[0];
         H1 = Hc[1];
         M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
+      }
+      if constexpr ((OPT & OPT_NEXTHDR) != 0) {
+        // issued after this sample's header words: waiting for them leaves it in flight
+        // (unconditional -- this sample's own line when there is none: a load under a branch
+        // makes the compiler wait for it before the header words)
+        tv = *(touch ? touch : reinterpret_cast<const uint32_t *>(A.binHdr + (size_t)cell * (kBinHdrWords / 4)));
       }
       const int b = bin_of(r, __uint_as_float(H0.x), __uint_as_float(H0.y), __uint_as_float(H0.z));
       const uint32_t m1 = b > 0 ? ~0u : 0u, m2 = b > 1 ? ~0u : 0u, m3 = b > 2 ? ~0u : 0u;
@@ -686,6 +697,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         fe = H0.w + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
       }
     }
+    if constexpr ((OPT & OPT_NEXTHDR) != 0) asm volatile("" ::"v"(tv));
     if (!want) return false;
     const float r = W.pt[lane].w;
     Found f = {0xFFFFFFFFu, 0u};
@@ -800,7 +812,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     // runs that wide groups cross in one round (2 % faster there, profiles/r02e_coop_cap).
     int lgCap = kMiss ? 6 : A.coopMaxLg;
     tmark(6);  // between woodcockFunc calls (sdda leaves, ranges)
-    for (;; lgCap = min(lgCap + A.coopRamp, 6)) {
+    for (int wr = 0;; lgCap = min(lgCap + A.coopRamp, 6), ++wr) {
       const uint64_t am = __ballot(active);
       if (am == 0ull) break;
       if constexpr ((OPT & OPT_STATS) != 0) ++cnt.rounds;
@@ -871,8 +883,24 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       float value = 0.f;
       tmark(2);  // round start: exchange, jumps, logf, prefix
       if constexpr (kWaveScan) {
+        const uint32_t *tp = nullptr;
+        if constexpr ((OPT & OPT_NEXTHDR) != 0) {
+          // the next sample if this one is located and rejected: two draws on (approximate
+          // step: only its header line is wanted)
+          if (solo && wr > 0 && used && !past) {
+            const float t1 = tk - woodcock_log(lcg_next(lcg_next(sk)), s_logf) * __builtin_amdgcn_rcpf(rq.z);
+            if (t1 <= rq.y) {
+              uint32_t sb;
+              const uint32_t c1 = cubemap_cell_fast(A.org.x + ry.x * t1, A.org.y + ry.y * t1, A.org.z + ry.z * t1,
+                                                    A.G, sb);
+              tp = reinterpret_cast<const uint32_t *>(A.binHdr + (size_t)c1 * (kBinHdrWords / 4));
+            }
+          }
+        } else {
+          (void)wr;
+        }
         found = locate_wave(used && !past, A.org.x + ry.x * tk, A.org.y + ry.y * tk, A.org.z + ry.z * tk,
-                            value, W, *SW);
+                            value, W, *SW, tp);
       } else if (used && !past) {
         found = locate(A.org.x + ry.x * tk, A.org.y + ry.y * tk, A.org.z + ry.z * tk, value);
       }
@@ -2120,7 +2148,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104)
 #else
 #define IRT_VARIANTS(X) X(5376) X(36864)
 #endif
