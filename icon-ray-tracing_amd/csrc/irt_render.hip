@@ -62,6 +62,9 @@ enum : int {
                             // cube-map header line of its ray's next sample (the one taken if
                             // this sample is located and rejected), in the same batch as this
                             // sample's header, so that the next round's header read hits L2
+  OPT_PAIR = 268435456,  // (A/B) the wave-wide scan's first step tests each lane's first two
+                         // candidates (both entries gathered together), so the dealt-out step
+                         // runs only for lanes whose first two fail
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
@@ -487,6 +490,12 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // lowest passing candidate of each list wins, as in the serial scan.  Samples exactly on a
   // radial bin edge (the two-bin scan) take locate_hdr's serial path.
   static constexpr bool kWaveScan = kCoop && (OPT & (OPT_WEDGE | OPT_GRID | OPT_SCAN1)) == 0;
+  static constexpr bool kPair = kWaveScan && (OPT & OPT_PAIR) != 0;
+  __device__ __forceinline__ static bool entry_passes(const float4 &a0, const float4 &a1, const float4 &a2,
+                                                     const float4 &am, float px, float py, float pz, float r) {
+    return !(r < am.x || r > am.y) && !(dot3(px, py, pz, a0.x, a0.y, a0.z) - a0.w > 0.f) &&
+           !(dot3(px, py, pz, a1.x, a1.y, a1.z) - a1.w > 0.f) && !(dot3(px, py, pz, a2.x, a2.y, a2.z) - a2.w > 0.f);
+  }
   __device__ __forceinline__ bool pass_entry(const float4 *F, float px, float py, float pz, float r,
                                              Found &f) {
     const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3];
@@ -569,6 +578,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     uint4 H0 = make_uint4(0u, 0u, 0u, 0u), H1 = H0;
     uint32_t M = 0u, cell = 0u, sub = 0u;
     uint32_t tv = 0u;  // OPT_NEXTHDR's loaded word, consumed after the scan
+    uint32_t fe2 = 0u; // OPT_PAIR: the pass's second candidate entry
     if constexpr ((OPT & OPT_HDRLDS) != 0) {
       if (want) cell = cubemap_cell_fast(px, py, pz, A.G, sub);
       stage_headers(want, cell, sub, H0, H1, M);
@@ -602,6 +612,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       lds_st16(&W.pt[lane], make_float4(px, py, pz, r));
       lds_st16(&W.lst[lane], make_uint4(H0.w + beg, m8, 0u, 0xFFFFFFFFu));
       fe = H0.w + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
+      if constexpr (kPair) fe2 = H0.w + beg + list_entry(m8, 1u);
       fr = r;
     }
     for (int pass = 0;; ++pass) {
@@ -609,7 +620,33 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       // every lane goes through the deal below, so a round's samples wait for one entry
       // gather instead of two when the wave's lists hold <= 64 candidates in all)
       uint32_t rem = (OPT & OPT_DEALALL) != 0 ? c : 0u;
-      if ((OPT & OPT_DEALALL) == 0 && c > 0u) {  // (from registers: no LDS round trip before the gather)
+      if (kPair && c > 0u) {
+        // both entries gathered before either is tested; the second counts only if the
+        // first fails (the serial scan's order)
+        const float4 *F1 = A.fat + (size_t)fe * kFatStride4;
+        const float4 *F2 = A.fat + (size_t)(c > 1u ? fe2 : fe) * kFatStride4;
+        const float4 a0 = F1[0], a1 = F1[1], a2 = F1[2], am = F1[3];
+        const float4 b0 = F2[0], b1 = F2[1], b2 = F2[2], bm = F2[3];
+        const bool ok1 = entry_passes(a0, a1, a2, am, px, py, pz, fr);
+        const bool ok2 = entry_passes(b0, b1, b2, bm, px, py, pz, fr);
+        const uint32_t rec1 = __float_as_uint(am.z), rec2 = __float_as_uint(bm.z);
+        if (rec1 < flim) {
+          ++specCand;
+          if (ok1) {
+            hit = true;
+            frm[lane] = make_uint2(rec1, record_path(__float_as_uint(am.w), am.x, am.y, fr));
+          } else if (c > 1u && rec2 < flim) {
+            ++specCand;
+            if (ok2) {
+              hit = true;
+              frm[lane] = make_uint2(rec2, record_path(__float_as_uint(bm.w), bm.x, bm.y, fr));
+            } else {
+              rem = c - 2u;
+              W.lst[lane].z = 2u;
+            }
+          }
+        }
+      } else if ((OPT & OPT_DEALALL) == 0 && c > 0u) {  // (from registers: no LDS round trip before the gather)
         Found f;
         const bool ok = pass_entry(A.fat + (size_t)fe * kFatStride4, px, py, pz, fr, f);
         if (f.rec < flim) {  // scan_fat stops, uncounted, at the first record >= the limit
@@ -695,6 +732,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         flim = hit ? frm[lane].x : 0xFFFFFFFFu;
         lds_st16(&W.lst[lane], make_uint4(H0.w + beg, m8, 0u, flim));
         fe = H0.w + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
+        if constexpr (kPair) fe2 = H0.w + beg + list_entry(m8, 1u);
       }
     }
     if constexpr ((OPT & OPT_NEXTHDR) != 0) asm volatile("" ::"v"(tv));
@@ -2148,7 +2186,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832)
 #else
 #define IRT_VARIANTS(X) X(5376) X(36864)
 #endif

@@ -14,7 +14,7 @@ for cfg in $CONFIGS; do
       vars=()
       if [ -n "$envs" ]; then
         IFS=@ read -r -a kv <<< "$envs"
-        for a in "${kv[@]}"; do vars+=("$a"); n="${n}_${a#*=}"; done
+        for a in "${kv[@]}"; do vars+=("$a"); v="${a#IRT_}"; [ "${a%%=*}" = IRT_RENDER_VARIANT ] && v="${a#*=}"; n="${n}_${v}"; done
       fi
       env IRT_LIB_PATH="$lib" "${vars[@]}" timeout -k 10 240 python3 bench.py --config $cfg --steps $steps \
         --warmup 5 --no-cpu-baseline >> "$OUT/${n}_$cfg.jsonl" 2>> "$OUT/${n}_$cfg.err" || exit 1
