@@ -137,6 +137,7 @@ struct irt_context {
   int coopMaxLg = 0;
   int coopRamp = 1;
   int probeExit = 0;           // IRT_PROBE_EXIT (measurement only, RenderArgs::probeExit)
+  uint32_t *wgTrace = nullptr; // irt_debug_set_wg_trace (measurement only, RenderArgs::wgTrace)
   // persistent launches (RenderArgs::queue, IRT_QUEUE=0|1): every resident wave pulls 8x8
   // packets from per-slot queue counters (kSlots x kQueueWords u32, zero between launches)
   bool queueOn = false;
@@ -538,6 +539,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.coopMaxLg = c->coopMaxLg;
   A.coopRamp = c->coopRamp;
   A.probeExit = c->probeExit;
+  A.wgTrace = c->wgTrace;
   A.numCells = c->n;
   A.G = c->G;
   A.srgbTh = c->d_srgb;
@@ -1648,6 +1650,15 @@ extern "C" int irt_debug_set_queue(irt_context *c, int on) {
     return IRT_E_INVALID;
   }
   c->queueOn = on != 0;
+  return IRT_OK;
+}
+
+extern "C" int irt_debug_set_wg_trace(irt_context *c, uint32_t *trace) {
+  if (!c) {
+    set_error("irt_debug_set_wg_trace: null context");
+    return IRT_E_INVALID;
+  }
+  c->wgTrace = trace;
   return IRT_OK;
 }
 

@@ -91,6 +91,10 @@ struct RenderArgs {
   // until none is left; the launch's last wave resets the counters for the next launch
   uint32_t *queue;
   uint32_t numPackets;
+  // measurement only (irt_debug_set_wg_trace, profiles/wg_trace.py): non-null: workgroup b
+  // writes {start, end} (s_memrealtime, 100 MHz, low 32 bits), HW_ID and XCC_ID to
+  // wgTrace[4b..4b+3] -- when the machine is idle at a launch's ramp and tail
+  uint32_t *wgTrace;
 };
 // a persistent launch's queue words (irt_render.hip queue_take): 8 per-XCD counters and the
 // done count, each on its own 128-B line

@@ -1886,6 +1886,12 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
   __shared__ float4 s_acc[lean ? 1 : 256];  // kCoop: the accum pixels, prefetched
   __shared__ uint2 s_jmp[kLcgJumps];  // lcg_jump's {mul, add} (kLcgJumpTab)
   const int tid = threadIdx.x;
+  if (A.wgTrace && tid == 0) {  // measurement only: the workgroup's start, where it ran
+    uint32_t *w = A.wgTrace + 4 * (blockIdx.y * gridDim.x + blockIdx.x);
+    w[0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    w[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    w[3] = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+  }
   if (A.probeExit == 1) return;  // measurement only
   uint64_t tStart = 0;
   if constexpr ((OPT & OPT_TIMING) != 0) tStart = __builtin_amdgcn_s_memtime();
@@ -2056,7 +2062,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
         if (hist[k]) atomicAdd(&A.counters[12 + k], (unsigned long long)hist[k]);
     }
   }
-  if (A.counters || A.schedCost) {
+  if (A.counters || A.schedCost || A.wgTrace) {
     const int lane = (int)__lane_id();
     if (A.counters && lane == 0 && launched) atomicAdd(&s_cnt[0], launched);  // rays launched, once per wave
     // The last wave of the workgroup to get here writes the workgroup's counts and duration.
@@ -2073,6 +2079,8 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
         const uint64_t dt = wall_clock64() - c0;
         A.schedCost[blk] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
       }
+      if (A.wgTrace && lane == 0)
+        A.wgTrace[4 * (blockIdx.y * gridDim.x + blockIdx.x) + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     }
   }
 }

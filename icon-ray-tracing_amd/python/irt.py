@@ -530,6 +530,13 @@ class Context:
         L.irt_debug_set_queue.argtypes = [C.c_void_p, C.c_int]
         _check(L.irt_debug_set_queue(self._h, 1 if on else 0), "irt_debug_set_queue")
 
+    def set_wg_trace(self, ptr: int):
+        """Measurement only: the next renders' workgroups write {start, end, HW_ID, XCC_ID}
+        to the device buffer at `ptr` (4 u32 per workgroup; 0: off)."""
+        L = lib()
+        L.irt_debug_set_wg_trace.argtypes = [C.c_void_p, C.c_void_p]
+        _check(L.irt_debug_set_wg_trace(self._h, C.c_void_p(ptr or None)), "irt_debug_set_wg_trace")
+
     def queue(self) -> bool:
         L = lib()
         L.irt_debug_get_queue.argtypes = [C.c_void_p]

@@ -137,6 +137,11 @@ int irt_debug_locate_wave(irt_context *ctx, const float *xyz, int n, int *found,
 /* Measured-cost scheduling state: the policy (IRT_SCHED; 0 = off), whether the last launch
  * ran its workgroups in a measured-cost order, and how many launches have. */
 int irt_debug_sched(irt_context *ctx, int *policy, int *lastApplied, long long *applied);
+/* Measurement only: the next renders' workgroups each write 4 words to the device buffer
+ * `trace` (NULL: off): {start, end} of the workgroup (s_memrealtime, 100 MHz, low 32 bits),
+ * the wave's HW_ID and XCC_ID registers; workgroup b of a launch at trace[4b].  The buffer
+ * must hold 4 words per workgroup (16 per 64x64 tile and frame); frames are unchanged. */
+int irt_debug_set_wg_trace(irt_context *ctx, uint32_t *trace);
 
 #ifdef __cplusplus
 }
