@@ -224,6 +224,10 @@ def main():
                          "off (default): the product renders without them, as the reference "
                          "does; the counts the roofline needs come from rendering the same "
                          "steps again afterwards with counting on (untimed, identical frames)")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="progressive frames per launch on one GPU (irt_render_accumulate: the "
+                         "reference's accumulation loop over accumID, frames chained in one "
+                         "launch; every frame's accum and fb are written). 1: one launch per frame")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path with host-staged collectives "
                          "(ranks may share a GPU); nccl (RCCL) is the measured path")
@@ -288,6 +292,9 @@ def main():
     # frames per step: 1 on one GPU or in frame mode; N in progressive mode on N GPUs
     strong = args.mode == "frame"
     frames = 1 if (world == 1 or strong) else world
+    batch = max(1, args.batch) if not dist_path and orbit is None else 1
+    if not dist_path:
+        frames = batch
     if not dist_path:
         fb = torch.zeros(W * H, dtype=torch.int32, device=dev)
         accum = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
@@ -314,7 +321,10 @@ def main():
             lp.org, lp.dir_00, lp.dir_du, lp.dir_dv = c.org, c.dir_00, c.dir_du, c.dir_dv
             lp.accumID = 0
         if not dist_path:
-            ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
+            if frames > 1:  # `frames` consecutive progressive frames in one launch
+                ctx.render_accumulate(lp, W, H, frames, fb.data_ptr(), accum.data_ptr(), stream)
+            else:
+                ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
             return
         pipe.step(s, lambda buf: split.render(ctx, lp, frames, buf.data_ptr(),
                                               tiles_acc.data_ptr(), stream))
@@ -410,8 +420,9 @@ def main():
                 "workload": desc + (", orbit camera (eye 1.4e7 (sin t, 0, cos t), -fovy 60), "
                                     "one orbit frame per step"
                                     if orbit is not None else
-                                    ", framing camera --camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60, "
-                                    "one frame per step") +
+                                    ", framing camera --camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60, " +
+                                    ("one frame per step" if frames == 1 else
+                                     f"{frames} consecutive progressive frames (accumID) per step")) +
                            ", woodcockTrackingWithAccel, " + ("sparse comb TF" if tf == "comb" else "default TF") +
                            ("" if args.sampler == "user" else
                             {"tri": ", TRIANGLE_MODE sampler", "cubql": ", CUBQL_MODE wedge sampler"}[args.sampler]) +

@@ -138,6 +138,14 @@ struct irt_context {
   int coopRamp = 1;
   int probeExit = 0;           // IRT_PROBE_EXIT (measurement only, RenderArgs::probeExit)
   uint32_t *wgTrace = nullptr; // irt_debug_set_wg_trace (measurement only, RenderArgs::wgTrace)
+  // chained progressive frames (RenderArgs::chain; IRT_CHAIN=0 / irt_debug_set_chain: the
+  // sample buffer + k_accumulate instead): per (block, wave) publish words, the next epoch, and
+  // the timeout word
+  bool chainOn = true;
+  uint32_t *d_chainFlag = nullptr;
+  size_t chainCap = 0;           // words in d_chainFlag
+  uint32_t chainEpoch = 1;
+  uint32_t *d_chainErr = nullptr;
   // persistent launches (RenderArgs::queue, IRT_QUEUE=0|1): every resident wave pulls 8x8
   // packets from per-slot queue counters (kSlots x kQueueWords u32, zero between launches)
   bool queueOn = false;
@@ -203,7 +211,7 @@ void free_all(irt_context *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
                   c->d_sphBits, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_gridBits, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
-                  c->d_lut, c->d_counters, c->d_meta, c->d_queue};
+                  c->d_lut, c->d_counters, c->d_meta, c->d_queue, c->d_chainFlag, c->d_chainErr};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->d_cells) (void)hipFree(c->d_cells);
@@ -628,7 +636,32 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     A.wgCounts = c->d_probeCounts;
   }
   A.numSamples = numFrames;
-  if (numFrames > 1) {
+  // chained frames: the cooperative kernels (not the one-lane-per-ray A/B variant), grid
+  // launches, no measurement-only early exit
+  A.chain = c->chainOn && numFrames > 1 && !queued && c->probeExit == 0 && (c->variant & 65536) == 0 ? 1 : 0;
+  if (A.chain) {
+    const size_t words = (size_t)numTiles * 16 * 4;  // one per (block, wave)
+    if (words > c->chainCap || c->chainEpoch > 0xF0000000u - (uint32_t)numFrames) {
+      if (words > c->chainCap) {
+        IRT_HIP(hipStreamSynchronize(s));
+        if (c->d_chainFlag) IRT_HIP(hipFree(c->d_chainFlag));
+        c->d_chainFlag = nullptr;
+        c->bytes -= c->chainCap * sizeof(uint32_t);
+        c->chainCap = 0;
+        int rc = dalloc(c, &c->d_chainFlag, words);
+        if (rc) return rc;
+        c->chainCap = words;
+        c->info.deviceBytes = c->bytes;
+      }
+      IRT_HIP(hipMemsetAsync(c->d_chainFlag, 0, c->chainCap * sizeof(uint32_t), s));
+      c->chainEpoch = 1;  // never 0: the zeroed words match no epoch
+    }
+    A.chainFlag = c->d_chainFlag;
+    A.chainErr = c->d_chainErr;
+    A.chainEpoch = c->chainEpoch;
+    c->chainEpoch += (uint32_t)numFrames;
+  }
+  if (numFrames > 1 && !A.chain) {
     const size_t need = lanes * (size_t)numFrames;
     if (need > c->sampleCap) {
       IRT_HIP(hipStreamSynchronize(s));
@@ -956,6 +989,9 @@ int irt_create_end(irt_context *c) {
   if (const char *e = getenv("IRT_PROBE_EXIT")) c->probeExit = atoi(e);
   if (const char *e = getenv("IRT_QUEUE")) c->queueOn = atoi(e) != 0;
   if (const char *e = getenv("IRT_QUEUE_WGS")) c->queuePerCU = std::max(0, atoi(e));
+  if (const char *e = getenv("IRT_CHAIN")) c->chainOn = atoi(e) != 0;
+  if ((rc = dalloc(c, &c->d_chainErr, 1))) return rc;
+  IRT_HIP(hipMemsetAsync(c->d_chainErr, 0, sizeof(uint32_t), c->stream));
   if ((rc = dalloc(c, &c->d_queue, (size_t)kQueueWords * irt_context::kSlots))) return rc;
   IRT_HIP(hipMemsetAsync(c->d_queue, 0, (size_t)kQueueWords * irt_context::kSlots * sizeof(uint32_t), c->stream));
   IRT_HIP(hipDeviceGetAttribute(&c->numCU, hipDeviceAttributeMultiprocessorCount, c->device));
@@ -1660,6 +1696,29 @@ extern "C" int irt_debug_set_wg_trace(irt_context *c, uint32_t *trace) {
   }
   c->wgTrace = trace;
   return IRT_OK;
+}
+
+extern "C" int irt_debug_set_chain(irt_context *c, int on) {
+  if (!c) {
+    set_error("irt_debug_set_chain: null context");
+    return IRT_E_INVALID;
+  }
+  c->chainOn = on != 0;
+  return IRT_OK;
+}
+
+extern "C" int irt_debug_chain_errors(irt_context *c) {
+  if (!c) {
+    set_error("irt_debug_chain_errors: null context");
+    return -1;
+  }
+  uint32_t v = 0;
+  if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(&v, c->d_chainErr, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) {
+    set_error("irt_debug_chain_errors: HIP error");
+    return -1;
+  }
+  return (int)v;
 }
 
 extern "C" int irt_debug_get_queue(const irt_context *c) { return c ? (c->queueOn ? 1 : 0) : -1; }

@@ -91,6 +91,16 @@ struct RenderArgs {
   // until none is left; the launch's last wave resets the counters for the next launch
   uint32_t *queue;
   uint32_t numPackets;
+  // chained progressive frames (numSamples > 1, irt_render_accumulate & co.): workgroup (b, f)
+  // of the launch renders block b of frame accumID + f and lerps straight into accum/fb, after
+  // waiting for (b, f - 1)'s wave to publish the same pixels -- chainFlag[4 b + wave] = chainEpoch
+  // + f after its write-through (sc1) stores -- instead of the sample buffer + k_accumulate.
+  // A frame's workgroups wait on the previous frame's, which the linear dispatch order puts
+  // earlier on the same XCD; a wait that times out sets *chainErr (pixels then unordered).
+  int chain;
+  uint32_t chainEpoch;
+  uint32_t *chainFlag;
+  uint32_t *chainErr;
   // measurement only (irt_debug_set_wg_trace, profiles/wg_trace.py): non-null: workgroup b
   // writes {start, end} (s_memrealtime, 100 MHz, low 32 bits), HW_ID and XCC_ID to
   // wgTrace[4b..4b+3] -- when the machine is idle at a launch's ramp and tail

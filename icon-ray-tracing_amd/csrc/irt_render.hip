@@ -1112,6 +1112,64 @@ __device__ __forceinline__ void write_pixel(const RenderArgs &A, size_t outIdx, 
   write_pixel(A, outIdx, cr, cg, cb, alpha, s_th, A.accum[outIdx]);
 }
 
+// Chained progressive frames (RenderArgs::chain).  Workgroup (b, f) of a launch renders block
+// b of frame accumID + f and lerps into accum/fb directly; the previous frame's colour of the
+// same pixel must be in accum first.  The hand-off (cdna_hip_programming.md Guideline 16, R1):
+// frame f - 1's wave stores its pixels write-through (sc1), drains them (vmcnt 0) and stores
+// chainEpoch + f to its (block, wave) word; frame f's wave polls that word (relaxed, agent
+// scope), then reads accum with sc1 loads (past this CU's L1).  Frame f's wave gets there at
+// the end of its rays, tens of microseconds after frame f - 1's workgroup -- dispatched
+// numBlocks workgroups earlier, on the same XCD -- finished, so the first poll normally hits.
+constexpr uint32_t kChainSpins = 1u << 20;  // ~0.1 s of s_sleep 2, then give up (chainErr)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t out_pixels(const RenderArgs &A) {
+  return A.packed ? (uint32_t)A.numTiles * 4096u : (uint32_t)A.W * (uint32_t)A.H;
+}
+__device__ __forceinline__ void chain_wait(const RenderArgs &A, uint32_t blk, int pwave, int frame) {
+  uint32_t *f = A.chainFlag + (size_t)blk * 4u + (uint32_t)pwave;
+  const uint32_t want = A.chainEpoch + (uint32_t)frame;  // frame - 1's publish
+  for (uint32_t spins = 0;; ++spins) {
+    const uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (v == want) break;
+    if (spins >= kChainSpins) {
+      if (__lane_id() == (unsigned)(__ffsll((long long)__ballot(1)) - 1))
+        __hip_atomic_fetch_add(A.chainErr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: the loads stay below
+}
+// the previous frame's accum pixel, past this CU's L1
+__device__ __forceinline__ float4 chain_load_accum(const RenderArgs &A, size_t outIdx) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)A.accum, 0, (int)(out_pixels(A) * 16u), 0x00020000);
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(outIdx * 16u), 0, 16));
+}
+// write_pixel's lerp and RGBA8 with the weight of this frame; publish: write-through (sc1)
+// stores that the next frame's wave reads, else streaming stores as write_pixel<true>
+__device__ __forceinline__ void write_pixel_chain(const RenderArgs &A, size_t outIdx, float cr, float cg, float cb,
+                                                  float alpha, float w, const float *s_th, float4 old, bool publish) {
+  float4 nv;
+  nv.x = w * cr + (1.f - w) * old.x;
+  nv.y = w * cg + (1.f - w) * old.y;
+  nv.z = w * cb + (1.f - w) * old.z;
+  nv.w = w * alpha + (1.f - w) * old.w;
+  const uint32_t rgba = srgb_byte(s_th, nv.x) + (srgb_byte(s_th, nv.y) << 8) +
+                        (srgb_byte(s_th, nv.z) << 16) + (make_8bit(nv.w) << 24);
+  if (publish) {
+    const uint32_t n = out_pixels(A);
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)A.accum, 0, (int)(n * 16u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc((void *)A.fb, 0, (int)(n * 4u), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, nv), ra, (int)(outIdx * 16u), 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b32(rgba, rf, (int)(outIdx * 4u), 0, 16);
+  } else {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v t = {nv.x, nv.y, nv.z, nv.w};
+    __builtin_nontemporal_store(t, reinterpret_cast<f4v *>(&A.accum[outIdx]));
+    __builtin_nontemporal_store(rgba, &A.fb[outIdx]);
+  }
+}
+
 // The workgroup's event counts (LDS) out to the launch's statistics, by the workgroup's
 // last wave to finish (k_render).  Default: one store of the kCnt counts per workgroup into
 // wgCounts, pinned host memory the host sums when asked (irt_context.hip finish_slot): no
@@ -1406,7 +1464,10 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     asm volatile("" : "+v"(lane));  // not CSE'd with the pixel's coordinates at the ray's start
     return (opaque_u(pwave) << 6) | lane;
   };
-  const bool toSample = A.numSamples > 1;
+  const bool toSample = A.numSamples > 1 && !A.chain;
+  // chained frames: frame f > 0 of the launch reads its accum pixel at the end, once frame
+  // f - 1's wave has published it (chain_wait); frame 0 prefetches it as a single frame does
+  const bool chainLate = A.chain && frame > 0;
   float4 *const slot0 = kRecompute || !toSample
                             ? nullptr
                             : A.sampleBuf + (size_t)frame * A.numTiles * 4096u + (size_t)blk * 256u + (size_t)ptid;
@@ -1442,7 +1503,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       t1box = t1;
       // the accum pixel the lerp reads at the end, fetched now straight into LDS (no VGPRs
       // held through the Woodcock rounds; its latency hides behind them)
-      if (!toSample && (OPT & OPT_LEAN) == 0)
+      if (!toSample && !chainLate && (OPT & OPT_LEAN) == 0)
         __builtin_amdgcn_global_load_lds((const void *)(A.accum + px.outIdx),
                                          (__attribute__((address_space(3))) void *)(s_acc + (tid & ~63)),
                                          16, 0, kRecompute ? 2 : 0);  // 2: nt (write_pixel)
@@ -1814,7 +1875,21 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     *sample_slot() = c;
   } else {
     const size_t outIdx = kRecompute ? pixel_of(A, (uint32_t)opaque_u((int)blk), ptid_late()).outIdx : px.outIdx;
-    if constexpr ((OPT & OPT_LEAN) != 0) {
+    if (A.chain) {
+      float4 old;
+      if (chainLate) {
+        chain_wait(A, blk, pwave, frame);
+        old = chain_load_accum(A, outIdx);
+      } else if constexpr ((OPT & OPT_LEAN) != 0) {
+        old = A.accum[outIdx];
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
+        old = lds_ld16(&s_acc[tl]);
+      }
+      // 1.f / (float)(accumID + 1) of this frame, correctly rounded as the host's A.accumW
+      write_pixel_chain(A, outIdx, c.x, c.y, c.z, c.w, 1.f / (float)(accumID + 1), s_th, old,
+                        frame < A.numSamples - 1);
+    } else if constexpr ((OPT & OPT_LEAN) != 0) {
       write_pixel(A, outIdx, c.x, c.y, c.z, c.w, s_th);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
@@ -2007,6 +2082,13 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
         render_pixel_coop<OPT>(A, T, ppx, th_p, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
                                &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, A.accumID + frame,
                                pblk, pw, frame);
+        if (A.chain && frame < A.numSamples - 1) {
+          // chained frames: this wave's pixels are written through; tell frame + 1's wave
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (__lane_id() == 0)
+            __hip_atomic_store(A.chainFlag + (size_t)pblk * 4u + (uint32_t)pw, A.chainEpoch + (uint32_t)frame + 1u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
       // the next packet once this one is done: a fetch issued at the packet's start (to
       // hide its round trip) made the packet's first gather wait for it as well (vector
@@ -2263,8 +2345,8 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
   } else {
     hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads), A.numSamples), dim3(threads), 0, s, A);
   }
-  // progressive batch: the lerp chain over the frames' samples
-  if (A.numSamples > 1) hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);
+  // progressive batch: the lerp chain over the frames' samples (chained frames lerp in k_render)
+  if (A.numSamples > 1 && !A.chain) hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);
 }
 
 template <int N>

@@ -537,6 +537,23 @@ class Context:
         L.irt_debug_set_wg_trace.argtypes = [C.c_void_p, C.c_void_p]
         _check(L.irt_debug_set_wg_trace(self._h, C.c_void_p(ptr or None)), "irt_debug_set_wg_trace")
 
+    def set_chain(self, on: bool):
+        """Chained progressive frames (default on): a multi-frame launch lerps each frame
+        straight into accum/fb instead of through the sample buffer + k_accumulate; frames are
+        identical either way."""
+        L = lib()
+        L.irt_debug_set_chain.argtypes = [C.c_void_p, C.c_int]
+        _check(L.irt_debug_set_chain(self._h, 1 if on else 0), "irt_debug_set_chain")
+
+    def chain_errors(self) -> int:
+        """Chained-frame waits that timed out (0 in every correct run); waits for the device."""
+        L = lib()
+        L.irt_debug_chain_errors.argtypes = [C.c_void_p]
+        n = L.irt_debug_chain_errors(self._h)
+        if n < 0:
+            raise IrtError("irt_debug_chain_errors failed")
+        return n
+
     def queue(self) -> bool:
         L = lib()
         L.irt_debug_get_queue.argtypes = [C.c_void_p]

@@ -142,6 +142,16 @@ int irt_debug_sched(irt_context *ctx, int *policy, int *lastApplied, long long *
  * the wave's HW_ID and XCC_ID registers; workgroup b of a launch at trace[4b].  The buffer
  * must hold 4 words per workgroup (16 per 64x64 tile and frame); frames are unchanged. */
 int irt_debug_set_wg_trace(irt_context *ctx, uint32_t *trace);
+/* Chained progressive frames on (default; IRT_CHAIN=0 turns it off per context) or off: a
+ * launch of several frames (irt_render_accumulate, irt_render_tiles_accumulate,
+ * irt_render_tile_list) lerps each frame straight into accum/fb, frame f's workgroup waiting for
+ * frame f - 1's to publish the same pixels; off: every frame's colour goes to a sample buffer
+ * and a second kernel runs the lerp chain.  Frames are identical either way. */
+int irt_debug_set_chain(irt_context *ctx, int on);
+/* Chained-frame waits that timed out since the context was created (a wait gives up after
+ * ~0.1 s: the previous frame's workgroup was not dispatched first); waits for the device.
+ * 0 in every correct run; -1 on error. */
+int irt_debug_chain_errors(irt_context *ctx);
 
 #ifdef __cplusplus
 }

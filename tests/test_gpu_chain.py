@@ -1,0 +1,105 @@
+"""Chained progressive frames (RenderArgs::chain, the default for multi-frame launches).
+
+irt_render_accumulate / irt_render_tile_list with k frames: workgroup (b, f) lerps frame f of
+block b straight into accum/fb once frame f - 1's wave of the same pixels has published them
+(write-through stores + a per-(block, wave) epoch word), instead of the per-frame sample buffer
+and the k_accumulate pass.  Bit-identical to the sample-buffer batch and to k single-frame
+launches (which the oracle pins in test_gpu_parity.py), counts included; no wait may time out.
+Frames small enough that all k frames' workgroups are resident at once exercise real waits;
+large ones (more workgroups than the chip holds) the normal case of an already-published word.
+"""
+import numpy as np
+import pytest
+
+import irt
+from helpers import FRAMING, bits
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(ctx, lp, W, H, k, first, chain, prior=0):
+    import torch
+    ctx.set_chain(chain)
+    fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    for aid in range(prior):
+        lp.accumID = aid
+        ctx.render(lp, W, H, fb.data_ptr(), acc.data_ptr())
+    lp.accumID = first
+    ctx.render_accumulate(lp, W, H, k, fb.data_ptr(), acc.data_ptr())
+    torch.cuda.synchronize()
+    st = ctx.stats()
+    return (fb.cpu().numpy().copy(), bits(acc.cpu().numpy()),
+            (st.raysLaunched, st.raysInBox, st.locateCalls, st.samplesFound, st.candidatesTested))
+
+
+@pytest.mark.parametrize("rn,bis,L,W,H,k,cam", [
+    (2, 2, 47, 96, 80, 2, FRAMING),      # 4 tiles: every frame resident at once
+    (2, 2, 47, 200, 136, 5, None),       # viewAll: rays that hit the box in some frames only
+    (2, 3, 90, 512, 512, 9, FRAMING),    # 1,024 workgroups per frame
+    (2, 3, 90, 1024, 1024, 3, FRAMING),  # 4,096 per frame: more than the chip holds
+])
+def test_chained_batch_equals_sample_buffer_batch(rn, bis, L, W, H, k, cam):
+    cells = irt.synth_grid(rn, bis, L)
+    setup = irt.setup_frame(cells, W, H, camera=cam)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    ref = _batch(ctx, setup.lp, W, H, k, 0, chain=False)
+    got = _batch(ctx, setup.lp, W, H, k, 0, chain=True)
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+    assert got[2] == ref[2]
+    # continuing an accumulation: two single frames, then a chained batch from accumID 2
+    ref = _batch(ctx, setup.lp, W, H, k, 2, chain=False, prior=2)
+    got = _batch(ctx, setup.lp, W, H, k, 2, chain=True, prior=2)
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+    assert ctx.chain_errors() == 0
+    ctx.close()
+
+
+def test_chained_tile_lists_equal_sample_buffer_tile_lists():
+    """A rank's tile list (the multi-GPU progressive mode) over k chained frames, repeated
+    (the epochs advance from launch to launch on the same publish words)."""
+    import torch
+    cells = irt.synth_grid(2, 2, 47)
+    W, H, k = 320, 256, 4
+    setup = irt.setup_frame(cells, W, H, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    tiles = np.array([5, 0, 19, 7, 6, 12], dtype=np.int32)
+    out = {}
+    for chain in (False, True):
+        ctx.set_chain(chain)
+        fbt = torch.zeros(len(tiles) * 4096, dtype=torch.int32, device="cuda")
+        acct = torch.zeros(len(tiles) * 4096 * 4, dtype=torch.float32, device="cuda")
+        res = []
+        for rep in range(3):
+            setup.lp.accumID = rep * k
+            ctx.render_tile_list(setup.lp, W, H, tiles, k, fbt.data_ptr(), acct.data_ptr())
+            torch.cuda.synchronize()
+            res.append((fbt.cpu().numpy().copy(), bits(acct.cpu().numpy())))
+        out[chain] = res
+    for (fa, aa), (fb_, ab) in zip(out[False], out[True]):
+        assert np.array_equal(fa, fb_) and np.array_equal(aa, ab)
+    assert ctx.chain_errors() == 0
+    ctx.close()
+
+
+@pytest.mark.parametrize("accel,sampler", [(irt.ACCEL_GRID, irt.MODE_USER_GEOM),
+                                           (0, irt.MODE_CUBQL)])
+def test_chained_batch_other_kernels(accel, sampler):
+    """The grid-accel and wedge-sampler kernels run the same chained epilogue."""
+    cells = irt.synth_grid(2, 0, 12)
+    W, H, k = 128, 128, 3
+    setup = irt.setup_frame(cells, W, H, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    if sampler != irt.MODE_USER_GEOM:
+        ctx.build_wedge_accel(cells)
+    setup.lp.accelMode = accel
+    setup.lp.mode = sampler
+    ref = _batch(ctx, setup.lp, W, H, k, 0, chain=False)
+    got = _batch(ctx, setup.lp, W, H, k, 0, chain=True)
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+    assert got[2] == ref[2]
+    assert ctx.chain_errors() == 0
+    ctx.close()
