@@ -175,7 +175,7 @@ def cpu_baseline(rn, bis, L, W, H, camera, tf, budget_s=15.0):
     return out
 
 
-def profiled_traffic(kernel, config):
+def profiled_traffic(kernel, config, frames=1):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 summary of the
     same workload (profiles/*/summary.json: FETCH_SIZE x 2 + WRITE_SIZE, per the gfx950
     correction of MI355X_MICROARCH.md), or None."""
@@ -185,7 +185,7 @@ def profiled_traffic(kernel, config):
             s = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if s.get("config_name") != config:
+        if s.get("config_name") != config or s.get("frames_per_launch", 1) != frames:
             continue
         if not any(k.endswith(kernel) for k in s.get("kernels", {})):
             continue
@@ -224,10 +224,13 @@ def main():
                          "off (default): the product renders without them, as the reference "
                          "does; the counts the roofline needs come from rendering the same "
                          "steps again afterwards with counting on (untimed, identical frames)")
-    ap.add_argument("--batch", type=int, default=1,
+    ap.add_argument("--batch", type=int, default=8,
                     help="progressive frames per launch on one GPU (irt_render_accumulate: the "
                          "reference's accumulation loop over accumID, frames chained in one "
                          "launch; every frame's accum and fb are written). 1: one launch per frame")
+    ap.add_argument("--no-single-compare", action="store_true",
+                    help="skip timing the same frames at one launch per frame after the timed "
+                         "region (profiling runs: one launch shape per kernel trace)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path with host-staged collectives "
                          "(ranks may share a GPU); nccl (RCCL) is the measured path")
@@ -289,12 +292,12 @@ def main():
         # s+1's unpack and render, ~20 us of barrier latency per step.
         torch.cuda.set_stream(torch.cuda.Stream(dev, priority=-1))
     stream = torch.cuda.current_stream(device).cuda_stream
-    # frames per step: 1 on one GPU or in frame mode; N in progressive mode on N GPUs
+    # frames per step: --batch consecutive progressive frames per GPU (chained in one launch;
+    # the orbit's frames are new views, one per step), times N in progressive mode on N GPUs
+    # (per-GPU work fixed as N grows); one frame split over the N GPUs in frame mode
     strong = args.mode == "frame"
-    frames = 1 if (world == 1 or strong) else world
-    batch = max(1, args.batch) if not dist_path and orbit is None else 1
-    if not dist_path:
-        frames = batch
+    batch = max(1, args.batch) if orbit is None and not strong else 1
+    frames = 1 if strong else batch * (world if dist_path else 1)
     if not dist_path:
         fb = torch.zeros(W * H, dtype=torch.int32, device=dev)
         accum = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
@@ -370,6 +373,22 @@ def main():
         counted, _ = ctx.stats_total()
         counted.kernelMs = tot.kernelMs
         tot = counted
+    single = None
+    if not dist_path and frames > 1 and not args.no_single_compare:
+        # the same workload at one launch per frame (irt_render), for comparison: the frames
+        # that follow the timed steps' accumulation, statistics as in the timed loop
+        ctx.set_statistics(args.stats == "on")
+        n1 = args.steps * frames
+        base = (args.warmup + args.steps) * frames
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for k in range(n1):
+            lp.accumID = base + k
+            ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
+        torch.cuda.synchronize()
+        e1 = time.perf_counter() - t1
+        single = {"ms_per_frame": round(e1 / n1 * 1e3, 4), "value": round(W * H * n1 / e1 / 1e6, 3),
+                  "frames": n1}
     log(f"[rank {rank}] timed {args.steps} steps ({launches} launches) in {elapsed:.4f} s "
         f"(host loop {host_loop:.4f} s); peak host RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.2f} GiB")
     samples, in_box = tot.samplesFound, tot.raysInBox
@@ -439,6 +458,7 @@ def main():
                 "candidates_per_sample": tot.candidatesTested / max(samples, 1),
                 "kernel_ms_rank0": round(avg_kernel_s * 1e3, 4),
                 "statistics_in_timed_loop": args.stats,
+                "frames_per_launch": frames,
                 "bytes_per_launch_rank0": bytes_per_launch,
             },
             "roofline": {
@@ -450,7 +470,9 @@ def main():
                 "traffic": None,
             },
         }
-        prof = profiled_traffic(f"k_render<{irt.default_kernel_id()}>", args.config)
+        if single is not None:
+            out["single_frame_launches"] = single  # the same frames, one launch each
+        prof = profiled_traffic(f"k_render<{irt.default_kernel_id()}>", args.config, frames)
         if prof and world == 1:
             out["roofline"]["traffic"] = prof[0]
             out["roofline"]["traffic_source"] = (

@@ -1468,6 +1468,13 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   // chained frames: frame f > 0 of the launch reads its accum pixel at the end, once frame
   // f - 1's wave has published it (chain_wait); frame 0 prefetches it as a single frame does
   const bool chainLate = A.chain && frame > 0;
+  // ... unless frame f - 1's wave has published by the time this wave's rays are set up (a
+  // large frame's previous-frame workgroup ran numBlocks workgroups earlier): its publish word,
+  // loaded now, compared after the box test, and then the accum pixel prefetched (sc1) as frame 0
+  uint32_t chainSeen = 0u;
+  if (chainLate)
+    chainSeen = __hip_atomic_load(A.chainFlag + (size_t)blk * 4u + (uint32_t)pwave, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
   float4 *const slot0 = kRecompute || !toSample
                             ? nullptr
                             : A.sampleBuf + (size_t)frame * A.numTiles * 4096u + (size_t)blk * 256u + (size_t)ptid;
@@ -1531,6 +1538,10 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       *sample_slot() = make_float4(0.f, 0.f, 0.f, kNoSample);  // deviceCode.cu:294-295
     }
   }
+  const bool chainReady = !chainLate || __builtin_amdgcn_readfirstlane(chainSeen) == A.chainEpoch + (uint32_t)frame;
+  if ((OPT & OPT_LEAN) == 0 && chainLate && chainReady && inBox)
+    __builtin_amdgcn_global_load_lds((const void *)(A.accum + px.outIdx),
+                                     (__attribute__((address_space(3))) void *)(s_acc + (tid & ~63)), 16, 0, 16);  // sc1
   // GRID_ACCEL_MODE (deviceCode.cu:326-328): dda3 (DDA.h:35-136) over the 256^3 grid as
   // render_grid walks it, each cell's woodcockFunc one of the wave's cooperative requests
   int gcx = 0, gcy = 0, gcz = 0, gsteps = 0, gdirs = 0;
@@ -1868,6 +1879,10 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       }
     }
   }
+  // chained frames: every wave of frame f > 0 waits for frame f - 1's wave of its pixels -- also
+  // a wave none of whose rays hit the box, so that the publish words advance in frame order and
+  // frame f - 1's word covers every earlier frame's stores
+  if (chainLate && !chainReady) chain_wait(A, blk, pwave, frame);
   if (!inBox) return;
   const int tl = tid_late();
   const float4 c = hit ? lds_ld16(&s_entry[tl]) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1877,8 +1892,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     const size_t outIdx = kRecompute ? pixel_of(A, (uint32_t)opaque_u((int)blk), ptid_late()).outIdx : px.outIdx;
     if (A.chain) {
       float4 old;
-      if (chainLate) {
-        chain_wait(A, blk, pwave, frame);
+      if (chainLate && (!chainReady || (OPT & OPT_LEAN) != 0)) {
         old = chain_load_accum(A, outIdx);
       } else if constexpr ((OPT & OPT_LEAN) != 0) {
         old = A.accum[outIdx];

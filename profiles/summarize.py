@@ -60,10 +60,12 @@ def main(d):
                         "kernel_ms_hip_events": cfg.get("kernel_ms_rank0"),
                         "samples_per_frame": cfg.get("samples_per_frame"),
                         "rays_in_box_per_frame": cfg.get("rays_in_box_per_frame"),
-                        "algorithmic_bytes_per_launch": 92 * cfg.get("samples_per_frame", 0)
-                        + 44 * cfg.get("rays_in_box_per_frame", 0)}
+                        "frames_per_launch": cfg.get("frames_per_launch", 1),
+                        "algorithmic_bytes_per_launch": (92 * cfg.get("samples_per_frame", 0)
+                        + 44 * cfg.get("rays_in_box_per_frame", 0)) * cfg.get("frames_per_launch", 1)}
         out["records"], out["width"] = cfg.get("records"), cfg.get("width")
         out["config_name"] = cfg.get("name")
+        out["frames_per_launch"] = cfg.get("frames_per_launch", 1)
     except Exception as e:  # noqa: BLE001
         out["bench_error"] = str(e)
     f = counters(os.path.join(d, "pmc_fetch"), "FETCH_SIZE")
