@@ -292,12 +292,13 @@ def main():
         # s+1's unpack and render, ~20 us of barrier latency per step.
         torch.cuda.set_stream(torch.cuda.Stream(dev, priority=-1))
     stream = torch.cuda.current_stream(device).cuda_stream
-    # frames per step: --batch consecutive progressive frames per GPU (chained in one launch;
-    # the orbit's frames are new views, one per step), times N in progressive mode on N GPUs
-    # (per-GPU work fixed as N grows); one frame split over the N GPUs in frame mode
+    # frames per step: --batch consecutive progressive frames (chained in one launch; the
+    # orbit's frames are new views, one per step), times N in progressive mode on N GPUs
+    # (per-GPU work fixed as N grows); in frame mode the same --batch frames split over the
+    # N GPUs (total work fixed)
     strong = args.mode == "frame"
-    batch = max(1, args.batch) if orbit is None and not strong else 1
-    frames = 1 if strong else batch * (world if dist_path else 1)
+    batch = max(1, args.batch) if orbit is None else 1
+    frames = batch * (world if dist_path and not strong else 1)
     if not dist_path:
         fb = torch.zeros(W * H, dtype=torch.int32, device=dev)
         accum = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
@@ -415,7 +416,8 @@ def main():
         if world == 1 and not dist_path:
             parallelism = "single GPU"
         elif strong:
-            parallelism = (f"{world} GPUs x 64x64 cost-balanced tiles of ONE frame per step, RCCL "
+            parallelism = (f"{world} GPUs x 64x64 cost-balanced tiles of the step's {frames} frame(s) "
+                           f"(one launch per rank), RCCL "
                            f"gather of the RGBA8 tiles to rank 0 overlapped with the next step")
         else:
             parallelism = (f"{world} GPUs x 64x64 cost-balanced frame tiles, {frames} progressive "

@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--modes", default="progressive,frame")
     ap.add_argument("--deals", default="mod,dealt")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="frames per launch (bench.py --batch): the single-GPU step renders B "
+                         "chained frames, a rank's step B (frame mode) or N*B (progressive)")
     args = ap.parse_args()
     rn, bis, L, W, H, tf, orbit, _ = bench.CONFIGS[args.config]
     torch.cuda.set_device(0)
@@ -61,17 +64,22 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t) / args.steps * 1e3
 
-    def single(s):
-        lp.accumID = s
-        ctx.render(lp, W, H, fb.data_ptr(), acc.data_ptr(), stream)
+    B = max(1, args.batch)
 
-    ms1 = timed(single)
-    print(json.dumps({"config": args.config, "mode": "single", "n": 1, "ms_per_step": round(ms1, 4),
-                      "mray_s": round(W * H / ms1 / 1e3, 1)}), flush=True)
+    def single(s):
+        lp.accumID = s * B
+        if B > 1:
+            ctx.render_accumulate(lp, W, H, B, fb.data_ptr(), acc.data_ptr(), stream)
+        else:
+            ctx.render(lp, W, H, fb.data_ptr(), acc.data_ptr(), stream)
+
+    ms1 = timed(single) / B  # per frame
+    print(json.dumps({"config": args.config, "mode": "single", "n": 1, "batch": B,
+                      "ms_per_frame": round(ms1, 4), "mray_s": round(W * H / ms1 / 1e3, 1)}), flush=True)
     for deal in args.deals.split(","):
         for mode in args.modes.split(","):
             for n in (int(v) for v in args.ranks.split(",")):
-                frames = 1 if mode == "frame" else n
+                frames = B if mode == "frame" else n * B
                 steps = []
                 for r in range(n):
                     split = (irt_dist.TileSplit.dealt(W, H, r, n, lp, ctx.info, frames) if deal == "dealt"
@@ -92,7 +100,7 @@ def main():
                 # run-to-run noise is ~3 %, more than the imbalance being measured)
                 per_rank = [min(v) for v in zip(*[[timed(f) for f in steps] for _ in range(3)])]
                 mx, mean = max(per_rank), sum(per_rank) / n
-                print(json.dumps({"config": args.config, "deal": deal, "mode": mode, "n": n,
+                print(json.dumps({"config": args.config, "deal": deal, "mode": mode, "n": n, "batch": B,
                                   "ms_per_rank": [round(v, 4) for v in per_rank],
                                   "max_over_mean": round(mx / mean, 4),
                                   "ms_per_step_max": round(mx, 4),

@@ -72,6 +72,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--launches", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1, help="chained frames per launch (bench.py --batch)")
     args = ap.parse_args()
     rn, bis, L, W, H, tf, orbit_cfg, desc = bench.CONFIGS[args.config]
     dev = torch.device("cuda:0")
@@ -88,17 +89,22 @@ def main():
     if orbit_cfg:
         orbit = [irt.camera_look_at(*bench.orbit_camera(k), W, H) for k in range(bench.ORBIT_FRAMES)]
 
+    B = max(1, args.batch) if orbit is None else 1
+
     def step(s):
-        lp.accumID = s
+        lp.accumID = s * B
         if orbit is not None:
             c = orbit[s % bench.ORBIT_FRAMES]
             lp.org, lp.dir_00, lp.dir_du, lp.dir_dv = c.org, c.dir_00, c.dir_du, c.dir_dv
             lp.accumID = 0
-        ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
+        if B > 1:
+            ctx.render_accumulate(lp, W, H, B, fb.data_ptr(), accum.data_ptr(), stream)
+        else:
+            ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
 
     for s in range(args.warmup):
         step(s)
-    nwg = irt.num_tiles(W, H) * 16
+    nwg = irt.num_tiles(W, H) * 16 * B
     bufs = [torch.zeros(nwg * 4, dtype=torch.int32, device=dev) for _ in range(args.launches)]
     torch.cuda.synchronize()
     for k in range(args.launches):
@@ -110,7 +116,7 @@ def main():
     for k in range(args.launches):
         tr = bufs[k].cpu().numpy().view(np.uint32).reshape(-1, 4)
         out, prev = analyse(tr, prev)
-        out.update({"config": args.config, "launch": k})
+        out.update({"config": args.config, "launch": k, "frames_per_launch": B})
         print(json.dumps(out), flush=True)
     ctx.close()
 
