@@ -179,7 +179,11 @@ int irt_render_tiles(irt_context *ctx, const irt_launch_params *lp, int width, i
  * launch, bit-identical to numFrames irt_render calls with accumID incremented (each
  * frame's lerp(new, old, 1/(accumID+1)), deviceCode.cu:333-334, applied in order; fb holds
  * the last frame's make_rgba(linear_to_srgb(accum))).  The _tiles form packs like
- * irt_render_tiles and is what each rank runs in the multi-GPU weak-scaling split. */
+ * irt_render_tiles and is what each rank runs in the multi-GPU weak-scaling split.
+ * The frames are chained per pixel inside the one launch (frame f's workgroup of a block
+ * lerps once frame f - 1's has published the same pixels), so the next frame's workgroups
+ * fill the chip while the previous frame's last ones finish; every frame's accum and fb
+ * are written, as numFrames separate launches would. */
 int irt_render_accumulate(irt_context *ctx, const irt_launch_params *lp, int width, int height,
                           int numFrames, uint32_t *d_fb, irt_vec4f *d_accum, void *stream);
 int irt_render_tiles_accumulate(irt_context *ctx, const irt_launch_params *lp, int width,
