@@ -146,7 +146,6 @@ struct irt_context {
   size_t chainCap = 0;           // words in d_chainFlag
   uint32_t chainEpoch = 1;
   uint32_t *d_chainErr = nullptr;
-  int chainLag = 0;              // IRT_CHAIN_LAG (measurement, RenderArgs::chainLag)
   // persistent launches (RenderArgs::queue, IRT_QUEUE=0|1): every resident wave pulls 8x8
   // packets from per-slot queue counters (kSlots x kQueueWords u32, zero between launches)
   bool queueOn = false;
@@ -660,7 +659,6 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     A.chainFlag = c->d_chainFlag;
     A.chainErr = c->d_chainErr;
     A.chainEpoch = c->chainEpoch;
-    A.chainLag = render_wg_per_block(A, c->variant) == 1 ? c->chainLag : 0;
     c->chainEpoch += (uint32_t)numFrames;
   }
   if (numFrames > 1 && !A.chain) {
@@ -992,7 +990,6 @@ int irt_create_end(irt_context *c) {
   if (const char *e = getenv("IRT_QUEUE")) c->queueOn = atoi(e) != 0;
   if (const char *e = getenv("IRT_QUEUE_WGS")) c->queuePerCU = std::max(0, atoi(e));
   if (const char *e = getenv("IRT_CHAIN")) c->chainOn = atoi(e) != 0;
-  if (const char *e = getenv("IRT_CHAIN_LAG")) c->chainLag = std::max(0, atoi(e)) / 16 * 16;
   if ((rc = dalloc(c, &c->d_chainErr, 1))) return rc;
   IRT_HIP(hipMemsetAsync(c->d_chainErr, 0, sizeof(uint32_t), c->stream));
   if ((rc = dalloc(c, &c->d_queue, (size_t)kQueueWords * irt_context::kSlots))) return rc;

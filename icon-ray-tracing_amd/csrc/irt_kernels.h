@@ -101,10 +101,7 @@ struct RenderArgs {
   uint32_t chainEpoch;
   uint32_t *chainFlag;
   uint32_t *chainErr;
-  // (measurement, IRT_CHAIN_LAG = D > 0, a multiple of 16) a 1-D launch whose workgroups run the
-  // chained frames in groups of D blocks: group g's frame 0, 1, ... F-1, then group g+1's --
-  // block b's frames D workgroups apart instead of numBlocks (L2 reuse across frames)
-  int chainLag;
+
   // measurement only (irt_debug_set_wg_trace, profiles/wg_trace.py): non-null: workgroup b
   // writes {start, end} (s_memrealtime, 100 MHz, low 32 bits), HW_ID and XCC_ID to
   // wgTrace[4b..4b+3] -- when the machine is idle at a launch's ramp and tail

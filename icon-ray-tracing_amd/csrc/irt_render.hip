@@ -2025,15 +2025,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
   const float *th_p = lean ? A.srgbTh : s_th;
   T.s_hdr = &s_hdrs[(OPT & OPT_HDRLDS) ? tid >> 6 : 0];
   // OPT_WAVEWG: four one-wave workgroups per 256-pixel block, the block's wave blockIdx.x & 3
-  uint32_t wgX = blockIdx.x;
-  int frameY = (int)blockIdx.y;
-  if (!wavewg && A.chainLag > 0) {  // (measurement) chained frames in groups of chainLag blocks
-    const uint32_t nb = (uint32_t)A.numTiles * 16u, D = (uint32_t)A.chainLag, F = (uint32_t)A.numSamples;
-    const uint32_t g = wgX / (D * F), Dg = min(D, nb - g * D), rem = wgX - g * D * F;
-    frameY = (int)(rem / Dg);
-    wgX = g * D + rem % Dg;
-  }
-  const uint32_t wg = wavewg ? wgX >> 2 : wgX;
+  const uint32_t wg = wavewg ? blockIdx.x >> 2 : blockIdx.x;
   const int ptid = wavewg ? (int)((blockIdx.x & 3u) * 64u) + tid : tid;
   if constexpr ((OPT & OPT_TIMING) != 0) {
     T.tLast = tStart;
@@ -2064,7 +2056,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
     bool more = !queued || p != 0xFFFFFFFFu;
     while (more) {
       uint32_t pblk = blk, nx = 0u;
-      int pw = wavewg ? (int)(blockIdx.x & 3u) : (tid >> 6), frame = frameY;
+      int pw = wavewg ? (int)(blockIdx.x & 3u) : (tid >> 6), frame = (int)blockIdx.y;
       if constexpr (queued) {
         const uint32_t g = p >> 2;  // the packet's block over all frames
         frame = A.numSamples > 1 ? (int)(g / perFrame) : 0;
@@ -2365,10 +2357,7 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(numBlocks), dim3(256), 0, s, A);
     numBlocks = A.numTiles * 16;
   } else {
-    if (A.chainLag > 0)  // one dimension: k_render decodes (block, frame)
-      hipLaunchKernelGGL(k, dim3(numBlocks * A.numSamples), dim3(threads), 0, s, A);
-    else
-      hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads), A.numSamples), dim3(threads), 0, s, A);
+    hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads), A.numSamples), dim3(threads), 0, s, A);
   }
   // progressive batch: the lerp chain over the frames' samples (chained frames lerp in k_render)
   if (A.numSamples > 1 && !A.chain) hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);
