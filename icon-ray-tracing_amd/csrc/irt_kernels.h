@@ -119,7 +119,11 @@ constexpr int kCnt = 8;
 // waves per SIMD).  All give identical results.
 // one kernel per frame, 5 waves/SIMD (96 VGPRs; spills only in the prologue/epilogue): against
 // 4 waves C3 -1.8 %, C4 -4.9 %, comb TF -9 %, C5 +1.9 % (profiles/r03u_waves/)
-constexpr int kDefaultVariant = 5376;
+// Round 4: one-wave workgroups with the leaner LDS (OPT_WAVEWG | OPT_LEAN, 5 waves/SIMD): a
+// finished wave frees its slot at once instead of when its 256-pixel block's slowest wave does;
+// against 5376 (four-wave workgroups) with chained frames C3 -1.7 %, C3s -5.8 %, C4 -1.1 %, C5
+// -2.3 %, a single C3 frame -1.1 % (profiles/r04p_ab/)
+constexpr int kDefaultVariant = 6296832;
 bool render_variant_available(int variant);
 int render_variants(int *out, int cap);  // the compiled variants (count; the first cap into out)
 // workgroups per 256-pixel block the launch of `variant` uses for these arguments (4 only for

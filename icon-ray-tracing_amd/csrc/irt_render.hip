@@ -2285,16 +2285,17 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
-// The product build instantiates the default and the statistics variant (IRT_COUNTERS,
-// profiles/wave_stats.py); the A/B variants are built only by `make VARIANTS=all`
+// The product build instantiates the default (one-wave workgroups), 5376 (four-wave
+// workgroups, which also has the persistent-launch kernel) and the statistics variant
+// (IRT_COUNTERS, profiles/wave_stats.py); the A/B variants are built only by `make VARIANTS=all`
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
 #define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832)
 #else
-#define IRT_VARIANTS(X) X(5376) X(36864)
+#define IRT_VARIANTS(X) X(6296832) X(5376) X(36864)
 #endif
-static_assert(kDefaultVariant == 5376, "the product build's variant list names the default");
+static_assert(kDefaultVariant == 6296832, "the product build's variant list names the default");
 
 int render_variants(int *out, int cap) {
   int n = 0;
@@ -2336,8 +2337,9 @@ template <int N>
 RenderKernel kernel_for(const RenderArgs &A, int &threads) {
   constexpr int K = N & ~OPT_MONO;
   constexpr int D = kDefaultVariant & ~OPT_MONO;
-  constexpr int DW = (D & ~0xF00) | OPT_WEDGE | (K & OPT_SERIAL);
-  constexpr int DG = (D & ~0xF00) | 0x400;  // the grid-accel raygen: 4 waves/SIMD as measured in round 2
+  constexpr int DB = D & ~(0xF00 | OPT_WAVEWG | OPT_LEAN);  // 256-thread workgroups, full LDS
+  constexpr int DW = DB | OPT_WEDGE | (K & OPT_SERIAL);
+  constexpr int DG = DB | 0x400;  // the grid-accel raygen: 4 waves/SIMD as measured in round 2
   const bool g = A.accelMode == IRT_ACCEL_GRID;
   threads = 256;
   if (A.sampler != IRT_MODE_USER_GEOM && g) return k_render<DW | OPT_GRID>;  // CUBQL / TRIANGLES

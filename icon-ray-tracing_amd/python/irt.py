@@ -33,7 +33,8 @@ MODE_USER_GEOM = 0     # Volume::mode (Params.h:29-31): sample() on the cells (d
 MODE_TRIANGLES = 1     # closest bottom triangle toward the centre (deviceCode.cu:61-76)
 MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
 # The raygen's render variants (irt_render.hip OPT_* bits), all bit-identical: the product
-# library compiles 5376 (the default, 5 waves/SIMD) and 36864 (per-wave statistics);
+# library compiles 6296832 (the default since round 4: one-wave workgroups, 5 waves/SIMD),
+# 5376 (256-thread workgroups; the persistent launch's base) and 36864 (per-wave statistics);
 # libicon_rt_hip_all.so (`make VARIANTS=all`) adds the A/B variants: 4096 no waves-per-SIMD
 # floor, 5120 at 4 waves/SIMD, 70656 the one-lane-per-ray Woodcock loop, 136192 per-lane
 # candidate scans, 529408 per-region shader-clock timing (profiles/probe.py), 1053696

@@ -11,6 +11,7 @@ ramp (time until 90 % of the peak is resident) and tail (time from the last mome
 the peak was resident to the end).  Measurement only: frames are unchanged by the trace.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -104,7 +105,7 @@ def main():
 
     for s in range(args.warmup):
         step(s)
-    nwg = irt.num_tiles(W, H) * 16 * B
+    nwg = irt.num_tiles(W, H) * 16 * 4 * B  # room for one-wave workgroups (4 per block)
     bufs = [torch.zeros(nwg * 4, dtype=torch.int32, device=dev) for _ in range(args.launches)]
     torch.cuda.synchronize()
     for k in range(args.launches):
@@ -115,6 +116,10 @@ def main():
     prev = None
     for k in range(args.launches):
         tr = bufs[k].cpu().numpy().view(np.uint32).reshape(-1, 4)
+        L = irt.lib()
+        L.irt_debug_get_variant.argtypes = [ctypes.c_void_p]
+        wpb = 4 if L.irt_debug_get_variant(ctx._h) & 4194304 else 1  # OPT_WAVEWG: 4 per block
+        tr = tr[:irt.num_tiles(W, H) * 16 * B * wpb]
         out, prev = analyse(tr, prev)
         out.update({"config": args.config, "launch": k, "frames_per_launch": B})
         print(json.dumps(out), flush=True)

@@ -819,6 +819,11 @@ def test_persistent_launch_identical():
     S = irt.setup_frame(cells, 8, 8, camera=FRAMING)
     ctx = irt.Context(cells, 0)
     ctx.set_transfunc(S.lut, S.value_range)
+    # the persistent launch runs the 256-thread-workgroup kernel (5376), not the default's
+    # one-wave workgroups
+    L = irt.lib()
+    L.irt_debug_set_variant.argtypes = [C.c_void_p, C.c_int]
+    assert L.irt_debug_set_variant(ctx._h, 5376) == 0
 
     def run(on, fn):
         ctx.set_queue(on)
@@ -848,6 +853,8 @@ def test_persistent_launch_identical():
     # many launches back to back through the ring of counter pairs (kSlots = 32)
     ctx.set_queue(True)
     first = frame(100, 100)
+    L.irt_debug_queue_wgs.argtypes = [C.c_void_p]
+    assert L.irt_debug_queue_wgs(ctx._h) > 0  # the launches above were persistent ones
     for k in range(40):
         same(frame(100, 100), first, f"launch {k}")
     s2 = torch.cuda.Stream()
