@@ -297,8 +297,16 @@ def main():
     # (per-GPU work fixed as N grows); in frame mode the same --batch frames split over the
     # N GPUs (total work fixed)
     strong = args.mode == "frame"
-    batch = max(1, args.batch) if orbit is None else 1
+    batch = max(1, args.batch) if (orbit is None or not dist_path) else 1
     frames = batch * (world if dist_path and not strong else 1)
+    orbit_lps = None
+    if orbit is not None:  # each orbit view as a whole launch-parameter record (accumID 0)
+        orbit_lps = []
+        for c in orbit:
+            q = irt.LaunchParams.from_buffer_copy(lp)
+            q.org, q.dir_00, q.dir_du, q.dir_dv = c.org, c.dir_00, c.dir_du, c.dir_dv
+            q.accumID = 0
+            orbit_lps.append(q)
     if not dist_path:
         fb = torch.zeros(W * H, dtype=torch.int32, device=dev)
         accum = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
@@ -320,6 +328,11 @@ def main():
 
     def step(s):
         lp.accumID = s * frames
+        if orbit is not None and not dist_path and frames > 1:
+            # `frames` consecutive orbit views in one launch (irt_render_sequence)
+            seq = [orbit_lps[(s * frames + k) % ORBIT_FRAMES] for k in range(frames)]
+            ctx.render_sequence(seq, W, H, fb.data_ptr(), accum.data_ptr(), stream)
+            return
         if orbit is not None:
             c = orbit[s % ORBIT_FRAMES]
             lp.org, lp.dir_00, lp.dir_du, lp.dir_dv = c.org, c.dir_00, c.dir_du, c.dir_dv
@@ -384,8 +397,11 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for k in range(n1):
-            lp.accumID = base + k
-            ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
+            if orbit is not None:
+                ctx.render(orbit_lps[(base + k) % ORBIT_FRAMES], W, H, fb.data_ptr(), accum.data_ptr(), stream)
+            else:
+                lp.accumID = base + k
+                ctx.render(lp, W, H, fb.data_ptr(), accum.data_ptr(), stream)
         torch.cuda.synchronize()
         e1 = time.perf_counter() - t1
         single = {"ms_per_frame": round(e1 / n1 * 1e3, 4), "value": round(W * H * n1 / e1 / 1e6, 3),
@@ -438,8 +454,9 @@ def main():
             "data": "synthetic",
             "config": {
                 "name": args.config,
-                "workload": desc + (", orbit camera (eye 1.4e7 (sin t, 0, cos t), -fovy 60), "
-                                    "one orbit frame per step"
+                "workload": desc + (", orbit camera (eye 1.4e7 (sin t, 0, cos t), -fovy 60), " +
+                                    ("one orbit frame per step" if frames == 1 else
+                                     f"{frames} consecutive orbit views per step (one launch)")
                                     if orbit is not None else
                                     ", framing camera --camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60, " +
                                     ("one frame per step" if frames == 1 else

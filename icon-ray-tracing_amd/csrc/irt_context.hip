@@ -94,6 +94,7 @@ struct irt_context {
   static constexpr size_t kWgCountsMax = size_t(1) << 18;
   size_t wgCountsMax = kWgCountsMax;  // IRT_WG_COUNTS_MAX overrides (tests)
   unsigned long long *d_counters = nullptr;  // kSlots x 16
+  unsigned long long *d_counterBuckets = nullptr;  // kSlots x kCounterBuckets x 8 (zeroed)
   unsigned long long *h_counters = nullptr;  // pinned, kSlots x 16
   unsigned long long *dh_counters = nullptr; // h_counters as the device sees it
   hipStream_t lastStream = nullptr;  // stream of the previous launch
@@ -146,6 +147,11 @@ struct irt_context {
   size_t chainCap = 0;           // words in d_chainFlag
   uint32_t chainEpoch = 1;
   uint32_t *d_chainErr = nullptr;
+  // irt_render_sequence: the frames' camera words on the device, and per launch slot their
+  // pinned staging (a slot is reused only after its launch is retired)
+  float4 *d_frameCams = nullptr;
+  float4 *h_frameCams = nullptr;
+  size_t frameCamCap = 0;        // frames per slot
   // persistent launches (RenderArgs::queue, IRT_QUEUE=0|1): every resident wave pulls 8x8
   // packets from per-slot queue counters (kSlots x kQueueWords u32, zero between launches)
   bool queueOn = false;
@@ -211,7 +217,8 @@ void free_all(irt_context *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
                   c->d_sphBits, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_gridBits, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
-                  c->d_lut, c->d_counters, c->d_meta, c->d_queue, c->d_chainFlag, c->d_chainErr};
+                  c->d_lut, c->d_counters, c->d_counterBuckets, c->d_meta, c->d_queue, c->d_chainFlag, c->d_chainErr,
+                  c->d_frameCams};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->d_cells) (void)hipFree(c->d_cells);
@@ -220,6 +227,7 @@ void free_all(irt_context *c) {
   if (c->h_wgCounts) (void)hipHostFree(c->h_wgCounts);
   if (c->h_schedCost) (void)hipHostFree(c->h_schedCost);
   if (c->h_schedOrder) (void)hipHostFree(c->h_schedOrder);
+  if (c->h_frameCams) (void)hipHostFree(c->h_frameCams);
   for (int i = 0; i < irt_context::kSlots; ++i) {
     if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
@@ -454,7 +462,7 @@ int ensure_grid(irt_context *c) {
 int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int packed,
                 int tileBegin, int tileStride, uint32_t *fb, irt_vec4f *accum, int *numTilesOut,
                 void *stream, int numFrames = 1, const int32_t *tileList = nullptr,
-                int listCount = 0) {
+                int listCount = 0, const irt_launch_params *seq = nullptr) {
   if (!c || !lp || W <= 0 || H <= 0 || !fb || !accum || tileStride <= 0 || tileBegin < 0 ||
       numFrames < 1 || numFrames > 65535 || listCount < 0 || (listCount > 0 && !tileList)) {
     set_error("irt_render: bad argument");
@@ -661,6 +669,37 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     A.chainEpoch = c->chainEpoch;
     c->chainEpoch += (uint32_t)numFrames;
   }
+  if (seq) {
+    // a sequence of views (irt_render_sequence): frame k's camera and accumID as 4 float4
+    if (!A.chain) {
+      set_error("irt_render_sequence: needs chained frames (a cooperative variant, IRT_CHAIN on)");
+      return IRT_E_INVALID;
+    }
+    if ((size_t)numFrames > c->frameCamCap) {
+      int rc = finish_stats(c);  // every slot's staging retired before it is reallocated
+      if (rc) return rc;
+      IRT_HIP(hipStreamSynchronize(s));
+      if (c->d_frameCams) IRT_HIP(hipFree(c->d_frameCams));
+      if (c->h_frameCams) IRT_HIP(hipHostFree(c->h_frameCams));
+      c->d_frameCams = c->h_frameCams = nullptr;
+      c->bytes -= c->frameCamCap * 4 * sizeof(float4);
+      c->frameCamCap = 0;
+      if ((rc = dalloc(c, &c->d_frameCams, (size_t)numFrames * 4))) return rc;
+      IRT_HIP(hipHostMalloc((void **)&c->h_frameCams, (size_t)irt_context::kSlots * numFrames * 4 * sizeof(float4)));
+      c->frameCamCap = (size_t)numFrames;
+      c->info.deviceBytes = c->bytes;
+    }
+    float4 *h = c->h_frameCams + (size_t)slot * c->frameCamCap * 4;
+    for (int k = 0; k < numFrames; ++k) {
+      const irt_launch_params &q = seq[k];
+      h[4 * k + 0] = make_float4(q.org.x, q.org.y, q.org.z, __builtin_bit_cast(float, q.accumID));
+      h[4 * k + 1] = make_float4(q.dir_00.x, q.dir_00.y, q.dir_00.z, 0.f);
+      h[4 * k + 2] = make_float4(q.dir_du.x, q.dir_du.y, q.dir_du.z, 0.f);
+      h[4 * k + 3] = make_float4(q.dir_dv.x, q.dir_dv.y, q.dir_dv.z, 0.f);
+    }
+    IRT_HIP(hipMemcpyAsync(c->d_frameCams, h, (size_t)numFrames * 4 * sizeof(float4), hipMemcpyHostToDevice, s));
+    A.frameCams = c->d_frameCams;
+  }
   if (numFrames > 1 && !A.chain) {
     const size_t need = lanes * (size_t)numFrames;
     if (need > c->sampleCap) {
@@ -700,6 +739,8 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   c->schedApplied += c->schedLastApplied ? 1 : 0;
   // the 16-counter block (device atomics) is only needed by the statistics variant and the
   // IRT_COUNTERS=atomic mode; it must start zeroed
+  // the atomic fallback of the per-workgroup counts adds into this slot's buckets
+  A.counterBuckets = A.counters && !A.wgCounts ? c->d_counterBuckets + (size_t)slot * kCounterBuckets * 8 : nullptr;
   const bool block = A.counters && (!A.wgCounts || statsVariant);
   if (block && !c->lastBlock) IRT_HIP(hipMemsetAsync(A.counters, 0, 16 * sizeof(unsigned long long), s));
   if (c->launches > 0 && s != c->lastStream) {
@@ -720,7 +761,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   if (c->timed[slot]) IRT_HIP(hipEventRecord(c->ev1[slot], s));
   if (block) {
     launch_stats_out(A.counters, c->dh_counters + 16 * slot,
-                     c->d_counters + 16 * ((c->launches + 1) % irt_context::kSlots), s);
+                     c->d_counters + 16 * ((c->launches + 1) % irt_context::kSlots), A.counterBuckets, s);
     IRT_HIP(hipGetLastError());
   }
   c->slotBlock[slot] = block;
@@ -970,6 +1011,9 @@ int irt_create_end(irt_context *c) {
   IRT_HIP(hipMemsetAsync(c->d_maxOp, 0, c->numMCs * sizeof(float), c->stream));
   if ((rc = upload(c, &c->d_srgb, th, 256))) return rc;
   if ((rc = dalloc(c, &c->d_counters, 16 * irt_context::kSlots))) return rc;
+  if ((rc = dalloc(c, &c->d_counterBuckets, (size_t)kCounterBuckets * 8 * irt_context::kSlots))) return rc;
+  IRT_HIP(hipMemsetAsync(c->d_counterBuckets, 0, (size_t)kCounterBuckets * 8 * irt_context::kSlots * sizeof(unsigned long long),
+                         c->stream));
   IRT_HIP(hipHostMalloc((void **)&c->h_counters, 16 * irt_context::kSlots * sizeof(unsigned long long)));
   for (int i = 0; i < irt_context::kSlots; ++i) {
     IRT_HIP(hipEventCreate(&c->ev0[i]));
@@ -1235,6 +1279,30 @@ int irt_render_tiles(irt_context *c, const irt_launch_params *lp, int W, int H, 
 int irt_render_accumulate(irt_context *c, const irt_launch_params *lp, int W, int H,
                           int numFrames, uint32_t *fb, irt_vec4f *accum, void *stream) {
   return render_impl(c, lp, W, H, 0, 0, 1, fb, accum, nullptr, stream, numFrames);
+}
+
+int irt_render_sequence(irt_context *c, const irt_launch_params *lps, int numFrames, int W, int H,
+                        uint32_t *fb, irt_vec4f *accum, void *stream) {
+  if (!c || !lps || numFrames < 1) {
+    set_error("irt_render_sequence: bad argument");
+    return IRT_E_INVALID;
+  }
+  // only the camera and accumID may change from frame to frame
+  const size_t fixed = offsetof(irt_launch_params, ambientColor);
+  for (int k = 1; k < numFrames; ++k)
+    if (memcmp((const char *)&lps[k] + fixed, (const char *)&lps[0] + fixed, sizeof(irt_launch_params) - fixed)) {
+      set_error("irt_render_sequence: frame %d differs from frame 0 in more than the camera and accumID", k);
+      return IRT_E_INVALID;
+    }
+  const bool chainable = c->chainOn && (c->variant & 65536) == 0 && !c->queueOn && c->probeExit == 0;
+  if (numFrames == 1 || !chainable) {  // one launch per frame
+    for (int k = 0; k < numFrames; ++k) {
+      int rc = render_impl(c, &lps[k], W, H, 0, 0, 1, fb, accum, nullptr, stream);
+      if (rc) return rc;
+    }
+    return IRT_OK;
+  }
+  return render_impl(c, &lps[0], W, H, 0, 0, 1, fb, accum, nullptr, stream, numFrames, nullptr, 0, lps);
 }
 
 int irt_render_tiles_accumulate(irt_context *c, const irt_launch_params *lp, int W, int H,

@@ -53,6 +53,10 @@ struct RenderArgs {
   int tileBegin, tileStride, numTiles, tilesX;
   const int32_t *tileList;  // explicit tile ids (irt_render_tile_list); null: tileBegin + k*tileStride
   unsigned long long *counters;  // [0] launched [1] inBox [2] locate [3] found [4] candidates
+  // the device-atomic fallback of the per-workgroup counts (a launch past wgCountsMax
+  // workgroups): kCounterBuckets x 8 counters, workgroup w adding into bucket w % 64 (one line
+  // would serialise every workgroup's adds), summed into counters[0..4] by k_stats_out
+  unsigned long long *counterBuckets;
   // The binned locator (irt_common.h): per cube-map cell a 32-B header, fat entries,
   // per-record height/value blocks.
   const uint4 *binHdr;
@@ -98,6 +102,10 @@ struct RenderArgs {
   // A frame's workgroups wait on the previous frame's, which the linear dispatch order puts
   // earlier on the same XCD; a wait that times out sets *chainErr (pixels then unordered).
   int chain;
+  // a sequence of views (irt_render_sequence; null otherwise): frame f's camera and accumID
+  // as 4 float4 {org, accumID bits} {dir_00} {dir_du} {dir_dv}, uploaded before the launch and
+  // read by the scalar unit in place of org/dir00/du/dv and accumID + f
+  const float4 *frameCams;
   uint32_t chainEpoch;
   uint32_t *chainFlag;
   uint32_t *chainErr;
@@ -152,8 +160,11 @@ void launch_grid_bits(const float *maxOp, uint32_t *bits, hipStream_t s);
 void launch_max_opacities(const float *valueRanges, size_t numMCs, const float4 *lut, int size,
                           float lo, float hi, float *maxOp, hipStream_t s);
 void launch_clear(uint32_t *fb, float4 *accum, size_t n, hipStream_t s);
+constexpr int kCounterBuckets = 64;
+// copies a launch's 16 counters to the host (plus, with `buckets`, the bucketed fallback
+// counts, whose buckets it zeroes again) and zeroes the next launch's block
 void launch_stats_out(const unsigned long long *cur, unsigned long long *host,
-                      unsigned long long *next, hipStream_t s);
+                      unsigned long long *next, unsigned long long *buckets, hipStream_t s);
 void launch_copy_u32(const uint32_t *src, uint32_t *dst, size_t n, hipStream_t s);
 // The scene build on the device (irt_build.hip): per-record blocks and the binned cube-map
 // locator (irt_build.h) from the cells and their glibc corner trig in HBM.  On success the

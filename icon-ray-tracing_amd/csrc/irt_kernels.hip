@@ -344,10 +344,19 @@ __global__ void k_unpack(const uint32_t *gathered, int numRanks, int maxTiles, i
 // release) and the next ring slot zeroed for the next launch.  (The default path needs no
 // such kernel: the render kernel's workgroups write their counts to host memory.)
 __global__ void k_stats_out(const unsigned long long *cur, unsigned long long *host,
-                            unsigned long long *next) {
-  const int i = threadIdx.x;
+                            unsigned long long *next, unsigned long long *buckets) {
+  const int i = threadIdx.x;  // 64 threads: bucket i's 8 counters
+  __shared__ unsigned long long s_b[kCounterBuckets][8];
+  for (int j = 0; j < 8; ++j) {
+    s_b[i][j] = buckets ? buckets[i * 8 + j] : 0ull;
+    if (buckets) buckets[i * 8 + j] = 0ull;  // clean for this slot's next launch
+  }
+  __syncthreads();
   if (i < 16) {
-    host[i] = cur[i];
+    unsigned long long v = cur[i];
+    if (i < 8)
+      for (int b = 0; b < kCounterBuckets; ++b) v += s_b[b][i];
+    host[i] = v;
     if (next != cur) next[i] = 0ull;
   }
 }
@@ -434,8 +443,8 @@ void launch_max_opacities(const float *vr, size_t numMCs, const float4 *lut, int
                      (const float2 *)vr, numMCs, lut, size, lo, hi, maxOp);
 }
 void launch_stats_out(const unsigned long long *cur, unsigned long long *host,
-                      unsigned long long *next, hipStream_t s) {
-  hipLaunchKernelGGL(k_stats_out, dim3(1), dim3(64), 0, s, cur, host, next);
+                      unsigned long long *next, unsigned long long *buckets, hipStream_t s) {
+  hipLaunchKernelGGL(k_stats_out, dim3(1), dim3(kCounterBuckets), 0, s, cur, host, next, buckets);
 }
 // a u32 array between device memory and mapped pinned host memory (either direction):
 // the scheduling costs and block orders, without an SDMA copy on the render stream

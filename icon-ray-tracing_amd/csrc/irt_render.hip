@@ -179,6 +179,26 @@ struct TimeAccOn {
   uint64_t tLast = 0, tAcc[kTimeRegions] = {};
 };
 
+// The camera of frame `frame` of a launch: the launch's own, or in a sequence of views
+// (RenderArgs::frameCams, irt_render_sequence) that frame's words, read through the constant
+// address space (scalar loads: uniform values, written by the host before the launch).
+typedef const __attribute__((address_space(4))) fvec4 *CamWords;
+__device__ __forceinline__ float4 cam_word(const RenderArgs &A, int frame, int k) {
+  return __builtin_bit_cast(float4, ((CamWords)A.frameCams)[4 * frame + k]);
+}
+__device__ __forceinline__ float3 cam_org(const RenderArgs &A, int frame) {
+  if (A.frameCams) {
+    const float4 w = cam_word(A, frame, 0);
+    return make_float3(w.x, w.y, w.z);
+  }
+  return A.org;
+}
+// the frame's accumID (deviceCode.cu:288-289): accumID + frame in a progressive batch
+__device__ __forceinline__ int cam_accum_id(const RenderArgs &A, int frame) {
+  if (A.frameCams) return (int)__float_as_uint(cam_word(A, frame, 0).w);
+  return A.accumID + frame;
+}
+
 template <int OPT>
 struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOff> {
   const RenderArgs &A;
@@ -191,6 +211,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // the cooperative loop's statistics, per lane (samples taken, their locates / found /
   // candidate tests), added into s_cnt at the end by flush_coop
   uint32_t nLocate = 0, nFound = 0, nCand = 0;
+  int frame = 0;  // the launch's frame this wave renders (its camera: cam_org)
   // OPT_TIMING: shader clocks per region (wave-uniform), in the TimeAcc base
   __device__ __forceinline__ void tmark(int region) {
     if constexpr ((OPT & OPT_TIMING) != 0) {
@@ -804,7 +825,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       st = lcg_next(st);
       t -= (woodcock_log(st, s_logf) / q);
       if (t > tmax) break;
-      const float px = A.org.x + dx * t, py = A.org.y + dy * t, pz = A.org.z + dz * t;
+      const float3 O = cam_org(A, frame);
+      const float px = O.x + dx * t, py = O.y + dy * t, pz = O.z + dz * t;
       float value = 0.f;
       if (counted) count(2);
       if (!locate(px, py, pz, value)) continue;
@@ -929,7 +951,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
             const float t1 = tk - woodcock_log(lcg_next(lcg_next(sk)), s_logf) * __builtin_amdgcn_rcpf(rq.z);
             if (t1 <= rq.y) {
               uint32_t sb;
-              const uint32_t c1 = cubemap_cell_fast(A.org.x + ry.x * t1, A.org.y + ry.y * t1, A.org.z + ry.z * t1,
+              const float3 O = cam_org(A, frame);
+              const uint32_t c1 = cubemap_cell_fast(O.x + ry.x * t1, O.y + ry.y * t1, O.z + ry.z * t1,
                                                     A.G, sb);
               tp = reinterpret_cast<const uint32_t *>(A.binHdr + (size_t)c1 * (kBinHdrWords / 4));
             }
@@ -937,10 +960,12 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         } else {
           (void)wr;
         }
-        found = locate_wave(used && !past, A.org.x + ry.x * tk, A.org.y + ry.y * tk, A.org.z + ry.z * tk,
+        const float3 O = cam_org(A, frame);
+        found = locate_wave(used && !past, O.x + ry.x * tk, O.y + ry.y * tk, O.z + ry.z * tk,
                             value, W, *SW, tp);
       } else if (used && !past) {
-        found = locate(A.org.x + ry.x * tk, A.org.y + ry.y * tk, A.org.z + ry.z * tk, value);
+        const float3 O = cam_org(A, frame);
+        found = locate(O.x + ry.x * tk, O.y + ry.y * tk, O.z + ry.z * tk, value);
       }
       tmark(5);  // locate's tail: sphere, getValue
       if (found) {
@@ -1053,7 +1078,7 @@ __device__ __forceinline__ Pixel pixel_of(const RenderArgs &A, uint32_t blkU, in
 // Random rnd(accumID*W*H + x, y) (deviceCode.cu:288-289) and generateRay (36-49); g++
 // draws the dir_dv jitter first.
 __device__ __forceinline__ void gen_ray(const RenderArgs &A, int accumID, int x, int y, uint32_t &st,
-                                        float &dx, float &dy, float &dz) {
+                                        float &dx, float &dy, float &dz, int frame = 0) {
   st = lcg_seed((uint32_t)accumID * (uint32_t)A.W * (uint32_t)A.H + (uint32_t)x, (uint32_t)y);
   st = lcg_next(st);
   const float jv = lcg_float(st);
@@ -1061,9 +1086,16 @@ __device__ __forceinline__ void gen_ray(const RenderArgs &A, int accumID, int x,
   const float ju = lcg_float(st);
   const float su = (float)x + .5f, sv = (float)y + .5f;
   const float a = su + ju, b = sv + jv;
-  dx = (A.dir00.x + a * A.du.x) + b * A.dv.x;
-  dy = (A.dir00.y + a * A.du.y) + b * A.dv.y;
-  dz = (A.dir00.z + a * A.du.z) + b * A.dv.z;
+  float3 d00 = A.dir00, du = A.du, dv = A.dv;
+  if (A.frameCams) {  // a sequence of views: this frame's camera
+    const float4 w1 = cam_word(A, frame, 1), w2 = cam_word(A, frame, 2), w3 = cam_word(A, frame, 3);
+    d00 = make_float3(w1.x, w1.y, w1.z);
+    du = make_float3(w2.x, w2.y, w2.z);
+    dv = make_float3(w3.x, w3.y, w3.z);
+  }
+  dx = (d00.x + a * du.x) + b * dv.x;
+  dy = (d00.y + a * du.y) + b * dv.y;
+  dz = (d00.z + a * du.z) + b * dv.z;
   const float len = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
   if (recip_ok(len)) {  // normalize's three quotients through one reciprocal (irt_device.h)
     const double r = recip_d(len);
@@ -1181,7 +1213,9 @@ __device__ __forceinline__ void flush_counters(const RenderArgs &A, const uint32
     const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
     if (lane < kCnt) A.wgCounts[wg * kCnt + lane] = s_cnt[lane];
   } else if (lane < 5 && s_cnt[lane]) {
-    atomicAdd(&A.counters[lane], (unsigned long long)s_cnt[lane]);
+    const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    unsigned long long *dst = A.counterBuckets ? A.counterBuckets + (wg % kCounterBuckets) * 8 : A.counters;
+    atomicAdd(&dst[lane], (unsigned long long)s_cnt[lane]);
   }
 }
 
@@ -1494,8 +1528,9 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   bool inBox = false;
   float t0box = 0.f, t1box = 0.f;
   if (px.active) {
-    gen_ray(A, accumID, px.x, px.y, st, dx, dy, dz);
-    const Ray ray = {A.org.x, A.org.y, A.org.z, 0.f, dx, dy, dz, 1e10f};
+    gen_ray(A, accumID, px.x, px.y, st, dx, dy, dz, frame);
+    const float3 O = cam_org(A, frame);
+    const Ray ray = {O.x, O.y, O.z, 0.f, dx, dy, dz, 1e10f};
     float t0, t1;
     const bool boxHit = box_test(ray, A, t0, t1);
     if (A.probeExit == 3) {  // measurement only: ray generation and boxTest, nothing written
@@ -1551,7 +1586,8 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     if (phase == kRange && !ae) {
       const float rtmin = t0box, rtmax = t1box;  // the box interval [t0, t1]
       const int D = kGridDim;
-      const float ox = A.org.x + rtmin * dx, oy = A.org.y + rtmin * dy, oz = A.org.z + rtmin * dz;
+      const float3 O = cam_org(A, frame);
+      const float ox = O.x + rtmin * dx, oy = O.y + rtmin * dy, oz = O.z + rtmin * dz;
       gtmax = rtmax - rtmin;
       grtmin = rtmin;
       const float rx = 1.f / dx, ry = 1.f / dy, rz = 1.f / dz;
@@ -1600,10 +1636,11 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       float r2, la2, lo2;
       int cy2 = 0, cz2 = 0;
       bool ok2 = false;
+      const float3 O = cam_org(A, frame);
       if constexpr (kFastSph)
-        ok2 = spherical_fast(A, A.org.x + dx * e2, A.org.y + dy * e2, A.org.z + dz * e2, r2, la2, lo2, cy2, cz2);
+        ok2 = spherical_fast(A, O.x + dx * e2, O.y + dy * e2, O.z + dz * e2, r2, la2, lo2, cy2, cz2);
       else
-        to_spherical(A.org.x + dx * e2, A.org.y + dy * e2, A.org.z + dz * e2, r2, la2, lo2);
+        to_spherical(O.x + dx * e2, O.y + dy * e2, O.z + dz * e2, r2, la2, lo2);
       const float4 en = lds_ld16(&s_entry[tid_late()]);
       const float r1 = en.x;
       const int sx = r1 < r2 ? 1 : -1;
@@ -1623,7 +1660,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
         for (int k = 0; k < 2; ++k) {  // the entry, then the exit point (one inlined copy)
           const float e = k == 0 ? en.w + sceneEPS() : upper - sceneEPS();
           float rr, la, lo;
-          to_spherical(A.org.x + dx * e, A.org.y + dy * e, A.org.z + dz * e, rr, la, lo);
+          to_spherical(O.x + dx * e, O.y + dy * e, O.z + dz * e, rr, la, lo);
           if (k == 0) {
             la1 = la;
             lo1 = lo;
@@ -1736,7 +1773,8 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
         cx = cy = cz = 0;
         if (!ae) {  // cellID of the entry point (ShellAccel.h:121-124)
           const float e1 = lower + sceneEPS();
-          const float x1 = A.org.x + dx * e1, y1 = A.org.y + dy * e1, z1 = A.org.z + dz * e1;
+          const float3 O = cam_org(A, frame);
+          const float x1 = O.x + dx * e1, y1 = O.y + dy * e1, z1 = O.z + dz * e1;
           float r1, la1, lo1;
           // OPT_FASTSPH: the certified fast lat/lon, glibc-exact when not certified
           if (!(kFastSph && spherical_fast(A, x1, y1, z1, r1, la1, lo1, cy, cz))) {
@@ -2093,8 +2131,9 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
       } else {
         const Pixel ppx = pixel_of(A, pblk, pw * 64 + (ltid & 63));
         launched += (uint32_t)__popcll(__ballot(ppx.active));
+        T.frame = frame;
         render_pixel_coop<OPT>(A, T, ppx, th_p, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
-                               &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, A.accumID + frame,
+                               &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, cam_accum_id(A, frame),
                                pblk, pw, frame);
         if (A.chain && frame < A.numSamples - 1) {
           // chained frames: this wave's pixels are written through; tell frame + 1's wave

@@ -143,6 +143,7 @@ def lib() -> C.CDLL:
             "irt_render_tiles": [P, C.POINTER(LaunchParams), I, I, I, I, P, P,
                                  C.POINTER(C.c_int), P],
             "irt_render_accumulate": [P, C.POINTER(LaunchParams), I, I, I, P, P, P],
+            "irt_render_sequence": [P, C.POINTER(LaunchParams), I, I, I, P, P, P],
             "irt_render_tiles_accumulate": [P, C.POINTER(LaunchParams), I, I, I, I, I, P, P,
                                             C.POINTER(C.c_int), P],
             "irt_unpack_tiles": [P, P, I, I, I, I, P, P],
@@ -576,6 +577,14 @@ class Context:
                                       tile_stride, C.c_void_p(fb_ptr), C.c_void_p(accum_ptr),
                                       C.byref(n), C.c_void_p(stream)), "irt_render_tiles")
         return n.value
+
+    def render_sequence(self, lps, width: int, height: int, fb_ptr: int, accum_ptr: int,
+                        stream: int = 0):
+        """irt_render_sequence: lps[k] (camera and accumID per frame) in one launch."""
+        arr = (LaunchParams * len(lps))(*lps)
+        _check(lib().irt_render_sequence(self._h, arr, len(lps), width, height, C.c_void_p(fb_ptr),
+                                         C.c_void_p(accum_ptr), C.c_void_p(stream)),
+               "irt_render_sequence")
 
     def render_accumulate(self, lp: LaunchParams, width: int, height: int, num_frames: int,
                           fb_ptr: int, accum_ptr: int, stream: int = 0):

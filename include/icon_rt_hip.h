@@ -186,6 +186,14 @@ int irt_render_tiles(irt_context *ctx, const irt_launch_params *lp, int width, i
  * are written, as numFrames separate launches would. */
 int irt_render_accumulate(irt_context *ctx, const irt_launch_params *lp, int width, int height,
                           int numFrames, uint32_t *d_fb, irt_vec4f *d_accum, void *stream);
+/* A sequence of views in one launch: frame k renders lps[k] -- its own camera (org, dir_00,
+ * dir_du, dir_dv) and accumID; every other member must equal lps[0]'s -- into the same fb and
+ * accum, bit-identical to numFrames irt_render calls in order (the reference's render loop,
+ * pipeline.cu:991-1075, with the camera moved between frames: an orbit or a camera path).  The
+ * frames are chained per pixel in the launch, as in irt_render_accumulate; with a variant or
+ * setting that cannot chain, one launch per frame. */
+int irt_render_sequence(irt_context *ctx, const irt_launch_params *lps, int numFrames, int width,
+                        int height, uint32_t *d_fb, irt_vec4f *d_accum, void *stream);
 int irt_render_tiles_accumulate(irt_context *ctx, const irt_launch_params *lp, int width,
                                 int height, int tileBegin, int tileStride, int numFrames,
                                 uint32_t *d_fb_tiles, irt_vec4f *d_accum_tiles, int *numTiles,

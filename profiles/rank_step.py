@@ -49,6 +49,7 @@ def main():
     cam = bench.orbit_camera(0) if orbit else bench.FRAMING
     setup = irt.setup_frame(None, W, H, camera=cam, info=ctx.info)
     ctx.set_transfunc(bench.make_lut(tf, setup.lut), setup.value_range)
+    ctx.set_statistics(False)  # as bench.py's timed loop
     lp = setup.lp
     stream = torch.cuda.current_stream(dev).cuda_stream
     fb = torch.zeros(W * H, dtype=torch.int32, device=dev)

@@ -49,10 +49,28 @@ def main(d):
     for r in rows(os.path.join(d, "stats", "**", "*kernel_stats.csv")):
         name = col(r, "Name")
         short = name.split("(")[0].replace("irt::", "")
-        out.setdefault("kernels", {})[short] = {
-            "calls": int(col(r, "Calls")), "avg_ns": float(col(r, "AverageNs")),
-            "total_ns": float(col(r, "TotalDurationNs")),
-            "min_ns": float(col(r, "MinNs")), "max_ns": float(col(r, "MaxNs"))}
+        k = {"calls": int(col(r, "Calls")), "avg_ns": float(col(r, "AverageNs")),
+             "total_ns": float(col(r, "TotalDurationNs")),
+             "min_ns": float(col(r, "MinNs")), "max_ns": float(col(r, "MaxNs"))}
+        out.setdefault("kernels", {})[short] = k
+    # The context's prewarm dispatch (one workgroup returning at once, irt_render.hip
+    # prewarm_render) runs the default kernel too: from the per-dispatch trace, the render
+    # kernels' statistics without single-workgroup dispatches
+    per = {}
+    for r in rows(os.path.join(d, "stats", "**", "*kernel_trace.csv")):
+        name = col(r, "Kernel_Name")
+        if "k_render" not in name:
+            continue
+        grid = int(col(r, "Grid_Size_X")) * int(col(r, "Grid_Size_Y")) * int(col(r, "Grid_Size_Z"))
+        wg = int(col(r, "Workgroup_Size_X")) * int(col(r, "Workgroup_Size_Y")) * int(col(r, "Workgroup_Size_Z"))
+        if grid <= wg:
+            continue
+        short = name.split("(")[0].replace("irt::", "")
+        per.setdefault(short, []).append(int(col(r, "End_Timestamp")) - int(col(r, "Start_Timestamp")))
+    for short, v in per.items():
+        k = out.setdefault("kernels", {}).setdefault(short, {})
+        k.update({"calls": len(v), "avg_ns": sum(v) / len(v), "total_ns": float(sum(v)),
+                  "min_ns": float(min(v)), "max_ns": float(max(v)), "single_workgroup_dispatches_excluded": True})
     try:
         bench = json.loads(open(os.path.join(d, "bench_stats.json")).read().strip().splitlines()[-1])
         cfg = bench["config"]

@@ -103,3 +103,61 @@ def test_chained_batch_other_kernels(accel, sampler):
     assert got[2] == ref[2]
     assert ctx.chain_errors() == 0
     ctx.close()
+
+
+def _views(setup, W, H, n, first=0, accum=None):
+    """n orbit views around the globe (a new view per frame, accumID 0 unless `accum`)."""
+    out = []
+    for k in range(n):
+        th = 2.0 * np.pi * (first + k) / 60.0
+        c = irt.camera_look_at((1.4e7 * np.sin(th), 0.0, 1.4e7 * np.cos(th)), (0.0, 0.0, 0.0),
+                               (0.0, 1.0, 0.0), 60.0, W, H)
+        q = irt.LaunchParams.from_buffer_copy(setup.lp)
+        q.org, q.dir_00, q.dir_du, q.dir_dv = c.org, c.dir_00, c.dir_du, c.dir_dv
+        q.accumID = 0 if accum is None else accum + k
+        out.append(q)
+    return out
+
+
+@pytest.mark.parametrize("W,H,n,accum", [(96, 80, 5, None), (512, 512, 7, None), (200, 136, 4, 3)])
+def test_sequence_equals_single_launches(W, H, n, accum):
+    """irt_render_sequence (an orbit: camera and accumID per frame, chained in one launch) ==
+    the same views rendered one launch each, counts included; a moving camera that keeps
+    accumulating (accumID 3, 4, ...) too."""
+    import torch
+    cells = irt.synth_grid(2, 3, 90)
+    setup = irt.setup_frame(cells, W, H, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    lps = _views(setup, W, H, n, accum=accum)
+    out = []
+    for seq in (False, True):
+        fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+        if seq:
+            ctx.render_sequence(lps, W, H, fb.data_ptr(), acc.data_ptr())
+        else:
+            for q in lps:
+                ctx.render(q, W, H, fb.data_ptr(), acc.data_ptr())
+        torch.cuda.synchronize()
+        out.append((fb.cpu().numpy().copy(), bits(acc.cpu().numpy())))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    # counts: the sequence's launch against the sum of the single launches
+    ctx.reset_stats_total()
+    fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    for q in lps:
+        ctx.render(q, W, H, fb.data_ptr(), acc.data_ptr())
+    ref, _ = ctx.stats_total()
+    ctx.reset_stats_total()
+    ctx.render_sequence(lps, W, H, fb.data_ptr(), acc.data_ptr())
+    got, _ = ctx.stats_total()
+    for f in ("raysLaunched", "raysInBox", "locateCalls", "samplesFound", "candidatesTested"):
+        assert getattr(got, f) == getattr(ref, f), f
+    assert ctx.chain_errors() == 0
+    # only the camera and accumID may differ between frames
+    bad = _views(setup, W, H, 2)
+    bad[1].ambientRadiance = bad[0].ambientRadiance * 2.0
+    with pytest.raises(irt.IrtError):
+        ctx.render_sequence(bad, W, H, fb.data_ptr(), acc.data_ptr())
+    ctx.close()
