@@ -2062,9 +2062,14 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
   T.s_gbits = s_gbits;
   const float *th_p = lean ? A.srgbTh : s_th;
   T.s_hdr = &s_hdrs[(OPT & OPT_HDRLDS) ? tid >> 6 : 0];
-  // OPT_WAVEWG: four one-wave workgroups per 256-pixel block, the block's wave blockIdx.x & 3
-  const uint32_t wg = wavewg ? blockIdx.x >> 2 : blockIdx.x;
-  const int ptid = wavewg ? (int)((blockIdx.x & 3u) * 64u) + tid : tid;
+  // OPT_WAVEWG: four one-wave workgroups per 256-pixel block.  The hardware deals workgroup i
+  // to XCD i % 8, so workgroup i renders wave (i >> 3) & 3 of block ((i >> 5) << 3) | (i & 7):
+  // a block's four packets share one XCD's L2, as the four waves of a 256-thread workgroup do
+  // (numBlocks is a multiple of 16)
+  const uint32_t bx = blockIdx.x;
+  const uint32_t wg = wavewg ? ((bx >> 5) << 3) | (bx & 7u) : bx;
+  const int wwave = wavewg ? (int)((bx >> 3) & 3u) : 0;  // the block's wave this workgroup renders
+  const int ptid = wavewg ? wwave * 64 + tid : tid;
   if constexpr ((OPT & OPT_TIMING) != 0) {
     T.tLast = tStart;
     T.tmark(0);  // prologue
@@ -2094,7 +2099,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
     bool more = !queued || p != 0xFFFFFFFFu;
     while (more) {
       uint32_t pblk = blk, nx = 0u;
-      int pw = wavewg ? (int)(blockIdx.x & 3u) : (tid >> 6), frame = (int)blockIdx.y;
+      int pw = wavewg ? wwave : (tid >> 6), frame = (int)blockIdx.y;
       if constexpr (queued) {
         const uint32_t g = p >> 2;  // the packet's block over all frames
         frame = A.numSamples > 1 ? (int)(g / perFrame) : 0;
@@ -2210,7 +2215,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
     prev = (uint32_t)__shfl((int)prev, 0, 64);
     if (prev == (blockDim.x >> 6) - 1u) {
       if (A.counters) flush_counters(A, s_cnt, lane);
-      if (A.schedCost && lane == 0 && (!wavewg || (blockIdx.x & 3u) == 0u)) {  // this workgroup's duration, for the next launches' order
+      if (A.schedCost && lane == 0 && (!wavewg || wwave == 0)) {  // this workgroup's duration, for the next launches' order
         const uint64_t dt = wall_clock64() - c0;
         A.schedCost[blk] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
       }

@@ -7,7 +7,7 @@ OUT=${1:?out}; CONFIGS=${2:?configs}; shift 2
 mkdir -p "$OUT"
 for cfg in $CONFIGS; do
   # frames per run as before round 4's chained batches; BATCH frames per launch (bench.py --batch)
-  B=${BATCH:-8}; [ "$cfg" = c5 ] && B=1
+  B=${BATCH:-8}
   steps=200; [ "$cfg" = c5 ] && steps=60; [ "$cfg" = c3s ] && steps=40; [ "$cfg" = c4 ] && steps=80
   steps=$(( (steps + B - 1) / B ))
   for round in $(seq 1 ${ROUNDS:-3}); do
