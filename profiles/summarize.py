@@ -39,6 +39,9 @@ def counters(d, name):
     for r in rows(os.path.join(d, "**", "*counter_collection.csv")):
         if KERNEL not in col(r, "Kernel_Name") or col(r, "Counter_Name") != name:
             continue
+        # the context's one-workgroup prewarm dispatch is not a render
+        if int(float(col(r, "Grid_Size"))) <= int(float(col(r, "Workgroup_Size"))):
+            continue
         key = col(r, "Dispatch_Id")
         vals[key] = vals.get(key, 0.0) + float(col(r, "Counter_Value"))
     return list(vals.values())
