@@ -62,6 +62,8 @@ enum : int {
                             // cube-map header line of its ray's next sample (the one taken if
                             // this sample is located and rejected), in the same batch as this
                             // sample's header, so that the next round's header read hits L2
+  OPT_WAVEWG2 = 536870912,  // (A/B, with OPT_LEAN) two-wave workgroups: a block's packets in pairs
+                            // (each pair sharing a CU's L1), a slot freed per two waves
   OPT_PAIR = 268435456,  // (A/B) the wave-wide scan's first step tests each lane's first two
                          // candidates (both entries gathered together), so the dealt-out step
                          // runs only for lanes whose first two fail
@@ -1994,18 +1996,21 @@ __device__ __forceinline__ void queue_done(uint32_t *Q) {
 
 // The raygen over the frame grid: one lane per pixel (see pixel_of).
 template <int OPT>
-__global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1)
+__global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2) ? 128 : 256),
+                                  ((OPT >> 8) & 15) ? ((OPT >> 8) & 15) : 1)
     k_render(RenderArgs A) {
   constexpr bool lean = (OPT & OPT_LEAN) != 0;
   constexpr bool wavewg = (OPT & OPT_WAVEWG) != 0;
-  static_assert(!wavewg || (lean && Tracer<OPT>::kCoop), "one-wave workgroups: lean, cooperative kernels");
-  constexpr int kT = wavewg ? 64 : 256;   // threads per workgroup
+  constexpr int kWpg = wavewg ? 1 : ((OPT & OPT_WAVEWG2) ? 2 : 4);  // waves per workgroup
+  constexpr bool split = kWpg < 4;  // several workgroups per 256-pixel block
+  static_assert(!split || (lean && Tracer<OPT>::kCoop), "one-/two-wave workgroups: lean, cooperative kernels");
+  constexpr int kT = 64 * kWpg;   // threads per workgroup
   constexpr int kW = kT / 64;            // waves per workgroup
   __shared__ float s_th[lean ? 1 : 256];
   __shared__ uint32_t s_cnt[kCnt];
   __shared__ LogfTab s_logf[16];
   __shared__ uint32_t s_sph[lean ? 1 : kSphBitWords];
-  __shared__ int4 s_dda[wavewg ? 1 : 256];  // sdda state needed only after a range's first leaf
+  __shared__ int4 s_dda[split ? 1 : 256];  // sdda state needed only after a range's first leaf
   __shared__ float4 s_entry[kT];
   __shared__ CoopWave s_coop[kW];   // the cooperative Woodcock loop (kCoop kernels)
   __shared__ ScanWave s_scan[Tracer<OPT>::kWaveScan ? kW : 1];  // its wave-wide candidate scan
@@ -2066,10 +2071,13 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
   // to XCD i % 8, so workgroup i renders wave (i >> 3) & 3 of block ((i >> 5) << 3) | (i & 7):
   // a block's four packets share one XCD's L2, as the four waves of a 256-thread workgroup do
   // (numBlocks is a multiple of 16)
+  // (OPT_WAVEWG2: two-wave workgroups, workgroup i the waves 2 ((i >> 3) & 1) + {0, 1} of block
+  // ((i >> 4) << 3) | (i & 7))
+  constexpr uint32_t kNwb = 4 / kWpg;  // workgroups per block
   const uint32_t bx = blockIdx.x;
-  const uint32_t wg = wavewg ? ((bx >> 5) << 3) | (bx & 7u) : bx;
-  const int wwave = wavewg ? (int)((bx >> 3) & 3u) : 0;  // the block's wave this workgroup renders
-  const int ptid = wavewg ? wwave * 64 + tid : tid;
+  const uint32_t wg = split ? (((bx >> 3) / kNwb) << 3) | (bx & 7u) : bx;
+  const int wwave = split ? (int)(((bx >> 3) % kNwb) * kWpg) : 0;  // the block's first wave in this workgroup
+  const int ptid = split ? wwave * 64 + tid : tid;
   if constexpr ((OPT & OPT_TIMING) != 0) {
     T.tLast = tStart;
     T.tmark(0);  // prologue
@@ -2090,7 +2098,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
     // renders exactly as in the grid launch (same block, wave, frame, seeds).  The next index
     // is fetched when a packet starts, so its round trip hides behind the packet's work.
     constexpr bool queued = (OPT & OPT_QUEUE) != 0;
-    static_assert(!queued || (!wavewg && (OPT & (OPT_STATS | OPT_TIMING | OPT_HDRLDS)) == 0),
+    static_assert(!queued || (!split && (OPT & (OPT_STATS | OPT_TIMING | OPT_HDRLDS)) == 0),
                   "persistent launches: 256-thread workgroups, no per-wave statistics");
     const uint32_t perFrame = (uint32_t)A.numTiles * 16u;  // blocks per frame
     const uint32_t blocksAll = perFrame * (uint32_t)A.numSamples;
@@ -2099,7 +2107,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
     bool more = !queued || p != 0xFFFFFFFFu;
     while (more) {
       uint32_t pblk = blk, nx = 0u;
-      int pw = wavewg ? wwave : (tid >> 6), frame = (int)blockIdx.y;
+      int pw = wwave + (tid >> 6), frame = (int)blockIdx.y;
       if constexpr (queued) {
         const uint32_t g = p >> 2;  // the packet's block over all frames
         frame = A.numSamples > 1 ? (int)(g / perFrame) : 0;
@@ -2215,7 +2223,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : 256, ((OPT >> 8) & 1
     prev = (uint32_t)__shfl((int)prev, 0, 64);
     if (prev == (blockDim.x >> 6) - 1u) {
       if (A.counters) flush_counters(A, s_cnt, lane);
-      if (A.schedCost && lane == 0 && (!wavewg || wwave == 0)) {  // this workgroup's duration, for the next launches' order
+      if (A.schedCost && lane == 0 && wwave == 0) {  // this workgroup's duration, for the next launches' order
         const uint64_t dt = wall_clock64() - c0;
         A.schedCost[blk] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
       }
@@ -2335,7 +2343,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440)
 #else
 #define IRT_VARIANTS(X) X(6296832) X(5376) X(36864)
 #endif
@@ -2359,12 +2367,12 @@ bool render_variant_available(int v) {
 }
 
 int render_wg_per_block(const RenderArgs &A, int variant) {
-  const bool waveWG = render_variant_available(variant) && (variant & OPT_WAVEWG) != 0;
-  return waveWG && A.sampler == IRT_MODE_USER_GEOM && A.accelMode != IRT_ACCEL_GRID ? 4 : 1;
+  const int per = (variant & OPT_WAVEWG) ? 4 : ((variant & OPT_WAVEWG2) ? 2 : 1);
+  return render_variant_available(variant) && A.sampler == IRT_MODE_USER_GEOM && A.accelMode != IRT_ACCEL_GRID ? per : 1;
 }
 
 // variant bits without a persistent form
-constexpr int kNoQueue = OPT_WAVEWG | OPT_SERIAL | OPT_STATS | OPT_TIMING | OPT_HDRLDS;
+constexpr int kNoQueue = OPT_WAVEWG | OPT_WAVEWG2 | OPT_SERIAL | OPT_STATS | OPT_TIMING | OPT_HDRLDS;
 bool render_queue_ok(const RenderArgs &A, int variant) {
   return render_variant_available(variant) && (variant & kNoQueue) == 0 &&
          A.sampler == IRT_MODE_USER_GEOM && A.accelMode != IRT_ACCEL_GRID;
@@ -2381,7 +2389,7 @@ template <int N>
 RenderKernel kernel_for(const RenderArgs &A, int &threads) {
   constexpr int K = N & ~OPT_MONO;
   constexpr int D = kDefaultVariant & ~OPT_MONO;
-  constexpr int DB = D & ~(0xF00 | OPT_WAVEWG | OPT_LEAN);  // 256-thread workgroups, full LDS
+  constexpr int DB = D & ~(0xF00 | OPT_WAVEWG | OPT_WAVEWG2 | OPT_LEAN);  // 256-thread workgroups, full LDS
   constexpr int DW = DB | OPT_WEDGE | (K & OPT_SERIAL);
   constexpr int DG = DB | 0x400;  // the grid-accel raygen: 4 waves/SIMD as measured in round 2
   const bool g = A.accelMode == IRT_ACCEL_GRID;
@@ -2390,6 +2398,7 @@ RenderKernel kernel_for(const RenderArgs &A, int &threads) {
   if (A.sampler != IRT_MODE_USER_GEOM) return k_render<DW>;
   if (g) return k_render<DG | OPT_GRID | (K & OPT_SERIAL)>;
   if ((K & OPT_WAVEWG) != 0) threads = 64;  // four one-wave workgroups per 256-pixel block
+  if ((K & OPT_WAVEWG2) != 0) threads = 128;  // two two-wave workgroups per block
   if constexpr ((K & kNoQueue) == 0)
     if (A.queue) return k_render<K | OPT_QUEUE>;
   return k_render<K>;
