@@ -7,6 +7,8 @@
 //           [Pipeline flags: --size W H, --camera ..., -fovy f, --xf f, --sample-limit N]
 //           [--synth rootN bisections levels]   (no .ic file: synthetic ICON grid)
 //           [--bench K]                         (render K extra frames, print timing)
+//           [--frames-per-launch B]             (--bench: B consecutive progressive frames
+//                                                per launch, irt_render_accumulate)
 //           [--true-size]                       (dir_du/dir_dv over the real W/H instead
 //                                                of the reference's hard-coded 512)
 //           [--accel sphere|grid]               (the "Accel mode" UI option,
@@ -17,6 +19,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <string>
 #include <vector>
@@ -35,6 +38,7 @@ struct AppState {  // hostCode.cu:65-92 (the parts this backend uses)
   irt_box1f lonRange{-INFINITY, INFINITY};
   int synth[3] = {0, 0, 0};
   int benchFrames = 0;
+  int framesPerLaunch = 1;
   bool trueSize = false;
   int accelMode = IRT_ACCEL_SPHERE;  // g_appState.accelMode (hostCode.cu:75)
   int mode = IRT_MODE_USER_GEOM;     // g_appState.mode: the sampler (Params.h:29-31)
@@ -66,6 +70,8 @@ void parseCommandLine(int argc, char *argv[]) {  // hostCode.cu:106-129
       for (int k = 0; k < 3; ++k) g.synth[k] = atoi(argv[++i]);
     } else if (arg == "--bench" && i + 1 < argc)
       g.benchFrames = atoi(argv[++i]);
+    else if (arg == "--frames-per-launch" && i + 1 < argc)
+      g.framesPerLaunch = atoi(argv[++i]) < 1 ? 1 : atoi(argv[i]);
     else if (arg == "--true-size")
       g.trueSize = true;
     else if (arg == "--accel" && i + 1 < argc)
@@ -183,11 +189,15 @@ int main(int argc, char *argv[]) {
 
   if (g.benchFrames > 0) {
     double total = 0.0, kernel = 0.0;
-    for (int k = 0; k < g.benchFrames; ++k) {
-      lp.accumID = 0;
+    const int B = g.framesPerLaunch;
+    for (int k = 0; k < g.benchFrames; k += B) {
+      const int n = std::min(B, g.benchFrames - k);
+      lp.accumID = B > 1 ? k : 0;  // B > 1: the progressive accumulation, n frames per launch
       auto a = std::chrono::steady_clock::now();
-      if (irt_render(ctx, &lp, fb.width, fb.height, fb.fbPointer, fb.accumBuffer, nullptr))
-        die("irt_render");
+      const int rc = n > 1 ? irt_render_accumulate(ctx, &lp, fb.width, fb.height, n, fb.fbPointer, fb.accumBuffer,
+                                                   nullptr)
+                           : irt_render(ctx, &lp, fb.width, fb.height, fb.fbPointer, fb.accumBuffer, nullptr);
+      if (rc) die("irt_render");
       irt_render_stats st;
       irt_get_render_stats(ctx, &st);
       total += std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
