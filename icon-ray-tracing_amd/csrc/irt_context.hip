@@ -651,13 +651,14 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     const size_t words = (size_t)numTiles * 16 * 4;  // one per (block, wave)
     if (words > c->chainCap || c->chainEpoch > 0xF0000000u - (uint32_t)numFrames) {
       if (words > c->chainCap) {
+        int rc = finish_stats(c);  // every launch that may still read the old words, on any stream
+        if (rc) return rc;
         IRT_HIP(hipStreamSynchronize(s));
         if (c->d_chainFlag) IRT_HIP(hipFree(c->d_chainFlag));
         c->d_chainFlag = nullptr;
         c->bytes -= c->chainCap * sizeof(uint32_t);
         c->chainCap = 0;
-        int rc = dalloc(c, &c->d_chainFlag, words);
-        if (rc) return rc;
+        if ((rc = dalloc(c, &c->d_chainFlag, words))) return rc;
         c->chainCap = words;
         c->info.deviceBytes = c->bytes;
       }
