@@ -1154,7 +1154,7 @@ __device__ __forceinline__ void write_pixel(const RenderArgs &A, size_t outIdx, 
 // scope), then reads accum with sc1 loads (past this CU's L1).  Frame f's wave gets there at
 // the end of its rays, tens of microseconds after frame f - 1's workgroup -- dispatched
 // numBlocks workgroups earlier, on the same XCD -- finished, so the first poll normally hits.
-constexpr uint32_t kChainSpins = 1u << 20;  // ~0.1 s of s_sleep 2, then give up (chainErr)
+constexpr uint32_t kChainSpins = 1u << 20;  // polls (an L2 round trip + s_sleep 2 each: ~1 s), then give up (chainErr)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t out_pixels(const RenderArgs &A) {
   return A.packed ? (uint32_t)A.numTiles * 4096u : (uint32_t)A.W * (uint32_t)A.H;

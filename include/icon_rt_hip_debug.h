@@ -149,7 +149,8 @@ int irt_debug_set_wg_trace(irt_context *ctx, uint32_t *trace);
  * and a second kernel runs the lerp chain.  Frames are identical either way. */
 int irt_debug_set_chain(irt_context *ctx, int on);
 /* Chained-frame waits that timed out since the context was created (a wait gives up after
- * ~0.1 s: the previous frame's workgroup was not dispatched first); waits for the device.
+ * 2^20 polls, about a second: the previous frame's workgroup was not dispatched first); waits
+ * for the device.
  * 0 in every correct run; -1 on error. */
 int irt_debug_chain_errors(irt_context *ctx);
 
