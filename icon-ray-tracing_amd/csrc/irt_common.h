@@ -328,7 +328,10 @@ IRT_HD uint32_t cubemap_cell(float px, float py, float pz, int G) {
   return (uint32_t)face * (uint32_t)G * (uint32_t)G + (uint32_t)j * (uint32_t)G + (uint32_t)i;
 }
 
-constexpr int kSubCells = 4;  // sub-cells per cell edge (irt_build.h kSub)
+#ifndef IRT_SUBCELLS
+#define IRT_SUBCELLS 4  // (measurement builds may set 2: 64-B cell headers, coarser masks)
+#endif
+constexpr int kSubCells = IRT_SUBCELLS;  // sub-cells per cell edge (irt_build.h kSub)
 constexpr int kMaskCand = 8;  // candidates per radial bin with a sub-cell mask (irt_build.h)
 
 // cubemap_cell on the kSubCells-times finer grid: the same cell (the scaling by a power of
@@ -380,8 +383,8 @@ constexpr int kHV = 64;
 // lowest-index answer (deviceCode.cu:119-122).
 constexpr int kMaxEdges = 3;
 // Cell header (irt_build.h): {e0, e1, e2, base} {end0, end1, end2, end3}, then the sub-cell
-// candidate masks: 128 B per cell
-constexpr int kBinHdrWords = 32;
+// candidate masks: 128 B per cell (64 B with 2 x 2 sub-cells)
+constexpr int kBinHdrWords = 8 + kSubCells * kSubCells <= 16 ? 16 : 32;
 IRT_HD int bin_of(float r, float e0, float e1, float e2) {
   return (e0 < r ? 1 : 0) + (e1 < r ? 1 : 0) + (e2 < r ? 1 : 0);
 }

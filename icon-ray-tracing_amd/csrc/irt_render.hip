@@ -562,12 +562,13 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     for (int p = 0; p < kHdrStage / 2; ++p) {
       const int k = 2 * p + (lane >> 5);
       v[p] = 0u;
-      if (k < ns) v[p] = reinterpret_cast<const uint32_t *>(A.binHdr)[(size_t)S.cell[k] * kBinHdrWords + (lane & 31)];
+      if (k < ns && (lane & 31) < kBinHdrWords)
+        v[p] = reinterpret_cast<const uint32_t *>(A.binHdr)[(size_t)S.cell[k] * kBinHdrWords + (lane & 31)];
     }
 #pragma unroll
     for (int p = 0; p < kHdrStage / 2; ++p) {
       const int k = 2 * p + (lane >> 5);
-      if (k < ns) S.w[k][lane & 31] = v[p];
+      if (k < ns && (lane & 31) < kBinHdrWords) S.w[k][lane & 31] = v[p];
     }
     __builtin_amdgcn_wave_barrier();
     if (slot >= 0) {
