@@ -155,6 +155,14 @@ def test_sequence_equals_single_launches(W, H, n, accum):
     for f in ("raysLaunched", "raysInBox", "locateCalls", "samplesFound", "candidatesTested"):
         assert getattr(got, f) == getattr(ref, f), f
     assert ctx.chain_errors() == 0
+    # without chaining the sequence is one launch per view (the host loop): the same frames
+    ctx.set_chain(False)
+    fb2 = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    acc2 = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    ctx.render_sequence(lps, W, H, fb2.data_ptr(), acc2.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(fb2.cpu().numpy(), out[0][0]) and np.array_equal(bits(acc2.cpu().numpy()), out[0][1])
+    ctx.set_chain(True)
     # only the camera and accumID may differ between frames
     bad = _views(setup, W, H, 2)
     bad[1].ambientRadiance = bad[0].ambientRadiance * 2.0
