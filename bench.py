@@ -297,7 +297,7 @@ def main():
     # (per-GPU work fixed as N grows); in frame mode the same --batch frames split over the
     # N GPUs (total work fixed)
     strong = args.mode == "frame"
-    batch = max(1, args.batch) if (orbit is None or not dist_path) else 1
+    batch = max(1, args.batch)
     frames = batch * (world if dist_path and not strong else 1)
     orbit_lps = None
     if orbit is not None:  # each orbit view as a whole launch-parameter record (accumID 0)
@@ -328,10 +328,15 @@ def main():
 
     def step(s):
         lp.accumID = s * frames
-        if orbit is not None and not dist_path and frames > 1:
-            # `frames` consecutive orbit views in one launch (irt_render_sequence)
+        if orbit is not None and frames > 1:
+            # `frames` consecutive orbit views in one launch (irt_render_sequence; on N GPUs
+            # every rank its tiles of them, irt_render_tile_list_sequence)
             seq = [orbit_lps[(s * frames + k) % ORBIT_FRAMES] for k in range(frames)]
-            ctx.render_sequence(seq, W, H, fb.data_ptr(), accum.data_ptr(), stream)
+            if not dist_path:
+                ctx.render_sequence(seq, W, H, fb.data_ptr(), accum.data_ptr(), stream)
+            else:
+                pipe.step(s, lambda buf: split.render_sequence(ctx, seq, buf.data_ptr(), tiles_acc.data_ptr(),
+                                                              stream))
             return
         if orbit is not None:
             c = orbit[s % ORBIT_FRAMES]

@@ -1282,9 +1282,11 @@ int irt_render_accumulate(irt_context *c, const irt_launch_params *lp, int W, in
   return render_impl(c, lp, W, H, 0, 0, 1, fb, accum, nullptr, stream, numFrames);
 }
 
-int irt_render_sequence(irt_context *c, const irt_launch_params *lps, int numFrames, int W, int H,
-                        uint32_t *fb, irt_vec4f *accum, void *stream) {
-  if (!c || !lps || numFrames < 1) {
+namespace {
+// irt_render_sequence and its tile-list form: one chained launch, or one launch per view
+int render_sequence(irt_context *c, const irt_launch_params *lps, int numFrames, int W, int H,
+                    const int32_t *tiles, int numTiles, uint32_t *fb, irt_vec4f *accum, void *stream) {
+  if (!c || !lps || numFrames < 1 || numTiles < 0 || (numTiles > 0 && !tiles)) {
     set_error("irt_render_sequence: bad argument");
     return IRT_E_INVALID;
   }
@@ -1296,14 +1298,34 @@ int irt_render_sequence(irt_context *c, const irt_launch_params *lps, int numFra
       return IRT_E_INVALID;
     }
   const bool chainable = c->chainOn && (c->variant & 65536) == 0 && !c->queueOn && c->probeExit == 0;
+  static const int32_t none = 0;
+  const int32_t *list = tiles ? (numTiles > 0 ? tiles : &none) : nullptr;  // null: the whole frame
+  const int packed = tiles ? 1 : 0;
   if (numFrames == 1 || !chainable) {  // one launch per frame
     for (int k = 0; k < numFrames; ++k) {
-      int rc = render_impl(c, &lps[k], W, H, 0, 0, 1, fb, accum, nullptr, stream);
+      int rc = render_impl(c, &lps[k], W, H, packed, 0, 1, fb, accum, nullptr, stream, 1, list, numTiles);
       if (rc) return rc;
     }
     return IRT_OK;
   }
-  return render_impl(c, &lps[0], W, H, 0, 0, 1, fb, accum, nullptr, stream, numFrames, nullptr, 0, lps);
+  return render_impl(c, &lps[0], W, H, packed, 0, 1, fb, accum, nullptr, stream, numFrames, list, numTiles, lps);
+}
+}  // namespace
+
+int irt_render_sequence(irt_context *c, const irt_launch_params *lps, int numFrames, int W, int H,
+                        uint32_t *fb, irt_vec4f *accum, void *stream) {
+  return render_sequence(c, lps, numFrames, W, H, nullptr, 0, fb, accum, stream);
+}
+
+int irt_render_tile_list_sequence(irt_context *c, const irt_launch_params *lps, int numFrames, int W, int H,
+                                  const int32_t *tiles, int numTiles, uint32_t *fb, irt_vec4f *accum,
+                                  void *stream) {
+  if (numTiles < 0 || (numTiles > 0 && !tiles)) {
+    set_error("irt_render_tile_list_sequence: bad tile list");
+    return IRT_E_INVALID;
+  }
+  static const int32_t none = 0;
+  return render_sequence(c, lps, numFrames, W, H, numTiles > 0 ? tiles : &none, numTiles, fb, accum, stream);
 }
 
 int irt_render_tiles_accumulate(irt_context *c, const irt_launch_params *lp, int W, int H,

@@ -586,6 +586,18 @@ class Context:
                                          C.c_void_p(accum_ptr), C.c_void_p(stream)),
                "irt_render_sequence")
 
+    def render_tile_list_sequence(self, lps, width: int, height: int, tiles, fb_tiles_ptr: int,
+                                  accum_tiles_ptr: int, stream: int = 0):
+        """irt_render_tile_list_sequence: lps[k] over the listed tiles, packed in list order."""
+        arr = (LaunchParams * len(lps))(*lps)
+        t = np.ascontiguousarray(tiles, dtype=np.int32)
+        L = lib()
+        L.irt_render_tile_list_sequence.argtypes = [C.c_void_p, C.POINTER(LaunchParams), C.c_int, C.c_int, C.c_int,
+                                                    C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        _check(L.irt_render_tile_list_sequence(self._h, arr, len(lps), width, height, _ptr(t), t.size,
+                                               C.c_void_p(fb_tiles_ptr), C.c_void_p(accum_tiles_ptr),
+                                               C.c_void_p(stream)), "irt_render_tile_list_sequence")
+
     def render_accumulate(self, lp: LaunchParams, width: int, height: int, num_frames: int,
                           fb_ptr: int, accum_ptr: int, stream: int = 0):
         """Frames lp.accumID .. lp.accumID+num_frames-1 of the progressive accumulation in

@@ -83,6 +83,11 @@ class TileSplit:
             ctx.render_tiles_accumulate(lp, self.width, self.height, self.rank, self.world,
                                         frames, buf_ptr, acc_ptr, stream)
 
+    def render_sequence(self, ctx, lps, buf_ptr: int, acc_ptr: int, stream: int = 0):
+        """This rank's tiles of the views lps[0..] (a camera path, one launch) into the packed
+        buffer buf_ptr (accum tiles acc_ptr)."""
+        ctx.render_tile_list_sequence(lps, self.width, self.height, self.tiles(), buf_ptr, acc_ptr, stream)
+
     def unpack(self, ctx, gathered_ptr: int, fb_ptr: int, stream: int = 0):
         """Rank 0: every rank's packed tiles (gathered rank-major) into the framebuffer."""
         if self.table is not None:

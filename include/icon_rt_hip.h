@@ -194,6 +194,11 @@ int irt_render_accumulate(irt_context *ctx, const irt_launch_params *lp, int wid
  * setting that cannot chain, one launch per frame. */
 int irt_render_sequence(irt_context *ctx, const irt_launch_params *lps, int numFrames, int width,
                         int height, uint32_t *d_fb, irt_vec4f *d_accum, void *stream);
+/* The same over one rank's tile list, packed as irt_render_tile_list packs it (the multi-GPU
+ * split of a camera path: every rank renders its tiles of the same views). */
+int irt_render_tile_list_sequence(irt_context *ctx, const irt_launch_params *lps, int numFrames,
+                                  int width, int height, const int32_t *tiles, int numTiles,
+                                  uint32_t *d_fb_tiles, irt_vec4f *d_accum_tiles, void *stream);
 int irt_render_tiles_accumulate(irt_context *ctx, const irt_launch_params *lp, int width,
                                 int height, int tileBegin, int tileStride, int numFrames,
                                 uint32_t *d_fb_tiles, irt_vec4f *d_accum_tiles, int *numTiles,

@@ -169,3 +169,36 @@ def test_sequence_equals_single_launches(W, H, n, accum):
     with pytest.raises(irt.IrtError):
         ctx.render_sequence(bad, W, H, fb.data_ptr(), acc.data_ptr())
     ctx.close()
+
+
+def test_tile_list_sequence_split_equals_full_sequence():
+    """irt_render_tile_list_sequence on every rank's tiles (the multi-GPU split of an orbit,
+    both deals), unpacked, equals the full-frame sequence."""
+    import torch
+    import irt_dist
+    cells = irt.synth_grid(2, 3, 90)
+    W, H, n = 320, 200, 5
+    setup = irt.setup_frame(cells, W, H, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    lps = _views(setup, W, H, n)
+    fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    ctx.render_sequence(lps, W, H, fb.data_ptr(), acc.data_ptr())
+    torch.cuda.synchronize()
+    ref = fb.cpu().numpy().copy()
+    for ranks in (2, 3):
+        for dealt in (False, True):
+            splits = [irt_dist.TileSplit.dealt(W, H, r, ranks, lps[0], ctx.info, n) if dealt
+                      else irt_dist.TileSplit(W, H, r, ranks) for r in range(ranks)]
+            maxt = max(sp.max_tiles for sp in splits)
+            g = torch.zeros(ranks * maxt * 4096, dtype=torch.int32, device="cuda")
+            for r, sp in enumerate(splits):
+                tacc = torch.zeros(maxt * 4096 * 4, dtype=torch.float32, device="cuda")
+                sp.render_sequence(ctx, lps, g[r * maxt * 4096:].data_ptr(), tacc.data_ptr())
+            out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            splits[0].unpack(ctx, g.data_ptr(), out.data_ptr())
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy(), ref), (ranks, dealt)
+    assert ctx.chain_errors() == 0
+    ctx.close()
