@@ -14,6 +14,9 @@ It prints one JSON line per (deal, mode, N) with the per-rank times, max/mean, a
 projected whole-job rate from the max rank (the exchange itself left out).
 
     python profiles/rank_step.py [--config c3] [--steps 50]
+
+The C5 orbit renders its consecutive views (irt_render_sequence on one GPU,
+irt_render_tile_list_sequence per rank).
 """
 import argparse
 import json
@@ -66,10 +69,24 @@ def main():
         return (time.perf_counter() - t) / args.steps * 1e3
 
     B = max(1, args.batch)
+    views = None
+    if orbit:  # the orbit's views as whole launch-parameter records (bench.py's orbit_lps)
+        views = []
+        for k in range(bench.ORBIT_FRAMES):
+            c = irt.camera_look_at(*bench.orbit_camera(k), W, H)
+            q = irt.LaunchParams.from_buffer_copy(lp)
+            q.org, q.dir_00, q.dir_du, q.dir_dv = c.org, c.dir_00, c.dir_du, c.dir_dv
+            q.accumID = 0
+            views.append(q)
+
+    def seq(s, n):  # the step's n consecutive orbit views
+        return [views[(s * n + k) % bench.ORBIT_FRAMES] for k in range(n)]
 
     def single(s):
         lp.accumID = s * B
-        if B > 1:
+        if views is not None:
+            ctx.render_sequence(seq(s, B), W, H, fb.data_ptr(), acc.data_ptr(), stream)
+        elif B > 1:
             ctx.render_accumulate(lp, W, H, B, fb.data_ptr(), acc.data_ptr(), stream)
         else:
             ctx.render(lp, W, H, fb.data_ptr(), acc.data_ptr(), stream)
@@ -92,7 +109,10 @@ def main():
 
                     def step(s, split=split, tiles=tiles, tacc=tacc, gathered=gathered, r=r):
                         lp.accumID = s * frames
-                        split.render(ctx, lp, frames, tiles.data_ptr(), tacc.data_ptr(), stream)
+                        if views is not None:  # irt_render_tile_list_sequence
+                            split.render_sequence(ctx, seq(s, frames), tiles.data_ptr(), tacc.data_ptr(), stream)
+                        else:
+                            split.render(ctx, lp, frames, tiles.data_ptr(), tacc.data_ptr(), stream)
                         if r == 0 and n > 1:
                             split.unpack(ctx, gathered.data_ptr(), fb.data_ptr(), stream)
 
