@@ -424,6 +424,15 @@ def main():
         samples_all, in_box_all, launched_all = (int(v) for v in agg.tolist())
     else:
         samples_all, in_box_all, launched_all = samples, in_box, tot.raysLaunched
+    # chained-frame waits that gave up (0 in a correct run: every frame then equals one
+    # launch per frame); counted over every launch of this context, all ranks summed
+    chain_timeouts = ctx.chain_errors()
+    if dist_path:
+        ct = torch.tensor([chain_timeouts], dtype=torch.float64, device=rdev)
+        dist.all_reduce(ct)
+        chain_timeouts = int(ct.item())
+    if chain_timeouts:
+        log(f"[rank {rank}] WARNING: {chain_timeouts} chained-frame waits timed out; frames may be wrong")
 
     ms_per_step = elapsed / args.steps * 1e3
     mray = W * H * frames * args.steps / elapsed / 1e6  # all ranks' rays
@@ -484,6 +493,7 @@ def main():
                 "statistics_in_timed_loop": args.stats,
                 "frames_per_launch": frames,
                 "bytes_per_launch_rank0": bytes_per_launch,
+                "chain_timeouts": chain_timeouts,
             },
             "roofline": {
                 "bound": "hbm",
