@@ -10,10 +10,10 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 timeout -s KILL 200 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_DRAM_sum \
-  --output-format csv -d "$OUT/req" -o run -- python3 "$ROOT/bench.py" --config "$CFG" --steps 20 --warmup 2 --no-cpu-baseline \
+  --output-format csv -d "$OUT/req" -o run -- python3 "$ROOT/bench.py" --config "$CFG" --steps 20 --warmup 2 --no-cpu-baseline --no-single-compare \
   > "$OUT/bench.json" 2> "$OUT/bench.err"
 timeout -s KILL 200 rocprofv3 --kernel-trace --pmc TCC_EA0_WRREQ_64B_sum TCC_EA0_WRREQ_sum \
-  --output-format csv -d "$OUT/wr" -o run -- python3 "$ROOT/bench.py" --config "$CFG" --steps 20 --warmup 2 --no-cpu-baseline \
+  --output-format csv -d "$OUT/wr" -o run -- python3 "$ROOT/bench.py" --config "$CFG" --steps 20 --warmup 2 --no-cpu-baseline --no-single-compare \
   > /dev/null 2>> "$OUT/bench.err" || echo "write-request pass failed" >&2
 python3 - "$OUT" <<'PY'
 import csv, glob, json, sys, collections
@@ -24,6 +24,8 @@ for f in glob.glob(out + "/*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         if "k_render" not in r["Kernel_Name"]:
             continue
+        if int(r.get("Grid_Size", 0) or 0) <= int(r.get("Workgroup_Size", 0) or 0):
+            continue  # the context's one-workgroup prewarm dispatch
         per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
     for d, c in per.items():
         for k, v in c.items():
