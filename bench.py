@@ -9,7 +9,8 @@ on the device (irt_create_synth), so host memory stays at one chunk at any size.
 Default workload (BASELINE.json configs[2], C3): synthetic R2B07 ICON grid (1,310,720
 cells) x 90 levels (3,932,160 `.ic` records), 1024x1024, framing camera
 `--camera 0 0 1.4e7 0 0 0 0 1 0 -fovy 60`, the reference's default transfer function.
-Other configs (--config): c2 (R2B05 x 47, 512^2), c3s (C3 with a sparse "comb" transfer
+Other configs (--config): c2 (R2B05 x 47, 512^2), c3t (C3's grid over terrain, as convert_icon
+writes it: per-column HSURF/HHL offsets and the inverted first layer), c3s (C3 with a sparse "comb" transfer
 function: alpha 0.01 except every 50th LUT entry at 1.0, so every macrocell's majorant stays
 1 while ~95 % of tentative collisions are rejected -- ~13x C3's samples, the sample-heavy
 regime where HBM bandwidth matters), c4 (C3's grid at 2048^2), c5 (R2B09 x 90 = 62.9 M
@@ -29,7 +30,7 @@ One step (--mode):
 Frames are enqueued back to back: per-launch statistics come back through a ring, never
 stalling the host between launches.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c3s|c2|c4|c5]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c3s|c3t|c2|c4|c5]
        [--mode progressive|frame]
        torchrun --nproc-per-node N bench.py --gpus N ...
 """
@@ -58,11 +59,19 @@ CONFIGS = {
     "c3s": (2, 7, 90, 1024, 1024, "comb", False,
             "C3s: R2B07 (1,310,720 cells) x 90 levels, 1024x1024, sparse comb TF (alpha 0.01, "
             "every 50th of the 300 LUT entries 1.0: sample-heavy)"),
+    "c3t": (2, 7, 90, 1024, 1024, "default", False,
+            "C3t: R2B07 (1,310,720 cells) x 90 levels over terrain (HSURF up to 4 km, "
+            "terrain-following HHL) as convert_icon writes it (inverted first layer over land, "
+            "last record 25 layers), 1024x1024"),
     "c4": (2, 7, 90, 2048, 2048, "default", False,
            "C4: R2B07 (1,310,720 cells) x 90 levels, 2048x2048"),
     "c5": (2, 9, 90, 1024, 1024, "default", True,
            "C5: R2B09 (20,971,520 cells) x 90 levels, 1024x1024, 60-frame orbit"),
 }
+
+
+# configs over terrain (irt_synth_grid_terrain): the maximum HSURF in metres
+TERRAIN = {"c3t": 4000.0}
 
 
 def make_lut(kind, lut):
@@ -108,7 +117,7 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(rn, bis, L, W, H, camera, tf, budget_s=15.0):
+def cpu_baseline(rn, bis, L, W, H, camera, tf, budget_s=15.0, terrain=0.0):
     """The reference's CPU path on the host cores, two ways (test-infrastructure oracle,
     oracle/; only this leg of bench.py touches it):
       * "port" (the primary number): the oracle's restatement of the reference raygen with
@@ -123,7 +132,7 @@ def cpu_baseline(rn, bis, L, W, H, camera, tf, budget_s=15.0):
     import irt
     import oracle as O
     cores = available_cores()
-    cells = irt.synth_grid(rn, bis, L)
+    cells = irt.synth_grid(rn, bis, L, terrain=terrain)
     S = O.OracleScene(cells)
     lut, vr = S.default_lut()
     S.set_transfunc(make_lut(tf, lut), vr)
@@ -262,7 +271,9 @@ def main():
 
     rn, bis, L, W, H, tf, orbit_cfg, desc = CONFIGS[args.config]
     t0 = time.time()
-    ctx = irt.Context.synth(rn, bis, L, device)  # streamed into HBM, built on the device
+    terrain = TERRAIN.get(args.config, 0.0)
+    # streamed into HBM, built on the device
+    ctx = irt.Context.synth(rn, bis, L, device, terrain=terrain)
     info = ctx.info
     setup = irt.setup_frame(None, W, H, camera=FRAMING, info=info)
     ctx.set_transfunc(make_lut(tf, setup.lut), setup.value_range)
@@ -280,7 +291,7 @@ def main():
     lp.mode = {"user": irt.MODE_USER_GEOM, "tri": irt.MODE_TRIANGLES, "cubql": irt.MODE_CUBQL}[args.sampler]
     lp.accelMode = irt.ACCEL_GRID if args.accel == "grid" else 0
     if args.sampler != "user":  # buildTriangleAccel / buildCuBQLAccel (hostCode.cu:440-649)
-        ctx.build_wedge_accel(irt.synth_grid(rn, bis, L))
+        ctx.build_wedge_accel(irt.synth_grid(rn, bis, L, terrain=terrain))
     orbit = None
     if orbit_cfg:  # one orbit frame per step (a new view: accumID 0)
         orbit = [irt.camera_look_at(*orbit_camera(k), W, H) for k in range(ORBIT_FRAMES)]
@@ -461,6 +472,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            "frames_per_launch": frames,
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
@@ -514,7 +526,7 @@ def main():
                 f"of the same kernel and workload")
         if world == 1 and not args.no_cpu_baseline:
             cam = orbit_camera(0) if orbit is not None else FRAMING
-            out["cpu_baseline"] = cpu_baseline(rn, bis, L, W, H, cam, tf, args.cpu_budget)
+            out["cpu_baseline"] = cpu_baseline(rn, bis, L, W, H, cam, tf, args.cpu_budget, terrain)
         print(json.dumps(out), file=json_out, flush=True)
     if dist_path:
         dist.barrier()

@@ -146,7 +146,12 @@ struct irt_context {
   uint32_t *d_chainFlag = nullptr;
   size_t chainCap = 0;           // words in d_chainFlag
   uint32_t chainEpoch = 1;
-  uint32_t *d_chainErr = nullptr;
+  // per launch slot, in pinned host memory: set by a chained wait of that launch that gave up
+  // (RenderArgs::chainFail); finish_slot reports it (IRT_E_CHAIN) and turns chaining off
+  uint32_t *h_chainFail = nullptr, *dh_chainFail = nullptr;
+  long long chainFailLaunches = 0;  // launches reported so (irt_debug_chain_errors)
+  uint32_t chainSpins = 0;          // irt_debug_set_chain_fault: poll cap (0: the kernel's default)
+  int chainWithhold = -1;           // ... and the frame whose waves do not publish (-1: none)
   // irt_render_sequence: the frames' camera words on the device, and per launch slot their
   // pinned staging (a slot is reused only after its launch is retired)
   float4 *d_frameCams = nullptr;
@@ -217,7 +222,7 @@ void free_all(irt_context *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
                   c->d_sphBits, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_gridBits, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
-                  c->d_lut, c->d_counters, c->d_counterBuckets, c->d_meta, c->d_queue, c->d_chainFlag, c->d_chainErr,
+                  c->d_lut, c->d_counters, c->d_counterBuckets, c->d_meta, c->d_queue, c->d_chainFlag,
                   c->d_frameCams};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -228,6 +233,7 @@ void free_all(irt_context *c) {
   if (c->h_schedCost) (void)hipHostFree(c->h_schedCost);
   if (c->h_schedOrder) (void)hipHostFree(c->h_schedOrder);
   if (c->h_frameCams) (void)hipHostFree(c->h_frameCams);
+  if (c->h_chainFail) (void)hipHostFree(c->h_chainFail);
   for (int i = 0; i < irt_context::kSlots; ++i) {
     if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
@@ -333,6 +339,16 @@ int finish_slot(irt_context *c, int i) {
   c->total.candidatesTested += st.candidatesTested;
   ++c->totalLaunches;
   c->pending[i] = false;
+  if (c->h_chainFail[i]) {
+    // a chained wait of this launch gave up: its frames were lerped out of order.  Report it
+    // (once), and render later multi-frame launches unchained (sample buffer + k_accumulate)
+    c->h_chainFail[i] = 0;
+    ++c->chainFailLaunches;
+    c->chainOn = false;
+    set_error("chained-frame hand-off timed out in launch %lld: its frames are not the sequential "
+              "frames (chaining is now off for this context)", c->slotLaunch[i]);
+    return IRT_E_CHAIN;
+  }
   return IRT_OK;
 }
 
@@ -579,11 +595,30 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.sphRec = c->d_sphRec;
   A.sphBits = c->d_sphBits;
 
+  // a launch in flight whose chained wait gave up (its pinned flag is set as it happens):
+  // report it now, from the next call, instead of when its slot is retired
+  for (int i = 0; i < irt_context::kSlots; ++i)
+    if (c->pending[i] && c->h_chainFail[i]) {
+      int rc = finish_slot(c, i);
+      if (rc) return rc;
+    }
   const int slot = (int)(c->launches % irt_context::kSlots);
   if (c->pending[slot]) {  // the ring is full: retire that launch (long done by now)
     int rc = finish_slot(c, slot);
     if (rc) return rc;
   }
+  // Launches of a context run in call order, also across streams: a launch on another stream
+  // than the previous one waits for it before anything of this call is queued (the chain words,
+  // the frame cameras and the counter block below are shared by every launch of the context;
+  // two chained launches in flight at once on two streams would overwrite each other's words)
+  if (c->launches > 0 && s != c->lastStream) {
+    const int prev = (int)((c->launches - 1) % irt_context::kSlots);
+    if (c->pending[prev]) {
+      const hipEvent_t e = done_event(c, prev);
+      if (e) IRT_HIP(hipStreamWaitEvent(s, e, 0));
+    }
+  }
+  c->lastStream = s;
   const size_t lanes = (size_t)numTiles * 4096;
   // persistent launch: the cooperative kernels, not for the measurement-only early exits
   // (every wave must reach the queue's done count)
@@ -646,7 +681,13 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.numSamples = numFrames;
   // chained frames: the cooperative kernels (not the one-lane-per-ray A/B variant), grid
   // launches, no measurement-only early exit
-  A.chain = c->chainOn && numFrames > 1 && !queued && c->probeExit == 0 && (c->variant & 65536) == 0 ? 1 : 0;
+  // The hand-off's buffer resources address accum with 32-bit byte offsets: frames of 2^27
+  // pixels or more (11,585^2) go through the sample buffer instead
+  const uint64_t outPixels = packed ? (uint64_t)numTiles * 4096u : (uint64_t)W * (uint64_t)H;
+  A.chain = c->chainOn && numFrames > 1 && !queued && c->probeExit == 0 && (c->variant & 65536) == 0 &&
+                    outPixels * 16u <= 0x7FFFFFFFull
+                ? 1
+                : 0;
   if (A.chain) {
     const size_t words = (size_t)numTiles * 16 * 4;  // one per (block, wave)
     if (words > c->chainCap || c->chainEpoch > 0xF0000000u - (uint32_t)numFrames) {
@@ -666,7 +707,10 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
       c->chainEpoch = 1;  // never 0: the zeroed words match no epoch
     }
     A.chainFlag = c->d_chainFlag;
-    A.chainErr = c->d_chainErr;
+    c->h_chainFail[slot] = 0;
+    A.chainFail = c->dh_chainFail + slot;
+    A.chainSpins = c->chainSpins ? c->chainSpins : kChainSpinsDefault;
+    A.chainWithhold = c->chainWithhold;
     A.chainEpoch = c->chainEpoch;
     c->chainEpoch += (uint32_t)numFrames;
   }
@@ -744,15 +788,6 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.counterBuckets = A.counters && !A.wgCounts ? c->d_counterBuckets + (size_t)slot * kCounterBuckets * 8 : nullptr;
   const bool block = A.counters && (!A.wgCounts || statsVariant);
   if (block && !c->lastBlock) IRT_HIP(hipMemsetAsync(A.counters, 0, 16 * sizeof(unsigned long long), s));
-  if (c->launches > 0 && s != c->lastStream) {
-    // this slot may have been zeroed by the previous launch's k_stats_out on another stream
-    const int prev = (int)((c->launches - 1) % irt_context::kSlots);
-    if (c->pending[prev]) {
-      const hipEvent_t e = done_event(c, prev);
-      if (e) IRT_HIP(hipStreamWaitEvent(s, e, 0));
-    }
-  }
-  c->lastStream = s;
   c->timed[slot] = c->launches % c->timingEvery == 0;
   if (c->timed[slot]) IRT_HIP(hipEventRecord(c->ev0[slot], s));
   if (numTiles > 0) {
@@ -1032,11 +1067,12 @@ int irt_create_end(irt_context *c) {
   if (const char *e = getenv("IRT_COOP_MAXLG")) c->coopMaxLg = std::min(6, std::max(0, atoi(e)));
   if (const char *e = getenv("IRT_COOP_RAMP")) c->coopRamp = std::min(6, std::max(0, atoi(e)));
   if (const char *e = getenv("IRT_PROBE_EXIT")) c->probeExit = atoi(e);
-  if (const char *e = getenv("IRT_QUEUE")) c->queueOn = atoi(e) != 0;
+  if (const char *e = getenv("IRT_QUEUE")) c->queueOn = atoi(e) != 0 && render_queue_compiled();
   if (const char *e = getenv("IRT_QUEUE_WGS")) c->queuePerCU = std::max(0, atoi(e));
   if (const char *e = getenv("IRT_CHAIN")) c->chainOn = atoi(e) != 0;
-  if ((rc = dalloc(c, &c->d_chainErr, 1))) return rc;
-  IRT_HIP(hipMemsetAsync(c->d_chainErr, 0, sizeof(uint32_t), c->stream));
+  IRT_HIP(hipHostMalloc((void **)&c->h_chainFail, irt_context::kSlots * sizeof(uint32_t)));
+  memset(c->h_chainFail, 0, irt_context::kSlots * sizeof(uint32_t));
+  IRT_HIP(hipHostGetDevicePointer((void **)&c->dh_chainFail, c->h_chainFail, 0));
   if ((rc = dalloc(c, &c->d_queue, (size_t)kQueueWords * irt_context::kSlots))) return rc;
   IRT_HIP(hipMemsetAsync(c->d_queue, 0, (size_t)kQueueWords * irt_context::kSlots * sizeof(uint32_t), c->stream));
   IRT_HIP(hipDeviceGetAttribute(&c->numCU, hipDeviceAttributeMultiprocessorCount, c->device));
@@ -1134,6 +1170,11 @@ int irt_create_from_file(const char *path, long maxNumCells, int device, irt_con
 
 int irt_create_synth(int rootN, int bisections, int levels, float topHeight, float noise,
                      uint32_t seed, int device, irt_context **out) {
+  return irt_create_synth_terrain(rootN, bisections, levels, topHeight, noise, seed, 0.f, device, out);
+}
+
+int irt_create_synth_terrain(int rootN, int bisections, int levels, float topHeight, float noise,
+                             uint32_t seed, float terrainHeight, int device, irt_context **out) {
   if (!out) {
     set_error("irt_create_synth: null argument");
     return IRT_E_INVALID;
@@ -1141,7 +1182,7 @@ int irt_create_synth(int rootN, int bisections, int levels, float topHeight, flo
   *out = nullptr;
   void *gen = nullptr;
   size_t n = 0;
-  int rc = synth_open(rootN, bisections, levels, topHeight, noise, seed, &gen, &n);
+  int rc = synth_open(rootN, bisections, levels, topHeight, noise, seed, terrainHeight, &gen, &n);
   if (rc) return rc;
   irt_context *c = nullptr;
   if ((rc = irt_create_begin(n, device, &c))) {
@@ -1776,6 +1817,11 @@ extern "C" int irt_debug_set_queue(irt_context *c, int on) {
     set_error("irt_debug_set_queue: null context");
     return IRT_E_INVALID;
   }
+  if (on && !render_queue_compiled()) {
+    set_error("irt_debug_set_queue: persistent launches are compiled into the A/B library only "
+              "(make VARIANTS=all, libicon_rt_hip_all.so)");
+    return IRT_E_INVALID;
+  }
   c->queueOn = on != 0;
   return IRT_OK;
 }
@@ -1787,6 +1833,16 @@ extern "C" int irt_debug_set_wg_trace(irt_context *c, uint32_t *trace) {
   }
   c->wgTrace = trace;
   return IRT_OK;
+}
+
+extern "C" long long irt_debug_launch_workgroups(const irt_context *c, int numTiles, int numFrames) {
+  if (!c || numTiles < 0 || numFrames < 1) {
+    set_error("irt_debug_launch_workgroups: bad argument");
+    return -1;
+  }
+  RenderArgs A;
+  memset(&A, 0, sizeof(A));  // the user-geometry sphere path (sampler 0, accelMode 0)
+  return (long long)numTiles * 16 * render_wg_per_block(A, c->variant) * numFrames;
 }
 
 extern "C" int irt_debug_set_chain(irt_context *c, int on) {
@@ -1803,13 +1859,23 @@ extern "C" int irt_debug_chain_errors(irt_context *c) {
     set_error("irt_debug_chain_errors: null context");
     return -1;
   }
-  uint32_t v = 0;
-  if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(&v, c->d_chainErr, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) {
-    set_error("irt_debug_chain_errors: HIP error");
-    return -1;
+  // retire every launch in flight (each reported hand-off failure is counted, not returned)
+  for (long long j = c->launches - irt_context::kSlots; j < c->launches; ++j) {
+    if (j < 0) continue;
+    const int rc = finish_slot(c, (int)(j % irt_context::kSlots));
+    if (rc && rc != IRT_E_CHAIN) return -1;
   }
-  return (int)v;
+  return (int)c->chainFailLaunches;
+}
+
+extern "C" int irt_debug_set_chain_fault(irt_context *c, uint32_t spins, int withholdFrame) {
+  if (!c) {
+    set_error("irt_debug_set_chain_fault: null context");
+    return IRT_E_INVALID;
+  }
+  c->chainSpins = spins;
+  c->chainWithhold = withholdFrame;
+  return IRT_OK;
 }
 
 extern "C" int irt_debug_get_queue(const irt_context *c) { return c ? (c->queueOn ? 1 : 0) : -1; }

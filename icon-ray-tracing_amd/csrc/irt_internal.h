@@ -110,6 +110,7 @@ int default_threads();
 
 // Synthetic RnBk grid generator (host/irt_synth.cpp): open once, fill any record range.
 int synth_open(int rootN, int bisections, int levels, float topHeight, float noise, uint32_t seed,
+               float terrainHeight,
                void **gen, size_t *total);
 void synth_fill(const void *gen, size_t first, size_t count, irt_icon_cell *out);
 void synth_close(void *gen);

@@ -99,8 +99,12 @@ struct RenderArgs {
   // of the launch renders block b of frame accumID + f and lerps straight into accum/fb, after
   // waiting for (b, f - 1)'s wave to publish the same pixels -- chainFlag[4 b + wave] = chainEpoch
   // + f after its write-through (sc1) stores -- instead of the sample buffer + k_accumulate.
-  // A frame's workgroups wait on the previous frame's, which the linear dispatch order puts
-  // earlier on the same XCD; a wait that times out sets *chainErr (pixels then unordered).
+  // The hand-off is cdna_hip_programming.md Guideline 16's R1 form (sc1 payload stores drained
+  // by the storing wave, an sc1 flag store; sc1 polls and sc1 loads of every handed-off byte),
+  // so it holds whichever XCD the two workgroups run on.  A frame's workgroups wait on the
+  // previous frame's, which the linear dispatch order starts earlier; a wait gives up after
+  // chainSpins polls and sets *chainFail (pinned host memory, one word per launch slot): the
+  // frames are then unordered and the host reports IRT_E_CHAIN.
   int chain;
   // a sequence of views (irt_render_sequence; null otherwise): frame f's camera and accumID
   // as 4 float4 {org, accumID bits} {dir_00} {dir_du} {dir_dv}, uploaded before the launch and
@@ -108,7 +112,9 @@ struct RenderArgs {
   const float4 *frameCams;
   uint32_t chainEpoch;
   uint32_t *chainFlag;
-  uint32_t *chainErr;
+  uint32_t *chainFail;
+  uint32_t chainSpins;   // polls before a wait gives up (kChainSpinsDefault; tests lower it)
+  int chainWithhold;     // test hook (irt_debug_set_chain_fault): this frame's waves never publish
 
   // measurement only (irt_debug_set_wg_trace, profiles/wg_trace.py): non-null: workgroup b
   // writes {start, end} (s_memrealtime, 100 MHz, low 32 bits), HW_ID and XCC_ID to
@@ -118,6 +124,8 @@ struct RenderArgs {
 // a persistent launch's queue words (irt_render.hip queue_take): 8 per-XCD counters and the
 // done count, each on its own 128-B line
 constexpr int kQueueLine = 32;
+// polls of a chained wait (an L2 round trip + s_sleep 2 each: ~1 s in all) before it gives up
+constexpr uint32_t kChainSpinsDefault = 1u << 20;
 constexpr int kQueueWords = 9 * kQueueLine;
 
 // Event counts kept per workgroup: [0] launched [1] inBox [2] locate [3] found [4] candidates
@@ -140,6 +148,7 @@ int render_wg_per_block(const RenderArgs &A, int variant);
 // whether `variant` can run as a persistent launch (RenderArgs::queue) with these arguments:
 // the cooperative user-geometry sphere-accel kernels with 256-thread workgroups
 bool render_queue_ok(const RenderArgs &A, int variant);
+bool render_queue_compiled();  // the A/B library (make VARIANTS=all) only
 // workgroups a persistent launch of `variant` runs on a device with numCU compute units:
 // every slot the kernel's occupancy allows (resident at once), at most `numBlocks`
 int render_queue_wgs(const RenderArgs &A, int variant, int numCU, int numBlocks);

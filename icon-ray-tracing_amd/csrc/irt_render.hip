@@ -1151,11 +1151,14 @@ __device__ __forceinline__ void write_pixel(const RenderArgs &A, size_t outIdx, 
 // b of frame accumID + f and lerps into accum/fb directly; the previous frame's colour of the
 // same pixel must be in accum first.  The hand-off (cdna_hip_programming.md Guideline 16, R1):
 // frame f - 1's wave stores its pixels write-through (sc1), drains them (vmcnt 0) and stores
-// chainEpoch + f to its (block, wave) word; frame f's wave polls that word (relaxed, agent
-// scope), then reads accum with sc1 loads (past this CU's L1).  Frame f's wave gets there at
-// the end of its rays, tens of microseconds after frame f - 1's workgroup -- dispatched
-// numBlocks workgroups earlier, on the same XCD -- finished, so the first poll normally hits.
-constexpr uint32_t kChainSpins = 1u << 20;  // polls (an L2 round trip + s_sleep 2 each: ~1 s), then give up (chainErr)
+// chainEpoch + f to its (block, wave) word (an sc1 store); frame f's wave polls that word
+// (relaxed, agent scope: sc1 loads), then reads accum with sc1 loads (past this CU's L1).
+// Every handed-off byte is stored and loaded sc1, so the hand-off does not depend on the two
+// workgroups sharing an XCD (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the
+// sc1 table).  Frame f's wave gets there at the end of its rays, tens of microseconds after
+// frame f - 1's workgroup -- dispatched numBlocks workgroups earlier -- finished, so the first
+// poll normally hits.  A wait gives up after A.chainSpins polls and flags the launch
+// (*A.chainFail, pinned host memory; the host returns IRT_E_CHAIN).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t out_pixels(const RenderArgs &A) {
   return A.packed ? (uint32_t)A.numTiles * 4096u : (uint32_t)A.W * (uint32_t)A.H;
@@ -1166,9 +1169,9 @@ __device__ __forceinline__ void chain_wait(const RenderArgs &A, uint32_t blk, in
   for (uint32_t spins = 0;; ++spins) {
     const uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if (v == want) break;
-    if (spins >= kChainSpins) {
+    if (spins >= A.chainSpins) {
       if (__lane_id() == (unsigned)(__ffsll((long long)__ballot(1)) - 1))
-        __hip_atomic_fetch_add(A.chainErr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(A.chainFail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
     __builtin_amdgcn_s_sleep(2);
@@ -2149,7 +2152,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
         render_pixel_coop<OPT>(A, T, ppx, th_p, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
                                &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, cam_accum_id(A, frame),
                                pblk, pw, frame);
-        if (A.chain && frame < A.numSamples - 1) {
+        if (A.chain && frame < A.numSamples - 1 && frame != A.chainWithhold) {
           // chained frames: this wave's pixels are written through; tell frame + 1's wave
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if (__lane_id() == 0)
@@ -2374,8 +2377,17 @@ int render_wg_per_block(const RenderArgs &A, int variant) {
 
 // variant bits without a persistent form
 constexpr int kNoQueue = OPT_WAVEWG | OPT_WAVEWG2 | OPT_SERIAL | OPT_STATS | OPT_TIMING | OPT_HDRLDS;
+// Persistent launches (OPT_QUEUE, 3-4x slower: DESIGN.md section 5) are compiled into the A/B
+// library only (make VARIANTS=all); the product library has no persistent kernel.
+bool render_queue_compiled() {
+#ifdef IRT_ALL_VARIANTS
+  return true;
+#else
+  return false;
+#endif
+}
 bool render_queue_ok(const RenderArgs &A, int variant) {
-  return render_variant_available(variant) && (variant & kNoQueue) == 0 &&
+  return render_queue_compiled() && render_variant_available(variant) && (variant & kNoQueue) == 0 &&
          A.sampler == IRT_MODE_USER_GEOM && A.accelMode != IRT_ACCEL_GRID;
 }
 
@@ -2400,8 +2412,10 @@ RenderKernel kernel_for(const RenderArgs &A, int &threads) {
   if (g) return k_render<DG | OPT_GRID | (K & OPT_SERIAL)>;
   if ((K & OPT_WAVEWG) != 0) threads = 64;  // four one-wave workgroups per 256-pixel block
   if ((K & OPT_WAVEWG2) != 0) threads = 128;  // two two-wave workgroups per block
+#ifdef IRT_ALL_VARIANTS
   if constexpr ((K & kNoQueue) == 0)
     if (A.queue) return k_render<K | OPT_QUEUE>;
+#endif
   return k_render<K>;
 }
 

@@ -18,6 +18,18 @@
 //  - records of <= 31 layers (MAX_LAYERS 32, ICONGrid.h:57), bottom to top, consecutive
 //    per column, the layer boundary height shared by neighbouring records
 //    (convert_icon.cpp:362-388).
+// Terrain (terrainHeight > 0, irt_synth_grid_terrain): synthetic DWD-like fields run through
+// convert_icon's `.ic` branch (convert_icon.cpp:353-391) expression by expression --
+//  - HSURF per column: terrainHeight * max(0, m)^1.5 of a smooth field m of the column centre
+//    plus hash noise, clamped to [0, 1] (~60 % of the columns are land, 0 m elsewhere);
+//  - HHL of half level k = 1..levels above the ground: z_k + HSURF (1 - z_k / Zd)^2 (z_k < Zd,
+//    Zd = min(top, 20 km)), z_k = top (k/L)^2: terrain-following near the ground, flat above
+//    (SLEVE-like), monotone in k since 2 HSURF < Zd;
+//  - records as convert_icon writes them: H[0] = R + HSURF for the first record of a column
+//    (prevH, 361), H[j] = R + HHL - HSURF (371, double arithmetic rounded to float), so the
+//    first layer of every land column is inverted (H[0] > H[1]); the last record of a column gets
+//    levels % 32 - 1 layers (365: 90 levels -> 31 + 31 + 25); levels % 32 == 0 is refused (the
+//    reference writes numLayers = -1, which irt_load_ic rejects).
 
 #include <math.h>
 #include <string.h>
@@ -77,18 +89,24 @@ struct SynthGen {
   int rootN = 0, bisections = 0, levels = 0, recsPerCol = 0;
   float noise = 0.f;
   uint32_t seed = 0;
+  double terrain = 0.0, top = 0.0, zd = 0.0;  // terrain: max HSURF (0: flat grid)
   size_t numTris = 0, total = 0;
   std::vector<Tri> roots;
   std::vector<float> H;
   double vmin = INFINITY, vmax = -INFINITY, vscale = 0.0;
 
-  int init(int rn, int bis, int lev, float topHeight, float nz, uint32_t sd) {
+  int init(int rn, int bis, int lev, float topHeight, float nz, uint32_t sd, float terrainHeight = 0.f) {
     using irt::set_error;
-    if (rn < 1 || bis < 0 || bis > 12 || lev < 1 || lev > 100000) {
+    if (rn < 1 || bis < 0 || bis > 12 || lev < 1 || lev > 100000 || !(terrainHeight >= 0.f) ||
+        (terrainHeight > 0.f && (lev % 32 == 0 || !(topHeight > 0.f) ||
+                                 2.0 * terrainHeight >= std::min(20000.0, (double)topHeight)))) {
       set_error("irt_synth_grid: bad argument");
       return IRT_E_INVALID;
     }
     rootN = rn, bisections = bis, levels = lev, noise = nz, seed = sd;
+    terrain = terrainHeight;
+    top = topHeight;
+    zd = std::min(20000.0, (double)topHeight);
     numTris = 20ull * rootN * rootN * (1ull << (2 * bisections));
     recsPerCol = (levels + 30) / 31;
     total = numTris * recsPerCol;
@@ -170,6 +188,53 @@ struct SynthGen {
     }
   }
 
+  // HSURF of column t (terrain grids)
+  double hsurf(size_t t) const {
+    const Tri tr = tri(t);
+    const D3 c = unit(add(add(tr.a, tr.b), tr.c));
+    double m = 0.5 * (sin(11 * c.x + 2) * cos(9 * c.y - 1) + sin(7 * c.z + 3 * c.x) * cos(13 * c.y)) + 0.1;
+    const uint32_t k = hash32((uint32_t)t * 0x9E3779B1u ^ (seed * 131u + 7u));
+    m += 0.15 * ((k >> 8) * (1.0 / 16777216.0) - 0.5);
+    m = std::min(m, 1.0);
+    return m > 0.0 ? terrain * pow(m, 1.5) : 0.0;
+  }
+  // HHL of half level k (1..levels) above the ground of a column with surface height hs
+  double hhl(int k, double hs) const {
+    const double f = (double)k / levels, z = top * f * f;
+    const double d = z < zd ? 1.0 - z / zd : 0.0;
+    return z + hs * d * d;
+  }
+  // the column's records as convert_icon.cpp:356-388 writes them (terrain grids)
+  void terrain_column(size_t t, const double *v, const float *lat, const float *lon, size_t first,
+                      size_t count, irt_icon_cell *out) const {
+    constexpr float R = 6.371229E6f;
+    const double hs = hsurf(t);
+    int valueIt = 0, hhlIt = 0;
+    float prevH = R + hs;  // (361)
+    for (int i = 0; i < recsPerCol; ++i) {
+      int nl = 31;
+      if ((i + 1) * nl > levels) nl = levels % 32 - 1;  // (364-366)
+      float H[32] = {};
+      float val[32] = {};
+      H[0] = prevH;
+      for (int j = 1; j <= nl; ++j) {
+        ++hhlIt;
+        H[j] = R + hhl(hhlIt, hs) - hs;  // (371): float + double - double, rounded to float
+        prevH = H[j];
+      }
+      for (int j = 0; j < nl; ++j) val[j] = (float)((v[valueIt++] - vmin) * vscale);
+      const size_t r = t * recsPerCol + i;
+      if (r < first || r >= first + count) continue;
+      irt_icon_cell &cell = out[r - first];
+      memset(&cell, 0, sizeof(cell));
+      memcpy(cell.lat, lat, 3 * sizeof(float));
+      memcpy(cell.lon, lon, 3 * sizeof(float));
+      cell.numLayers = nl;
+      memcpy(cell.height, H, sizeof(H));
+      memcpy(cell.value, val, sizeof(val));
+    }
+  }
+
   // records [first, first + count), in parallel over columns
   void fill(size_t first, size_t count, irt_icon_cell *out) const {
     if (!count) return;
@@ -190,6 +255,10 @@ struct SynthGen {
             lon[k] = (float)atan2(cs[k].y, cs[k].x);
           }
           values(t, v.data());
+          if (terrain > 0.0) {
+            terrain_column(t, v.data(), lat, lon, first, count, out);
+            continue;
+          }
           for (int rc = 0; rc < recsPerCol; ++rc) {
             const size_t r = t * recsPerCol + rc;
             if (r < first || r >= first + count) continue;
@@ -213,9 +282,9 @@ struct SynthGen {
 
 namespace irt {
 int synth_open(int rootN, int bisections, int levels, float topHeight, float noise, uint32_t seed,
-               void **gen, size_t *total) {
+               float terrainHeight, void **gen, size_t *total) {
   SynthGen *g = new SynthGen();
-  int rc = g->init(rootN, bisections, levels, topHeight, noise, seed);
+  int rc = g->init(rootN, bisections, levels, topHeight, noise, seed, terrainHeight);
   if (rc) {
     delete g;
     return rc;
@@ -230,26 +299,37 @@ void synth_fill(const void *gen, size_t first, size_t count, irt_icon_cell *out)
 void synth_close(void *gen) { delete static_cast<SynthGen *>(gen); }
 }  // namespace irt
 
-extern "C" int irt_synth_grid(int rootN, int bisections, int levels, float topHeight,
-                              float noise, uint32_t seed, irt_icon_cell *out, size_t capacity,
-                              size_t *count) {
+extern "C" int irt_synth_grid_terrain(int rootN, int bisections, int levels, float topHeight,
+                                      float noise, uint32_t seed, float terrainHeight,
+                                      irt_icon_cell *out, size_t capacity, size_t *count) {
   using irt::set_error;
-  if (!count || rootN < 1 || bisections < 0 || bisections > 12 || levels < 1 ||
-      levels > 100000) {
+  if (!count) {
     set_error("irt_synth_grid: bad argument");
     return IRT_E_INVALID;
   }
-  const size_t numTris = 20ull * rootN * rootN * (1ull << (2 * bisections));
-  const size_t total = numTris * ((levels + 30) / 31);
-  *count = total;
-  if (!out) return IRT_OK;
-  if (capacity < total) {
-    set_error("irt_synth_grid: capacity %zu < %zu", capacity, total);
-    return IRT_E_INVALID;
+  if (!out) {  // the count only: no value pass
+    if (rootN < 1 || bisections < 0 || bisections > 12 || levels < 1 || levels > 100000) {
+      set_error("irt_synth_grid: bad argument");
+      return IRT_E_INVALID;
+    }
+    *count = 20ull * rootN * rootN * (1ull << (2 * bisections)) * ((levels + 30) / 31);
+    return IRT_OK;
   }
   SynthGen g;
-  int rc = g.init(rootN, bisections, levels, topHeight, noise, seed);
+  int rc = g.init(rootN, bisections, levels, topHeight, noise, seed, terrainHeight);
   if (rc) return rc;
-  g.fill(0, total, out);
+  *count = g.total;
+  if (capacity < g.total) {
+    set_error("irt_synth_grid: capacity %zu < %zu", capacity, g.total);
+    return IRT_E_INVALID;
+  }
+  g.fill(0, g.total, out);
   return IRT_OK;
+}
+
+extern "C" int irt_synth_grid(int rootN, int bisections, int levels, float topHeight,
+                              float noise, uint32_t seed, irt_icon_cell *out, size_t capacity,
+                              size_t *count) {
+  return irt_synth_grid_terrain(rootN, bisections, levels, topHeight, noise, seed, 0.f, out,
+                                capacity, count);
 }

@@ -54,8 +54,13 @@ def compiled_variants() -> tuple:
     return tuple(out)
 
 
+E_INVALID, E_HIP, E_DATA, E_IO, E_CHAIN = -1, -2, -3, -4, -5  # IRT_E_* (icon_rt_hip.h)
+
+
 class IrtError(RuntimeError):
-    pass
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 class Vec3(C.Structure):
@@ -133,6 +138,7 @@ def lib() -> C.CDLL:
             "irt_create_end": [P],
             "irt_create_from_file": [C.c_char_p, C.c_long, I, C.POINTER(P)],
             "irt_create_synth": [I, I, I, F, F, C.c_uint32, I, C.POINTER(P)],
+            "irt_create_synth_terrain": [I, I, I, F, F, C.c_uint32, F, I, C.POINTER(P)],
             "irt_debug_context_array": [P, I, P, S, C.POINTER(S)],
             "irt_debug_scene_array": [P, I, P, S, C.POINTER(S)],
             "irt_destroy": [P],
@@ -170,6 +176,7 @@ def lib() -> C.CDLL:
             "irt_camera_view_all": [Box3, F, I, I, C.POINTER(LaunchParams)],
             "irt_camera_look_at": [Vec3, Vec3, Vec3, F, I, I, C.POINTER(LaunchParams)],
             "irt_synth_grid": [I, I, I, F, F, C.c_uint32, P, S, C.POINTER(S)],
+            "irt_synth_grid_terrain": [I, I, I, F, F, C.c_uint32, F, P, S, C.POINTER(S)],
             # host-only inspection (include/icon_rt_hip_debug.h)
             "irt_debug_asinf": [F],
             "irt_debug_atan2f": [F, F],
@@ -207,7 +214,7 @@ def lib() -> C.CDLL:
 def _check(rc: int, what: str):
     if rc != 0:
         msg = lib().irt_last_error().decode(errors="replace")
-        raise IrtError(f"{what} failed ({rc}): {msg}")
+        raise IrtError(f"{what} failed ({rc}): {msg}", rc)
 
 
 def _ptr(a: np.ndarray) -> C.c_void_p:
@@ -230,14 +237,15 @@ def default_kernel_id() -> int:
 
 
 def synth_grid(root_n: int, bisections: int, levels: int, top_height: float = 75e3,
-               noise: float = 0.0, seed: int = 1234) -> np.ndarray:
-    """Synthetic RnBk ICON grid as `.ic` records (host/irt_synth.cpp)."""
+               noise: float = 0.0, seed: int = 1234, terrain: float = 0.0) -> np.ndarray:
+    """Synthetic RnBk ICON grid as `.ic` records (host/irt_synth.cpp); terrain > 0: over
+    terrain up to `terrain` metres, as convert_icon writes it (irt_synth_grid_terrain)."""
     n = C.c_size_t()
-    _check(lib().irt_synth_grid(root_n, bisections, levels, top_height, noise, seed, None, 0,
-                                C.byref(n)), "irt_synth_grid")
+    _check(lib().irt_synth_grid_terrain(root_n, bisections, levels, top_height, noise, seed, terrain,
+                                        None, 0, C.byref(n)), "irt_synth_grid")
     cells = np.zeros(n.value, dtype=CELL_DTYPE)
-    _check(lib().irt_synth_grid(root_n, bisections, levels, top_height, noise, seed,
-                                _ptr(cells), n.value, C.byref(n)), "irt_synth_grid")
+    _check(lib().irt_synth_grid_terrain(root_n, bisections, levels, top_height, noise, seed, terrain,
+                                        _ptr(cells), n.value, C.byref(n)), "irt_synth_grid")
     return cells
 
 
@@ -462,11 +470,13 @@ class Context:
 
     @classmethod
     def synth(cls, root_n: int, bisections: int, levels: int, device: int = 0,
-              top_height: float = 75e3, noise: float = 0.0, seed: int = 1234) -> "Context":
-        """The grid of synth_grid(...), generated straight into HBM (irt_create_synth)."""
+              top_height: float = 75e3, noise: float = 0.0, seed: int = 1234,
+              terrain: float = 0.0) -> "Context":
+        """The grid of synth_grid(...), generated straight into HBM (irt_create_synth /
+        irt_create_synth_terrain)."""
         h = C.c_void_p()
-        _check(lib().irt_create_synth(root_n, bisections, levels, top_height, noise, seed, device,
-                                      C.byref(h)), "irt_create_synth")
+        _check(lib().irt_create_synth_terrain(root_n, bisections, levels, top_height, noise, seed,
+                                              terrain, device, C.byref(h)), "irt_create_synth")
         return cls(device=device, _handle=h)
 
     @classmethod
@@ -548,12 +558,31 @@ class Context:
         _check(L.irt_debug_set_chain(self._h, 1 if on else 0), "irt_debug_set_chain")
 
     def chain_errors(self) -> int:
-        """Chained-frame waits that timed out (0 in every correct run); waits for the device."""
+        """Launches whose chained-frame waits timed out (0 in every correct run); retires
+        every launch in flight (waits for the device)."""
         L = lib()
         L.irt_debug_chain_errors.argtypes = [C.c_void_p]
         n = L.irt_debug_chain_errors(self._h)
         if n < 0:
             raise IrtError("irt_debug_chain_errors failed")
+        return n
+
+    def set_chain_fault(self, spins: int, withhold_frame: int = -1):
+        """Test hook: chained waits give up after `spins` polls (0: default) and frame
+        `withhold_frame`'s waves never publish (-1: none) -- the IRT_E_CHAIN path."""
+        L = lib()
+        L.irt_debug_set_chain_fault.argtypes = [C.c_void_p, C.c_uint32, C.c_int]
+        _check(L.irt_debug_set_chain_fault(self._h, spins, withhold_frame), "irt_debug_set_chain_fault")
+
+    def launch_workgroups(self, num_tiles: int, frames: int = 1) -> int:
+        """Workgroups of one launch of num_tiles tiles x frames (the wg-trace buffer needs 4
+        u32 per workgroup)."""
+        L = lib()
+        L.irt_debug_launch_workgroups.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.irt_debug_launch_workgroups.restype = C.c_longlong
+        n = L.irt_debug_launch_workgroups(self._h, num_tiles, frames)
+        if n < 0:
+            raise IrtError("irt_debug_launch_workgroups failed")
         return n
 
     def queue(self) -> bool:

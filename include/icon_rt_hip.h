@@ -22,6 +22,9 @@
  *    so work launched there is ordered with every blocking stream of the process (torch's
  *    default stream included).
  *  - A context is single-caller.  Multi-GPU = one process (one context) per GPU.
+ *  - Launches of one context execute in call order, whatever streams they are given: a call
+ *    on another stream than the previous call's makes its stream wait for the previous launch
+ *    first (the reference has one launch stream per pipeline, pipeline.cu:1064).
  */
 #ifndef ICON_RT_HIP_H
 #define ICON_RT_HIP_H
@@ -38,6 +41,9 @@ extern "C" {
 #define IRT_E_HIP (-2)       /* HIP runtime error (no device, OOM, launch failure) */
 #define IRT_E_DATA (-3)      /* unusable cell data (numLayers out of [0,31], non-finite) */
 #define IRT_E_IO (-4)        /* file I/O */
+#define IRT_E_CHAIN (-5)     /* a chained multi-frame launch's per-pixel hand-off timed out: that
+                                launch's frames were lerped out of order (see
+                                irt_render_accumulate) */
 
 /* == icon_rt::ICONCell (icon_rt/ICONGrid.h:59-76); 284 bytes; the `.ic` record. */
 typedef struct irt_icon_cell {
@@ -144,6 +150,9 @@ int irt_create_from_file(const char *path, long maxNumCells, int device, irt_con
 /* A synthetic RnBk grid (irt_synth_grid) generated chunk by chunk straight into a context. */
 int irt_create_synth(int rootN, int bisections, int levels, float topHeight, float noise,
                      uint32_t seed, int device, irt_context **out);
+/* ... with terrain (irt_synth_grid_terrain). */
+int irt_create_synth_terrain(int rootN, int bisections, int levels, float topHeight, float noise,
+                             uint32_t seed, float terrainHeight, int device, irt_context **out);
 void irt_destroy(irt_context *ctx);
 int irt_get_volume_info(const irt_context *ctx, irt_volume_info *info);
 
@@ -183,7 +192,14 @@ int irt_render_tiles(irt_context *ctx, const irt_launch_params *lp, int width, i
  * The frames are chained per pixel inside the one launch (frame f's workgroup of a block
  * lerps once frame f - 1's has published the same pixels), so the next frame's workgroups
  * fill the chip while the previous frame's last ones finish; every frame's accum and fb
- * are written, as numFrames separate launches would. */
+ * are written, as numFrames separate launches would.
+ * A hand-off wait is bounded (~1 s).  If one ever gives up, the launch's frames were lerped
+ * out of order, and the launch fails loudly instead of returning wrong pixels silently: the
+ * next call on the context that sees it -- any irt_render* call, irt_get_render_stats*,
+ * irt_reset_render_stats_total -- returns IRT_E_CHAIN, irt_last_error() names the launch, and
+ * the context renders later multi-frame launches without chaining (per-frame sample buffer +
+ * a lerp pass).  (The reference's launch either renders the frame or aborts,
+ * pipeline.cu:1038-1075.)  Frames of 2^27 pixels or more are never chained. */
 int irt_render_accumulate(irt_context *ctx, const irt_launch_params *lp, int width, int height,
                           int numFrames, uint32_t *d_fb, irt_vec4f *d_accum, void *stream);
 /* A sequence of views in one launch: frame k renders lps[k] -- its own camera (org, dir_00,
@@ -241,7 +257,9 @@ int irt_unpack_tile_table(irt_context *ctx, const uint32_t *d_gathered, int numR
 
 /* Statistics of the most recent launch (waits for it).  Launches never wait for earlier
  * ones' statistics: counters are read back through a ring, so frames queue back to back
- * like the reference's GPU path (owlLaunch2D is asynchronous, pipeline.cu:1064). */
+ * like the reference's GPU path (owlLaunch2D is asynchronous, pipeline.cu:1064).
+ * Returns IRT_E_CHAIN once for a chained launch whose hand-off timed out (see
+ * irt_render_accumulate). */
 int irt_get_render_stats(const irt_context *ctx, irt_render_stats *stats);
 /* Sums over every launch since the last reset; *launches = count.  kernelMs is the mean
  * of the timed launches times the launch count (see irt_set_timing_interval). */
@@ -364,6 +382,16 @@ int irt_camera_look_at(irt_vec3f vp, irt_vec3f vi, irt_vec3f vu, float fovyDeg, 
  * of <= 31 layers, bottom to top, consecutive per column.  out == NULL -> count only. */
 int irt_synth_grid(int rootN, int bisections, int levels, float topHeight, float noise,
                    uint32_t seed, irt_icon_cell *out, size_t capacity, size_t *count);
+/* The same grid over terrain, as tools/convert_icon's `.ic` branch (convert_icon.cpp:353-391)
+ * would write it from DWD-like fields: HSURF per column up to terrainHeight metres (~60 % of the
+ * columns land), HHL terrain-following near the ground and flat above (the per-column offset
+ * HSURF (1 - z/Zd)^2 shrinking with height z, Zd = min(topHeight, 20 km)), records with
+ * H[0] = R + HSURF and H[j] = R + HHL - HSURF (so every land column's first layer is inverted)
+ * and the last record of a column holding levels % 32 - 1 layers.  terrainHeight 0 ==
+ * irt_synth_grid; needs levels % 32 != 0 and 2 terrainHeight < Zd. */
+int irt_synth_grid_terrain(int rootN, int bisections, int levels, float topHeight, float noise,
+                           uint32_t seed, float terrainHeight, irt_icon_cell *out,
+                           size_t capacity, size_t *count);
 
 #ifdef __cplusplus
 }

@@ -98,7 +98,9 @@ int irt_debug_get_variant(const irt_context *ctx);
 int irt_debug_variants(int *out, int capacity);
 /* Persistent launches on or off for this context (IRT_QUEUE sets the default): every
  * resident wave pulls 8x8-pixel packets from a per-launch counter (RenderArgs::queue) instead
- * of one workgroup per 16x16 block.  Frames are identical either way.  get: 1/0, -1 for NULL. */
+ * of one workgroup per 16x16 block.  Frames are identical either way.  Only the A/B library
+ * (make VARIANTS=all) compiles the persistent kernels: the product library refuses on = 1
+ * (IRT_E_INVALID).  get: 1/0, -1 for NULL. */
 int irt_debug_set_queue(irt_context *ctx, int on);
 int irt_debug_get_queue(const irt_context *ctx);
 /* Workgroups of this context's last persistent launch (0 if none yet; -1 for NULL):
@@ -140,19 +142,27 @@ int irt_debug_sched(irt_context *ctx, int *policy, int *lastApplied, long long *
 /* Measurement only: the next renders' workgroups each write 4 words to the device buffer
  * `trace` (NULL: off): {start, end} of the workgroup (s_memrealtime, 100 MHz, low 32 bits),
  * the wave's HW_ID and XCC_ID registers; workgroup b of a launch at trace[4b].  The buffer
- * must hold 4 words per workgroup (16 per 64x64 tile and frame); frames are unchanged. */
+ * must hold 4 words per workgroup of the launch: irt_debug_launch_workgroups gives the count
+ * (the default variant's one-wave workgroups: 64 per 64x64 tile and frame); frames are
+ * unchanged. */
 int irt_debug_set_wg_trace(irt_context *ctx, uint32_t *trace);
+/* Workgroups one launch of numTiles 64x64 tiles x numFrames frames runs with this context's
+ * variant and settings (the size irt_debug_set_wg_trace's buffer needs, in units of 4 words). */
+long long irt_debug_launch_workgroups(const irt_context *ctx, int numTiles, int numFrames);
 /* Chained progressive frames on (default; IRT_CHAIN=0 turns it off per context) or off: a
  * launch of several frames (irt_render_accumulate, irt_render_tiles_accumulate,
  * irt_render_tile_list) lerps each frame straight into accum/fb, frame f's workgroup waiting for
  * frame f - 1's to publish the same pixels; off: every frame's colour goes to a sample buffer
  * and a second kernel runs the lerp chain.  Frames are identical either way. */
 int irt_debug_set_chain(irt_context *ctx, int on);
-/* Chained-frame waits that timed out since the context was created (a wait gives up after
- * 2^20 polls, about a second: the previous frame's workgroup was not dispatched first); waits
- * for the device.
- * 0 in every correct run; -1 on error. */
+/* Launches whose chained-frame waits timed out since the context was created (a wait gives up
+ * after 2^20 polls, about a second); retires every launch in flight first (waits for them),
+ * counting -- not returning -- their IRT_E_CHAIN.  0 in every correct run; -1 on error. */
 int irt_debug_chain_errors(irt_context *ctx);
+/* Test hook for the failure path: chained waits give up after `spins` polls (0: the default),
+ * and the waves of frame `withholdFrame` of every chained launch (-1: none) never publish, so
+ * frame withholdFrame + 1's waves time out. */
+int irt_debug_set_chain_fault(irt_context *ctx, uint32_t spins, int withholdFrame);
 
 #ifdef __cplusplus
 }

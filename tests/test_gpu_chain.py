@@ -202,3 +202,122 @@ def test_tile_list_sequence_split_equals_full_sequence():
             assert np.array_equal(out.cpu().numpy(), ref), (ranks, dealt)
     assert ctx.chain_errors() == 0
     ctx.close()
+
+
+def _sequential(ctx, lp, W, H, k):
+    """k single-frame launches (accumID 0 .. k-1): the frames a chained batch must equal."""
+    import torch
+    fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    for aid in range(k):
+        lp.accumID = aid
+        ctx.render(lp, W, H, fb.data_ptr(), acc.data_ptr())
+    torch.cuda.synchronize()
+    return fb.cpu().numpy().copy(), bits(acc.cpu().numpy())
+
+
+def test_chained_launches_on_two_streams_equal_sequential_frames():
+    """Two chained launches of one context in flight on two streams at once (two images, two
+    cameras): a spin kernel holds the first stream, so without ordering the second launch
+    would run while the first still polls the same (block, wave) publish words.  Launches of a
+    context run in call order across streams (the second stream waits for the first launch),
+    so both images equal their sequential frames and no wait times out."""
+    import torch
+    cells = irt.synth_grid(2, 3, 90)
+    W, H, k = 256, 192, 4
+    sa = irt.setup_frame(cells, W, H, camera=FRAMING)
+    sb = irt.setup_frame(cells, W, H, camera=None)  # viewAll: another image
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(sa.lut, sa.value_range)
+    ref_a = _sequential(ctx, sa.lp, W, H, k)
+    ref_b = _sequential(ctx, sb.lp, W, H, k)
+    assert not np.array_equal(ref_a[0], ref_b[0])
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for rep in range(3):
+        bufs = [(torch.zeros(W * H, dtype=torch.int32, device="cuda"),
+                 torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")) for _ in range(2)]
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s1):
+            torch.cuda._sleep(20_000_000)  # ~10 ms: launch A queues behind it
+        sa.lp.accumID = 0
+        ctx.render_accumulate(sa.lp, W, H, k, bufs[0][0].data_ptr(), bufs[0][1].data_ptr(), s1.cuda_stream)
+        sb.lp.accumID = 0
+        ctx.render_accumulate(sb.lp, W, H, k, bufs[1][0].data_ptr(), bufs[1][1].data_ptr(), s2.cuda_stream)
+        torch.cuda.synchronize()
+        for (fb, acc), (rf, ra) in zip(bufs, (ref_a, ref_b)):
+            assert np.array_equal(fb.cpu().numpy(), rf), rep
+            assert np.array_equal(bits(acc.cpu().numpy()), ra), rep
+    assert ctx.chain_errors() == 0
+    ctx.close()
+
+
+def test_chain_timeout_fails_loudly():
+    """The failure path of the hand-off: frame 0's waves withhold their publish and a wait gives
+    up after one poll, so frame 1 is lerped against an unpublished accum.  The library must not
+    return those pixels silently: the next call that sees the launch -- here a render, then
+    (for a second faulty launch) irt_get_render_stats -- returns IRT_E_CHAIN, and the context
+    then renders multi-frame launches unchained, equal to the sequential frames again."""
+    import torch
+    cells = irt.synth_grid(2, 2, 47)
+    W, H, k = 96, 80, 3
+    setup = irt.setup_frame(cells, W, H, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    ref = _sequential(ctx, setup.lp, W, H, k)
+    fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    ctx.set_chain_fault(1, 0)
+    setup.lp.accumID = 0
+    ctx.render_accumulate(setup.lp, W, H, k, fb.data_ptr(), acc.data_ptr())  # queued: IRT_OK
+    torch.cuda.synchronize()
+    with pytest.raises(irt.IrtError) as e:  # the next call reports it
+        ctx.render_accumulate(setup.lp, W, H, k, fb.data_ptr(), acc.data_ptr())
+    assert e.value.code == irt.E_CHAIN and "timed out" in str(e.value)
+    # chaining is off now: the same batch renders through the sample buffer, correctly
+    fb.zero_()
+    acc.zero_()
+    ctx.render_accumulate(setup.lp, W, H, k, fb.data_ptr(), acc.data_ptr())
+    torch.cuda.synchronize()
+    ctx.stats()  # no error
+    assert np.array_equal(fb.cpu().numpy(), ref[0]) and np.array_equal(bits(acc.cpu().numpy()), ref[1])
+    # a second faulty launch, reported by irt_get_render_stats
+    ctx.set_chain(True)
+    ctx.render_accumulate(setup.lp, W, H, k, fb.data_ptr(), acc.data_ptr())
+    with pytest.raises(irt.IrtError) as e:
+        ctx.stats()
+    assert e.value.code == irt.E_CHAIN
+    assert ctx.chain_errors() == 2
+    ctx.set_chain_fault(0, -1)
+    ctx.set_chain(True)
+    _batch(ctx, setup.lp, W, H, k, 0, chain=True)
+    assert ctx.chain_errors() == 2  # no new failure
+    ctx.close()
+
+
+def test_chained_frames_stay_on_one_xcd():
+    """Where chained workgroups run (measurement, not a correctness condition: the hand-off
+    stores and loads every byte sc1): frame f's workgroup of a block and frame f - 1's, one frame
+    of workgroups apart, land on the same XCD under the dispatcher's round-robin deal -- the L2
+    locality the kernel's block-to-workgroup mapping was chosen for.  Reported, and asserted
+    only for the hand-off's frames, which must also equal the sequential frames."""
+    import torch
+    cells = irt.synth_grid(2, 3, 90)
+    W, H, k = 512, 512, 3
+    setup = irt.setup_frame(cells, W, H, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    nt = irt.num_tiles(W, H)
+    nwg = ctx.launch_workgroups(nt, k)
+    per = nwg // k
+    trace = torch.zeros(4 * nwg, dtype=torch.int32, device="cuda")
+    ctx.set_wg_trace(trace.data_ptr())
+    got = _batch(ctx, setup.lp, W, H, k, 0, chain=True)
+    ctx.set_wg_trace(0)
+    t = trace.cpu().numpy().view(np.uint32).reshape(k, per, 4)
+    xcc = t[:, :, 3] & 0xF
+    same = float(np.mean(xcc[1:] == xcc[:-1]))
+    print(f"chained predecessor on the same XCD: {same:.4f} of {per * (k - 1)} workgroups")
+    ref = _sequential(ctx, setup.lp, W, H, k)
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+    assert ctx.chain_errors() == 0
+    ctx.close()

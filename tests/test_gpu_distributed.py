@@ -32,7 +32,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, mode, out_path, deal):
+def _worker(rank, world, port, mode, out_path, deal, backend="gloo"):
     sys.path[:0] = [os.path.join(HERE, "..", "icon-ray-tracing_amd", "python"), HERE]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
@@ -42,15 +42,18 @@ def _worker(rank, world, port, mode, out_path, deal):
     import irt_dist
     from helpers import FRAMING
 
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
+    if backend == "nccl":  # RCCL: its communicator, stream and Work.wait() semantics
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda:0"))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     ctx = irt.Context.synth(*GRID, 0)
     setup = irt.setup_frame(None, W, H, camera=FRAMING, info=ctx.info)
     ctx.set_transfunc(setup.lut, setup.value_range)
     lp = setup.lp
     split = (irt_dist.TileSplit.dealt(W, H, rank, world, lp, ctx.info) if deal == "dealt"
              else irt_dist.TileSplit(W, H, rank, world))
-    fg = irt_dist.FrameGather(split, "cuda:0", buffers=8, stage_cpu=True)
+    fg = irt_dist.FrameGather(split, "cuda:0", buffers=8, stage_cpu=backend == "gloo")
     acc = torch.zeros(split.max_tiles * 4096 * 4, dtype=torch.float32, device="cuda:0")
     fb = torch.zeros(W * H, dtype=torch.int32, device="cuda:0")
     frames = 1 if mode == "frame" else world
@@ -67,19 +70,11 @@ def _worker(rank, world, port, mode, out_path, deal):
     ctx.close()
 
 
-@pytest.mark.parametrize("deal", ["dealt", "mod"])
-@pytest.mark.parametrize("mode", ["frame", "progressive"])
-def test_two_rank_hip_frame_split(tmp_path, mode, deal):
+def _reference_frame(mode, world):
     import torch
-    import torch.multiprocessing as mp
 
     import irt
     from helpers import FRAMING
-
-    world = 2
-    out = str(tmp_path / "frame.npy")
-    mp.start_processes(_worker, args=(world, _free_port(), mode, out, deal), nprocs=world, join=True,
-                       start_method="spawn")
     ctx = irt.Context.synth(*GRID, 0)
     setup = irt.setup_frame(None, W, H, camera=FRAMING, info=ctx.info)
     ctx.set_transfunc(setup.lut, setup.value_range)
@@ -95,7 +90,39 @@ def test_two_rank_hip_frame_split(tmp_path, mode, deal):
             ctx.render_accumulate(lp, W, H, frames, fb.data_ptr(), acc.data_ptr())
     torch.cuda.synchronize()
     ref = fb.cpu().numpy()
+    ctx.close()
+    return ref
+
+
+@pytest.mark.parametrize("deal", ["dealt", "mod"])
+@pytest.mark.parametrize("mode", ["frame", "progressive"])
+def test_two_rank_hip_frame_split(tmp_path, mode, deal):
+    import torch.multiprocessing as mp
+
+    world = 2
+    out = str(tmp_path / "frame.npy")
+    mp.start_processes(_worker, args=(world, _free_port(), mode, out, deal), nprocs=world, join=True,
+                       start_method="spawn")
+    ref = _reference_frame(mode, world)
     got = np.load(out)
     assert (ref != 0).mean() > 0.3
     assert np.array_equal(got, ref), int((got != ref).sum())
-    ctx.close()
+
+
+@pytest.mark.parametrize("deal", ["dealt", "mod"])
+@pytest.mark.parametrize("mode", ["frame", "progressive"])
+def test_rccl_process_group_frame_pipeline(tmp_path, mode, deal):
+    """The measured multi-GPU path on RCCL itself: a process group on backend "nccl" (one rank:
+    the GPU box has one GPU, and RCCL refuses two ranks on one device) runs FramePipeline --
+    tile render on a high-priority stream, dist.gather of the packed RGBA8 tiles on RCCL's own
+    stream (no host staging), Work.wait() before buffer reuse, rank 0's unpack on a side
+    stream -- for STEPS steps; the assembled frame must equal irt_render's bit for bit."""
+    import torch.multiprocessing as mp
+
+    out = str(tmp_path / "frame.npy")
+    mp.start_processes(_worker, args=(1, _free_port(), mode, out, deal, "nccl"), nprocs=1, join=True,
+                       start_method="spawn")
+    ref = _reference_frame(mode, 1)
+    got = np.load(out)
+    assert (ref != 0).mean() > 0.3
+    assert np.array_equal(got, ref), int((got != ref).sum())

@@ -367,10 +367,11 @@ def test_ab_library_variants_identical():
     process: one HIP library per process (IRT_LIB_PATH selects it at load)."""
     env = dict(os.environ, IRT_LIB_PATH=irt.ALL_LIB_PATH)
     r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
-                        f"{__file__}::test_all_render_variants_identical"],
+                        f"{__file__}::test_all_render_variants_identical",
+                        f"{__file__}::test_persistent_launch_identical"],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert "1 passed" in r.stdout
+    assert "2 passed" in r.stdout
 
 
 def test_all_render_variants_identical():
@@ -813,12 +814,19 @@ def test_persistent_launch_identical():
     common/thread_pool.h:146-161) render every frame, count and progressive batch exactly as
     the grid launch: single frames at ragged sizes (partial packets), progressive batches,
     tile lists and strided tile splits, many launches in a row (the counter pair is reset by
-    each launch's last wave), and two streams."""
+    each launch's last wave), and two streams.  The persistent kernels live in the A/B library
+    only (test_ab_library_variants_identical runs this there); the product library refuses
+    them."""
     import torch
     cells = irt.synth_grid(2, 3, 90)
     S = irt.setup_frame(cells, 8, 8, camera=FRAMING)
     ctx = irt.Context(cells, 0)
     ctx.set_transfunc(S.lut, S.value_range)
+    if irt.LIB_PATH != irt.ALL_LIB_PATH:
+        with pytest.raises(irt.IrtError):
+            ctx.set_queue(True)
+        ctx.close()
+        return
     # the persistent launch runs the 256-thread-workgroup kernel (5376), not the default's
     # one-wave workgroups
     L = irt.lib()

@@ -75,6 +75,47 @@ def test_synthetic_grid_shape():
         assert cells["value"].max() <= 1.0 and cells["value"].min() >= 0.0
 
 
+@pytest.mark.parametrize("L", [90, 65, 40])
+def test_terrain_grid_follows_convert_icon(L):
+    """irt_synth_grid_terrain writes the records convert_icon.cpp:353-391 would: per column the
+    first record starts at H[0] = R + HSURF (361), every later height is R + HHL - HSURF (371)
+    with HHL - HSURF increasing with height (so H[0] > H[1] on land: the inverted first layer),
+    records chain (H[0] of record i = the last height of record i - 1), and the last record holds
+    L % 32 - 1 layers (365).  Ocean columns (HSURF = 0) have the flat grid's heights."""
+    R = np.float32(6.371229e6)
+    t = irt.synth_grid(2, 1, L, terrain=4000.0)
+    f = irt.synth_grid(2, 1, L)
+    per_col = (L + 30) // 31
+    assert t.size == f.size == 20 * 4 * 4 * per_col
+    nl = t["numLayers"].reshape(-1, per_col)
+    want = [31] * (per_col - 1) + [L % 32 - 1]
+    assert (nl == np.array(want)).all()
+    h = t["height"].reshape(-1, per_col, 32)
+    hs = h[:, 0, 0].astype(np.float64) - float(R)
+    land = hs > 0
+    assert 0.3 < land.mean() < 0.8 and hs.max() <= 4000.0 and hs.min() >= 0.0
+    dz1 = float(f["height"][0][1]) - float(R)  # the first half level above the ground
+    steep = hs > dz1 + 1.0
+    assert steep.mean() > 0.3
+    assert (h[steep, 0, 0] > h[steep, 0, 1]).all()  # the inverted first layer
+    for r in range(per_col):
+        k = nl[0, r]
+        if r:
+            assert (h[:, r, 0] == h[:, r - 1, nl[0, r - 1]]).all()
+        lo = 1 if r == 0 else 0
+        if k > lo:
+            assert (np.diff(h[:, r, lo:k + 1], axis=1) > 0).all()
+    # ocean columns (H[0] = R): the flat grid's heights (R + z in double, rounded), layer for
+    # layer, to within one float step at 6.4e6 m (a coast's HSURF can be far below a metre)
+    hf = f["height"].reshape(-1, per_col, 32)
+    ocean = ~land
+    assert ocean.sum() > 10
+    assert (np.abs(h[ocean, 0, :32].astype(np.float64) - hf[ocean, 0, :32]) <= 0.5).all()
+    assert t["value"].max() <= 1.0 and t["value"].min() >= 0.0
+    # deterministic, and the count-only call agrees
+    assert t.tobytes() == irt.synth_grid(2, 1, L, terrain=4000.0).tobytes()
+
+
 def test_libm_restatements_match_glibc():
     libm = C.CDLL("libm.so.6")
     libm.asinf.restype = libm.atan2f.restype = libm.logf.restype = C.c_float
@@ -231,13 +272,16 @@ def _on_radius(v, r):
     return p
 
 
-def test_binned_locator_on_terrain_following_columns():
+@pytest.mark.parametrize("kind", ["perturbed", "convert_icon"])
+def test_binned_locator_on_terrain_following_columns(kind):
     """The binned lists (per-cell radial edges, fat entries) against the brute-force first
     hit on columns whose record boundaries differ from column to column (terrain-following
     levels, like ICON's HHL), records with unsorted heights, zero-thickness records and
     inverted records -- at random radii, exactly on every record boundary and its float
-    neighbours."""
-    cells = terrain_cells(11)
+    neighbours.  "convert_icon": the terrain grid as convert_icon writes it (inverted first
+    layers over land; 65 levels, so the last record of every column is a zero-thickness
+    sphere at the top)."""
+    cells = terrain_cells(11) if kind == "perturbed" else irt.synth_grid(2, 1, 65, terrain=4000.0)
     rng = np.random.default_rng(12)
     D = irt.DebugScene(cells)
     Lb = O.olib()
