@@ -518,7 +518,7 @@ def main():
         }
         if single is not None:
             out["single_frame_launches"] = single  # the same frames, one launch each
-        prof = profiled_traffic(f"k_render<{irt.default_kernel_id()}>", args.config, frames)
+        prof = profiled_traffic(f"k_render<{irt.default_kernel_id(ctx)}>", args.config, frames)
         if prof and world == 1:
             out["roofline"]["traffic"] = prof[0]
             out["roofline"]["traffic_source"] = (

@@ -147,17 +147,29 @@ IRT_HD float eval_plane(const float *p, float px, float py, float pz) {
 
 // meta word (irt_common.h): numLayers, the coarse flag, the quantised coarse keys
 IRT_HD uint32_t record_meta(const float *height, int nl) {
-  // non-decreasing in float_key order (which implies float order; a -0/+0 pair in the wrong
-  // order takes the literal path)
-  bool coarse = true;
-  for (int j = 1; j <= nl; ++j)
+  // height[1..numLayers] non-decreasing in float_key order (which implies float order; a -0/+0
+  // pair in the wrong order takes the literal path).  findHeight never reads height[0]
+  // (ICONGrid.h:125-135 compares hpos with *(it+1) only), so height[0] may sit above
+  // height[1]: convert_icon's first record of a land column, H[0] = R + HSURF over
+  // H[1] = R + HHL - HSURF (convert_icon.cpp:361, 371).  Keys below height[0] are a prefix of
+  // the sorted keys; the radial test (r >= height[0]) makes every one of them count, so only
+  // their number is kept (bits 30-31).
+  bool coarse = nl >= 1 && float_key(height[0]) <= float_key(height[nl]);
+  for (int j = 2; j <= nl; ++j)
     if (!(float_key(height[j - 1]) <= float_key(height[j]))) coarse = false;
   uint32_t m = (uint32_t)nl;
   if (coarse) {
     m |= kMetaCoarse;
     const uint32_t k0 = float_key(height[0]), S = meta_quantum(k0, float_key(height[nl]));
-    for (int j = 0; j < 3 && 8 * j + 7 <= nl; ++j)
-      m |= ((float_key(height[8 * j + 7]) - k0) / S) << (6 + 8 * j);
+    uint32_t below = 0;
+    for (int j = 0; j < 3 && 8 * j + 7 <= nl; ++j) {
+      const uint32_t kj = float_key(height[8 * j + 7]);
+      if (kj < k0)
+        ++below;
+      else
+        m |= ((kj - k0) / S) << (6 + 8 * j);
+    }
+    m |= below << kMetaBelowShift;
   }
   return m;
 }

@@ -424,13 +424,18 @@ IRT_HD uint32_t float_key(float v) {
 
 // The meta word of a record (its fat entry's last word; irt_build.h record_meta):
 //   bits 0-4   numLayers
-//   bit 5      coarse: height[1..numLayers] non-decreasing and height[0] <= height[1], so
-//              findHeight's 8-height block follows from the keys height[7], height[15],
-//              height[23] (irt_common.h rec_coarse_block; height[31] never counts)
+//   bit 5      coarse: height[1..numLayers] non-decreasing and height[0] <= height[numLayers],
+//              so findHeight's 8-height block follows from the keys height[7], height[15],
+//              height[23] (irt_common.h rec_coarse_block; height[31] never counts).
+//              height[0] may exceed height[1] (convert_icon's inverted first layer over land):
+//              findHeight never reads it
 //   bits 6-29  q_j, j = 0,1,2: float_key(height[8j+7]) - float_key(height[0]), in units of
 //              meta_quantum, floored (8 bits each): key j lies in [q_j S, q_j S + S - 1]
 //              above height[0]'s key
+//   bits 30-31 the number of keys below height[0] (a prefix of the sorted keys; their q_j are
+//              0): with r >= height[0] they always count
 constexpr uint32_t kMetaCoarse = 32u;
+constexpr int kMetaBelowShift = 30;
 IRT_HD uint32_t meta_quantum(uint32_t k0, uint32_t kN) { return ((kN - k0) >> 8) + 1u; }
 // rec_coarse_block from the quantised keys, for r in [h0, hN] (the radial test passed):
 // exact wherever r's key is more than one unit outside every key's interval (one unit: the
@@ -440,12 +445,15 @@ IRT_HD int rec_coarse_block_q(uint32_t meta, float h0, float hN, float r) {
   const int nl = (int)(meta & 31u);
   const uint32_t k0 = float_key(h0), S = meta_quantum(k0, float_key(hN));
   const uint32_t d = float_key(r) - k0;
+  const int below = (int)(meta >> kMetaBelowShift);
   int b = 0;
   bool amb = false;
   for (int j = 0; j < 3; ++j) {
     if (8 * j + 7 > nl) break;
     const uint32_t lo = ((meta >> (6 + 8 * j)) & 255u) * S, hi = lo + (S - 1u);
-    if (d > hi + 1u)
+    if (j < below)
+      ++b;  // key < height[0] <= r
+    else if (d > hi + 1u)
       ++b;  // r > key: !(r <= key) counts
     else if (d + 1u >= lo)
       amb = true;

@@ -177,6 +177,15 @@ struct irt_context {
   // records are folded on the host in record order
   bool building = false;
   size_t expected = 0, received = 0;
+  // Holes in the volume, folded in record order (append_chunk): columns that start at
+  // different radii (convert_icon's first record of a land column starts at R + HSURF, so
+  // nothing covers [R, R + HSURF)), or records that leave a gap in their column.  Samples
+  // there are outside every cell and come in runs; the raygen's miss mode takes such a run
+  // in one cooperative round (irt_render.hip Tracer::kMiss).  A scene without holes runs
+  // the variant without it (OPT_NOMISS: 2-3 % faster where nearly every sample is located).
+  float bottomMin = INFINITY, bottomMax = -INFINITY;
+  bool voids = false;
+  bool variantFixed = false;  // IRT_RENDER_VARIANT chose the variant
   irt_icon_cell *d_cells = nullptr;  // freed once the scene is built
   float4 *d_trig = nullptr;          // corner trig: kept for the lazy grid build
   VolumeAcc vacc{};
@@ -846,6 +855,7 @@ int irt_create_begin(size_t numCells, int device, irt_context **out) {
     const int var = atoi(v);
     if (render_variant_available(var)) {
       c->variant = var;
+      c->variantFixed = true;
     }
   }
   auto fail = [&](int code) {
@@ -894,6 +904,8 @@ int append_chunk(irt_context *c, const irt_icon_cell *cells, size_t n, float *tr
     VolumeAcc acc;
     size_t runs = 0, bad = SIZE_MAX;
     std::vector<irt_context::Sphere> sph;
+    float bottomMin = INFINITY, bottomMax = -INFINITY;  // height[0] of the columns' first records
+    bool gap = false;  // a record that does not continue its column (or holds no radius)
   };
   std::vector<Part> part(threads);
   auto work = [&](int t) {
@@ -918,7 +930,14 @@ int append_chunk(irt_context *c, const irt_icon_cell *cells, size_t n, float *tr
       cell_bounds(x, tr, lo, hi);
       volume_acc_add(P.acc, x, lo, hi);
       const irt_icon_cell &prev = i ? cells[i - 1] : c->last;
-      if (base + i == 0 || !same_corners(x.lat, x.lon, prev.lat, prev.lon)) ++P.runs;
+      if (base + i == 0 || !same_corners(x.lat, x.lon, prev.lat, prev.lon)) {
+        ++P.runs;
+        P.bottomMin = std::min(P.bottomMin, x.height[0]);
+        P.bottomMax = std::max(P.bottomMax, x.height[0]);
+      } else if (!(x.height[0] == prev.height[prev.numLayers])) {
+        P.gap = true;
+      }
+      if (!(x.height[0] <= x.height[x.numLayers])) P.gap = true;
       if (x.height[0] == x.height[x.numLayers])  // a sphere record
         P.sph.push_back({x.height[0], (uint32_t)(base + i), x.numLayers});
     }
@@ -944,6 +963,9 @@ int append_chunk(irt_context *c, const irt_icon_cell *cells, size_t n, float *tr
     volume_acc_merge(c->vacc, P.acc);
     c->numRuns += P.runs;
     c->sph.insert(c->sph.end(), P.sph.begin(), P.sph.end());
+    c->bottomMin = std::min(c->bottomMin, P.bottomMin);
+    c->bottomMax = std::max(c->bottomMax, P.bottomMax);
+    c->voids = c->voids || P.gap;
   }
   IRT_HIP(hipSetDevice(c->device));
   if (trigPinned) {
@@ -994,6 +1016,7 @@ int irt_create_end(irt_context *c) {
   };
   volume_acc_finish(c->vacc, c->info);
   c->n = (uint32_t)numCells;
+  if (!c->variantFixed && c->variant == kDefaultVariant) c->variant = scene_variant(c->voids || c->bottomMin < c->bottomMax);
   c->G = locator_resolution(c->numRuns);
   // the scene build on the device (irt_build.hip)
   DeviceScene D;

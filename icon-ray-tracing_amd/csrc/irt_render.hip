@@ -64,6 +64,10 @@ enum : int {
                             // sample's header, so that the next round's header read hits L2
   OPT_WAVEWG2 = 536870912,  // (A/B, with OPT_LEAN) two-wave workgroups: a block's packets in pairs
                             // (each pair sharing a CU's L1), a slot freed per two waves
+  OPT_NOMISS = 262144,  // (A/B) the user-geometry cooperative loop without its miss mode:
+                        // every sample outside all cells ends its ray's round (round 4's
+                        // default); convert_icon terrain leaves voids under land, where such runs
+                        // cost one round per miss
   OPT_PAIR = 268435456,  // (A/B) the wave-wide scan's first step tests each lane's first two
                          // candidates (both entries gathered together), so the dealt-out step
                          // runs only for lanes whose first two fail
@@ -250,9 +254,17 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // the cooperative Woodcock loop (woodcock_wave) runs in every kernel (any sampler, either
   // accelerator) but the OPT_SERIAL comparison one
   static constexpr bool kCoop = (OPT & OPT_SERIAL) == 0;
-  // the miss mode of woodcock_wave: only where misses come in runs (the unstructured
-  // samplers, the grid accel); user-geometry samples almost always land in a cell
-  static constexpr bool kMiss = (OPT & (OPT_WEDGE | OPT_GRID)) != 0;
+  // the miss mode of woodcock_wave: after a sample outside every cell, a ray's next round
+  // places its samples as if none were located, until one is.  Misses come in runs wherever
+  // the volume has holes: the unstructured samplers' gaps, the grid accel's empty cells, and
+  // in the user-geometry sampler the voids convert_icon leaves under land (a column's first
+  // record starts at R + HSURF, convert_icon.cpp:361: nothing covers [R, R + HSURF)) -- at C3t a
+  // third of the samples miss, in runs of up to ~280 draws, and without the miss mode every
+  // miss cost its ray a round (single-frame launches 1.07 ms against 0.09 ms at C3, a few
+  // waves running ~1 ms: profiles/r05c_c3t/).  Flat grids almost never miss (C3: 707 of 1.01 M
+  // samples).  The kernels with misses everywhere (wedges, grid) start with whole-wave groups.
+  static constexpr bool kMiss = kCoop && (OPT & OPT_NOMISS) == 0;
+  static constexpr bool kWideStart = (OPT & (OPT_WEDGE | OPT_GRID)) != 0;
 
   // one wave-aggregated LDS add per event site
   __device__ __forceinline__ void count(int k) {
@@ -873,7 +885,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     // (sparse TFs) reach whole-wave groups after six rounds.  The miss-mode kernels (wedge
     // samplers, grid accel) keep whole-wave groups from the start: their misses come in
     // runs that wide groups cross in one round (2 % faster there, profiles/r02e_coop_cap).
-    int lgCap = kMiss ? 6 : A.coopMaxLg;
+    int lgCap = kWideStart ? 6 : A.coopMaxLg;
     tmark(6);  // between woodcockFunc calls (sdda leaves, ranges)
     for (int wr = 0;; lgCap = min(lgCap + A.coopRamp, 6), ++wr) {
       const uint64_t am = __ballot(active);
@@ -2347,11 +2359,12 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976)
 #else
-#define IRT_VARIANTS(X) X(6296832) X(5376) X(36864)
+#define IRT_VARIANTS(X) X(6296832) X(6558976) X(5376) X(36864)
 #endif
-static_assert(kDefaultVariant == 6296832, "the product build's variant list names the default");
+static_assert(kDefaultVariant == 6296832 && (kDefaultVariant | kNoMissBit) == 6558976 && kNoMissBit == OPT_NOMISS,
+              "the product build's variant list names the default and its hole-free form");
 
 int render_variants(int *out, int cap) {
   int n = 0;

@@ -33,7 +33,8 @@ MODE_USER_GEOM = 0     # Volume::mode (Params.h:29-31): sample() on the cells (d
 MODE_TRIANGLES = 1     # closest bottom triangle toward the centre (deviceCode.cu:61-76)
 MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
 # The raygen's render variants (irt_render.hip OPT_* bits), all bit-identical: the product
-# library compiles 6296832 (the default since round 4: one-wave workgroups, 5 waves/SIMD),
+# library compiles 6296832 (the default since round 4: one-wave workgroups, 5 waves/SIMD; since
+# round 5 with the miss mode, and 6558976 its form without, which hole-free scenes run),
 # 5376 (256-thread workgroups; the persistent launch's base) and 36864 (per-wave statistics);
 # libicon_rt_hip_all.so (`make VARIANTS=all`) adds the A/B variants: 4096 no waves-per-SIMD
 # floor, 5120 at 4 waves/SIMD, 70656 the one-lane-per-ray Woodcock loop, 136192 per-lane
@@ -230,10 +231,15 @@ def box1(lo, hi) -> Box1:
 
 
 # ----------------------------------------------------------------------- host helpers
-def default_kernel_id() -> int:
-    """Template id of the raygen kernel the default variant launches (k_render<id>), as
-    rocprofv3 names it."""
-    return int(lib().irt_debug_default_variant()) & ~4096  # OPT_MONO: one kernel per frame
+def default_kernel_id(ctx=None) -> int:
+    """Template id of the raygen kernel (k_render<id>, as rocprofv3 names it) that `ctx`
+    launches -- the default variant, or its hole-free form (bit 262144) on scenes without
+    holes -- or, without a context, that of the default variant."""
+    L = lib()
+    if ctx is not None:
+        L.irt_debug_get_variant.argtypes = [C.c_void_p]
+        return int(L.irt_debug_get_variant(ctx._h)) & ~4096
+    return int(L.irt_debug_default_variant()) & ~4096  # OPT_MONO: one kernel per frame
 
 
 def synth_grid(root_n: int, bisections: int, levels: int, top_height: float = 75e3,

@@ -89,8 +89,10 @@ int irt_debug_scene_array(const irt_debug_scene *s, int which, void *dst, size_t
 int irt_debug_set_variant(irt_context *ctx, int variant);
 /* The variant a new context launches (IRT_RENDER_VARIANT overrides it per context). */
 int irt_debug_default_variant(void);
-/* The variant this context launches: the default for every scene, unless
- * IRT_RENDER_VARIANT or irt_debug_set_variant chose another; -1 for NULL. */
+/* The variant this context launches: the default on scenes with holes (columns starting at
+ * different radii, as convert_icon's terrain does, or gaps inside columns: the raygen's miss
+ * mode), the default | 262144 (no miss mode) on scenes without, unless IRT_RENDER_VARIANT or
+ * irt_debug_set_variant chose another; -1 for NULL. */
 int irt_debug_get_variant(const irt_context *ctx);
 /* The variants this build compiled: returns their count and writes the first `capacity` of
  * them to `out` (may be NULL).  The product build has the default and the statistics

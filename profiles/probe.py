@@ -25,7 +25,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "icon-ray-tracing_amd", "python"))
 
 CONFIGS = {"c2": (2, 5, 47, 512), "c3": (2, 7, 90, 1024), "c4": (2, 7, 90, 2048),
-           "small": (2, 3, 90, 256)}
+           "small": (2, 3, 90, 256), "c3t": (2, 7, 90, 1024), "smallt": (2, 3, 90, 256)}
+TERRAIN = {"c3t": 4000.0, "smallt": 4000.0}  # bench.py's C3t grid (irt_synth_grid_terrain)
 CAMS = {"framing": ((0.0, 0.0, 1.4e7), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0),
         "away": ((0.0, 0.0, 1.4e7), (0.0, 0.0, 2.8e7), (0.0, 1.0, 0.0), 60.0),
         "viewall": None}
@@ -58,7 +59,7 @@ def main():
     L.irt_debug_set_variant.argtypes = [C.c_void_p, C.c_int]
     L.irt_debug_counters.argtypes = [C.c_void_p, C.c_void_p]
     rn, bis, lev, W = CONFIGS[args.config]
-    cells = irt.synth_grid(rn, bis, lev)
+    cells = irt.synth_grid(rn, bis, lev, terrain=TERRAIN.get(args.config, 0.0))
     cases = [parse(c) for c in args.cases.split(";")]
     fb = torch.zeros(W * W, dtype=torch.int32, device="cuda")
     acc = torch.zeros(W * W * 4, dtype=torch.float32, device="cuda")

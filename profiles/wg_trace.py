@@ -77,7 +77,7 @@ def main():
     args = ap.parse_args()
     rn, bis, L, W, H, tf, orbit_cfg, desc = bench.CONFIGS[args.config]
     dev = torch.device("cuda:0")
-    ctx = irt.Context.synth(rn, bis, L, 0)
+    ctx = irt.Context.synth(rn, bis, L, 0, terrain=bench.TERRAIN.get(args.config, 0.0))
     setup = irt.setup_frame(None, W, H, camera=bench.FRAMING, info=ctx.info)
     ctx.set_transfunc(bench.make_lut(tf, setup.lut), setup.value_range)
     ctx.set_statistics(False)

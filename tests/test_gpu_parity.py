@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 import irt
-from helpers import FRAMING, bits, gpu_frame, oracle_frame, terrain_cells
+from helpers import FRAMING, GpuFrame, bits, gpu_frame, oracle_frame, terrain_cells
 
 pytestmark = pytest.mark.gpu
 
@@ -359,6 +359,34 @@ def test_terrain_and_degenerate_records_bit_exact():
         assert_same_frame(a_gpu, f_gpu, a_ref, f_ref, "terrain")
         assert st_gpu[0].locateCalls == st_ref[0].locate_calls
         assert st_gpu[0].samplesFound == st_ref[0].samples_found
+
+
+@pytest.mark.parametrize("levels", [90, 65])
+def test_convert_icon_terrain_bit_exact_with_and_without_miss_mode(levels):
+    """The terrain grid as convert_icon writes it (irt_synth_grid_terrain: voids under land,
+    the inverted first layer over land, coarse blocks whose keys fall below height[0]; 65
+    levels: zero-thickness top records) against the oracle, counts included, with the raygen's
+    miss mode (the variant such a scene runs) and without it (the hole-free variant forced)."""
+    cells = irt.synth_grid(2, 3, levels, terrain=4000.0)
+    W = 160
+    a_ref, f_ref, st_ref, _ = oracle_frame(cells, W, W, camera=FRAMING)
+    setup = irt.setup_frame(cells, W, W, camera=FRAMING)
+    ctx = irt.Context(cells, 0)
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    L = irt.lib()
+    L.irt_debug_set_variant.argtypes = [C.c_void_p, C.c_int]
+    L.irt_debug_get_variant.argtypes = [C.c_void_p]
+    d = L.irt_debug_default_variant()
+    assert L.irt_debug_get_variant(ctx._h) == d  # holes: the miss mode
+    for v in (d, d | 262144):
+        assert L.irt_debug_set_variant(ctx._h, v) == 0
+        fr = GpuFrame(ctx, W, W)
+        st = fr.render(setup.lp)
+        a, f = fr.host()
+        assert_same_frame(a, f, a_ref, f_ref, f"terrain L{levels} variant {v}")
+        assert (st.locateCalls, st.samplesFound) == (st_ref[0].locate_calls, st_ref[0].samples_found)
+        assert st.locateCalls > st.samplesFound  # the voids: samples outside every cell
+    ctx.close()
 
 
 @pytest.mark.skipif(not os.path.exists(irt.ALL_LIB_PATH), reason="make VARIANTS=all not built")

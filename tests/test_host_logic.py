@@ -220,7 +220,8 @@ def test_render_record_layout_gives_findheight_value():
     (irt_common.h: coarse keys + one height/value block, or the literal search for
     unsorted columns).  Host evaluation of that path == the literal binary search
     (ICONGrid.h:117-164) at every layer boundary, its float neighbours and random radii,
-    for sorted and deliberately unsorted columns of every layer count."""
+    for sorted and deliberately unsorted columns of every layer count, and for records whose
+    height[0] sits above some of their other heights (convert_icon's inverted first layer)."""
     cells = irt.synth_grid(2, 1, 93)  # records of 31, 31, 31 layers (and a short tail)
     rng = np.random.default_rng(7)
     cells = cells[:400].copy()
@@ -233,6 +234,12 @@ def test_render_record_layout_gives_findheight_value():
             a, b = rng.choice(np.arange(1, nl + 1), 2, replace=False)
             h = cells["height"][i]
             h[a], h[b] = h[b], h[a]
+        elif i % 3 == 1 and nl >= 2:
+            # convert_icon's inverted first layer (H[0] = R + HSURF above H[1..j]): height[0]
+            # moved up to (or just past) height[j], so coarse keys fall below it
+            j = int(rng.integers(1, nl + 1))
+            h = cells["height"][i]
+            h[0] = h[j] if i % 2 else np.nextafter(h[j], np.float32(np.inf))
     D = irt.DebugScene(cells)
     checked = 0
     for i in range(cells.size):
