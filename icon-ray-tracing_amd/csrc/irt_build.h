@@ -457,144 +457,6 @@ IRT_HD uint32_t cell_header(const E &en, int n, const float *edges, int ne, uint
   return cum;
 }
 
-// The compact entry's triangle (irt_common.h kCmp4, word [1]) of record i in cube-map cell
-// `cell` of a G x G-per-face map: out4 = {V0, V1, V2 as int16 pairs, margin bits}.
-//
-// On face f (dominant axis ax, sign s) a point is p = |p_ax| (s e_ax + u e_ua + v e_va), so the
-// reference's plane value N.p - w (ICONGrid.h:176-179, evaluated in float) is |p_ax| L(u, v) - w
-// with L linear: in the cell's local units (X, Y) = ((u + 1) G/2 - i, (v + 1) G/2 - j) kCmpQ,
-// L = a X + b Y + c.  The plane's boundary is L = w / |p_ax|; the lines are shifted by w / p_mid
-// (|p_ax| at the record's mid radius and the cell's centre) and the rest of w / |p_ax| over the
-// cell goes into the margin.  The three lines meet in the triangle's vertices (V_k on lines
-// k-1 and k, in double), rounded to integers; edge k runs from V_k to V_(k+1) along line k with
-// the outside (L_k > w / |p_ax|) on its left (else the cycle is stored reversed).  The margin M,
-// in local units, bounds for every point of the cell (X, Y in [0, Q]) whose radius is in
-// [h0, hN]:
-//   D_k  the distance between the rounded edge and its line (largest at a cell corner);
-//   T_k  (E_k / |p_ax|min + |w_k| max |1/|p_ax| - 1/p_mid|) / |grad L_k|: the reference's float
-//        error on N.p - w (three products, two sums, one difference: E_k <= 3.1 u r |N|, by
-//        Cauchy-Schwarz on sum |p_i N_i|) and the rest of the offset, as distances; |p_ax| =
-//        r / sqrt(1 + u^2 + v^2) over the cell and [h0, hN];
-//   3 e  the kernel's position error e: its (X, Y) from the hardware reciprocal (irt_render.hip
-//        cubemap_cell_fast) is within 1.8e-7 G Q of the true one per axis (3e-7 G Q taken for
-//        the Euclidean distance), counted for the point and twice for the edge's drift from its
-//        line when the point is just outside the cell square;
-//   0.25 units for the kernel's float evaluation of the edge function;
-// with T_k times 1.25.  The kernel compares the edge function (length |V_(k+1) - V_k| times the
-// distance) with M (0.41422 |d|_1 + 0.58579 |d|_inf) >= M |d|_2.
-// Degenerate cases -- zero-thickness or empty records, near-parallel lines, vertices beyond
-// +-32000 units (triangles much larger than a cell) -- get M = +inf: always the exact test.
-// Double arithmetic of + - * / sqrt and floor only: the host and device builds agree bit for
-// bit.
-IRT_HD void compact_triangle(const float *pl, float h0, float hN, uint32_t cell, int G, uint32_t *out4) {
-  out4[0] = out4[1] = out4[2] = 0u;
-  out4[3] = f2u(__builtin_inff());
-  if (!(h0 < hN) || !(h0 > 0.f)) return;
-  const uint32_t GG = (uint32_t)G * (uint32_t)G;
-  const int face = (int)(cell / GG);
-  const int cj = (int)((cell % GG) / (uint32_t)G), ci = (int)(cell % (uint32_t)G);
-  int ax, ua, va;
-  double sgn;
-  face_axes(face, ax, ua, va, sgn);
-  const double Q = (double)kCmpQ, cw = 2.0 / (double)G, gq = cw / Q;
-  const double u0 = -1.0 + (double)ci * cw, v0 = -1.0 + (double)cj * cw;
-  // |u|, |v| over the cell (a little beyond it), for the range of |p_ax|
-  const double pad = 0.01 * cw;
-  const double ua0 = u0 - pad, ua1 = u0 + cw + pad, va0 = v0 - pad, va1 = v0 + cw + pad;
-  const double uMax = dmax(ua0 < 0 ? -ua0 : ua0, ua1 < 0 ? -ua1 : ua1);
-  const double vMax = dmax(va0 < 0 ? -va0 : va0, va1 < 0 ? -va1 : va1);
-  const double uMin = (ua0 <= 0.0 && ua1 >= 0.0) ? 0.0 : dmin(ua0 < 0 ? -ua0 : ua0, ua1 < 0 ? -ua1 : ua1);
-  const double vMin = (va0 <= 0.0 && va1 >= 0.0) ? 0.0 : dmin(va0 < 0 ? -va0 : va0, va1 < 0 ? -va1 : va1);
-  const double pMin = (double)h0 / sqrt(1.0 + uMax * uMax + vMax * vMax) * 0.9999999;
-  const double pMax = (double)hN / sqrt(1.0 + uMin * uMin + vMin * vMin) * 1.0000001;
-  const double uc = u0 + 0.5 * cw, vc = v0 + 0.5 * cw;
-  const double pMid = 0.5 * ((double)h0 + (double)hN) / sqrt(1.0 + uc * uc + vc * vc);
-  double a[3], b[3], c[3], T[3];
-  for (int k = 0; k < 3; ++k) {
-    const double N[3] = {(double)pl[4 * k], (double)pl[4 * k + 1], (double)pl[4 * k + 2]};
-    const double w = (double)pl[4 * k + 3], aw = w < 0 ? -w : w;
-    a[k] = N[ua] * gq;
-    b[k] = N[va] * gq;
-    c[k] = sgn * N[ax] + u0 * N[ua] + v0 * N[va] - w / pMid;
-    const double g = sqrt(a[k] * a[k] + b[k] * b[k]);
-    const double n2 = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
-    if (!(g > 0.0) || !(n2 > 0.0)) return;
-    const double E = 3.1 * (1.0 / 16777216.0) * (double)hN * n2;
-    const double wv = aw * dmax(1.0 / pMin - 1.0 / pMid, 1.0 / pMid - 1.0 / pMax);
-    T[k] = (E / pMin + wv) / g;
-  }
-  // vertices V_k on lines k-1 and k
-  double vx[3], vy[3];
-  for (int k = 0; k < 3; ++k) {
-    const int p = (k + 2) % 3;
-    const double det = a[p] * b[k] - a[k] * b[p];
-    const double np = sqrt(a[p] * a[p] + b[p] * b[p]), nk = sqrt(a[k] * a[k] + b[k] * b[k]);
-    if (!((det < 0 ? -det : det) > 1e-3 * np * nk)) return;  // nearly parallel
-    vx[k] = (b[p] * c[k] - b[k] * c[p]) / det;
-    vy[k] = (a[k] * c[p] - a[p] * c[k]) / det;
-    if (!(vx[k] > -32000.0 && vx[k] < 32000.0 && vy[k] > -32000.0 && vy[k] < 32000.0)) return;
-  }
-  // orientation: edge k (V_k -> V_(k+1)) has line k's outside on its left, for every k, or on
-  // its right for every k (then the cycle is reversed)
-  int side = 0;
-  for (int k = 0; k < 3; ++k) {
-    const int q = (k + 1) % 3;
-    const double dx = vx[q] - vx[k], dy = vy[q] - vy[k];
-    const double dot = -dy * a[k] + dx * b[k];  // the left normal (-dy, dx) against grad L_k
-    const int sd = dot > 0.0 ? 1 : (dot < 0.0 ? -1 : 0);
-    if (sd == 0 || (side != 0 && sd != side)) return;
-    side = sd;
-  }
-  double qx[3], qy[3];
-  for (int k = 0; k < 3; ++k) {
-    qx[k] = floor(vx[k] + 0.5);
-    qy[k] = floor(vy[k] + 0.5);
-  }
-  // the rounded edges in storage order, each with the line it stands for
-  int ord[3] = {0, 1, 2};
-  if (side < 0) {
-    ord[1] = 2;
-    ord[2] = 1;
-  }
-  const double eps = 3e-7 * (double)G * Q;
-  double M = 0.0;
-  for (int e = 0; e < 3; ++e) {
-    const int i0 = ord[e], i1 = ord[(e + 1) % 3];
-    // the line of this edge: both endpoints lie on it (V_k on lines k-1 and k)
-    const int k = side > 0 ? i0 : i1;
-    const double ex = qx[i1] - qx[i0], ey = qy[i1] - qy[i0];
-    const double len = sqrt(ex * ex + ey * ey);
-    if (!(len > 0.0)) return;
-    const double g = sqrt(a[k] * a[k] + b[k] * b[k]);
-    double D = 0.0;
-    for (int cc = 0; cc < 4; ++cc) {
-      const double X = (cc & 1) ? Q : 0.0, Y = (cc & 2) ? Q : 0.0;
-      const double dq = (ex * (Y - qy[i0]) - ey * (X - qx[i0])) / len;  // left-side distance
-      const double dl = (a[k] * X + b[k] * Y + c[k]) / g;               // outside distance
-      const double dd = dq - dl;
-      D = dmax(D, dd < 0 ? -dd : dd);
-    }
-    const double m = 1.25 * T[k] + D + 3.0 * eps + 0.25;
-    M = dmax(M, m);
-  }
-  if (!(M < 1e6)) return;
-  for (int e = 0; e < 3; ++e) {
-    const int i0 = ord[e];
-    out4[e] = ((uint32_t)(uint16_t)(int16_t)(int)qx[i0]) | ((uint32_t)(uint16_t)(int16_t)(int)qy[i0] << 16);
-  }
-  out4[3] = f2u((float)M * 1.0000002f);
-}
-
-// One compact entry (kCmp4 float4, irt_common.h) of record i in cube-map cell `cell`.
-IRT_HD void compact_entry(uint32_t i, const float *planes, const float *rng, const uint32_t *meta,
-                          uint32_t cell, int G, uint32_t *W8) {
-  W8[0] = f2u(rng[2 * (size_t)i]);
-  W8[1] = f2u(rng[2 * (size_t)i + 1]);
-  W8[2] = i;
-  W8[3] = meta[i];
-  compact_triangle(planes + 12 * (size_t)i, rng[2 * (size_t)i], rng[2 * (size_t)i + 1], cell, G, W8 + 4);
-}
-
 // One fat entry (kFat4 float4, irt_common.h) of record i.
 IRT_HD void fat_entry(uint32_t i, const float *planes, const float *rng, const uint32_t *meta,
                       float *F) {

@@ -256,8 +256,7 @@ __global__ void k_cell_header(const uint32_t *offsets, uint32_t numCells, const 
 
 __global__ void k_cell_fill(const uint32_t *offsets, uint32_t numCells, const unsigned long long *vals,
                             const float2 *rng, const float4 *edges, const uint64_t *cellBase,
-                            uint32_t *hdr, const float *planes, const uint32_t *meta, float4 *fat,
-                            uint4 *cmp, int G) {
+                            uint32_t *hdr, const float *planes, const uint32_t *meta, float4 *fat) {
   for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < numCells; c += gridDim.x * blockDim.x) {
     const uint32_t q0 = offsets[c], n = offsets[c + 1] - q0;
     const uint64_t base = cellBase[c];
@@ -274,14 +273,9 @@ __global__ void k_cell_fill(const uint32_t *offsets, uint32_t numCells, const un
         if (!in_bin(h.x, h.y, lo, hi)) continue;
         float F[4 * kFat4];
         fat_entry(rec, planes, reinterpret_cast<const float *>(rng), meta, F);
-        float4 *o = fat + (size_t)at * kFatStride4;
+        float4 *o = fat + (size_t)(at++) * kFatStride4;
         for (int j = 0; j < kFat4; ++j) o[j] = make_float4(F[4 * j], F[4 * j + 1], F[4 * j + 2], F[4 * j + 3]);
         for (int j = kFat4; j < kFatStride4; ++j) o[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        uint32_t Wc[4 * kCmp4];
-        compact_entry(rec, planes, reinterpret_cast<const float *>(rng), meta, c, G, Wc);
-        uint4 *oc = cmp + (size_t)at * kCmp4;
-        for (int j = 0; j < kCmp4; ++j) oc[j] = make_uint4(Wc[4 * j], Wc[4 * j + 1], Wc[4 * j + 2], Wc[4 * j + 3]);
-        ++at;
       }
     }
   }
@@ -564,11 +558,9 @@ int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_
   // --- 9. fat entries
   BHIP(hipMalloc((void **)&out.fat, std::max<uint64_t>(numFat, 1) * kFatStride4 * sizeof(float4)));
   out.bytes += std::max<uint64_t>(numFat, 1) * kFatStride4 * sizeof(float4);
-  BHIP(hipMalloc((void **)&out.cmp, std::max<uint64_t>(numFat, 1) * kCmp4 * sizeof(uint4)));
-  out.bytes += std::max<uint64_t>(numFat, 1) * kCmp4 * sizeof(uint4);
   clk.mark("fat entries allocated");
   hipLaunchKernelGGL(k_cell_fill, dim3(nc), dim3(64), 0, s, offsets, numCells, pv2, rng, edges, cellBase,
-                     reinterpret_cast<uint32_t *>(out.binHdr), planesF, meta, out.fat, out.cmp, G);
+                     reinterpret_cast<uint32_t *>(out.binHdr), planesF, meta, out.fat);
   BHIP(hipGetLastError());
   BHIP(hipStreamSynchronize(s));
   clk.mark("fat entries");

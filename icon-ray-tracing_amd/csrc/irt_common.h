@@ -333,8 +333,6 @@ IRT_HD uint32_t cubemap_cell(float px, float py, float pz, int G) {
 #endif
 constexpr int kSubCells = IRT_SUBCELLS;  // sub-cells per cell edge (irt_build.h kSub)
 constexpr int kMaskCand = 8;  // candidates per radial bin with a sub-cell mask (irt_build.h)
-constexpr int kCmp4 = 2;         // float4 per compact entry (below)
-constexpr float kCmpQ = 4096.f;  // compact entries' local units per cube-map cell edge
 
 // cubemap_cell on the kSubCells-times finer grid: the same cell (the scaling by a power of
 // two is exact) and the sub-cell s = sj * kSubCells + si within it.
@@ -364,39 +362,6 @@ IRT_HD uint32_t cubemap_cell_sub(float px, float py, float pz, int G, uint32_t &
   sub = (uint32_t)((j % kSubCells) * kSubCells + (i % kSubCells));
   return (uint32_t)face * (uint32_t)G * (uint32_t)G + (uint32_t)(j / kSubCells) * (uint32_t)G +
          (uint32_t)(i / kSubCells);
-}
-
-// cubemap_cell_sub plus the point's position in the cell's local frame of the compact
-// entries (irt_common.h kCmpQ units; the kernel's cubemap_cell_fast computes the same from the
-// hardware reciprocal).
-IRT_HD uint32_t cubemap_cell_local(float px, float py, float pz, int G, uint32_t &sub, float &X, float &Y) {
-  const float ax = __builtin_fabsf(px), ay = __builtin_fabsf(py), az = __builtin_fabsf(pz);
-  int face;
-  float u, v;
-  if (ax >= ay && ax >= az) {
-    face = px >= 0.f ? 0 : 1;
-    u = py / ax;
-    v = pz / ax;
-  } else if (ay >= az) {
-    face = py >= 0.f ? 2 : 3;
-    u = px / ay;
-    v = pz / ay;
-  } else {
-    face = pz >= 0.f ? 4 : 5;
-    u = px / az;
-    v = py / az;
-  }
-  const int GS = G * kSubCells;
-  const float fg = 0.5f * (float)GS;
-  const float xs = (u + 1.f) * fg, ys = (v + 1.f) * fg;
-  int i = (int)xs, j = (int)ys;
-  i = i < 0 ? 0 : (i >= GS ? GS - 1 : i);
-  j = j < 0 ? 0 : (j >= GS ? GS - 1 : j);
-  sub = (uint32_t)((j % kSubCells) * kSubCells + (i % kSubCells));
-  const int ci = i / kSubCells, cj = j / kSubCells;
-  X = (xs - (float)(kSubCells * ci)) * (kCmpQ / (float)kSubCells);
-  Y = (ys - (float)(kSubCells * cj)) * (kCmpQ / (float)kSubCells);
-  return (uint32_t)face * (uint32_t)G * (uint32_t)G + (uint32_t)cj * (uint32_t)G + (uint32_t)ci;
 }
 
 // Per-record height/value block: 64 floats = 256 B, two 128-B lines.
@@ -440,41 +405,6 @@ IRT_HD uint32_t sph_hash(float r) {
 //           meta: see record_meta (irt_build.h) and record_path below
 constexpr int kFat4 = 4;
 constexpr int kFatStride4 = 4;
-// Compact entry (round 5): the same candidate in 32 B, two float4, four to a 128-B line,
-// parallel to the fat entries (entry q of both arrays is the same candidate):
-//   [0]     {height[0], height[numLayers], record index, meta}  (the fat entry's [3])
-//   [1]     the record's three side planes as a triangle in the cube-map cell's local frame
-//           (kCmpQ units per cell edge, origin at the cell's corner): vertices V0, V1, V2 as
-//           int16 pairs {x, y} in words 0..2 -- edge k from V_k to V_(k+1) lies on plane k's
-//           line on the cube face, outside on its left -- and in word 3 the certification
-//           margin M (float; +inf: never certain)
-// A point of the cell at local (X, Y) with left-side distance l_k / |V_(k+1) - V_k| > M from
-// some edge certainly fails sample()'s plane tests as the reference evaluates them in float
-// (ICONGrid.h:197-203), and one < -M from every edge certainly passes them; anything closer
-// takes the exact planes of the fat entry.  M covers the vertex rounding, the kernel's
-// position error, the reference's float evaluation error and the planes' offset w
-// (irt_build.h compact_triangle).
-// -1: certainly fails the plane tests, 1: certainly passes them, 0: undecided (exact test)
-IRT_HD int tri_test(uint32_t v0, uint32_t v1, uint32_t v2, float m, float X, float Y) {
-  const float ax = (float)(int16_t)(v0 & 0xFFFFu), ay = (float)(int16_t)(v0 >> 16);
-  const float bx = (float)(int16_t)(v1 & 0xFFFFu), by = (float)(int16_t)(v1 >> 16);
-  const float cx = (float)(int16_t)(v2 & 0xFFFFu), cy = (float)(int16_t)(v2 >> 16);
-  bool out = false, in = true;
-  auto edge = [&](float px, float py, float qx, float qy) {
-    const float dx = qx - px, dy = qy - py;
-    const float l = dx * (Y - py) - dy * (X - px);
-    const float adx = __builtin_fabsf(dx), ady = __builtin_fabsf(dy);
-    // m times a bound of the edge's length: 0.41422 |d|_1 + 0.58579 |d|_inf >= |d|_2
-    const float th = m * (0.41422f * (adx + ady) + 0.58579f * (adx > ady ? adx : ady));
-    out = out || l > th;
-    in = in && l < -th;
-  };
-  edge(ax, ay, bx, by);
-  edge(bx, by, cx, cy);
-  edge(cx, cy, ax, ay);
-  return out ? -1 : (in ? 1 : 0);
-}
-
 // Per-record height/value blocks (the render record without its planes/keys), kBlk4
 // float4 = 256 B: block b (4 float4) = {height[8b..8b+3]}, {height[8b+4..8b+7]},
 // {value[8b-1..8b+2]}, {value[8b+3..8b+6]}.  Block 0's value[-1] slot holds value[31]: the

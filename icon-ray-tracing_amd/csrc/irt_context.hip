@@ -39,7 +39,6 @@ struct irt_context {
   // HBM
   uint4 *d_binHdr = nullptr;   // binned locator (irt_common.h)
   float4 *d_fat = nullptr;
-  uint4 *d_cmp = nullptr;      // compact entries (irt_common.h kCmp4), parallel to d_fat
   float4 *d_blocks = nullptr;
   size_t binEntries = 0;       // fat entries
   uint32_t numSph = 0;         // zero-thickness records (spheres): distinct radii
@@ -230,7 +229,7 @@ int upload(irt_context *c, T **p, const T *src, size_t count) {
 void free_all(irt_context *c) {
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_cmp, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
+  void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
                   c->d_sphBits, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_gridBits, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
                   c->d_lut, c->d_counters, c->d_counterBuckets, c->d_meta, c->d_queue, c->d_chainFlag,
                   c->d_frameCams};
@@ -598,7 +597,6 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.counters = c->d_counters + 16 * (c->launches % irt_context::kSlots);
   A.binHdr = c->d_binHdr;
   A.fat = c->d_fat;
-  A.cmp = c->d_cmp;
   A.blocks = c->d_blocks;
   A.numSph = c->numSph;
   A.sphR = c->d_sphR;
@@ -1027,7 +1025,6 @@ int irt_create_end(irt_context *c) {
   c->d_meta = D.meta;
   c->d_binHdr = D.binHdr;
   c->d_fat = D.fat;
-  c->d_cmp = D.cmp;
   c->bytes += D.bytes;
   if (rc) return rc;
   c->info.locatorFaceRes = c->G;
@@ -1739,7 +1736,6 @@ static int debug_locate(irt_context *c, const float *xyz, int n, int *found, flo
   A.G = c->G;
   A.binHdr = c->d_binHdr;
   A.fat = c->d_fat;
-  A.cmp = c->d_cmp;
   A.blocks = c->d_blocks;
   A.numSph = c->numSph;
   A.sphR = c->d_sphR;
@@ -1808,7 +1804,6 @@ extern "C" int irt_debug_context_array(const irt_context *c, int which, void *ds
   switch (which) {
     case IRT_DEBUG_ARRAY_BIN_HDR: src = c->d_binHdr; n = (size_t)6 * c->G * c->G * kBinHdrWords * 4; break;
     case IRT_DEBUG_ARRAY_FAT: src = c->d_fat; n = c->binEntries * kFatStride4 * 16; break;
-    case IRT_DEBUG_ARRAY_CMP: src = c->d_cmp; n = c->binEntries * kCmp4 * 16; break;
     case IRT_DEBUG_ARRAY_BLOCKS: src = c->d_blocks; n = (size_t)c->n * kBlk4 * 16; break;
     case IRT_DEBUG_ARRAY_SPH_R: src = c->d_sphR; n = (size_t)c->numSph * 4; break;
     case IRT_DEBUG_ARRAY_SPH_OFF: src = c->d_sphOff; n = c->numSph ? ((size_t)c->numSph + 1) * 4 : 4; break;

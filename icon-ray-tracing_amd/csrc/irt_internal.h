@@ -35,7 +35,6 @@ struct HostScene {
   // the product locator (irt_build.h)
   std::vector<uint32_t> binHdr;   // 6*G*G * kBinHdrWords
   std::vector<float> fat;         // binEntries * kFatStride4 * 4
-  std::vector<uint32_t> cmp;      // binEntries * kCmp4 * 4: the compact entries (irt_common.h)
   size_t binEntries = 0;
   // zero-thickness records (spheres): distinct radii, CSR into record indices (ascending),
   // and a hash bitmap of the radii (irt_common.h sph_hash) the kernel keeps in LDS

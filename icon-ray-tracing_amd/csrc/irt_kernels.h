@@ -61,7 +61,6 @@ struct RenderArgs {
   // per-record height/value blocks.
   const uint4 *binHdr;
   const float4 *fat;
-  const uint4 *cmp;      // compact entries (round 5), parallel to fat: the hot path's copy
   const float4 *blocks;
   // zero-thickness records (spheres, host/irt_scene.cpp): sorted distinct radii, CSR into
   // (record, numLayers) pairs, and the radius hash bitmap (kSphBitWords words)
@@ -190,7 +189,6 @@ struct DeviceScene {
   uint32_t *meta = nullptr;  // per record (irt_build.h record_meta), kept for the lazy grid build
   uint4 *binHdr = nullptr;
   float4 *fat = nullptr;
-  uint4 *cmp = nullptr;  // the compact entries (irt_common.h kCmp4), parallel to fat
   size_t entries = 0, binEntries = 0, bigCells = 0, bytes = 0;
 };
 int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_t n, size_t numRuns,

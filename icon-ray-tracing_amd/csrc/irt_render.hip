@@ -115,44 +115,6 @@ __device__ __forceinline__ uint32_t cubemap_cell_fast(float px, float py, float 
   uint32_t sub;
   return cubemap_cell_fast(px, py, pz, G, sub);
 }
-// ... and the point's position (X, Y) in the cell's local frame of the compact entries
-// (irt_common.h kCmpQ units; cubemap_cell_local is the host's form): within 1.8e-7 G Q per axis
-// of the exact one (the margin's position term, irt_build.h compact_triangle)
-__device__ __forceinline__ uint32_t cubemap_cell_fast(float px, float py, float pz, int G,
-                                                      uint32_t &sub, float &X, float &Y) {
-  const float ax = __builtin_fabsf(px), ay = __builtin_fabsf(py), az = __builtin_fabsf(pz);
-  uint32_t face;
-  float num0, num1, den;
-  if (ax >= ay && ax >= az) {
-    face = px >= 0.f ? 0u : 1u;
-    num0 = py;
-    num1 = pz;
-    den = ax;
-  } else if (ay >= az) {
-    face = py >= 0.f ? 2u : 3u;
-    num0 = px;
-    num1 = pz;
-    den = ay;
-  } else {
-    face = pz >= 0.f ? 4u : 5u;
-    num0 = px;
-    num1 = py;
-    den = az;
-  }
-  const float inv = __builtin_amdgcn_rcpf(den);
-  const int GS = opaque_u(G) * kSubCells;
-  const float fg = 0.5f * (float)GS;
-  const float xs = (num0 * inv + 1.f) * fg, ys = (num1 * inv + 1.f) * fg;
-  int i = (int)xs;
-  int j = (int)ys;
-  i = i < 0 ? 0 : (i >= GS ? GS - 1 : i);
-  j = j < 0 ? 0 : (j >= GS ? GS - 1 : j);
-  sub = (uint32_t)((j & (kSubCells - 1)) * kSubCells + (i & (kSubCells - 1)));
-  X = (xs - (float)(i & ~(kSubCells - 1))) * (kCmpQ / (float)kSubCells);
-  Y = (ys - (float)(j & ~(kSubCells - 1))) * (kCmpQ / (float)kSubCells);
-  return face * (uint32_t)G * (uint32_t)G + (uint32_t)(j / kSubCells) * (uint32_t)G +
-         (uint32_t)(i / kSubCells);
-}
 
 // Per-wave LDS of the cooperative Woodcock loop (Tracer::woodcock_wave).
 struct CoopWave {
@@ -164,13 +126,8 @@ struct CoopWave {
 // Per-wave LDS of Tracer::locate_wave's candidate scan
 struct ScanWave {
   float4 pt[64];    // lane l's sample {point, r}
-  uint4 lst[64];    // its candidate list {first entry, sub-cell mask | exact flag << 8, next
-                    // position, record limit}
-  float2 xy[64];    // the sample's position in its cube-map cell's local frame (compact entries)
+  uint4 lst[64];    // its candidate list {first entry, sub-cell mask, next position, record limit}
 };
-// lst[l].y bit 8: the candidate at the list's next position was undecided by its compact test
-// and is tested on its fat entry's exact planes
-constexpr uint32_t kExactNext = 256u;
 // OPT_HDRLDS: up to kHdrStage distinct header lines of a wave's samples, staged in LDS
 constexpr int kHdrStage = 8;
 struct HdrStage {
@@ -331,6 +288,21 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     return Bf[blk_value_pos(first)];
   }
 
+  // sample()'s point test (ICONGrid.h:184, 197-203) on one fat entry {p0, p1, p2, m}:
+  // the radial range and the three ccw side planes
+  __device__ __forceinline__ bool pass_fat(const float4 &p0, const float4 &p1, const float4 &p2,
+                                           const float4 &m, float px, float py, float pz, float r) {
+    if constexpr (kCoop)
+      ++specCand;  // counted only if the sample is one the reference takes (woodcock_wave)
+    else
+      count(4);
+    if (r < m.x || r > m.y) return false;                                 // ICONGrid.h:184
+    if (dot3(px, py, pz, p0.x, p0.y, p0.z) - p0.w > 0.f) return false;  // ICONGrid.h:201
+    if (dot3(px, py, pz, p1.x, p1.y, p1.z) - p1.w > 0.f) return false;  // 202
+    if (dot3(px, py, pz, p2.x, p2.y, p2.z) - p2.w > 0.f) return false;  // 203
+    return true;
+  }
+
   // The record a point test found: index and its getValue path at the sample's radius
   // (irt_common.h record_path: numLayers, which 64-B block, or the literal search).
   struct Found {
@@ -342,8 +314,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // that can reach the sample's sub-cell, irt_build.h), then every later one.  Only the
   // point test runs in the (lane-divergent) loop; getValue's gathers come after.
   __device__ __forceinline__ bool scan_fat(uint32_t q, uint32_t qe, uint32_t mask, uint32_t limit,
-                                           float px, float py, float pz, float r, float X, float Y,
-                                           Found &f) {
+                                           float px, float py, float pz, float r, Found &f) {
     const uint32_t n = qe - q;
     for (uint32_t j = 0;; ++j) {
       if (j < (uint32_t)kMaskCand) {
@@ -351,42 +322,15 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         j = m ? j + (uint32_t)__builtin_ctz(m) : (uint32_t)kMaskCand;
       }
       if (j >= n) break;
-      // the compact entry first; its exact planes (the fat entry) only when undecided
-      const uint4 *E = A.cmp + (size_t)(q + j) * kCmp4;
-      const uint4 am = E[0], T = E[1];
-      if (am.z >= limit) return false;
-      if constexpr (kCoop)
-        ++specCand;  // counted only if the sample is one the reference takes (woodcock_wave)
-      else
-        count(4);
-      const float h0 = __uint_as_float(am.x), hN = __uint_as_float(am.y);
-      if (r < h0 || r > hN) continue;  // ICONGrid.h:184
-      const int t = tri_test(T.x, T.y, T.z, __uint_as_float(T.w), X, Y);
-      if (t < 0) continue;
-      if (t == 0) {
-        const float4 *F = A.fat + (size_t)(q + j) * kFatStride4;
-        if (!planes_pass(F[0], F[1], F[2], px, py, pz)) continue;
+      const float4 *F = A.fat + (size_t)(q + j) * kFatStride4;
+      const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3];
+      if (__float_as_uint(am.z) >= limit) return false;
+      if (pass_fat(a0, a1, a2, am, px, py, pz, r)) {
+        f = {__float_as_uint(am.z), record_path(__float_as_uint(am.w), am.x, am.y, r)};
+        return true;
       }
-      f = {am.z, record_path(am.w, h0, hN, r)};
-      return true;
     }
     return false;
-  }
-  // sample()'s three plane tests (ICONGrid.h:197-203) on a fat entry's planes
-  __device__ __forceinline__ static bool planes_pass(const float4 &a0, const float4 &a1, const float4 &a2,
-                                                     float px, float py, float pz) {
-    return !(dot3(px, py, pz, a0.x, a0.y, a0.z) - a0.w > 0.f) && !(dot3(px, py, pz, a1.x, a1.y, a1.z) - a1.w > 0.f) &&
-           !(dot3(px, py, pz, a2.x, a2.y, a2.z) - a2.w > 0.f);
-  }
-  // a compact entry's test: -1 certainly not, 1 certainly the point's record (exactly as the
-  // reference's sample() decides, ICONGrid.h:184, 197-203), 0 undecided (the fat entry's exact
-  // planes decide); f its record and getValue path
-  __device__ __forceinline__ int cmp_entry(const uint4 *E, float r, float X, float Y, Found &f) {
-    const uint4 am = E[0], T = E[1];
-    const float h0 = __uint_as_float(am.x), hN = __uint_as_float(am.y);
-    f = {am.z, record_path(am.w, h0, hN, r)};
-    if (r < h0 || r > hN) return -1;  // ICONGrid.h:184
-    return tri_test(T.x, T.y, T.z, __uint_as_float(T.w), X, Y);
   }
 
   // getValue (ICONGrid.h:147-164) of the found record at radius r: sorted heights take the
@@ -521,17 +465,16 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     }
     const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
     uint32_t sub;
-    float X, Y;
-    const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G, sub, X, Y);
+    const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G, sub);
     // the cell header's words 0..7 and the sub-cell's mask word: one 128-B line
     const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
     const uint4 H0 = Hc[0], H1 = Hc[1];
     const uint32_t M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
-    return locate_hdr(px, py, pz, r, X, Y, H0, H1, M, value);
+    return locate_hdr(px, py, pz, r, H0, H1, M, value);
   }
 
-  __device__ __forceinline__ bool locate_hdr(float px, float py, float pz, float r, float X, float Y,
-                                             const uint4 &H0, const uint4 &H1, uint32_t M, float &value) {
+  __device__ __forceinline__ bool locate_hdr(float px, float py, float pz, float r, const uint4 &H0,
+                                             const uint4 &H1, uint32_t M, float &value) {
     const float e0 = __uint_as_float(H0.x), e1 = __uint_as_float(H0.y), e2 = __uint_as_float(H0.z);
     const int b = bin_of(r, e0, e1, e2);
     // bin b's [beg, end) from the cumulative ends, and its upper edge, selected with masks
@@ -549,7 +492,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     uint32_t qb = H0.w + beg, qe = H0.w + end;
     for (int pass = 0; pass < 2; ++pass) {
       Found g;
-      if (scan_fat(qb, qe, (M >> (8 * (b + pass))) & 0xFFu, f.rec, px, py, pz, r, X, Y, g)) {
+      if (scan_fat(qb, qe, (M >> (8 * (b + pass))) & 0xFFu, f.rec, px, py, pz, r, g)) {
         f = g;
         hit = true;
       }
@@ -672,15 +615,14 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     uint32_t M = 0u, cell = 0u, sub = 0u;
     uint32_t tv = 0u;  // OPT_NEXTHDR's loaded word, consumed after the scan
     uint32_t fe2 = 0u; // OPT_PAIR: the pass's second candidate entry
-    float fx = 0.f, fy = 0.f;  // the sample in its cell's local frame (compact entries)
     if constexpr ((OPT & OPT_HDRLDS) != 0) {
-      if (want) cell = cubemap_cell_fast(px, py, pz, A.G, sub, fx, fy);
+      if (want) cell = cubemap_cell_fast(px, py, pz, A.G, sub);
       stage_headers(want, cell, sub, H0, H1, M);
     }
     if (want) {
       const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
       if constexpr ((OPT & OPT_HDRLDS) == 0) {
-        cell = cubemap_cell_fast(px, py, pz, A.G, sub, fx, fy);
+        cell = cubemap_cell_fast(px, py, pz, A.G, sub);
         const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
         H0 = Hc[0];
         H1 = Hc[1];
@@ -705,7 +647,6 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       c = (uint32_t)__popc(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
       lds_st16(&W.pt[lane], make_float4(px, py, pz, r));
       lds_st16(&W.lst[lane], make_uint4(H0.w + beg, m8, 0u, 0xFFFFFFFFu));
-      W.xy[lane] = make_float2(fx, fy);
       fe = H0.w + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
       if constexpr (kPair) fe2 = H0.w + beg + list_entry(m8, 1u);
       fr = r;
@@ -742,21 +683,16 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
           }
         }
       } else if ((OPT & OPT_DEALALL) == 0 && c > 0u) {  // (from registers: no LDS round trip before the gather)
-        // the compact entry (32 B): certainly the record, certainly not, or undecided -- then
-        // the same candidate goes through the deal below on its fat entry's exact planes
         Found f;
-        const int tr = cmp_entry(A.cmp + (size_t)fe * kCmp4, fr, fx, fy, f);
+        const bool ok = pass_entry(A.fat + (size_t)fe * kFatStride4, px, py, pz, fr, f);
         if (f.rec < flim) {  // scan_fat stops, uncounted, at the first record >= the limit
           ++specCand;
-          if (tr > 0) {
+          if (ok) {
             hit = true;
             frm[lane] = make_uint2(f.rec, f.path);
-          } else if (tr < 0) {
+          } else {
             rem = c - 1u;
             W.lst[lane].z = 1u;
-          } else {
-            rem = c;
-            W.lst[lane].y |= kExactNext;
           }
         }
       }
@@ -778,59 +714,34 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         const bool task = t < total;
         const uint32_t s0 = task ? 63u - (uint32_t)__builtin_clzll(sm & (~0ull >> (63u - t))) : 0u;
         const uint32_t o = own[s0];
-        // tp: the task's candidate is the record; tu: its compact test is undecided; tl: past the
-        // limit; tc: a compact test (each candidate is counted once, by its compact test)
-        bool tp = false, tl = false, tu = false, tc = false;
+        bool tp = false, tl = false;
         Found g;
         if (task) {
           const float4 po = lds_ld16(&W.pt[o]);
           const uint4 d = lds_ld16(&W.lst[o]);
-          const uint32_t q = d.x + list_entry(d.y & 0xFFu, d.z + (t - s0));
-          if (t == s0 && (d.y & kExactNext) != 0u) {
-            // the owner's undecided candidate, on its fat entry's exact planes
-            tp = pass_entry(A.fat + (size_t)q * kFatStride4, po.x, po.y, po.z, po.w, g);
-          } else {
-            const float2 xy = W.xy[o];
-            const int tr = cmp_entry(A.cmp + (size_t)q * kCmp4, po.w, xy.x, xy.y, g);
-            tp = tr > 0;
-            tu = tr == 0;
-            tc = true;
-          }
+          tp = pass_entry(A.fat + (size_t)(d.x + list_entry(d.y, d.z + (t - s0))) * kFatStride4, po.x, po.y,
+                          po.z, po.w, g);
           tl = g.rec >= d.w;  // past the limit: the serial scan stops there
           tp = tp && !tl;
-          tu = tu && !tl;
-          tc = tc && !tl;
         }
-        const uint64_t pm = __ballot(tp), lm = __ballot(tl), um = __ballot(tu), cm = __ballot(tc);
-        // the lowest event of each owner's tasks: a passing record (it hands it over), the
-        // limit, or an undecided candidate (tested exactly next; nothing after it counts yet)
+        const uint64_t pm = __ballot(tp), lm = __ballot(tl);
+        // the lowest event of each owner's tasks: a passing record (it hands it over) or the limit
         const uint64_t below = t ? (~0ull >> (64u - t)) : 0ull;  // tasks < t
-        if (tp && ((pm | lm | um) & below & (~0ull << s0)) == 0ull) frm[o] = make_uint2(g.rec, g.path);
+        if (tp && ((pm | lm) & below & (~0ull << s0)) == 0ull) frm[o] = make_uint2(g.rec, g.path);
         __builtin_amdgcn_wave_barrier();
         if (owns) {
           const uint32_t k = min(rem, 64u - start);  // this owner's tasks in this batch
-          const uint64_t rng = (k >= 64u ? ~0ull : ((1ull << k) - 1ull)) << start;
-          const uint64_t ev = (pm | lm | um) & rng;
+          const uint64_t ev = (pm | lm) & ((k >= 64u ? ~0ull : ((1ull << k) - 1ull)) << start);
           if (ev) {
             const uint32_t e = (uint32_t)__builtin_ctzll(ev) - start;
-            const bool ps = (pm >> (start + e)) & 1ull, us = (um >> (start + e)) & 1ull;
-            // the compact tests up to the event, the event's own unless it is the limit
-            const uint32_t upto = e + (ps || us ? 1u : 0u);
-            specCand += (uint32_t)__popcll(cm & rng & (upto >= 64u ? ~0ull : (((1ull << upto) - 1ull) << start)));
-            if (us) {
-              rem -= e;
-              W.lst[lane].z += e;
-              W.lst[lane].y |= kExactNext;
-              need = true;
-            } else {
-              hit = hit || ps;
-              need = false;
-            }
+            const bool ps = (pm >> (start + e)) & 1ull;
+            specCand += e + (ps ? 1u : 0u);
+            hit = hit || ps;
+            need = false;
           } else {
-            specCand += (uint32_t)__popcll(cm & rng);
+            specCand += k;
             rem -= k;
             W.lst[lane].z += k;
-            W.lst[lane].y &= 0xFFu;
             need = rem > 0u;
           }
         }
@@ -856,9 +767,6 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         c = (uint32_t)__popc(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
         flim = hit ? frm[lane].x : 0xFFFFFFFFu;
         lds_st16(&W.lst[lane], make_uint4(H0.w + beg, m8, 0u, flim));
-        // (from LDS: not held in VGPRs through the deal)
-        fx = W.xy[lane].x;
-        fy = W.xy[lane].y;
         fe = H0.w + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
         if constexpr (kPair) fe2 = H0.w + beg + list_entry(m8, 1u);
       }
@@ -2453,7 +2361,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 #ifdef IRT_ALL_VARIANTS
 #define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976)
 #else
-#define IRT_VARIANTS(X) X(6296832) X(6558976) X(36864)
+#define IRT_VARIANTS(X) X(6296832) X(6558976) X(5376) X(36864)
 #endif
 static_assert(kDefaultVariant == 6296832 && (kDefaultVariant | kNoMissBit) == 6558976 && kNoMissBit == OPT_NOMISS,
               "the product build's variant list names the default and its hole-free form");

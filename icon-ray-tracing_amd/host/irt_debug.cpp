@@ -5,7 +5,6 @@
 #include <string.h>
 
 #include "icon_rt_hip_debug.h"
-#include "irt_build.h"
 #include "irt_internal.h"
 
 using namespace irt;
@@ -53,39 +52,6 @@ int irt_debug_scene_build(const irt_icon_cell *cells, size_t n, irt_debug_scene 
     return rc;
   }
   *out = d;
-  return IRT_OK;
-}
-
-int irt_debug_scene_certify(const irt_debug_scene *s, const float *xyz, size_t n, uint64_t *out4) {
-  if (!s || !out4 || (n && !xyz)) return IRT_E_INVALID;
-  const HostScene &S = s->s;
-  uint64_t tests = 0, wrong = 0, undecided = 0, certain = 0;
-  for (size_t k = 0; k < n && S.G > 0; ++k) {
-    const float px = xyz[3 * k], py = xyz[3 * k + 1], pz = xyz[3 * k + 2];
-    uint32_t sub;
-    float X, Y;
-    const uint32_t cell = cubemap_cell_local(px, py, pz, S.G, sub, X, Y);
-    const uint32_t *H = &S.binHdr[(size_t)cell * kBinHdrWords];
-    const uint32_t beg = H[3], end = H[3] + H[7];
-    for (uint32_t q = beg; q < end; ++q) {
-      const float *F = &S.fat[(size_t)q * kFatStride4 * 4];
-      const uint32_t *C = &S.cmp[(size_t)q * kCmp4 * 4];
-      bool pass = true;
-      for (int p = 0; p < 3; ++p)
-        if (eval_plane(F + 4 * p, px, py, pz) > 0.f) pass = false;
-      const float r = sqrtf(px * px + py * py + pz * pz);
-      if (r < F[12] || r > F[13]) continue;  // the radial test decides first, exactly
-      const int t = tri_test(C[4], C[5], C[6], u2f(C[7]), X, Y);
-      ++tests;
-      if (t == 0) ++undecided;
-      else ++certain;
-      if ((t > 0 && !pass) || (t < 0 && pass)) ++wrong;
-    }
-  }
-  out4[0] = tests;
-  out4[1] = wrong;
-  out4[2] = undecided;
-  out4[3] = certain;
   return IRT_OK;
 }
 
@@ -167,7 +133,6 @@ int irt_debug_scene_array(const irt_debug_scene *s, int which, void *dst, size_t
   switch (which) {
     case IRT_DEBUG_ARRAY_BIN_HDR: src = S.binHdr.data(); n = S.binHdr.size() * 4; break;
     case IRT_DEBUG_ARRAY_FAT: src = S.fat.data(); n = S.fat.size() * 4; break;
-    case IRT_DEBUG_ARRAY_CMP: src = S.cmp.data(); n = S.cmp.size() * 4; break;
     case IRT_DEBUG_ARRAY_BLOCKS: src = S.blocks.data(); n = S.blocks.size() * 4; break;
     case IRT_DEBUG_ARRAY_SPH_R: src = S.sphR.data(); n = S.sphR.size() * 4; break;
     case IRT_DEBUG_ARRAY_SPH_OFF: src = S.sphOff.data(); n = S.sphOff.size() * 4; break;

@@ -258,7 +258,6 @@ int build_bins(HostScene &S, int threads) {
   }
   S.binEntries = total;
   S.fat.assign(total * kFatStride4 * 4, 0.f);
-  S.cmp.assign(total * kCmp4 * 4, 0u);
   // pass 2: the fat entries, bin by bin
   parallel_ranges(numGridCells, threads, [&](int, size_t b, size_t e) {
     for (size_t cell = b; cell < e; ++cell) {
@@ -273,10 +272,7 @@ int build_bins(HostScene &S, int threads) {
         for (uint32_t q = S.offsets[cell]; q < S.offsets[cell + 1]; ++q) {
           const uint32_t rec = S.entryRec[q];
           if (!in_bin(S.rng[2 * (size_t)rec], S.rng[2 * (size_t)rec + 1], lo, hi)) continue;
-          fat_entry(rec, S.planes.data(), S.rng.data(), S.meta.data(), &S.fat[at * kFatStride4 * 4]);
-          compact_entry(rec, S.planes.data(), S.rng.data(), S.meta.data(), (uint32_t)cell, S.G,
-                        &S.cmp[at * kCmp4 * 4]);
-          ++at;
+          fat_entry(rec, S.planes.data(), S.rng.data(), S.meta.data(), &S.fat[at++ * kFatStride4 * 4]);
         }
       }
     }
@@ -344,8 +340,7 @@ int locate_bins_host(const HostScene &s, float px, float py, float pz, float &va
   if (s.n == 0 || s.G == 0) return 0;
   const float r = sqrtf(px * px + py * py + pz * pz);
   uint32_t sub = 0;
-  float X, Y;
-  const uint32_t cell = cubemap_cell_local(px, py, pz, s.G, sub, X, Y);
+  const uint32_t cell = cubemap_cell_sub(px, py, pz, s.G, sub);
   const uint32_t *H = &s.binHdr[(size_t)cell * kBinHdrWords];
   const float e[3] = {u2f(H[0]), u2f(H[1]), u2f(H[2])};
   const int b = bin_of(r, e[0], e[1], e[2]);
@@ -369,20 +364,7 @@ int locate_bins_host(const HostScene &s, float px, float py, float pz, float &va
       const float *F = &s.fat[(size_t)(beg + j) * kFatStride4 * 4];
       if (hit && f2u(F[14]) >= best) break;  // the second bin: only lower records
       if (tested) ++*tested;
-      // the kernel's order: the compact entry's certified test, the exact planes only when it
-      // is undecided (both give sample()'s answer)
-      const uint32_t *C = &s.cmp[(size_t)(beg + j) * kCmp4 * 4];
-      if (r < u2f(C[0]) || r > u2f(C[1])) continue;  // ICONGrid.h:184
-      const int t = tri_test(C[4], C[5], C[6], u2f(C[7]), X, Y);
-      if (t < 0) continue;
       float v;
-      if (t > 0) {  // certain: no plane test (a wrong certificate shows against the brute force)
-        v = record_value_host(s, C[2], record_path(C[3], u2f(C[0]), u2f(C[1]), r), r);
-        hit = 1;
-        best = C[2];
-        bestV = v;
-        break;
-      }
       if (test_fat(s, F, px, py, pz, r, v)) {
         hit = 1;
         best = f2u(F[14]);

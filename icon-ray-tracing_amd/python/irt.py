@@ -444,7 +444,7 @@ def setup_frame(cells: np.ndarray, width: int, height: int, camera=None,
 
 # scene arrays the render kernel reads (irt_debug_context_array / irt_debug_scene_array)
 SCENE_ARRAYS = {"bin_hdr": 0, "fat": 1, "blocks": 2, "sph_r": 3, "sph_off": 4, "sph_rec": 5,
-                "sph_bits": 6, "cmp": 7}
+                "sph_bits": 6}
 
 
 def _array(fn, h, name):

@@ -51,10 +51,6 @@ int irt_debug_scene_values(const irt_debug_scene *s, uint32_t rec, float r, floa
 /* Candidate list of the cube-map cell containing direction p. */
 int irt_debug_scene_candidates(const irt_debug_scene *s, irt_vec3f p, uint32_t *records,
                                int capacity);
-/* The compact entries' certified plane test (irt_common.h tri_test) against the exact float
- * planes (ICONGrid.h:197-203), at every point of xyz[3n] for every entry of its cube-map cell
- * whose radial range holds it: out4 = {tests, contradictions (must be 0), undecided, certain}. */
-int irt_debug_scene_certify(const irt_debug_scene *s, const float *xyz, size_t n, uint64_t *out4);
 /* Per-record side planes (3 x vec4) as uploaded. */
 int irt_debug_scene_planes(const irt_debug_scene *s, uint32_t record, float *out12);
 void irt_debug_scene_free(irt_debug_scene *s);
@@ -76,13 +72,12 @@ int irt_debug_intersect_wedge(const float *v24, irt_vec3f p, float *value);
  * only *bytes is set. */
 enum {
   IRT_DEBUG_ARRAY_BIN_HDR = 0,  /* cube-map cell headers, kBinHdrWords u32 each */
-  IRT_DEBUG_ARRAY_FAT = 1,      /* fat candidate entries, 64 B each */
+  IRT_DEBUG_ARRAY_FAT = 1,      /* fat candidate entries, 80 B each */
   IRT_DEBUG_ARRAY_BLOCKS = 2,   /* per-record height/value blocks, 256 B each */
   IRT_DEBUG_ARRAY_SPH_R = 3,    /* sphere radii (f32) */
   IRT_DEBUG_ARRAY_SPH_OFF = 4,  /* CSR offsets (u32) */
   IRT_DEBUG_ARRAY_SPH_REC = 5,  /* (record, numLayers) u32 pairs */
-  IRT_DEBUG_ARRAY_SPH_BITS = 6, /* radius hash bitmap (u32) */
-  IRT_DEBUG_ARRAY_CMP = 7       /* compact entries, 32 B each, parallel to the fat entries */
+  IRT_DEBUG_ARRAY_SPH_BITS = 6  /* radius hash bitmap (u32) */
 };
 int irt_debug_context_array(const irt_context *ctx, int which, void *dst, size_t capacity,
                             size_t *bytes);

@@ -602,34 +602,3 @@ def test_atanf_reduction_as_one_division_matches_glibc(tmp_path):
     lib.check.restype = ctypes.c_long
     lib.check.argtypes = [ctypes.c_uint32, ctypes.c_long]
     assert lib.check(61, 4_000_000) == 0
-
-
-@pytest.mark.parametrize("grid", ["r2b04", "r2b04_terrain", "r2b06", "r1b00"])
-def test_compact_entries_never_contradict_the_exact_planes(grid):
-    """The compact entries' certified plane test (irt_common.h tri_test over the triangle and
-    margin irt_build.h compact_triangle stores) against sample()'s float plane tests
-    (ICONGrid.h:197-203) for every entry of the point's cube-map cell: a certain answer is
-    never wrong -- at random points and at points on record corners, edges and layer
-    boundaries (locator_points) -- and random points are undecided (exact planes) rarely."""
-    import ctypes as C
-    from helpers import locator_points
-    cells = {"r2b04": lambda: irt.synth_grid(2, 4, 47),
-             "r2b04_terrain": lambda: irt.synth_grid(2, 4, 90, terrain=4000.0),
-             "r2b06": lambda: irt.synth_grid(2, 6, 20),
-             "r1b00": lambda: irt.synth_grid(1, 0, 4)}[grid]()
-    L = irt.lib()
-    L.irt_debug_scene_certify.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
-    D = irt.DebugScene(cells)
-    rng = np.random.default_rng(5)
-    d = rng.normal(size=(30000, 3))
-    d /= np.linalg.norm(d, axis=1, keepdims=True)
-    top, bot = float(cells["height"].max()), float(cells["height"][:, 0].min())
-    rnd = (d * rng.uniform(bot, top, (30000, 1))).astype(np.float32)
-    edge = locator_points(cells, 3, n_random=0, n_cols=300)
-    for pts, name in ((rnd, "random"), (edge, "boundaries")):
-        out = np.zeros(4, np.uint64)
-        assert L.irt_debug_scene_certify(D._h, pts.ctypes.data, len(pts), out.ctypes.data) == 0
-        tests, wrong, undecided, certain = (int(v) for v in out)
-        assert tests > 1000 and wrong == 0, (name, out)
-        if name == "random" and grid != "r1b00":  # R1B00's triangles span many cells: exact
-            assert undecided < 0.005 * tests, (name, out)
