@@ -137,9 +137,6 @@ struct irt_context {
   // ramp, 2^coopMaxLg without (IRT_COOP_MAXLG, IRT_COOP_RAMP; profiles/r02e_dist/)
   int coopMaxLg = 0;
   int coopRamp = 1;
-  // a single frame's last splitTail one-wave workgroups render half packets (irt_kernels.h
-  // RenderArgs::splitFrom); 0: none
-  int splitTail = 0;
   int probeExit = 0;           // IRT_PROBE_EXIT (measurement only, RenderArgs::probeExit)
   uint32_t *wgTrace = nullptr; // irt_debug_set_wg_trace (measurement only, RenderArgs::wgTrace)
   // chained progressive frames (RenderArgs::chain; IRT_CHAIN=0 / irt_debug_set_chain: the
@@ -487,15 +484,6 @@ int ensure_grid(irt_context *c) {
   return IRT_OK;
 }
 
-
-// A single frame's last packets as half packets (RenderArgs::splitFrom): the one-wave-workgroup
-// grid launch of one frame, its last c->splitTail workgroups (a multiple of 8), each rendered by
-// two workgroups of 32 rays.  Returns the number of packets split (0: none).
-static size_t split_workgroups(const irt_context *c, size_t frameWG, int numFrames, int wgPerBlock) {
-  if (numFrames != 1 || wgPerBlock != 4 || c->splitTail <= 0 || c->probeExit != 0) return 0;
-  return std::min(frameWG, (size_t)c->splitTail) & ~(size_t)7;
-}
-
 int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int packed,
                 int tileBegin, int tileStride, uint32_t *fb, irt_vec4f *accum, int *numTilesOut,
                 void *stream, int numFrames = 1, const int32_t *tileList = nullptr,
@@ -652,15 +640,10 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
                                 : render_queue_wgs(A, c->variant, c->numCU, numTiles * 16 * numFrames);
     c->lastQueueWG = queueWG;
   }
-  // a single frame's last workgroups as half packets (one-wave workgroups, grid launch)
-  const int wgPerBlock = render_wg_per_block(A, c->variant);
-  const size_t frameWG = (size_t)numTiles * 16 * (size_t)wgPerBlock;
-  const size_t splitWG = queued ? 0 : split_workgroups(c, frameWG, numFrames, wgPerBlock);
-  A.splitFrom = splitWG ? (uint32_t)(frameWG - splitWG) : ~0u;
   // workgroups of this launch: 16 per 64x64 tile, x4 for the one-wave-workgroup variants
-  // (irt_render.hip OPT_WAVEWG, bit 4194304), per frame, + one per split packet; a persistent
-  // launch's resident ones
-  const size_t numWG = queued ? (size_t)queueWG : frameWG * (size_t)numFrames + splitWG;
+  // (irt_render.hip OPT_WAVEWG, bit 4194304), per frame; a persistent launch's resident ones
+  const size_t numWG = queued ? (size_t)queueWG
+                              : (size_t)numTiles * 16 * (size_t)render_wg_per_block(A, c->variant) * (size_t)numFrames;
   // Per-workgroup counts need kSlots x 32 B of pinned host memory per workgroup and frame
   // (1 KiB): a launch past kWgCountsMax workgroups (a large progressive batch) counts through
   // the device-atomic block instead, for that launch only.
@@ -1106,7 +1089,6 @@ int irt_create_end(irt_context *c) {
   if (const char *e = getenv("IRT_WG_COUNTS_MAX")) c->wgCountsMax = (size_t)std::max(0LL, atoll(e));
   if (const char *e = getenv("IRT_COOP_MAXLG")) c->coopMaxLg = std::min(6, std::max(0, atoi(e)));
   if (const char *e = getenv("IRT_COOP_RAMP")) c->coopRamp = std::min(6, std::max(0, atoi(e)));
-  if (const char *e = getenv("IRT_SPLIT_TAIL")) c->splitTail = std::max(0, atoi(e));
   if (const char *e = getenv("IRT_PROBE_EXIT")) c->probeExit = atoi(e);
   if (const char *e = getenv("IRT_QUEUE")) c->queueOn = atoi(e) != 0 && render_queue_compiled();
   if (const char *e = getenv("IRT_QUEUE_WGS")) c->queuePerCU = std::max(0, atoi(e));
@@ -1883,18 +1865,7 @@ extern "C" long long irt_debug_launch_workgroups(const irt_context *c, int numTi
   }
   RenderArgs A;
   memset(&A, 0, sizeof(A));  // the user-geometry sphere path (sampler 0, accelMode 0)
-  const int per = render_wg_per_block(A, c->variant);
-  const size_t frameWG = (size_t)numTiles * 16 * per;
-  return (long long)(frameWG * numFrames + split_workgroups(c, frameWG, numFrames, per));
-}
-
-extern "C" int irt_debug_set_split_tail(irt_context *c, int workgroups) {
-  if (!c || workgroups < 0) {
-    set_error("irt_debug_set_split_tail: bad argument");
-    return IRT_E_INVALID;
-  }
-  c->splitTail = workgroups;
-  return IRT_OK;
+  return (long long)numTiles * 16 * render_wg_per_block(A, c->variant) * numFrames;
 }
 
 extern "C" int irt_debug_set_chain(irt_context *c, int on) {

@@ -120,10 +120,6 @@ struct RenderArgs {
   // writes {start, end} (s_memrealtime, 100 MHz, low 32 bits), HW_ID and XCC_ID to
   // wgTrace[4b..4b+3] -- when the machine is idle at a launch's ramp and tail
   uint32_t *wgTrace;
-  // a single frame's tail (one-wave workgroups, numSamples == 1): workgroups from splitFrom on
-  // (a multiple of 8) render half packets, 32 rays each, two per packet of the launch's last
-  // packets, so the launch's last waves are shorter (irt_render.hip k_render); ~0u: none
-  uint32_t splitFrom;
 };
 // a persistent launch's queue words (irt_render.hip queue_take): 8 per-XCD counters and the
 // done count, each on its own 128-B line

@@ -1495,8 +1495,7 @@ template <int OPT>
 __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
                                                   const float *s_th, int4 *s_dda, float4 *s_entry,
                                                   float4 *s_acc, CoopWave &W, ScanWave *SW, const uint2 *jmp,
-                                                  int tid, int accumID, uint32_t blk, int pwave, int frame,
-                                                  int half = -1) {
+                                                  int tid, int accumID, uint32_t blk, int pwave, int frame) {
   // At 5+ waves/SIMD the pixel's output addresses are recomputed where they are used (from the
   // workgroup's uniform block index), not held in VGPRs through the rounds: a progressive
   // batch's sample slot (k_accumulate reads it) and the frame index.  (At 4 waves there is
@@ -1515,7 +1514,6 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     if constexpr (!kRecompute) return ptid;
     int lane = (int)__lane_id();
     asm volatile("" : "+v"(lane));  // not CSE'd with the pixel's coordinates at the ray's start
-    if (half >= 0) lane = (opaque_u(half) << 5) | (lane & 31);  // a half packet (k_render)
     return (opaque_u(pwave) << 6) | lane;
   };
   const bool toSample = A.numSamples > 1 && !A.chain;
@@ -2092,18 +2090,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   // (OPT_WAVEWG2: two-wave workgroups, workgroup i the waves 2 ((i >> 3) & 1) + {0, 1} of block
   // ((i >> 4) << 3) | (i & 7))
   constexpr uint32_t kNwb = 4 / kWpg;  // workgroups per block
-  // A single frame's tail (A.splitFrom): physical workgroup splitFrom + j renders half `half` of
-  // logical workgroup splitFrom + (((j >> 4) << 3) | (j & 7)) -- its packet's rows 4 half .. 4 half
-  // + 3, 32 rays on lanes 0-31 -- so a packet's two halves run on one XCD (j and j + 8).
-  uint32_t bx = blockIdx.x;
-  int half = -1;
-  if constexpr (wavewg) {
-    if (bx >= A.splitFrom) {
-      const uint32_t j = bx - A.splitFrom;
-      half = (int)((j >> 3) & 1u);
-      bx = A.splitFrom + (((j >> 4) << 3) | (j & 7u));
-    }
-  }
+  const uint32_t bx = blockIdx.x;
   const uint32_t wg = split ? (((bx >> 3) / kNwb) << 3) | (bx & 7u) : bx;
   const int wwave = split ? (int)(((bx >> 3) % kNwb) * kWpg) : 0;  // the block's first wave in this workgroup
   const int ptid = split ? wwave * 64 + tid : tid;
@@ -2171,13 +2158,12 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
                                pblk, pw, frame);
         TL.flush_coop();  // this packet's counts (nothing carried from packet to packet)
       } else {
-        Pixel ppx = pixel_of(A, pblk, pw * 64 + (half < 0 ? (ltid & 63) : (half << 5) | (ltid & 31)));
-        if (half >= 0) ppx.active = ppx.active && (ltid & 63) < 32;
+        const Pixel ppx = pixel_of(A, pblk, pw * 64 + (ltid & 63));
         launched += (uint32_t)__popcll(__ballot(ppx.active));
         T.frame = frame;
         render_pixel_coop<OPT>(A, T, ppx, th_p, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
                                &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, cam_accum_id(A, frame),
-                               pblk, pw, frame, half);
+                               pblk, pw, frame);
         if (A.chain && frame < A.numSamples - 1 && frame != A.chainWithhold) {
           // chained frames: this wave's pixels are written through; tell frame + 1's wave
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2454,8 +2440,7 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(numBlocks), dim3(256), 0, s, A);
     numBlocks = A.numTiles * 16;
   } else {
-    const int split = threads == 64 && A.splitFrom != ~0u ? numBlocks * 4 - (int)A.splitFrom : 0;
-    hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads) + split, A.numSamples), dim3(threads), 0, s, A);
+    hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads), A.numSamples), dim3(threads), 0, s, A);
   }
   // progressive batch: the lerp chain over the frames' samples (chained frames lerp in k_render)
   if (A.numSamples > 1 && !A.chain) hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);

@@ -580,12 +580,6 @@ class Context:
         L.irt_debug_set_chain_fault.argtypes = [C.c_void_p, C.c_uint32, C.c_int]
         _check(L.irt_debug_set_chain_fault(self._h, spins, withhold_frame), "irt_debug_set_chain_fault")
 
-    def set_split_tail(self, workgroups: int):
-        """A single frame's last `workgroups` packets rendered as half packets (0: off)."""
-        L = lib()
-        L.irt_debug_set_split_tail.argtypes = [C.c_void_p, C.c_int]
-        _check(L.irt_debug_set_split_tail(self._h, workgroups), "irt_debug_set_split_tail")
-
     def launch_workgroups(self, num_tiles: int, frames: int = 1) -> int:
         """Workgroups of one launch of num_tiles tiles x frames (the wg-trace buffer needs 4
         u32 per workgroup)."""

@@ -165,11 +165,6 @@ int irt_debug_chain_errors(irt_context *ctx);
  * and the waves of frame `withholdFrame` of every chained launch (-1: none) never publish, so
  * frame withholdFrame + 1's waves time out. */
 int irt_debug_set_chain_fault(irt_context *ctx, uint32_t spins, int withholdFrame);
-/* A single frame's tail in half packets (IRT_SPLIT_TAIL): a one-frame launch of the one-wave-
- * workgroup kernel renders its last `workgroups` packets (rounded down to a multiple of 8) with
- * two workgroups of 32 rays each instead of one of 64, so the launch's last waves are shorter.
- * 0: off.  Frames and counts are unchanged. */
-int irt_debug_set_split_tail(irt_context *ctx, int workgroups);
 
 #ifdef __cplusplus
 }
