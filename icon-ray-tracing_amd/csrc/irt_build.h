@@ -427,27 +427,15 @@ IRT_HD int cell_candidates(const E &en, int n, float *cand, double &rmin, double
 //   [4..7]   cumulative ends of bins 0..3 (relative to base)
 //   [8..23]  per sub-cell s (kSub x kSub, s = sj*kSub + si): byte k = which of the first
 //            kMaskCand candidates of bin k can reach sub-cell s
-//   [24..31] per sub-cell s, the 16-bit field s (word kHdrLowWord + s/2 = 24 + s/2, the low half
-//            for even s):
-//            min(65535, float_key(f) - lowKey), f the lowest bottom height height[0] among the
-//            candidates a point of sub-cell s is tested against, in every bin (the masked ones
-//            and every one past the first kMaskCand); lowKey = float_key of the scene's lowest
-//            height[0] (scene_low_key).  A point with float_key(r) < lowKey + field lies below
-//            every one of them: no candidate can hold it (sample()'s r >= height[0],
-//            ICONGrid.h:184), so the kernel's raygen skips the scan (kernels with holes only;
-//            irt_render.hip locate_wave).  65535 with no candidate at all.
-// The kernel loads words 0..7, word 8+s and (scenes with holes) word 24+s/2 from the same line.
-// (IRT_SUBCELLS=2: 2 x 2 sub-cells, words 8..11 and 12..13 of a 64-B header.)
+//   [24..31] 0
+// The kernel loads words 0..7 and word 8+s from the same line.
 //
 // Fills every word but the base from a cell's n entries (in record order: bottom/top
 // heights and sub-cell masks) and its ne edges; returns the cell's number of fat entries.
 template <class E>
-IRT_HD uint32_t cell_header(const E &en, int n, const float *edges, int ne, uint32_t lowKey, uint32_t *H) {
-  constexpr int kS = kSub * kSub;
+IRT_HD uint32_t cell_header(const E &en, int n, const float *edges, int ne, uint32_t *H) {
   for (int w = 0; w < kBinHdrWords; ++w) H[w] = 0u;
   for (int k = 0; k < kMaxEdges; ++k) H[k] = f2u(k < ne ? edges[k] : __builtin_inff());
-  uint32_t low[kS];
-  for (int s = 0; s < kS; ++s) low[s] = 0xFFFFFFFFu;
   uint32_t cum = 0;
   for (int k = 0; k <= kMaxEdges; ++k) {
     if (k <= ne) {
@@ -455,12 +443,10 @@ IRT_HD uint32_t cell_header(const E &en, int n, const float *edges, int ne, uint
       int j = 0;
       for (int e = 0; e < n; ++e) {
         if (!in_bin(en.h0(e), en.hN(e), lo, hi)) continue;
-        const uint32_t sm = j < kMaskCand ? en.sub(e) : 0xFFFFFFFFu;  // past kMaskCand: every sub-cell
-        const uint32_t key = float_key(en.h0(e));
-        for (int s = 0; s < kS; ++s) {
-          if (!((sm >> s) & 1u)) continue;
-          if (j < kMaskCand) H[8 + s] |= 1u << (8 * k + j);
-          if (key < low[s]) low[s] = key;
+        if (j < kMaskCand) {
+          const uint32_t sm = en.sub(e);
+          for (int s = 0; s < kSub * kSub; ++s)
+            if ((sm >> s) & 1u) H[8 + s] |= 1u << (8 * k + j);
         }
         ++j;
         ++cum;
@@ -468,18 +454,7 @@ IRT_HD uint32_t cell_header(const E &en, int n, const float *edges, int ne, uint
     }
     H[4 + k] = cum;
   }
-  for (int s = 0; s < kS; ++s) {
-    const uint32_t d = low[s] == 0xFFFFFFFFu || low[s] - lowKey > 65535u ? 65535u : low[s] - lowKey;
-    H[kHdrLowWord + s / 2] |= d << (16 * (s & 1));
-  }
   return cum;
-}
-
-// The scene's lowKey for cell_header: the least float_key(height[0]) over every record (so every
-// candidate's bottom lies at or above it); 0xFFFFFFFF for no record.
-IRT_HD uint32_t scene_low_key(uint32_t key, float h0) {
-  const uint32_t k = float_key(h0);
-  return k < key ? k : key;
 }
 
 // One fat entry (kFat4 float4, irt_common.h) of record i.

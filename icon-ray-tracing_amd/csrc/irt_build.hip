@@ -240,7 +240,7 @@ __global__ void k_cell_edges(const uint32_t *offsets, uint32_t numCells, const u
 }
 
 __global__ void k_cell_header(const uint32_t *offsets, uint32_t numCells, const unsigned long long *vals,
-                              const float2 *rng, const float4 *edges, uint32_t lowKey, uint32_t *hdr,
+                              const float2 *rng, const float4 *edges, uint32_t *hdr,
                               uint64_t *cellCount) {
   for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < numCells; c += gridDim.x * blockDim.x) {
     const uint32_t q0 = offsets[c], n = offsets[c + 1] - q0;
@@ -248,7 +248,7 @@ __global__ void k_cell_header(const uint32_t *offsets, uint32_t numCells, const 
     const float4 E = edges[c];
     const float e[kMaxEdges] = {E.x, E.y, E.z};
     uint32_t H[kBinHdrWords];
-    cellCount[c] = cell_header(en, (int)n, e, (int)__float_as_uint(E.w), lowKey, H);
+    cellCount[c] = cell_header(en, (int)n, e, (int)__float_as_uint(E.w), H);
     uint4 *out = reinterpret_cast<uint4 *>(hdr + (size_t)c * kBinHdrWords);
     for (int k = 0; k < kBinHdrWords / 4; ++k) out[k] = make_uint4(H[4 * k], H[4 * k + 1], H[4 * k + 2], H[4 * k + 3]);
   }
@@ -364,7 +364,7 @@ struct StageClock {
 };
 
 int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_t n, size_t numRuns,
-                       int G, uint32_t lowKey, hipStream_t s, DeviceScene &out) {
+                       int G, hipStream_t s, DeviceScene &out) {
   out = DeviceScene();
   Scratch S;
   StageClock clk;
@@ -544,7 +544,7 @@ int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_
   BHIP(hipMemsetAsync(cellCount + numCells, 0, sizeof(uint64_t), s));
   BHIP(hipMalloc((void **)&out.binHdr, (size_t)numCells * kBinHdrWords * sizeof(uint32_t)));
   out.bytes += (size_t)numCells * kBinHdrWords * sizeof(uint32_t);
-  hipLaunchKernelGGL(k_cell_header, dim3(nc), dim3(64), 0, s, offsets, numCells, pv2, rng, edges, lowKey,
+  hipLaunchKernelGGL(k_cell_header, dim3(nc), dim3(64), 0, s, offsets, numCells, pv2, rng, edges,
                      reinterpret_cast<uint32_t *>(out.binHdr), cellCount);
   BHIP(hipGetLastError());
   if ((rc = exclusive_sum(cellCount, cellBase, numCells + 1, s, S))) return rc;

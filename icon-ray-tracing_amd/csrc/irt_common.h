@@ -383,10 +383,8 @@ constexpr int kHV = 64;
 // lowest-index answer (deviceCode.cu:119-122).
 constexpr int kMaxEdges = 3;
 // Cell header (irt_build.h): {e0, e1, e2, base} {end0, end1, end2, end3}, then the sub-cell
-// candidate masks and the sub-cells' lowest-bottom fields: 128 B per cell (64 B with 2 x 2
-// sub-cells)
+// candidate masks: 128 B per cell (64 B with 2 x 2 sub-cells)
 constexpr int kBinHdrWords = 8 + kSubCells * kSubCells <= 16 ? 16 : 32;
-constexpr int kHdrLowWord = 8 + kSubCells * kSubCells;  // the sub-cells' lowest-bottom fields (irt_build.h)
 IRT_HD int bin_of(float r, float e0, float e1, float e2) {
   return (e0 < r ? 1 : 0) + (e1 < r ? 1 : 0) + (e2 < r ? 1 : 0);
 }

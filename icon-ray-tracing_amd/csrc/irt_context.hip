@@ -184,7 +184,6 @@ struct irt_context {
   // in one cooperative round (irt_render.hip Tracer::kMiss).  A scene without holes runs
   // the variant without it (OPT_NOMISS: 2-3 % faster where nearly every sample is located).
   float bottomMin = INFINITY, bottomMax = -INFINITY;
-  uint32_t lowKey = 0xFFFFFFFFu;  // the headers' lowest-bottom base (irt_build.h scene_low_key)
   bool voids = false;
   bool variantFixed = false;  // IRT_RENDER_VARIANT chose the variant
   irt_icon_cell *d_cells = nullptr;  // freed once the scene is built
@@ -599,7 +598,6 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.binHdr = c->d_binHdr;
   A.fat = c->d_fat;
   A.blocks = c->d_blocks;
-  A.lowKey = c->lowKey;
   A.numSph = c->numSph;
   A.sphR = c->d_sphR;
   A.sphOff = c->d_sphOff;
@@ -907,7 +905,6 @@ int append_chunk(irt_context *c, const irt_icon_cell *cells, size_t n, float *tr
     size_t runs = 0, bad = SIZE_MAX;
     std::vector<irt_context::Sphere> sph;
     float bottomMin = INFINITY, bottomMax = -INFINITY;  // height[0] of the columns' first records
-    uint32_t lowKey = 0xFFFFFFFFu;                      // irt_build.h scene_low_key
     bool gap = false;  // a record that does not continue its column (or holds no radius)
   };
   std::vector<Part> part(threads);
@@ -941,7 +938,6 @@ int append_chunk(irt_context *c, const irt_icon_cell *cells, size_t n, float *tr
         P.gap = true;
       }
       if (!(x.height[0] <= x.height[x.numLayers])) P.gap = true;
-      P.lowKey = scene_low_key(P.lowKey, x.height[0]);
       if (x.height[0] == x.height[x.numLayers])  // a sphere record
         P.sph.push_back({x.height[0], (uint32_t)(base + i), x.numLayers});
     }
@@ -969,7 +965,6 @@ int append_chunk(irt_context *c, const irt_icon_cell *cells, size_t n, float *tr
     c->sph.insert(c->sph.end(), P.sph.begin(), P.sph.end());
     c->bottomMin = std::min(c->bottomMin, P.bottomMin);
     c->bottomMax = std::max(c->bottomMax, P.bottomMax);
-    c->lowKey = std::min(c->lowKey, P.lowKey);
     c->voids = c->voids || P.gap;
   }
   IRT_HIP(hipSetDevice(c->device));
@@ -1025,7 +1020,7 @@ int irt_create_end(irt_context *c) {
   c->G = locator_resolution(c->numRuns);
   // the scene build on the device (irt_build.hip)
   DeviceScene D;
-  int rc = build_scene_device(c->d_cells, c->d_trig, numCells, c->numRuns, c->G, c->lowKey, c->stream, D);
+  int rc = build_scene_device(c->d_cells, c->d_trig, numCells, c->numRuns, c->G, c->stream, D);
   c->d_blocks = D.blocks;
   c->d_meta = D.meta;
   c->d_binHdr = D.binHdr;

@@ -29,7 +29,6 @@ struct HostScene {
   std::vector<uint32_t> meta;     // n: record_meta (numLayers, coarse flag, quantised keys)
   std::vector<float> blocks;      // n * kBlk4 * 4: height/value blocks
   int G = 0;                      // cube-map cells per face edge
-  uint32_t lowKey = 0xFFFFFFFFu;  // scene_low_key over every record's height[0] (irt_build.h)
   std::vector<uint32_t> offsets;  // 6*G*G + 1 CSR offsets
   std::vector<uint32_t> entryRec; // candidate lists (each sorted by record index) ...
   std::vector<uint32_t> entrySub; // ... and each entry's sub-cell mask

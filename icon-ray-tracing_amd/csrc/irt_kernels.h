@@ -57,13 +57,11 @@ struct RenderArgs {
   // workgroups): kCounterBuckets x 8 counters, workgroup w adding into bucket w % 64 (one line
   // would serialise every workgroup's adds), summed into counters[0..4] by k_stats_out
   unsigned long long *counterBuckets;
-  // The binned locator (irt_common.h): per cube-map cell a 128-B header, 64-B fat entries,
-  // per-record height/value blocks; lowKey: the headers' lowest-bottom base (irt_build.h
-  // cell_header), which the raygen of scenes with holes compares radii against.
+  // The binned locator (irt_common.h): per cube-map cell a 32-B header, fat entries,
+  // per-record height/value blocks.
   const uint4 *binHdr;
   const float4 *fat;
   const float4 *blocks;
-  uint32_t lowKey;
   // zero-thickness records (spheres, host/irt_scene.cpp): sorted distinct radii, CSR into
   // (record, numLayers) pairs, and the radius hash bitmap (kSphBitWords words)
   uint32_t numSph;
@@ -193,9 +191,8 @@ struct DeviceScene {
   float4 *fat = nullptr;
   size_t entries = 0, binEntries = 0, bigCells = 0, bytes = 0;
 };
-// lowKey: irt_build.h scene_low_key over every record's height[0]
 int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_t n, size_t numRuns,
-                       int G, uint32_t lowKey, hipStream_t s, DeviceScene &out);
+                       int G, hipStream_t s, DeviceScene &out);
 void launch_unpack(const uint32_t *gathered, int numRanks, int maxTiles, int W, int H,
                    uint32_t *fb, hipStream_t s, const int32_t *table = nullptr);
 

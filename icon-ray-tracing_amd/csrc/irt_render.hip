@@ -526,9 +526,6 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // radial bin edge (the two-bin scan) take locate_hdr's serial path.
   static constexpr bool kWaveScan = kCoop && (OPT & (OPT_WEDGE | OPT_GRID | OPT_SCAN1)) == 0;
   static constexpr bool kPair = kWaveScan && (OPT & OPT_PAIR) != 0;
-  // scenes with holes (the miss-mode kernels): a sample below the lowest bottom of its sub-cell's
-  // candidates skips the candidate scan (the voids under convert_icon's land columns)
-  static constexpr bool kLowSkip = kWaveScan && (OPT & (OPT_NOMISS | OPT_HDRLDS)) == 0;
   __device__ __forceinline__ static bool entry_passes(const float4 &a0, const float4 &a1, const float4 &a2,
                                                      const float4 &am, float px, float py, float pz, float r) {
     return !(r < am.x || r > am.y) && !(dot3(px, py, pz, a0.x, a0.y, a0.z) - a0.w > 0.f) &&
@@ -616,7 +613,6 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     bool hit = false, edge = false;
     uint4 H0 = make_uint4(0u, 0u, 0u, 0u), H1 = H0;
     uint32_t M = 0u, cell = 0u, sub = 0u;
-    uint32_t L = 0u;   // kLowSkip: the header word with the sub-cell's lowest-bottom field
     uint32_t tv = 0u;  // OPT_NEXTHDR's loaded word, consumed after the scan
     uint32_t fe2 = 0u; // OPT_PAIR: the pass's second candidate entry
     if constexpr ((OPT & OPT_HDRLDS) != 0) {
@@ -631,7 +627,6 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         H0 = Hc[0];
         H1 = Hc[1];
         M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
-        if constexpr (kLowSkip) L = reinterpret_cast<const uint32_t *>(Hc)[kHdrLowWord + (sub >> 1)];
       }
       if constexpr ((OPT & OPT_NEXTHDR) != 0) {
         // issued after this sample's header words: waiting for them leaves it in flight
@@ -650,16 +645,6 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       const uint32_t n = end - beg;
       const uint32_t m8 = (M >> (8 * b)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
       c = (uint32_t)__popc(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
-      if constexpr (kLowSkip) {
-        // below the bottom of every candidate of the sub-cell, in every bin (irt_build.h
-        // cell_header): none can hold the point -- the scan's answer without the scan, its c
-        // tests counted as the serial scan makes them (an edge sample keeps its two passes)
-        const uint32_t low = (L >> ((sub & 1u) << 4)) & 0xFFFFu;
-        if (!edge && float_key(r) < A.lowKey + low) {
-          specCand += c;
-          c = 0u;
-        }
-      }
       lds_st16(&W.pt[lane], make_float4(px, py, pz, r));
       lds_st16(&W.lst[lane], make_uint4(H0.w + beg, m8, 0u, 0xFFFFFFFFu));
       fe = H0.w + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);

@@ -120,8 +120,6 @@ int build_scene(const irt_icon_cell *cells, size_t n, HostScene &S, int threads)
     }
   });
 
-  for (size_t i = 0; i < n; ++i) S.lowKey = scene_low_key(S.lowKey, S.rng[2 * i]);
-
   // --- columns: runs of consecutive records with identical corners
   std::vector<size_t> runStart;
   for (size_t i = 0; i < n; ++i)
@@ -249,7 +247,7 @@ int build_bins(HostScene &S, int threads) {
       const int nc = cell_candidates(en, (int)n, cand.data(), rmin, rmax);
       float edges[kMaxEdges] = {0.f, 0.f, 0.f};
       const int ne = choose_edges(en, (int)n, cand.data(), nc, rmin, rmax, edges);
-      cellCount[cell + 1] = cell_header(en, (int)n, edges, ne, S.lowKey, &S.binHdr[cell * kBinHdrWords]);
+      cellCount[cell + 1] = cell_header(en, (int)n, edges, ne, &S.binHdr[cell * kBinHdrWords]);
     }
   });
   for (uint32_t k = 0; k < numGridCells; ++k) cellCount[k + 1] += cellCount[k];
