@@ -139,7 +139,10 @@ constexpr int kCnt = 8;
 // finished wave frees its slot at once instead of when its 256-pixel block's slowest wave does;
 // against 5376 (four-wave workgroups) with chained frames C3 -1.7 %, C3s -5.8 %, C4 -1.1 %, C5
 // -2.3 %, a single C3 frame -1.1 % (profiles/r04p_ab/)
-constexpr int kDefaultVariant = 6296832;
+// Round 5: + OPT_DMATAB (67108864: the prologue's LCG-jump and logf tables by LDS-DMA, with no
+// wait before the ray generation): against 6296832 C3 -1.2 %, one frame per launch -1.7 %, C5
+// -2.5 %, C3t -1.2 %, C3s -0.3 % (profiles/r05k_dmatab/)
+constexpr int kDefaultVariant = 73405696;
 // Round 5: the raygen's miss mode (woodcock_wave) is on in the default variant; a scene
 // without holes (every column starting at the same radius, no gaps inside columns) runs it
 // without (bit 262144, OPT_NOMISS): C3 -2.3 %, while convert_icon terrain (voids under land)

@@ -64,6 +64,8 @@ enum : int {
                             // sample's header, so that the next round's header read hits L2
   OPT_WAVEWG2 = 536870912,  // (A/B, with OPT_LEAN) two-wave workgroups: a block's packets in pairs
                             // (each pair sharing a CU's L1), a slot freed per two waves
+  OPT_DMATAB = 67108864,  // (A/B) one-wave workgroups: the LCG jump and logf tables loaded into
+                          // LDS by LDS-DMA, not waited for in the prologue (k_render)
   OPT_NOMISS = 262144,  // (A/B) the user-geometry cooperative loop without its miss mode:
                         // every sample outside all cells ends its ray's round (round 4's
                         // default); convert_icon terrain leaves voids under land, where such runs
@@ -189,6 +191,13 @@ struct TimeAccOn {
 // (RenderArgs::frameCams, irt_render_sequence) that frame's words, read through the constant
 // address space (scalar loads: uniform values, written by the host before the launch).
 typedef const __attribute__((address_space(4))) fvec4 *CamWords;
+// a uniform word of a host-written table (tile lists, block orders) through the scalar unit: a
+// vector load's wait would also wait for every vector load before it (the counter retires in
+// order), the prologue's LDS-DMA table loads included
+typedef const __attribute__((address_space(4))) uint32_t *ScalarWords;
+__device__ __forceinline__ uint32_t scalar_word(const void *table, uint32_t i) {
+  return ((ScalarWords)table)[i];
+}
 __device__ __forceinline__ float4 cam_word(const RenderArgs &A, int frame, int k) {
   return __builtin_bit_cast(float4, ((CamWords)A.frameCams)[4 * frame + k]);
 }
@@ -1080,7 +1089,7 @@ __device__ __forceinline__ Pixel pixel_of(const RenderArgs &A, uint32_t blkU, in
   const int wave = tid >> 6, lane = tid & 63;
   const int lx = ((sub & 3) << 4) | ((wave & 1) << 3) | (lane & 7);
   const int ly = ((sub >> 2) << 4) | ((wave >> 1) << 3) | (lane >> 3);
-  const int tileId = !A.tileList ? A.tileBegin + k * A.tileStride : (k < A.numTiles ? A.tileList[k] : 0);
+  const int tileId = !A.tileList ? A.tileBegin + k * A.tileStride : (k < A.numTiles ? (int)scalar_word(A.tileList, (uint32_t)k) : 0);
   const int tx = tileId % A.tilesX, ty = tileId / A.tilesX;
   Pixel p;
   p.x = tx * 64 + lx;
@@ -2043,9 +2052,25 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   if (A.probeExit == 1) return;  // measurement only
   uint64_t tStart = 0;
   if constexpr ((OPT & OPT_TIMING) != 0) tStart = __builtin_amdgcn_s_memtime();
+  // OPT_DMATAB (one-wave workgroups): the LCG jump and logf tables go straight from global
+  // memory into LDS (global_load_lds, 16 B per lane: 1,040 + 256 B), and nothing waits for them
+  // here -- the compiler's LDS-DMA tracking puts the vmcnt wait before their first read, in the
+  // first Woodcock round, so the ray generation and setup overlap the loads (the register path
+  // below waits for two round trips before the first ray is generated)
+  constexpr bool dmaTab = (OPT & OPT_DMATAB) != 0 && kT == 64 && Tracer<OPT>::kCoop;
+  if constexpr (dmaTab) {
+    typedef __attribute__((address_space(3))) void *LdsPtr;
+    const char *jt = reinterpret_cast<const char *>(&kLcgJumpTab.ma[0][0]);
+    static_assert(sizeof(kLcgJumpTab.ma) == kLcgJumps * 8 && kLcgJumps * 8 <= 64 * 16 + 16, "jump table: 65 chunks");
+    __builtin_amdgcn_global_load_lds((const void *)(jt + 16 * tid), (LdsPtr)s_jmp, 16, 0, 0);
+    if (tid == 0)
+      __builtin_amdgcn_global_load_lds((const void *)(jt + 1024), (LdsPtr)(reinterpret_cast<char *>(s_jmp) + 1024), 16, 0, 0);
+    static_assert(sizeof(LogfTab) == 16, "logf table: one chunk per entry");
+    if (tid < 16) __builtin_amdgcn_global_load_lds((const void *)(kLogfTab + tid), (LdsPtr)s_logf, 16, 0, 0);
+  }
   // the prologue's global loads issued together, one wait (not one round trip each)
   const float th = lean ? 0.f : A.srgbTh[tid];
-  const LogfTab lt = kLogfTab[tid & 15];
+  const LogfTab lt = dmaTab ? LogfTab{0.0, 0.0} : kLogfTab[tid & 15];
   uint32_t sph[kSphBitWords / 256];
   if (!lean && A.numSph) {
 #pragma unroll
@@ -2056,15 +2081,15 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   for (int k = 0; k < (kLcgJumps + kT - 1) / kT; ++k) {
     const int j = tid + kT * k;
     jmpv[k] = make_uint2(0u, 0u);
-    if (Tracer<OPT>::kCoop && j < kLcgJumps) jmpv[k] = make_uint2(kLcgJumpTab.ma[j][0], kLcgJumpTab.ma[j][1]);
+    if (!dmaTab && Tracer<OPT>::kCoop && j < kLcgJumps) jmpv[k] = make_uint2(kLcgJumpTab.ma[j][0], kLcgJumpTab.ma[j][1]);
   }
 #pragma unroll
   for (int k = 0; k < (kLcgJumps + kT - 1) / kT; ++k) {
     const int j = tid + kT * k;
-    if (Tracer<OPT>::kCoop && j < kLcgJumps) *reinterpret_cast<uvec2 *>(&s_jmp[j]) = __builtin_bit_cast(uvec2, jmpv[k]);
+    if (!dmaTab && Tracer<OPT>::kCoop && j < kLcgJumps) *reinterpret_cast<uvec2 *>(&s_jmp[j]) = __builtin_bit_cast(uvec2, jmpv[k]);
   }
   if constexpr (!lean) s_th[tid] = th;
-  if (tid < 16) s_logf[tid] = lt;
+  if (!dmaTab && tid < 16) s_logf[tid] = lt;
   if (!lean && A.numSph) {
 #pragma unroll
     for (int k = 0; k < kSphBitWords / 256; ++k) s_sph[tid + 256 * k] = sph[k];
@@ -2077,7 +2102,10 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
 #pragma unroll
     for (int k = 0; k < kGridBitWords / 256; ++k) s_gbits[tid + 256 * k] = A.gridBits[tid + 256 * k];
   }
-  __syncthreads();
+  if constexpr (dmaTab)
+    __builtin_amdgcn_wave_barrier();  // one wave: its LDS writes are ordered; no wait for the DMA
+  else
+    __syncthreads();
   if (A.probeExit == 2) return;  // measurement only
   Tracer<OPT> T{{}, A, s_logf, lean ? A.sphBits : s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
   T.s_gbits = s_gbits;
@@ -2102,7 +2130,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   // grid.y = frame k of a progressive batch (accumID + k), whose colour goes to the sample
   // buffer for k_accumulate; a single frame writes accum/fb directly.  With measured-cost
   // scheduling (irt_context.hip) workgroup b renders block order[b].
-  const uint32_t blk = __builtin_amdgcn_readfirstlane(A.schedOrder ? A.schedOrder[wg] : wg);  // uniform: an SGPR
+  const uint32_t blk = A.schedOrder ? scalar_word(A.schedOrder, wg) : wg;  // uniform: an SGPR
   uint32_t launched = 0u;  // rays of this wave's pixels (uniform)
   bool pxActive = false;   // the one-lane-per-ray kernel's pixel
   if constexpr (Tracer<OPT>::kCoop) {
@@ -2349,7 +2377,9 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 // 1053696 = 5120 | OPT_HDRLDS: the cell headers staged through LDS (profiles/r03s_variants/).
 // 2102272 = 5120 | OPT_LEAN (24 KB of LDS per workgroup), 2102528 the same at 5 waves/SIMD;
 // 8393728 / 8393984 = 5120 / 5376 | OPT_DEALALL (profiles/r03t_regs/); 6296576 / 6296832 =
-// 2102272 / 2102528 | OPT_WAVEWG (one-wave workgroups).  All variants give identical results.
+// 2102272 / 2102528 | OPT_WAVEWG (one-wave workgroups); 73405696 = 6296832 | OPT_DMATAB (the
+// default since round 5), 73667840 its hole-free form (| OPT_NOMISS).  All variants give
+// identical results.
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
@@ -2359,11 +2389,11 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840)
 #else
-#define IRT_VARIANTS(X) X(6296832) X(6558976) X(5376) X(36864)
+#define IRT_VARIANTS(X) X(73405696) X(73667840) X(5376) X(36864)
 #endif
-static_assert(kDefaultVariant == 6296832 && (kDefaultVariant | kNoMissBit) == 6558976 && kNoMissBit == OPT_NOMISS,
+static_assert(kDefaultVariant == 73405696 && (kDefaultVariant | kNoMissBit) == 73667840 && kNoMissBit == OPT_NOMISS,
               "the product build's variant list names the default and its hole-free form");
 
 int render_variants(int *out, int cap) {

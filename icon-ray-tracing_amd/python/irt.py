@@ -33,14 +33,16 @@ MODE_USER_GEOM = 0     # Volume::mode (Params.h:29-31): sample() on the cells (d
 MODE_TRIANGLES = 1     # closest bottom triangle toward the centre (deviceCode.cu:61-76)
 MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
 # The raygen's render variants (irt_render.hip OPT_* bits), all bit-identical: the product
-# library compiles 6296832 (the default since round 4: one-wave workgroups, 5 waves/SIMD; since
-# round 5 with the miss mode, and 6558976 its form without, which hole-free scenes run),
+# library compiles 73405696 (the default: one-wave workgroups since round 4, 5 waves/SIMD; since
+# round 5 with the miss mode and the LDS-DMA prologue tables, and 73667840 its form without the
+# miss mode, which hole-free scenes run),
 # 5376 (256-thread workgroups; the persistent launch's base) and 36864 (per-wave statistics);
 # libicon_rt_hip_all.so (`make VARIANTS=all`) adds the A/B variants: 4096 no waves-per-SIMD
 # floor, 5120 at 4 waves/SIMD, 70656 the one-lane-per-ray Woodcock loop, 136192 per-lane
 # candidate scans, 529408 per-region shader-clock timing (profiles/probe.py), 1053696
 # LDS-staged cell headers, 2102272 / 2102528 less LDS per workgroup, 8393728 / 8393984
-# every candidate dealt out, 6296576 / 6296832 one-wave workgroups, 529664 the timing variant
+# every candidate dealt out, 6296576 / 6296832 one-wave workgroups (6558976 the latter without
+# the miss mode: round 4's and early round 5's defaults), 529664 the timing variant
 # at 5 waves/SIMD, 2102784 the lean-LDS build at 6 waves/SIMD, 33559808 the certified fast
 # lat/lon for the sdda cells (OPT_FASTSPH).
 ALL_LIB_PATH = os.path.join(PKG_DIR, "libicon_rt_hip_all.so")
