@@ -270,7 +270,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // record starts at R + HSURF, convert_icon.cpp:361: nothing covers [R, R + HSURF)) -- at C3t a
   // third of the samples miss, in runs of up to ~280 draws, and without the miss mode every
   // miss cost its ray a round (single-frame launches 1.07 ms against 0.09 ms at C3, a few
-  // waves running ~1 ms: profiles/r05c_c3t/).  Flat grids almost never miss (C3: 707 of 1.01 M
+  // waves running ~1 ms: profiles/r05d_missmode/).  Flat grids almost never miss (C3: 707 of 1.01 M
   // samples).  The kernels with misses everywhere (wedges, grid) start with whole-wave groups.
   static constexpr bool kMiss = kCoop && (OPT & OPT_NOMISS) == 0;
   static constexpr bool kWideStart = (OPT & (OPT_WEDGE | OPT_GRID)) != 0;
@@ -1565,8 +1565,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       return;
     }
     if (boxHit) {
-      inBox = true;
-      T.count(1);
+      inBox = true;  // counted at the ray's end: an LDS add here would wait for the prologue's LDS-DMA
       phase = kRange;
       t0box = t0;
       t1box = t1;
@@ -1948,6 +1947,10 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   // a wave none of whose rays hit the box, so that the publish words advance in frame order and
   // frame f - 1's word covers every earlier frame's stores
   if (chainLate && !chainReady) chain_wait(A, blk, pwave, frame);
+  {
+    const uint64_t ib = __ballot(inBox);  // rays in the box (T.count(1) at the box test)
+    if (ib && __lane_id() == (unsigned)__builtin_ctzll(ib)) atomicAdd(&T.s_cnt[1], (uint32_t)__popcll(ib));
+  }
   if (!inBox) return;
   const int tl = tid_late();
   const float4 c = hit ? lds_ld16(&s_entry[tl]) : make_float4(0.f, 0.f, 0.f, 0.f);
