@@ -2382,7 +2382,8 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 // 8393728 / 8393984 = 5120 / 5376 | OPT_DEALALL (profiles/r03t_regs/); 6296576 / 6296832 =
 // 2102272 / 2102528 | OPT_WAVEWG (one-wave workgroups); 73405696 = 6296832 | OPT_DMATAB (the
 // default since round 5), 73667840 its hole-free form (| OPT_NOMISS).  All variants give
-// identical results.
+// identical results.  73929984 / 74192128: the default / its hole-free form with OPT_TIMING
+// (per-region shader clocks, profiles/probe.py).
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
@@ -2392,7 +2393,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73929984) X(74192128)
 #else
 #define IRT_VARIANTS(X) X(73405696) X(73667840) X(5376) X(36864)
 #endif
