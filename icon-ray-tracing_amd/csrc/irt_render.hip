@@ -64,6 +64,10 @@ enum : int {
                             // sample's header, so that the next round's header read hits L2
   OPT_WAVEWG2 = 536870912,  // (A/B, with OPT_LEAN) two-wave workgroups: a block's packets in pairs
                             // (each pair sharing a CU's L1), a slot freed per two waves
+  OPT_DPPSCAN = 32,  // (A/B) groups of 2, 4, 16 and 64 lanes take the round's prefix t0 - d0 - ... - dk
+                     // by DPP steps across lanes (woodcock_wave), not each lane from LDS
+  OPT_XPAIR = 64,  // (A/B, one-wave workgroups) an XCD's two blocks of a 64x64 tile vertically
+                   // adjacent (a 16x32-pixel region) instead of two block rows apart
   OPT_DMATAB = 67108864,  // (A/B) one-wave workgroups: the LCG jump and logf tables loaded into
                           // LDS by LDS-DMA, not waited for in the prologue (k_render)
   OPT_NOMISS = 262144,  // (A/B) the user-geometry cooperative loop without its miss mode:
@@ -178,6 +182,29 @@ __device__ __forceinline__ float coop_prefix(float t0, const float *d, int k) {
     }
   }
   return t;
+}
+
+// The same prefix by DPP steps across the lanes of groups of G = 2, 4, 16 or 64 (OPT_DPPSCAN):
+// lane k starts at t0 - d_k (final for k = 0), and step s sets y_k = y_{k-1} - d_k, so that after
+// step s the lanes k <= s hold ((t0 - d0) - d1) - ... - dk, subtracted in the serial loop's order.
+// A group's first lane reads itself (quad_perm) or has no source lane (row_shr / wave_shr with
+// bound_ctrl off: the old value) and subtracts +0, which leaves every float as it is.
+template <int G>
+__device__ __forceinline__ float dpp_prefix(float t0, float dk, int k) {
+  static_assert(G == 2 || G == 4 || G == 16 || G == 64, "DPP prefix: groups of 2, 4, 16, 64");
+  constexpr int ctrl = G == 2 ? 0xA0 : G == 4 ? 0x90 : G == 16 ? 0x111 : 0x138;  // quad_perm [0,0,2,2] /
+                                                                                // [0,0,1,2], row_shr:1,
+                                                                                // wave_shr:1
+  const float e = k == 0 ? 0.f : dk;
+  float y = t0 - dk;
+#pragma unroll
+  for (int s = 1; s < G; ++s) {
+    const float prev = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, y),
+                                                                             __builtin_bit_cast(int, y), ctrl, 0xf,
+                                                                             0xf, false));
+    y = prev - e;
+  }
+  return y;
 }
 
 // OPT_TIMING's per-wave region clocks (Tracer::tmark); empty in every other kernel
@@ -947,8 +974,12 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       }
       const float dk = woodcock_log(sk, s_logf) / rq.z;
       float tk;
+      constexpr bool dppScan = (OPT & OPT_DPPSCAN) != 0;
       if (solo) {
         tk = rq.x - dk;
+      } else if (dppScan && (lg == 1 || lg == 2 || lg == 4 || lg == 6)) {
+        tk = lg == 1 ? dpp_prefix<2>(rq.x, dk, k)
+                     : lg == 2 ? dpp_prefix<4>(rq.x, dk, k) : lg == 4 ? dpp_prefix<16>(rq.x, dk, k) : dpp_prefix<64>(rq.x, dk, k);
       } else {
         W.step[lane] = dk;
         __builtin_amdgcn_wave_barrier();
@@ -2122,7 +2153,13 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   // ((i >> 4) << 3) | (i & 7))
   constexpr uint32_t kNwb = 4 / kWpg;  // workgroups per block
   const uint32_t bx = blockIdx.x;
-  const uint32_t wg = split ? (((bx >> 3) / kNwb) << 3) | (bx & 7u) : bx;
+  uint32_t wg = split ? (((bx >> 3) / kNwb) << 3) | (bx & 7u) : bx;
+  if constexpr ((OPT & OPT_XPAIR) != 0 && wavewg) {
+    // tile t's blocks 8 h + x (h = 0, 1: the tile's halves) run on XCD x; here block (x & 3,
+    // 2 (x >> 2) + h) of the tile's 4 x 4, so XCD x's two blocks share a block edge
+    const uint32_t q = bx >> 5, x = bx & 7u;
+    wg = ((q >> 1) << 4) | (x & 3u) | ((x >> 2) << 3) | ((q & 1u) << 2);
+  }
   const int wwave = split ? (int)(((bx >> 3) % kNwb) * kWpg) : 0;  // the block's first wave in this workgroup
   const int ptid = split ? wwave * 64 + tid : tid;
   if constexpr ((OPT & OPT_TIMING) != 0) {
@@ -2395,7 +2432,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 #ifdef IRT_ALL_VARIANTS
 #define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73929984) X(74192128)
 #else
-#define IRT_VARIANTS(X) X(73405696) X(73667840) X(5376) X(36864)
+#define IRT_VARIANTS(X) X(73405696) X(73667840) X(5376) X(36864) X(73405760) X(73667904) X(73405728) X(73667872)
 #endif
 static_assert(kDefaultVariant == 73405696 && (kDefaultVariant | kNoMissBit) == 73667840 && kNoMissBit == OPT_NOMISS,
               "the product build's variant list names the default and its hole-free form");
