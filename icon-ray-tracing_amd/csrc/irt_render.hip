@@ -64,6 +64,8 @@ enum : int {
                             // sample's header, so that the next round's header read hits L2
   OPT_WAVEWG2 = 536870912,  // (A/B, with OPT_LEAN) two-wave workgroups: a block's packets in pairs
                             // (each pair sharing a CU's L1), a slot freed per two waves
+  OPT_ACCPF = 16,  // (A/B, with OPT_LEAN) a single frame's (or a chain's first frame's) accum pixel
+                   // fetched into LDS by LDS-DMA at the wave's start, not loaded at the ray's end
   OPT_DPPSCAN = 32,  // (A/B) groups of 2, 4, 16 and 64 lanes take the round's prefix t0 - d0 - ... - dk
                      // by DPP steps across lanes (woodcock_wave), not each lane from LDS
   OPT_XPAIR = 64,  // (A/B, one-wave workgroups) an XCD's two blocks of a 64x64 tile vertically
@@ -1579,6 +1581,13 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   constexpr bool kFastSph = (OPT & OPT_FASTSPH) != 0;
   constexpr bool grid = (OPT & OPT_GRID) != 0;
   const bool ae = A.raygen == 1;
+  // OPT_ACCPF: the lerp's accum pixel straight into the wave's LDS slots now (a distinct LDS
+  // array: the compiler's LDS-DMA tracking waits for it only where the slots are read, at the end)
+  constexpr bool accPf = (OPT & OPT_ACCPF) != 0 && (OPT & OPT_LEAN) != 0;
+  const bool accEarly = accPf && !toSample && !chainLate;
+  if (accEarly && px.active)
+    __builtin_amdgcn_global_load_lds((const void *)(A.accum + px.outIdx),
+                                     (__attribute__((address_space(3))) void *)(s_acc + (tid & ~63)), 16, 0, 0);
   uint32_t st = 0;
   float dx = 1.f, dy = 1.f, dz = 1.f;
   float rlo0 = 0.f, rhi0 = 0.f, rlo1 = __builtin_inff(), rhi1 = -__builtin_inff();
@@ -1993,6 +2002,9 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       float4 old;
       if (chainLate && (!chainReady || (OPT & OPT_LEAN) != 0)) {
         old = chain_load_accum(A, outIdx);
+      } else if constexpr (accPf) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
+        old = lds_ld16(&s_acc[tl]);
       } else if constexpr ((OPT & OPT_LEAN) != 0) {
         old = A.accum[outIdx];
       } else {
@@ -2002,7 +2014,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       // 1.f / (float)(accumID + 1) of this frame, correctly rounded as the host's A.accumW
       write_pixel_chain(A, outIdx, c.x, c.y, c.z, c.w, 1.f / (float)(accumID + 1), s_th, old,
                         frame < A.numSamples - 1);
-    } else if constexpr ((OPT & OPT_LEAN) != 0) {
+    } else if constexpr ((OPT & OPT_LEAN) != 0 && !accPf) {
       write_pixel(A, outIdx, c.x, c.y, c.z, c.w, s_th);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
@@ -2074,7 +2086,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   __shared__ CoopWave s_coop[kW];   // the cooperative Woodcock loop (kCoop kernels)
   __shared__ ScanWave s_scan[Tracer<OPT>::kWaveScan ? kW : 1];  // its wave-wide candidate scan
   __shared__ HdrStage s_hdrs[(OPT & OPT_HDRLDS) ? kW : 1];       // OPT_HDRLDS: staged header lines
-  __shared__ float4 s_acc[lean ? 1 : 256];  // kCoop: the accum pixels, prefetched
+  __shared__ float4 s_acc[lean ? ((OPT & OPT_ACCPF) ? 64 : 1) : 256];  // kCoop: the accum pixels, prefetched
   __shared__ uint2 s_jmp[kLcgJumps];  // lcg_jump's {mul, add} (kLcgJumpTab)
   const int tid = threadIdx.x;
   if (A.wgTrace && tid == 0) {  // measurement only: the workgroup's start, where it ran
@@ -2432,7 +2444,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 #ifdef IRT_ALL_VARIANTS
 #define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73929984) X(74192128)
 #else
-#define IRT_VARIANTS(X) X(73405696) X(73667840) X(5376) X(36864) X(73405760) X(73667904) X(73405728) X(73667872)
+#define IRT_VARIANTS(X) X(73405696) X(73667840) X(5376) X(36864) X(73405760) X(73667904) X(73405728) X(73667872) X(73405712) X(73667856)
 #endif
 static_assert(kDefaultVariant == 73405696 && (kDefaultVariant | kNoMissBit) == 73667840 && kNoMissBit == OPT_NOMISS,
               "the product build's variant list names the default and its hole-free form");
