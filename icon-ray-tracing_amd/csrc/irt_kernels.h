@@ -141,8 +141,9 @@ constexpr int kCnt = 8;
 // -2.3 %, a single C3 frame -1.1 % (profiles/r04p_ab/)
 // Round 5: + OPT_DMATAB (67108864: the prologue's LCG-jump and logf tables by LDS-DMA, with no
 // wait before the ray generation): against 6296832 C3 -1.2 %, one frame per launch -1.7 %, C5
-// -2.5 %, C3t -1.2 %, C3s -0.3 % (profiles/r05k_dmatab/)
-constexpr int kDefaultVariant = 73405696;
+// -2.5 %, C3t -1.2 %, C3s -0.3 % (profiles/r05k_dmatab/); + OPT_DPPSCAN (32: the round's prefix
+// by DPP steps across lanes): C3t -1.1 %, comb TF -1.3 %, C3 -0.3 % (profiles/r05p_ab/)
+constexpr int kDefaultVariant = 73405728;
 // Round 5: the raygen's miss mode (woodcock_wave) is on in the default variant; a scene
 // without holes (every column starting at the same radius, no gaps inside columns) runs it
 // without (bit 262144, OPT_NOMISS): C3 -2.3 %, while convert_icon terrain (voids under land)

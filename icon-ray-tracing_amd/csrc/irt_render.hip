@@ -2429,10 +2429,11 @@ void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *foun
 // 1053696 = 5120 | OPT_HDRLDS: the cell headers staged through LDS (profiles/r03s_variants/).
 // 2102272 = 5120 | OPT_LEAN (24 KB of LDS per workgroup), 2102528 the same at 5 waves/SIMD;
 // 8393728 / 8393984 = 5120 / 5376 | OPT_DEALALL (profiles/r03t_regs/); 6296576 / 6296832 =
-// 2102272 / 2102528 | OPT_WAVEWG (one-wave workgroups); 73405696 = 6296832 | OPT_DMATAB (the
-// default since round 5), 73667840 its hole-free form (| OPT_NOMISS).  All variants give
-// identical results.  73929984 / 74192128: the default / its hole-free form with OPT_TIMING
-// (per-region shader clocks, profiles/probe.py).
+// 2102272 / 2102528 | OPT_WAVEWG (one-wave workgroups); 73405696 = 6296832 | OPT_DMATAB,
+// 73405728 = 73405696 | OPT_DPPSCAN (the default since round 5), 73667872 its hole-free form (|
+// OPT_NOMISS); 73405760 / 73405712 = 73405696 | OPT_XPAIR / OPT_ACCPF (profiles/r05p_ab/).  All
+// variants give identical results.  73930016 / 74192160: the default / its hole-free form with
+// OPT_TIMING (per-region shader clocks, profiles/probe.py; s_memtime slows them ~17x).
 constexpr int OPT_MONO = 4096;
 static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 
@@ -2442,11 +2443,11 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73929984) X(74192128)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73405760) X(73667904) X(73405712) X(73667856) X(73930016) X(74192160)
 #else
-#define IRT_VARIANTS(X) X(73405696) X(73667840) X(5376) X(36864) X(73405760) X(73667904) X(73405728) X(73667872) X(73405712) X(73667856)
+#define IRT_VARIANTS(X) X(73405728) X(73667872) X(5376) X(36864)
 #endif
-static_assert(kDefaultVariant == 73405696 && (kDefaultVariant | kNoMissBit) == 73667840 && kNoMissBit == OPT_NOMISS,
+static_assert(kDefaultVariant == 73405728 && (kDefaultVariant | kNoMissBit) == 73667872 && kNoMissBit == OPT_NOMISS,
               "the product build's variant list names the default and its hole-free form");
 
 int render_variants(int *out, int cap) {

@@ -33,9 +33,9 @@ MODE_USER_GEOM = 0     # Volume::mode (Params.h:29-31): sample() on the cells (d
 MODE_TRIANGLES = 1     # closest bottom triangle toward the centre (deviceCode.cu:61-76)
 MODE_CUBQL = 2         # wedges + intersectWedgeEXT (deviceCode.cu:90-115)
 # The raygen's render variants (irt_render.hip OPT_* bits), all bit-identical: the product
-# library compiles 73405696 (the default: one-wave workgroups since round 4, 5 waves/SIMD; since
-# round 5 with the miss mode and the LDS-DMA prologue tables, and 73667840 its form without the
-# miss mode, which hole-free scenes run),
+# library compiles 73405728 (the default: one-wave workgroups since round 4, 5 waves/SIMD; since
+# round 5 with the miss mode, the LDS-DMA prologue tables and the DPP prefix, and 73667872 its
+# form without the miss mode, which hole-free scenes run),
 # 5376 (256-thread workgroups; the persistent launch's base) and 36864 (per-wave statistics);
 # libicon_rt_hip_all.so (`make VARIANTS=all`) adds the A/B variants: 4096 no waves-per-SIMD
 # floor, 5120 at 4 waves/SIMD, 70656 the one-lane-per-ray Woodcock loop, 136192 per-lane
