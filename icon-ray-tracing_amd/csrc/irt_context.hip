@@ -127,8 +127,15 @@ struct irt_context {
   // (h_schedCost, pinned, in the stats ring), and once that copy has landed the host
   // orders the frame tiles by descending cost (longest-processing-time first) and uploads
   // the order (d_schedOrder) for later launches with the same grid.
-  uint32_t *d_schedOrder = nullptr, *d_schedCost = nullptr;  // 2 x cap (ping-pong), cap
-  uint32_t *h_schedCost = nullptr, *h_schedOrder = nullptr;  // pinned: kSlots x cap, 2 x cap
+  // Per order buffer (2, ping-pong; sched_stride words each): the block order (cap words), the
+  // split packets (kMaxSplit words) and their bitmap (4 cap / 32 words); costs per packet
+  // (4 cap words per launch slot)
+  uint32_t *d_schedOrder = nullptr, *d_schedCost = nullptr;  // 2 x stride, 4 cap
+  uint32_t *h_schedCost = nullptr, *h_schedOrder = nullptr;  // pinned: kSlots x 4 cap, 2 x stride
+  uint32_t schedSplit[2] = {0, 0};  // split packets in each order buffer
+  uint32_t lastNumSplit = 0;        // the last launch's split packets
+  int splitLg = 1;                  // parts per split packet: 2^splitLg (IRT_SPLIT_LG; 0: no splits)
+  float splitFactor = 4.f;          // a packet splits when its cost exceeds this x the median
   int schedBuf = 0;             // the order buffer launches read now
   long long schedSwitch = 0;    // first launch reading it
   size_t schedCap = 0;
@@ -376,8 +383,11 @@ int finish_stats(irt_context *c) {
 // Measured-cost scheduling, host side (see irt_context::d_schedOrder): (re)allocate for
 // the grid, drop the order when the grid changes, and rebuild it from the newest landed
 // cost copy of a launch with the same grid.
+// words of one order buffer: the block order, the split list, the split bitmap
+size_t sched_stride(size_t cap) { return cap + kMaxSplit + (4 * cap + 31) / 32; }
+
 int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int tileBegin,
-                  int tileStride, int numTiles, const irt_launch_params *lp, hipStream_t s) {
+                  int tileStride, int numTiles, const irt_launch_params *lp, bool wavewg, hipStream_t s) {
   if ((size_t)numBlocks > c->schedCap) {
     IRT_HIP(hipStreamSynchronize(s));
     if (c->d_schedOrder) IRT_HIP(hipFree(c->d_schedOrder));
@@ -385,15 +395,18 @@ int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int t
     if (c->h_schedCost) IRT_HIP(hipHostFree(c->h_schedCost));
     if (c->h_schedOrder) IRT_HIP(hipHostFree(c->h_schedOrder));
     c->d_schedOrder = c->d_schedCost = c->h_schedCost = c->h_schedOrder = nullptr;
-    c->bytes -= 3 * c->schedCap * sizeof(uint32_t);
+    c->bytes -= (2 * sched_stride(c->schedCap) + 4 * c->schedCap) * sizeof(uint32_t);
     c->schedCap = 0;
     int rc;
-    if ((rc = dalloc(c, &c->d_schedOrder, 2 * (size_t)numBlocks)) ||
-        (rc = dalloc(c, &c->d_schedCost, numBlocks)))
+    if ((rc = dalloc(c, &c->d_schedOrder, 2 * sched_stride((size_t)numBlocks))) ||
+        (rc = dalloc(c, &c->d_schedCost, 4 * (size_t)numBlocks)))
       return rc;
-    IRT_HIP(hipHostMalloc((void **)&c->h_schedCost, (size_t)irt_context::kSlots * numBlocks * sizeof(uint32_t)));
-    IRT_HIP(hipHostMalloc((void **)&c->h_schedOrder, 2 * (size_t)numBlocks * sizeof(uint32_t)));
+    IRT_HIP(hipMemsetAsync(c->d_schedCost, 0, 4 * (size_t)numBlocks * sizeof(uint32_t), s));
+    IRT_HIP(hipHostMalloc((void **)&c->h_schedCost, (size_t)irt_context::kSlots * 4 * numBlocks * sizeof(uint32_t)));
+    memset(c->h_schedCost, 0, (size_t)irt_context::kSlots * 4 * numBlocks * sizeof(uint32_t));
+    IRT_HIP(hipHostMalloc((void **)&c->h_schedOrder, 2 * sched_stride((size_t)numBlocks) * sizeof(uint32_t)));
     c->schedCap = numBlocks;
+    c->schedSplit[0] = c->schedSplit[1] = 0;
     c->schedOrderValid = false;
     for (auto &v : c->schedCopied) v = -1;
     c->info.deviceBytes = c->bytes;
@@ -420,7 +433,7 @@ int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int t
   if (bestSlot < 0) return IRT_OK;
   // longest-processing-time first over whole 64x64 tiles (16 consecutive workgroups, kept
   // together for the locator's cache locality)
-  const uint32_t *cost = c->h_schedCost + (size_t)bestSlot * c->schedCap;
+  const uint32_t *cost = c->h_schedCost + (size_t)bestSlot * 4 * c->schedCap;  // per packet
   const int nt = numBlocks / 16;
   // group size in tiles: 1, or a band of consecutive launch tiles (one image row of tiles)
   const int tilesX = (W + 63) / 64;
@@ -430,7 +443,7 @@ int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int t
   for (int g = 0; g < ng; ++g) {
     uint64_t sum = 0;
     for (int t = g * band; t < std::min(nt, (g + 1) * band); ++t)
-      for (int j = 0; j < 16; ++j) sum += cost[16 * t + j];
+      for (int j = 0; j < 64; ++j) sum += cost[64 * t + j];
     groups[g] = {c->schedPolicy == 3 ? (uint64_t)g : sum, g};
   }
   std::stable_sort(groups.begin(), groups.end(),
@@ -438,14 +451,40 @@ int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int t
                      return a.first > b.first;
                    });
   const int nb = c->schedOrderValid ? 1 - c->schedBuf : c->schedBuf;
-  uint32_t *h = c->h_schedOrder + (size_t)nb * c->schedCap;
+  const size_t stride = sched_stride(c->schedCap);
+  uint32_t *h = c->h_schedOrder + (size_t)nb * stride;
   int p = 0;
   for (const auto &g : groups)
     for (int t = g.second * band; t < std::min(nt, (g.second + 1) * band); ++t, ++p)
       for (int j = 0; j < 16; ++j) h[16 * p + j] = (uint32_t)(16 * t + j);
+  // the packets that split (one-wave workgroups only): cost over splitFactor x the median, the
+  // costliest kMaxSplit, a multiple of 8; their parts run first, at most a tenth of the frame
+  uint32_t *list = h + c->schedCap, *mask = list + kMaxSplit;
+  memset(mask, 0, (4 * c->schedCap + 31) / 32 * sizeof(uint32_t));
+  uint32_t ns = 0;
+  if (c->splitLg > 0 && wavewg) {
+    const size_t np = 4 * (size_t)numBlocks;
+    std::vector<uint32_t> byCost(np);
+    for (size_t k = 0; k < np; ++k) byCost[k] = (uint32_t)k;
+    std::vector<uint32_t> sorted(cost, cost + np);
+    std::nth_element(sorted.begin(), sorted.begin() + np / 2, sorted.end());
+    const double thr = c->splitFactor * (double)sorted[np / 2];
+    const size_t cap = std::min<size_t>(kMaxSplit, np / 10) & ~(size_t)7;
+    std::partial_sort(byCost.begin(), byCost.begin() + std::min(cap, np), byCost.end(),
+                      [&](uint32_t a, uint32_t b) { return cost[a] > cost[b] || (cost[a] == cost[b] && a < b); });
+    size_t n = 0;
+    while (n < cap && (double)cost[byCost[n]] > thr && cost[byCost[n]] > 0) ++n;
+    n &= ~(size_t)7;
+    for (size_t k = 0; k < n; ++k) {
+      list[k] = byCost[k];
+      mask[byCost[k] >> 5] |= 1u << (byCost[k] & 31);
+    }
+    ns = (uint32_t)n;
+  }
+  c->schedSplit[nb] = ns;
   uint32_t *dh = nullptr;
   IRT_HIP(hipHostGetDevicePointer((void **)&dh, h, 0));
-  launch_copy_u32(dh, c->d_schedOrder + (size_t)nb * c->schedCap, (size_t)numBlocks, s);
+  launch_copy_u32(dh, c->d_schedOrder + (size_t)nb * stride, stride, s);
   IRT_HIP(hipGetLastError());
   c->schedBuf = nb;
   c->schedSwitch = c->launches;
@@ -642,10 +681,45 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
                                 : render_queue_wgs(A, c->variant, c->numCU, numTiles * 16 * numFrames);
     c->lastQueueWG = queueWG;
   }
+  // measured-cost scheduling: single-frame launches of the one-kernel raygen only (before the
+  // workgroup count: the split packets' parts are extra workgroups)
+  A.schedOrder = nullptr;
+  A.schedCost = nullptr;
+  A.splitList = A.splitMask = nullptr;
+  A.numSplit = 0;
+  A.splitLg = 0;
+  const int numBlocks = numTiles * 16;
+  bool copyCosts = false;
+  if (c->schedOn && numFrames == 1 && numBlocks > 0 && !dList && !queued) {
+    int rc = sched_prepare(c, numBlocks, W, H, packed, tileBegin, tileStride, numTiles, lp,
+                           render_wg_per_block(A, c->variant) == 4, s);
+    if (rc) return rc;
+    const uint32_t *ob = c->d_schedOrder + (size_t)c->schedBuf * sched_stride(c->schedCap);
+    A.schedOrder = c->schedOrderValid ? ob : nullptr;
+    if (c->schedOrderValid && c->schedSplit[c->schedBuf] && render_wg_per_block(A, c->variant) == 4 &&
+        c->probeExit == 0) {
+      A.splitList = ob + c->schedCap;
+      A.splitMask = ob + c->schedCap + kMaxSplit;
+      A.numSplit = c->schedSplit[c->schedBuf];
+      A.splitLg = c->splitLg;
+    }
+    // every 8th launch writes its workgroups' durations straight into this slot's pinned
+    // host copy; the others into device memory nobody reads
+    copyCosts = c->launches - c->schedLastCopy >= 8;
+    if (copyCosts) {
+      uint32_t *dh = nullptr;
+      IRT_HIP(hipHostGetDevicePointer((void **)&dh, c->h_schedCost + (size_t)slot * 4 * c->schedCap, 0));
+      A.schedCost = dh;
+    } else {
+      A.schedCost = c->d_schedCost;
+    }
+  }
   // workgroups of this launch: 16 per 64x64 tile, x4 for the one-wave-workgroup variants
-  // (irt_render.hip OPT_WAVEWG, bit 4194304), per frame; a persistent launch's resident ones
+  // (irt_render.hip OPT_WAVEWG, bit 4194304), per frame, + the split packets' parts; a
+  // persistent launch's resident ones
   const size_t numWG = queued ? (size_t)queueWG
-                              : (size_t)numTiles * 16 * (size_t)render_wg_per_block(A, c->variant) * (size_t)numFrames;
+                              : (size_t)numTiles * 16 * (size_t)render_wg_per_block(A, c->variant) * (size_t)numFrames +
+                                    ((size_t)A.numSplit << A.splitLg);
   // Per-workgroup counts need kSlots x 32 B of pinned host memory per workgroup and frame
   // (1 KiB): a launch past kWgCountsMax workgroups (a large progressive batch) counts through
   // the device-atomic block instead, for that launch only.
@@ -772,26 +846,8 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   }
   A.sampleBuf = c->d_samples;
   // measured-cost scheduling: single-frame launches of the one-kernel raygen only
-  A.schedOrder = nullptr;
-  A.schedCost = nullptr;
-  const int numBlocks = numTiles * 16;
-  bool copyCosts = false;
-  if (c->schedOn && numFrames == 1 && numBlocks > 0 && !dList && !queued) {
-    int rc = sched_prepare(c, numBlocks, W, H, packed, tileBegin, tileStride, numTiles, lp, s);
-    if (rc) return rc;
-    A.schedOrder = c->schedOrderValid ? c->d_schedOrder + (size_t)c->schedBuf * c->schedCap : nullptr;
-    // every 8th launch writes its workgroups' durations straight into this slot's pinned
-    // host copy; the others into device memory nobody reads
-    copyCosts = c->launches - c->schedLastCopy >= 8;
-    if (copyCosts) {
-      uint32_t *dh = nullptr;
-      IRT_HIP(hipHostGetDevicePointer((void **)&dh, c->h_schedCost + (size_t)slot * c->schedCap, 0));
-      A.schedCost = dh;
-    } else {
-      A.schedCost = c->d_schedCost;
-    }
-  }
   c->schedLastApplied = A.schedOrder != nullptr;
+  c->lastNumSplit = A.numSplit;
   c->schedApplied += c->schedLastApplied ? 1 : 0;
   // the 16-counter block (device atomics) is only needed by the statistics variant and the
   // IRT_COUNTERS=atomic mode; it must start zeroed
@@ -869,6 +925,8 @@ int irt_create_begin(size_t numCells, int device, irt_context **out) {
     set_error("irt_create: cannot initialise device %d", device);
     return fail(IRT_E_HIP);
   }
+  if (const char *e = getenv("IRT_SPLIT_LG")) c->splitLg = std::min(3, std::max(0, atoi(e)));
+  if (const char *e = getenv("IRT_SPLIT_FACTOR")) c->splitFactor = (float)atof(e);
   if (const char *e = getenv("IRT_SCHED")) {
     c->schedOn = atoi(e) != 0;
     c->schedPolicy = atoi(e);
@@ -1876,7 +1934,21 @@ extern "C" long long irt_debug_launch_workgroups(const irt_context *c, int numTi
   }
   RenderArgs A;
   memset(&A, 0, sizeof(A));  // the user-geometry sphere path (sampler 0, accelMode 0)
-  return (long long)numTiles * 16 * render_wg_per_block(A, c->variant) * numFrames;
+  const int per = render_wg_per_block(A, c->variant);
+  // a single frame in measured-cost order may add the split packets' parts (at most kMaxSplit
+  // packets of 2^splitLg workgroups)
+  const size_t extra = c->schedOn && numFrames == 1 && per == 4 ? (size_t)kMaxSplit << c->splitLg : 0;
+  return (long long)((size_t)numTiles * 16 * per * numFrames + extra);
+}
+
+extern "C" int irt_debug_sched_split(const irt_context *c, int *numSplit, int *splitLg) {
+  if (!c || !numSplit || !splitLg) {
+    set_error("irt_debug_sched_split: null argument");
+    return IRT_E_INVALID;
+  }
+  *numSplit = (int)c->lastNumSplit;
+  *splitLg = c->splitLg;
+  return IRT_OK;
 }
 
 extern "C" int irt_debug_set_chain(irt_context *c, int on) {

@@ -1537,7 +1537,8 @@ template <int OPT>
 __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
                                                   const float *s_th, int4 *s_dda, float4 *s_entry,
                                                   float4 *s_acc, CoopWave &W, ScanWave *SW, const uint2 *jmp,
-                                                  int tid, int accumID, uint32_t blk, int pwave, int frame) {
+                                                  int tid, int accumID, uint32_t blk, int pwave, int frame,
+                                                  int partSel = -1) {
   // At 5+ waves/SIMD the pixel's output addresses are recomputed where they are used (from the
   // workgroup's uniform block index), not held in VGPRs through the rounds: a progressive
   // batch's sample slot (k_accumulate reads it) and the frame index.  (At 4 waves there is
@@ -1556,6 +1557,10 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     if constexpr (!kRecompute) return ptid;
     int lane = (int)__lane_id();
     asm volatile("" : "+v"(lane));  // not CSE'd with the pixel's coordinates at the ray's start
+    if (partSel >= 0) {  // a split packet's part (k_render): pn rays from ray part * pn
+      const int ps = opaque_u(partSel), pn = 64 >> (ps & 255);
+      lane = ((ps >> 8) * pn) | (lane & (pn - 1));
+    }
     return (opaque_u(pwave) << 6) | lane;
   };
   const bool toSample = A.numSamples > 1 && !A.chain;
@@ -2164,7 +2169,24 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   // (OPT_WAVEWG2: two-wave workgroups, workgroup i the waves 2 ((i >> 3) & 1) + {0, 1} of block
   // ((i >> 4) << 3) | (i & 7))
   constexpr uint32_t kNwb = 4 / kWpg;  // workgroups per block
-  const uint32_t bx = blockIdx.x;
+  // A single frame's costliest packets split (A.numSplit, measured-cost scheduling): the launch's
+  // first numSplit << splitLg workgroups render part `part` of packet splitList[i] -- its rays
+  // part * (64 >> splitLg) .. on lanes 0 .. (64 >> splitLg) - 1 --, i = ((b >> (3 + splitLg)) << 3) |
+  // (b & 7), part (b >> 3) & (parts - 1), so a packet's parts run on one XCD; the regular
+  // workgroups follow, and those of split packets render nothing.
+  uint32_t bx = blockIdx.x;
+  int partSel = -1;  // (part << 8) | splitLg for a split packet's part, -1 for a whole packet
+  uint32_t splitP = 0u;
+  if constexpr (wavewg) {
+    const uint32_t ns = A.numSplit << A.splitLg;
+    if (bx < ns) {
+      const uint32_t lg = (uint32_t)A.splitLg;
+      partSel = (int)((((bx >> 3) & ((1u << lg) - 1u)) << 8) | lg);
+      splitP = scalar_word(A.splitList, ((bx >> (3 + lg)) << 3) | (bx & 7u));
+    } else {
+      bx -= ns;
+    }
+  }
   uint32_t wg = split ? (((bx >> 3) / kNwb) << 3) | (bx & 7u) : bx;
   if constexpr ((OPT & OPT_XPAIR) != 0 && wavewg) {
     // tile t's blocks 8 h + x (h = 0, 1: the tile's halves) run on XCD x; here block (x & 3,
@@ -2172,7 +2194,8 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
     const uint32_t q = bx >> 5, x = bx & 7u;
     wg = ((q >> 1) << 4) | (x & 3u) | ((x >> 2) << 3) | ((q & 1u) << 2);
   }
-  const int wwave = split ? (int)(((bx >> 3) % kNwb) * kWpg) : 0;  // the block's first wave in this workgroup
+  const int wwave = partSel >= 0 ? (int)(splitP & 3u)
+                                  : split ? (int)(((bx >> 3) % kNwb) * kWpg) : 0;  // the block's first wave in this workgroup
   const int ptid = split ? wwave * 64 + tid : tid;
   if constexpr ((OPT & OPT_TIMING) != 0) {
     T.tLast = tStart;
@@ -2182,7 +2205,10 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   // grid.y = frame k of a progressive batch (accumID + k), whose colour goes to the sample
   // buffer for k_accumulate; a single frame writes accum/fb directly.  With measured-cost
   // scheduling (irt_context.hip) workgroup b renders block order[b].
-  const uint32_t blk = A.schedOrder ? scalar_word(A.schedOrder, wg) : wg;  // uniform: an SGPR
+  const uint32_t blk = partSel >= 0 ? splitP >> 2 : A.schedOrder ? scalar_word(A.schedOrder, wg) : wg;  // uniform: an SGPR
+  // a split packet's regular workgroup: nothing to render (its counts and trace are still written)
+  const uint32_t pkt = blk * 4u + (uint32_t)wwave;
+  const bool splitAway = wavewg && partSel < 0 && A.numSplit && ((scalar_word(A.splitMask, pkt >> 5) >> (pkt & 31u)) & 1u);
   uint32_t launched = 0u;  // rays of this wave's pixels (uniform)
   bool pxActive = false;   // the one-lane-per-ray kernel's pixel
   if constexpr (Tracer<OPT>::kCoop) {
@@ -2238,12 +2264,15 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
                                pblk, pw, frame);
         TL.flush_coop();  // this packet's counts (nothing carried from packet to packet)
       } else {
-        const Pixel ppx = pixel_of(A, pblk, pw * 64 + (ltid & 63));
+        const int pl = partSel & 255, pn = 64 >> pl;  // a split packet's part: pn rays
+        Pixel ppx = pixel_of(A, pblk, pw * 64 + (partSel < 0 ? (ltid & 63) : ((partSel >> 8) * pn) | (ltid & (pn - 1))));
+        if (partSel >= 0) ppx.active = ppx.active && (ltid & 63) < pn;
+        if (splitAway) ppx.active = false;
         launched += (uint32_t)__popcll(__ballot(ppx.active));
         T.frame = frame;
         render_pixel_coop<OPT>(A, T, ppx, th_p, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
                                &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, cam_accum_id(A, frame),
-                               pblk, pw, frame);
+                               pblk, pw, frame, partSel);
         if (A.chain && frame < A.numSamples - 1 && frame != A.chainWithhold) {
           // chained frames: this wave's pixels are written through; tell frame + 1's wave
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2319,9 +2348,12 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
     prev = (uint32_t)__shfl((int)prev, 0, 64);
     if (prev == (blockDim.x >> 6) - 1u) {
       if (A.counters) flush_counters(A, s_cnt, lane);
-      if (A.schedCost && lane == 0 && wwave == 0) {  // this workgroup's duration, for the next launches' order
-        const uint64_t dt = wall_clock64() - c0;
-        A.schedCost[blk] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
+      if (A.schedCost && lane == 0 && (wavewg || wwave == 0) && !splitAway) {  // this workgroup's duration, for the next launches' order
+        // per packet (4 per block; a 256-thread workgroup's in its first packet's slot), a split
+        // packet's part counted for the whole packet (parts x its duration)
+        uint64_t dt = wall_clock64() - c0;
+        if (partSel >= 0) dt <<= (partSel & 255);
+        A.schedCost[pkt] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
       }
       if (A.wgTrace && lane == 0)
         A.wgTrace[4 * (blockIdx.y * gridDim.x + blockIdx.x) + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -2524,7 +2556,8 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(numBlocks), dim3(256), 0, s, A);
     numBlocks = A.numTiles * 16;
   } else {
-    hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads), A.numSamples), dim3(threads), 0, s, A);
+    const int split = threads == 64 ? (int)(A.numSplit << A.splitLg) : 0;  // split packets' parts first
+    hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads) + split, A.numSamples), dim3(threads), 0, s, A);
   }
   // progressive batch: the lerp chain over the frames' samples (chained frames lerp in k_render)
   if (A.numSamples > 1 && !A.chain) hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);

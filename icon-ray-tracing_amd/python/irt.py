@@ -582,6 +582,14 @@ class Context:
         L.irt_debug_set_chain_fault.argtypes = [C.c_void_p, C.c_uint32, C.c_int]
         _check(L.irt_debug_set_chain_fault(self._h, spins, withhold_frame), "irt_debug_set_chain_fault")
 
+    def sched_split(self):
+        """(packets split by the last launch, log2 of their parts) -- measured-cost scheduling."""
+        L = lib()
+        L.irt_debug_sched_split.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        n, lg = C.c_int(), C.c_int()
+        _check(L.irt_debug_sched_split(self._h, C.byref(n), C.byref(lg)), "irt_debug_sched_split")
+        return n.value, lg.value
+
     def launch_workgroups(self, num_tiles: int, frames: int = 1) -> int:
         """Workgroups of one launch of num_tiles tiles x frames (the wg-trace buffer needs 4
         u32 per workgroup)."""

@@ -105,7 +105,7 @@ def main():
 
     for s in range(args.warmup):
         step(s)
-    nwg = irt.num_tiles(W, H) * 16 * 4 * B  # room for one-wave workgroups (4 per block)
+    nwg = ctx.launch_workgroups(irt.num_tiles(W, H), B)  # incl. a single frame's split packets
     bufs = [torch.zeros(nwg * 4, dtype=torch.int32, device=dev) for _ in range(args.launches)]
     torch.cuda.synchronize()
     for k in range(args.launches):
@@ -118,8 +118,8 @@ def main():
         tr = bufs[k].cpu().numpy().view(np.uint32).reshape(-1, 4)
         L = irt.lib()
         L.irt_debug_get_variant.argtypes = [ctypes.c_void_p]
-        wpb = 4 if L.irt_debug_get_variant(ctx._h) & 4194304 else 1  # OPT_WAVEWG: 4 per block
-        tr = tr[:irt.num_tiles(W, H) * 16 * B * wpb]
+        # the rows this launch wrote (a split single frame has extra workgroups, first)
+        tr = tr[tr[:, 1] != 0]
         out, prev = analyse(tr, prev)
         out.update({"config": args.config, "launch": k, "frames_per_launch": B})
         print(json.dumps(out), flush=True)
