@@ -134,8 +134,8 @@ struct irt_context {
   uint32_t *h_schedCost = nullptr, *h_schedOrder = nullptr;  // pinned: kSlots x 4 cap, 2 x stride
   uint32_t schedSplit[2] = {0, 0};  // split packets in each order buffer
   uint32_t lastNumSplit = 0;        // the last launch's split packets
-  int splitLg = 1;                  // parts per split packet: 2^splitLg (IRT_SPLIT_LG; 0: no splits)
-  float splitFactor = 4.f;          // a packet splits when its cost exceeds this x the median
+  int splitLg = 2;                  // parts per split packet: 2^splitLg (IRT_SPLIT_LG; 0: no splits)
+  float splitFactor = 1.5f;         // a packet splits when its cost exceeds this x the median
   int schedBuf = 0;             // the order buffer launches read now
   long long schedSwitch = 0;    // first launch reading it
   size_t schedCap = 0;

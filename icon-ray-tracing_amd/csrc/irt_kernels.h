@@ -160,7 +160,7 @@ constexpr int kDefaultVariant = 73405728;
 constexpr int kNoMissBit = 262144;
 // measured-cost scheduling (irt_context.hip sched_prepare): at most this many packets of a single
 // frame split into parts (RenderArgs::splitList), a multiple of 8
-constexpr uint32_t kMaxSplit = 512;
+constexpr uint32_t kMaxSplit = 1024;
 inline int scene_variant(bool holes) { return holes ? kDefaultVariant : kDefaultVariant | kNoMissBit; }
 bool render_variant_available(int variant);
 int render_variants(int *out, int cap);  // the compiled variants (count; the first cap into out)

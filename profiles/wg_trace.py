@@ -49,8 +49,10 @@ def analyse(tr, prev_end):
     xcc = tr[:, 3] & 0xF
     per_xcc_end = [round(float(en[xcc == x].max()) / 100, 2) if (xcc == x).any() else None for x in range(8)]
     per_xcc_busy = [round(float(dur[xcc == x].sum()) / 100, 1) for x in range(8)]
+    top = np.argsort(-dur)[:8]
     out = {
         "workgroups": int(len(tr)),
+        "longest": [[int(i), round(float(dur[i]) / 100, 2), round(float(st[i]) / 100, 2)] for i in top],
         "span_us": span / 100,
         "gap_from_prev_us": None if prev_end is None else ((int(tr[:, 0].min()) - prev_end) & 0xFFFFFFFF) / 100
         if ((int(tr[:, 0].min()) - prev_end) & 0xFFFFFFFF) < 2**31 else -(((prev_end - int(tr[:, 0].min())) & 0xFFFFFFFF) / 100),
