@@ -135,7 +135,7 @@ struct irt_context {
   uint32_t schedSplit[2] = {0, 0};  // split packets in each order buffer
   uint32_t lastNumSplit = 0;        // the last launch's split packets
   int splitLg = 2;                  // parts per split packet: 2^splitLg (IRT_SPLIT_LG; 0: no splits)
-  float splitFactor = 1.5f;         // a packet splits when its cost exceeds this x the median
+  float splitFactor = 1.f;          // a packet splits when its cost exceeds this x the frame's ideal span
   int schedBuf = 0;             // the order buffer launches read now
   long long schedSwitch = 0;    // first launch reading it
   size_t schedCap = 0;
@@ -457,29 +457,41 @@ int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int t
   for (const auto &g : groups)
     for (int t = g.second * band; t < std::min(nt, (g.second + 1) * band); ++t, ++p)
       for (int j = 0; j < 16; ++j) h[16 * p + j] = (uint32_t)(16 * t + j);
-  // the packets that split (one-wave workgroups only): cost over splitFactor x the median, the
-  // costliest kMaxSplit, a multiple of 8; their parts run first, at most a tenth of the frame
+  // Work items ahead of the regular order (one-wave workgroups only), costliest first: every
+  // packet whose measured duration exceeds splitFactor x the frame's ideal span (all packets'
+  // durations over the resident slots), in 2^splitLg parts of 64 >> splitLg rays -- such a packet
+  // would end the frame after the rest, and it is lane-bound: its parts take about 1/2^splitLg of
+  // its time. (Packets shorter than the span are better left whole and in place: listing them
+  // first, whole, or splitting them cost C3 +16 to +27 %, profiles/r05s_split/.) A packet's parts
+  // are 8 items apart, so they run on one XCD; at most a tenth of the packets, kMaxSplit items.
   uint32_t *list = h + c->schedCap, *mask = list + kMaxSplit;
   memset(mask, 0, (4 * c->schedCap + 31) / 32 * sizeof(uint32_t));
   uint32_t ns = 0;
-  if (c->splitLg > 0 && wavewg) {
+  if (c->splitLg > 0 && c->splitFactor > 0.f && wavewg) {
     const size_t np = 4 * (size_t)numBlocks;
+    double total = 0.0;
+    for (size_t k = 0; k < np; ++k) total += cost[k];
+    const double span = total / (double)std::max(1, 20 * c->numCU);  // 5 waves x 4 SIMDs per CU
+    const size_t cap = np / 10;
     std::vector<uint32_t> byCost(np);
     for (size_t k = 0; k < np; ++k) byCost[k] = (uint32_t)k;
-    std::vector<uint32_t> sorted(cost, cost + np);
-    std::nth_element(sorted.begin(), sorted.begin() + np / 2, sorted.end());
-    const double thr = c->splitFactor * (double)sorted[np / 2];
-    const size_t cap = std::min<size_t>(kMaxSplit, np / 10) & ~(size_t)7;
     std::partial_sort(byCost.begin(), byCost.begin() + std::min(cap, np), byCost.end(),
                       [&](uint32_t a, uint32_t b) { return cost[a] > cost[b] || (cost[a] == cost[b] && a < b); });
-    size_t n = 0;
-    while (n < cap && (double)cost[byCost[n]] > thr && cost[byCost[n]] > 0) ++n;
-    n &= ~(size_t)7;
-    for (size_t k = 0; k < n; ++k) {
-      list[k] = byCost[k];
-      mask[byCost[k] >> 5] |= 1u << (byCost[k] & 31);
+    const uint32_t parts = 1u << c->splitLg;
+    std::vector<uint32_t> heavy;
+    for (size_t k = 0; k < cap && (heavy.size() + 8) * parts <= kMaxSplit; ++k) {
+      const double v = (double)cost[byCost[k]];
+      if (!(v > c->splitFactor * span) || v <= 0.0) break;
+      heavy.push_back(byCost[k]);
     }
-    ns = (uint32_t)n;
+    while (heavy.size() % 8) heavy.push_back(~0u);  // empty packets: their parts render nothing
+    for (size_t g = 0; g < heavy.size(); g += 8)
+      for (uint32_t part = 0; part < parts; ++part)
+        for (size_t j = 0; j < 8; ++j)
+          list[ns++] = heavy[g + j] == ~0u ? ~0u : (heavy[g + j] << 8) | (part << 4) | (uint32_t)c->splitLg;
+    while (ns % 8) list[ns++] = ~0u;
+    for (size_t k = 0; k < ns; ++k)
+      if (list[k] != ~0u) mask[(list[k] >> 8) >> 5] |= 1u << ((list[k] >> 8) & 31);
   }
   c->schedSplit[nb] = ns;
   uint32_t *dh = nullptr;
@@ -687,7 +699,6 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.schedCost = nullptr;
   A.splitList = A.splitMask = nullptr;
   A.numSplit = 0;
-  A.splitLg = 0;
   const int numBlocks = numTiles * 16;
   bool copyCosts = false;
   if (c->schedOn && numFrames == 1 && numBlocks > 0 && !dList && !queued) {
@@ -701,7 +712,6 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
       A.splitList = ob + c->schedCap;
       A.splitMask = ob + c->schedCap + kMaxSplit;
       A.numSplit = c->schedSplit[c->schedBuf];
-      A.splitLg = c->splitLg;
     }
     // every 8th launch writes its workgroups' durations straight into this slot's pinned
     // host copy; the others into device memory nobody reads
@@ -719,7 +729,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   // persistent launch's resident ones
   const size_t numWG = queued ? (size_t)queueWG
                               : (size_t)numTiles * 16 * (size_t)render_wg_per_block(A, c->variant) * (size_t)numFrames +
-                                    ((size_t)A.numSplit << A.splitLg);
+                                    (size_t)A.numSplit;
   // Per-workgroup counts need kSlots x 32 B of pinned host memory per workgroup and frame
   // (1 KiB): a launch past kWgCountsMax workgroups (a large progressive batch) counts through
   // the device-atomic block instead, for that launch only.
@@ -1935,9 +1945,8 @@ extern "C" long long irt_debug_launch_workgroups(const irt_context *c, int numTi
   RenderArgs A;
   memset(&A, 0, sizeof(A));  // the user-geometry sphere path (sampler 0, accelMode 0)
   const int per = render_wg_per_block(A, c->variant);
-  // a single frame in measured-cost order may add the split packets' parts (at most kMaxSplit
-  // packets of 2^splitLg workgroups)
-  const size_t extra = c->schedOn && numFrames == 1 && per == 4 ? (size_t)kMaxSplit << c->splitLg : 0;
+  // a single frame in measured-cost order may add its work items (at most kMaxSplit workgroups)
+  const size_t extra = c->schedOn && numFrames == 1 && per == 4 ? (size_t)kMaxSplit : 0;
   return (long long)((size_t)numTiles * 16 * per * numFrames + extra);
 }
 

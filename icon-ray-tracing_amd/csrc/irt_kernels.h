@@ -120,15 +120,14 @@ struct RenderArgs {
   // writes {start, end} (s_memrealtime, 100 MHz, low 32 bits), HW_ID and XCC_ID to
   // wgTrace[4b..4b+3] -- when the machine is idle at a launch's ramp and tail
   uint32_t *wgTrace;
-  // a single frame's costliest packets split (one-wave workgroups, measured-cost scheduling:
-  // irt_context.hip sched_prepare): numSplit packets (a multiple of 8; 0: none), packet p = 4 block
-  // + wave in splitList[i], each rendered by 2^splitLg one-wave workgroups of 64 >> splitLg rays,
-  // the launch's first numSplit << splitLg workgroups; splitMask bit p marks them (their regular
-  // workgroups render nothing)
+  // a single frame's costliest packets first (one-wave workgroups, measured-cost scheduling:
+  // irt_context.hip sched_prepare): numSplit work items (a multiple of 8; 0: none), item i =
+  // (packet << 8) | (part << 4) | lg -- part `part` of 2^lg of packet 4 block + wave, 64 >> lg rays
+  // -- rendered by the launch's workgroup i (~0u: nothing); splitMask bit p marks the listed
+  // packets (their regular workgroups render nothing)
   const uint32_t *splitList;
   const uint32_t *splitMask;
   uint32_t numSplit;
-  int splitLg;
 };
 // a persistent launch's queue words (irt_render.hip queue_take): 8 per-XCD counters and the
 // done count, each on its own 128-B line
@@ -158,9 +157,9 @@ constexpr int kDefaultVariant = 73405728;
 // without (bit 262144, OPT_NOMISS): C3 -2.3 %, while convert_icon terrain (voids under land)
 // runs 2.25x faster with it (profiles/r05d/)
 constexpr int kNoMissBit = 262144;
-// measured-cost scheduling (irt_context.hip sched_prepare): at most this many packets of a single
-// frame split into parts (RenderArgs::splitList), a multiple of 8
-constexpr uint32_t kMaxSplit = 1024;
+// measured-cost scheduling (irt_context.hip sched_prepare): at most this many work items run first
+// in a single frame (RenderArgs::splitList), a multiple of 8
+constexpr uint32_t kMaxSplit = 4096;
 inline int scene_variant(bool holes) { return holes ? kDefaultVariant : kDefaultVariant | kNoMissBit; }
 bool render_variant_available(int variant);
 int render_variants(int *out, int cap);  // the compiled variants (count; the first cap into out)

@@ -2169,22 +2169,23 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   // (OPT_WAVEWG2: two-wave workgroups, workgroup i the waves 2 ((i >> 3) & 1) + {0, 1} of block
   // ((i >> 4) << 3) | (i & 7))
   constexpr uint32_t kNwb = 4 / kWpg;  // workgroups per block
-  // A single frame's costliest packets split (A.numSplit, measured-cost scheduling): the launch's
-  // first numSplit << splitLg workgroups render part `part` of packet splitList[i] -- its rays
-  // part * (64 >> splitLg) .. on lanes 0 .. (64 >> splitLg) - 1 --, i = ((b >> (3 + splitLg)) << 3) |
-  // (b & 7), part (b >> 3) & (parts - 1), so a packet's parts run on one XCD; the regular
-  // workgroups follow, and those of split packets render nothing.
+  // A single frame's costliest packets first (A.numSplit, measured-cost scheduling): the
+  // launch's first numSplit workgroups render the work items splitList[b] = (packet << 8) | (part
+  // << 4) | lg -- part `part` of 2^lg of the packet: its rays part * (64 >> lg) .. on lanes 0 ..
+  // (64 >> lg) - 1 (lg = 0: the whole packet) --, ~0u an empty item (numSplit is a multiple of 8);
+  // the regular workgroups follow, and those of the listed packets render nothing.
   uint32_t bx = blockIdx.x;
-  int partSel = -1;  // (part << 8) | splitLg for a split packet's part, -1 for a whole packet
+  int partSel = -1;  // (part << 8) | lg for a listed item, -1 for a regular workgroup
   uint32_t splitP = 0u;
+  bool emptyItem = false;
   if constexpr (wavewg) {
-    const uint32_t ns = A.numSplit << A.splitLg;
-    if (bx < ns) {
-      const uint32_t lg = (uint32_t)A.splitLg;
-      partSel = (int)((((bx >> 3) & ((1u << lg) - 1u)) << 8) | lg);
-      splitP = scalar_word(A.splitList, ((bx >> (3 + lg)) << 3) | (bx & 7u));
+    if (bx < A.numSplit) {
+      const uint32_t item = scalar_word(A.splitList, bx);
+      emptyItem = item == ~0u;
+      partSel = emptyItem ? 0 : (int)((((item >> 4) & 15u) << 8) | (item & 15u));
+      splitP = emptyItem ? 0u : item >> 8;
     } else {
-      bx -= ns;
+      bx -= A.numSplit;
     }
   }
   uint32_t wg = split ? (((bx >> 3) / kNwb) << 3) | (bx & 7u) : bx;
@@ -2267,7 +2268,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
         const int pl = partSel & 255, pn = 64 >> pl;  // a split packet's part: pn rays
         Pixel ppx = pixel_of(A, pblk, pw * 64 + (partSel < 0 ? (ltid & 63) : ((partSel >> 8) * pn) | (ltid & (pn - 1))));
         if (partSel >= 0) ppx.active = ppx.active && (ltid & 63) < pn;
-        if (splitAway) ppx.active = false;
+        if (splitAway || emptyItem) ppx.active = false;
         launched += (uint32_t)__popcll(__ballot(ppx.active));
         T.frame = frame;
         render_pixel_coop<OPT>(A, T, ppx, th_p, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
@@ -2348,7 +2349,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
     prev = (uint32_t)__shfl((int)prev, 0, 64);
     if (prev == (blockDim.x >> 6) - 1u) {
       if (A.counters) flush_counters(A, s_cnt, lane);
-      if (A.schedCost && lane == 0 && (wavewg || wwave == 0) && !splitAway) {  // this workgroup's duration, for the next launches' order
+      if (A.schedCost && lane == 0 && (wavewg || wwave == 0) && !splitAway && !emptyItem) {  // this workgroup's duration, for the next launches' order
         // per packet (4 per block; a 256-thread workgroup's in its first packet's slot), a split
         // packet's part counted for the whole packet (parts x its duration)
         uint64_t dt = wall_clock64() - c0;
@@ -2556,7 +2557,7 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(numBlocks), dim3(256), 0, s, A);
     numBlocks = A.numTiles * 16;
   } else {
-    const int split = threads == 64 ? (int)(A.numSplit << A.splitLg) : 0;  // split packets' parts first
+    const int split = threads == 64 ? (int)A.numSplit : 0;  // the listed work items first
     hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads) + split, A.numSamples), dim3(threads), 0, s, A);
   }
   // progressive batch: the lerp chain over the frames' samples (chained frames lerp in k_render)

@@ -150,14 +150,13 @@ int irt_debug_sched(irt_context *ctx, int *policy, int *lastApplied, long long *
 int irt_debug_set_wg_trace(irt_context *ctx, uint32_t *trace);
 /* Workgroups one launch of numTiles 64x64 tiles x numFrames frames runs with this context's
  * variant and settings, at most (the size irt_debug_set_wg_trace's buffer needs, in units of 4
- * words; with measured-cost scheduling a single frame adds up to 1024 << splitLg workgroups for
- * its split packets, which come first; rows a launch does not use stay as they were). */
+ * words; with measured-cost scheduling a single frame adds up to 4096 workgroups for its work
+ * items, which come first; rows a launch does not use stay as they were). */
 long long irt_debug_launch_workgroups(const irt_context *ctx, int numTiles, int numFrames);
-/* Measured-cost scheduling's split packets (IRT_SCHED; on by default for scenes with holes): the
- * last launch's number of packets rendered in 2^splitLg parts of 64 >> splitLg rays each, the
- * costliest ones -- over IRT_SPLIT_FACTOR (1.5) x the median packet's duration, at most 1024 and a
- * tenth of the frame --, first, in quarters by default (0: none;
- * IRT_SPLIT_LG=0 turns splitting off).  Frames are unchanged. */
+/* Measured-cost scheduling (IRT_SCHED; on by default for scenes with holes): the last launch's
+ * split packets -- those longer than IRT_SPLIT_FACTOR (1) x the frame's ideal span (the packets'
+ * durations over the resident slots), rendered first in 2^splitLg parts of 64 >> splitLg rays
+ * (IRT_SPLIT_LG, default 2; 0: no splits) -- and splitLg.  Frames are unchanged. */
 int irt_debug_sched_split(const irt_context *ctx, int *numSplit, int *splitLg);
 /* Chained progressive frames on (default; IRT_CHAIN=0 turns it off per context) or off: a
  * launch of several frames (irt_render_accumulate, irt_render_tiles_accumulate,

@@ -2,10 +2,10 @@
 
 Single frames of a scene with holes run in measured-cost order by default: every 8th launch
 records each packet's duration, and later launches start the costliest 64x64 tiles first and
-render the costliest packets (over IRT_SPLIT_FACTOR x the median) in 2^splitLg parts of
-64 >> splitLg rays, one one-wave workgroup each, ahead of the rest.  Only the lane layout
-changes, so every frame and every count must equal an unscheduled context's.  IRT_SPLIT_FACTOR=0
-splits the costliest packets whatever their cost (up to a tenth of the frame).
+render the packets longer than IRT_SPLIT_FACTOR x the frame's ideal span ahead of the rest, in
+2^splitLg parts of 64 >> splitLg rays, one one-wave workgroup each.  Only the lane layout
+changes, so every frame and every count must equal an unscheduled context's.  A tiny
+IRT_SPLIT_FACTOR splits the costliest tenth of the packets whatever their cost.
 """
 import numpy as np
 import pytest
@@ -40,7 +40,7 @@ def test_split_packets_equal_unscheduled(monkeypatch, terrain, lg):
     monkeypatch.setenv("IRT_SCHED", "0")
     ref_ctx = irt.Context(cells, 0)
     monkeypatch.setenv("IRT_SCHED", "1")  # the default for terrain; forced on the flat grid
-    monkeypatch.setenv("IRT_SPLIT_FACTOR", "0")
+    monkeypatch.setenv("IRT_SPLIT_FACTOR", "1e-6")
     monkeypatch.setenv("IRT_SPLIT_LG", str(lg))
     ctx = irt.Context(cells, 0)
     for c in (ref_ctx, ctx):
