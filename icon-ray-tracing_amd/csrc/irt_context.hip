@@ -703,11 +703,11 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   bool copyCosts = false;
   if (c->schedOn && numFrames == 1 && numBlocks > 0 && !dList && !queued) {
     int rc = sched_prepare(c, numBlocks, W, H, packed, tileBegin, tileStride, numTiles, lp,
-                           render_wg_per_block(A, c->variant) == 4, s);
+                           render_split_ok(A, c->variant), s);
     if (rc) return rc;
     const uint32_t *ob = c->d_schedOrder + (size_t)c->schedBuf * sched_stride(c->schedCap);
     A.schedOrder = c->schedOrderValid ? ob : nullptr;
-    if (c->schedOrderValid && c->schedSplit[c->schedBuf] && render_wg_per_block(A, c->variant) == 4 &&
+    if (c->schedOrderValid && c->schedSplit[c->schedBuf] && render_split_ok(A, c->variant) &&
         c->probeExit == 0) {
       A.splitList = ob + c->schedCap;
       A.splitMask = ob + c->schedCap + kMaxSplit;

@@ -170,6 +170,9 @@ int render_wg_per_block(const RenderArgs &A, int variant);
 // the cooperative user-geometry sphere-accel kernels with 256-thread workgroups
 bool render_queue_ok(const RenderArgs &A, int variant);
 bool render_queue_compiled();  // the A/B library (make VARIANTS=all) only
+// whether a single frame of `variant` can run measured-cost work items (RenderArgs::splitList):
+// the default kernels with one-wave workgroups
+bool render_split_ok(const RenderArgs &A, int variant);
 // workgroups a persistent launch of `variant` runs on a device with numCU compute units:
 // every slot the kernel's occupancy allows (resident at once), at most `numBlocks`
 int render_queue_wgs(const RenderArgs &A, int variant, int numCU, int numBlocks);

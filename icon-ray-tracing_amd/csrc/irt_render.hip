@@ -64,6 +64,8 @@ enum : int {
                             // sample's header, so that the next round's header read hits L2
   OPT_WAVEWG2 = 536870912,  // (A/B, with OPT_LEAN) two-wave workgroups: a block's packets in pairs
                             // (each pair sharing a CU's L1), a slot freed per two waves
+  OPT_SPLIT = 8,  // measured-cost work items (RenderArgs::splitList): the launches of a single frame
+                  // that split packets run this instantiation of the default kernels (kernel_for)
   OPT_ACCPF = 16,  // (A/B, with OPT_LEAN) a single frame's (or a chain's first frame's) accum pixel
                    // fetched into LDS by LDS-DMA at the wave's start, not loaded at the ray's end
   OPT_DPPSCAN = 32,  // (A/B) groups of 2, 4, 16 and 64 lanes take the round's prefix t0 - d0 - ... - dk
@@ -2178,7 +2180,8 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   int partSel = -1;  // (part << 8) | lg for a listed item, -1 for a regular workgroup
   uint32_t splitP = 0u;
   bool emptyItem = false;
-  if constexpr (wavewg) {
+  constexpr bool splitOk = wavewg && (OPT & OPT_SPLIT) != 0;
+  if constexpr (splitOk) {
     if (bx < A.numSplit) {
       const uint32_t item = scalar_word(A.splitList, bx);
       emptyItem = item == ~0u;
@@ -2209,7 +2212,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   const uint32_t blk = partSel >= 0 ? splitP >> 2 : A.schedOrder ? scalar_word(A.schedOrder, wg) : wg;  // uniform: an SGPR
   // a split packet's regular workgroup: nothing to render (its counts and trace are still written)
   const uint32_t pkt = blk * 4u + (uint32_t)wwave;
-  const bool splitAway = wavewg && partSel < 0 && A.numSplit && ((scalar_word(A.splitMask, pkt >> 5) >> (pkt & 31u)) & 1u);
+  const bool splitAway = splitOk && partSel < 0 && ((scalar_word(A.splitMask, pkt >> 5) >> (pkt & 31u)) & 1u);
   uint32_t launched = 0u;  // rays of this wave's pixels (uniform)
   bool pxActive = false;   // the one-lane-per-ray kernel's pixel
   if constexpr (Tracer<OPT>::kCoop) {
@@ -2509,6 +2512,10 @@ int render_wg_per_block(const RenderArgs &A, int variant) {
 constexpr int kNoQueue = OPT_WAVEWG | OPT_WAVEWG2 | OPT_SERIAL | OPT_STATS | OPT_TIMING | OPT_HDRLDS;
 // Persistent launches (OPT_QUEUE, 3-4x slower: DESIGN.md section 5) are compiled into the A/B
 // library only (make VARIANTS=all); the product library has no persistent kernel.
+bool render_split_ok(const RenderArgs &A, int variant) {
+  return (variant == kDefaultVariant || variant == (kDefaultVariant | kNoMissBit)) && render_wg_per_block(A, variant) == 4;
+}
+
 bool render_queue_compiled() {
 #ifdef IRT_ALL_VARIANTS
   return true;
@@ -2546,6 +2553,9 @@ RenderKernel kernel_for(const RenderArgs &A, int &threads) {
   if constexpr ((K & kNoQueue) == 0)
     if (A.queue) return k_render<K | OPT_QUEUE>;
 #endif
+  // a single frame with measured-cost work items: the default kernels' split-capable form
+  if constexpr (K == (kDefaultVariant & ~OPT_MONO) || K == ((kDefaultVariant | kNoMissBit) & ~OPT_MONO))
+    if (A.numSplit) return k_render<K | OPT_SPLIT>;
   return k_render<K>;
 }
 
@@ -2557,7 +2567,7 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(numBlocks), dim3(256), 0, s, A);
     numBlocks = A.numTiles * 16;
   } else {
-    const int split = threads == 64 ? (int)A.numSplit : 0;  // the listed work items first
+    const int split = A.numSplit ? (int)A.numSplit : 0;  // the listed work items first (kernel_for: OPT_SPLIT)
     hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads) + split, A.numSamples), dim3(threads), 0, s, A);
   }
   // progressive batch: the lerp chain over the frames' samples (chained frames lerp in k_render)
@@ -2600,6 +2610,10 @@ void prewarm_variant(hipStream_t s) {
   int threads = 256;
   const RenderKernel k = kernel_for<N>(A, threads);  // sets threads (64 for one-wave workgroups)
   hipLaunchKernelGGL(k, dim3(1), dim3(threads), 0, s, A);
+  A.numSplit = 8;  // the split-capable form of the default kernels (never read: it returns first)
+  const RenderKernel ks = kernel_for<N>(A, threads);
+  if (ks != k) hipLaunchKernelGGL(ks, dim3(1), dim3(threads), 0, s, A);
+  A.numSplit = 0;
   A.queue = reinterpret_cast<uint32_t *>(16);  // never dereferenced: the kernel returns first
   const RenderKernel kq = kernel_for<N>(A, threads);
   if (kq != kernel_for<N>(RenderArgs{}, threads)) hipLaunchKernelGGL(kq, dim3(1), dim3(256), 0, s, A);
