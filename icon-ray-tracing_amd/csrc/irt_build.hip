@@ -19,6 +19,8 @@
 //   7. k_cell_edges  per cell: the radial edges (cells with > kLocalEntries entries: host)
 //   8. k_cell_header per cell: bin ends, sub-cell masks, entry count; scan -> bases
 //   9. k_cell_fill   the fat entries, bin by bin
+//  10. k_slot_fill   (scenes whose cells share their radial edges) the slot table
+//                    (irt_common.h kSlot4), from the headers and entries: build_slots_device
 
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -567,6 +569,71 @@ int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_
   out.entries = numPairs;
   out.binEntries = numFat;
   out.bigCells = numBig;
+  return IRT_OK;
+}
+
+// ---------------------------------------------------------------- the slot table
+// every cell's radial edges (header words 0-2) against cell 0's
+__global__ void k_slot_uniform(const uint32_t *hdr, uint32_t numCells, uint32_t *differs) {
+  const uint32_t e0 = hdr[0], e1 = hdr[1], e2 = hdr[2];
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < numCells; c += gridDim.x * blockDim.x) {
+    const uint32_t *H = hdr + (size_t)c * kBinHdrWords;
+    if (H[0] != e0 || H[1] != e1 || H[2] != e2) atomicOr(differs, 1u);
+  }
+}
+
+// one thread per slot (cell, sub-cell, bin)
+__global__ void k_slot_fill(const uint32_t *hdr, const float *fat, uint32_t numCells, int bins, float4 *slots) {
+  const uint64_t total = (uint64_t)numCells * kSubCells * kSubCells * bins;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(i % bins);
+    const uint64_t cs = i / bins;
+    const int sc = (int)(cs % (kSubCells * kSubCells));
+    const uint64_t c = cs / (kSubCells * kSubCells);
+    float S[4 * kSlot4];
+    slot_fill(hdr + c * kBinHdrWords, fat, sc, b, S);
+    float4 *o = slots + i * kSlot4;
+    for (int k = 0; k < kSlot4; ++k) o[k] = make_float4(S[4 * k], S[4 * k + 1], S[4 * k + 2], S[4 * k + 3]);
+  }
+}
+
+int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells, size_t maxBytes, hipStream_t s,
+                       SlotTable &out) {
+  out = SlotTable{};
+  if (numCells == 0) return IRT_OK;
+  uint32_t e[3];
+  int rc;
+  if ((rc = read_back(e, hdr, 3, s))) return rc;
+  Scratch S;
+  uint32_t *differs;
+  BHIP(S.alloc(&differs, 1));
+  BHIP(hipMemsetAsync(differs, 0, sizeof(uint32_t), s));
+  hipLaunchKernelGGL(k_slot_uniform, dim3(grid_for(numCells)), dim3(256), 0, s, hdr, numCells, differs);
+  BHIP(hipGetLastError());
+  uint32_t d = 0;
+  if ((rc = read_back(&d, differs, 1, s))) return rc;
+  if (d) return IRT_OK;
+  int ne = 0;
+  while (ne < kMaxEdges && !__builtin_isinf(u2f(e[ne]))) ++ne;
+  const int bins = ne + 1;
+  const size_t bytes = (size_t)numCells * kSubCells * kSubCells * bins * kSlot4 * sizeof(float4);
+  if (bytes > maxBytes) return IRT_OK;
+  float4 *slots = nullptr;
+  if (hipMalloc((void **)&slots, bytes) != hipSuccess) {
+    (void)hipGetLastError();  // not enough memory: the scene renders without the table
+    return IRT_OK;
+  }
+  hipLaunchKernelGGL(k_slot_fill, dim3(std::min<uint64_t>(grid_for(bytes / (kSlot4 * sizeof(float4))), 1u << 20)),
+                     dim3(256), 0, s, hdr, reinterpret_cast<const float *>(fat), numCells, bins, slots);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+    (void)hipFree(slots);
+    set_error("slot table build failed");
+    return IRT_E_HIP;
+  }
+  out.slots = slots;
+  out.bins = bins;
+  out.bytes = bytes;
+  for (int k = 0; k < kMaxEdges; ++k) out.edges[k] = u2f(e[k]);
   return IRT_OK;
 }
 

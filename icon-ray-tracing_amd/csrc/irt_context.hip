@@ -40,6 +40,7 @@ struct irt_context {
   uint4 *d_binHdr = nullptr;   // binned locator (irt_common.h)
   float4 *d_fat = nullptr;
   float4 *d_blocks = nullptr;
+  SlotTable slot;              // the slot table (irt_common.h kSlot4; IRT_SLOTS=0: none)
   size_t binEntries = 0;       // fat entries
   uint32_t numSph = 0;         // zero-thickness records (spheres): distinct radii
   uint32_t numSphRec = 0;      // ... and records
@@ -238,7 +239,7 @@ int upload(irt_context *c, T **p, const T *src, size_t count) {
 void free_all(irt_context *c) {
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void *ptrs[] = {c->d_binHdr, c->d_fat, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
+  void *ptrs[] = {c->d_binHdr, c->d_fat, c->slot.slots, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
                   c->d_sphBits, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_gridBits, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
                   c->d_lut, c->d_counters, c->d_counterBuckets, c->d_meta, c->d_queue, c->d_chainFlag,
                   c->d_frameCams};
@@ -651,6 +652,9 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.binHdr = c->d_binHdr;
   A.fat = c->d_fat;
   A.blocks = c->d_blocks;
+  A.slots = c->slot.slots;
+  A.slotBins = c->slot.bins;
+  for (int k = 0; k < 3; ++k) A.slotEdge[k] = c->slot.edges[k];
   A.numSph = c->numSph;
   A.sphR = c->d_sphR;
   A.sphOff = c->d_sphOff;
@@ -1110,6 +1114,24 @@ int irt_create_end(irt_context *c) {
   c->info.locatorEntries = D.entries;
   c->binEntries = D.binEntries;
   mark("device scene build");
+  // the slot table, when the cells share their radial edges, their headers outgrow the
+  // last-level cache (kSlotAutoHdrBytes) and it fits: at most IRT_SLOTS_MAX_GB (default: the
+  // device's free memory less 16 GiB); IRT_SLOTS=1: whatever the headers' size, 0: none
+  {
+    const char *e = getenv("IRT_SLOTS");
+    const size_t hdrBytes = (size_t)6 * c->G * c->G * kBinHdrWords * 4;
+    if (e ? atoi(e) != 0 : hdrBytes > kSlotAutoHdrBytes) {
+      size_t fr = 0, tot = 0;
+      IRT_HIP(hipMemGetInfo(&fr, &tot));
+      size_t cap = fr > ((size_t)16 << 30) ? fr - ((size_t)16 << 30) : 0;
+      if (const char *g = getenv("IRT_SLOTS_MAX_GB")) cap = std::min(cap, (size_t)(atof(g) * (double)(1ull << 30)));
+      if ((rc = build_slots_device(reinterpret_cast<const uint32_t *>(c->d_binHdr), c->d_fat, 6u * c->G * c->G, cap,
+                                   c->stream, c->slot)))
+        return rc;
+      c->bytes += c->slot.bytes;
+    }
+  }
+  mark("slot table");
   // zero-thickness records (spheres): sorted by (radius, record) -- see host/irt_scene.cpp
   {
     std::sort(c->sph.begin(), c->sph.end(), [](const irt_context::Sphere &a, const irt_context::Sphere &b) {
@@ -1816,6 +1838,9 @@ static int debug_locate(irt_context *c, const float *xyz, int n, int *found, flo
   A.binHdr = c->d_binHdr;
   A.fat = c->d_fat;
   A.blocks = c->d_blocks;
+  A.slots = c->slot.slots;
+  A.slotBins = c->slot.bins;
+  for (int k = 0; k < 3; ++k) A.slotEdge[k] = c->slot.edges[k];
   A.numSph = c->numSph;
   A.sphR = c->d_sphR;
   A.sphOff = c->d_sphOff;
@@ -1888,6 +1913,7 @@ extern "C" int irt_debug_context_array(const irt_context *c, int which, void *ds
     case IRT_DEBUG_ARRAY_SPH_OFF: src = c->d_sphOff; n = c->numSph ? ((size_t)c->numSph + 1) * 4 : 4; break;
     case IRT_DEBUG_ARRAY_SPH_REC: src = c->d_sphRec; n = (size_t)c->numSphRec * 8; break;
     case IRT_DEBUG_ARRAY_SPH_BITS: src = c->d_sphBits; n = (size_t)kSphBitWords * 4; break;
+    case IRT_DEBUG_ARRAY_SLOTS: src = c->slot.slots; n = c->slot.bytes; break;
     default:
       set_error("irt_debug_context_array: unknown array %d", which);
       return IRT_E_INVALID;

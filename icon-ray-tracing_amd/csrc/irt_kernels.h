@@ -128,6 +128,12 @@ struct RenderArgs {
   const uint32_t *splitList;
   const uint32_t *splitMask;
   uint32_t numSplit;
+  // the slot table (irt_common.h kSlot4; null: none -- the scene's cells do not share their
+  // radial edges, or IRT_SLOTS=0): slotEdge = the shared edges, slotBins = bins per sub-cell.
+  // Launches with a table run the default kernels' OPT_SLOT form (kernel_for).
+  const float4 *slots;
+  float slotEdge[3];
+  int slotBins;
 };
 // a persistent launch's queue words (irt_render.hip queue_take): 8 per-XCD counters and the
 // done count, each on its own 128-B line
@@ -211,6 +217,19 @@ struct DeviceScene {
 };
 int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_t n, size_t numRuns,
                        int G, hipStream_t s, DeviceScene &out);
+// The slot table (irt_common.h kSlot4) of a built scene whose cells all share their radial
+// edges, if it fits in maxBytes (and the device's free memory); otherwise slots stays null.
+struct SlotTable {
+  float4 *slots = nullptr;
+  int bins = 0;
+  float edges[3] = {0.f, 0.f, 0.f};
+  size_t bytes = 0;
+};
+// Round 5: with the table C5 -9 %, C3s -3 %, but C3 +4 %, C4 +3 % (profiles/r05aa/): on by
+// default only when the headers exceed the 256-MB last-level cache (C5: 2.7 GB; C3: 167 MB)
+constexpr size_t kSlotAutoHdrBytes = (size_t)256 << 20;
+int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells, size_t maxBytes, hipStream_t s,
+                       SlotTable &out);
 void launch_unpack(const uint32_t *gathered, int numRanks, int maxTiles, int W, int H,
                    uint32_t *fb, hipStream_t s, const int32_t *table = nullptr);
 

@@ -81,6 +81,10 @@ enum : int {
   OPT_PAIR = 268435456,  // (A/B) the wave-wide scan's first step tests each lane's first two
                          // candidates (both entries gathered together), so the dealt-out step
                          // runs only for lanes whose first two fail
+  OPT_SLOT = 128,  // the wave-wide scan starts from the slot table (RenderArgs::slots, irt_common.h
+                   // kSlot4): the first admitted candidate and the list's position in one gather,
+                   // instead of the header, then the entry; launches on a scene with a table run
+                   // this instantiation of the default kernels (kernel_for)
   // bits 8-11: minimum waves per SIMD asked of the register allocator (0: none)
 };
 
@@ -655,11 +659,32 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     uint32_t M = 0u, cell = 0u, sub = 0u;
     uint32_t tv = 0u;  // OPT_NEXTHDR's loaded word, consumed after the scan
     uint32_t fe2 = 0u; // OPT_PAIR: the pass's second candidate entry
+    constexpr bool kSlot = (OPT & OPT_SLOT) != 0;
+    static_assert(!kSlot || (OPT & (OPT_HDRLDS | OPT_PAIR | OPT_DEALALL | OPT_NEXTHDR)) == 0, "slot table: the default scan");
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, sm = s0;  // OPT_SLOT: the first candidate
     if constexpr ((OPT & OPT_HDRLDS) != 0) {
       if (want) cell = cubemap_cell_fast(px, py, pz, A.G, sub);
       stage_headers(want, cell, sub, H0, H1, M);
     }
-    if (want) {
+    if (kSlot && want) {
+      // the slot of the sample's (cell, sub-cell, bin): the bins from the scene's shared edges
+      const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
+      cell = cubemap_cell_fast(px, py, pz, A.G, sub);
+      const float e0 = A.slotEdge[0], e1 = A.slotEdge[1], e2 = A.slotEdge[2];
+      const int b = bin_of(r, e0, e1, e2);
+      const float4 *S = A.slots + ((size_t)(cell * (uint32_t)(kSubCells * kSubCells) + sub) * (uint32_t)A.slotBins + (uint32_t)b) * kSlot4;
+      s0 = S[0];
+      s1 = S[1];
+      s2 = S[2];
+      sm = S[3];
+      const uint4 info = reinterpret_cast<const uint4 *>(S)[4];
+      const float eb = b == 0 ? e0 : (b == 1 ? e1 : e2);
+      edge = b < kMaxEdges && r == eb;
+      c = info.x;
+      lds_st16(&W.pt[lane], make_float4(px, py, pz, r));
+      lds_st16(&W.lst[lane], make_uint4(info.y, info.z, 0u, 0xFFFFFFFFu));
+      fr = r;
+    } else if (want) {
       const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
       if constexpr ((OPT & OPT_HDRLDS) == 0) {
         cell = cubemap_cell_fast(px, py, pz, A.G, sub);
@@ -724,7 +749,13 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         }
       } else if ((OPT & OPT_DEALALL) == 0 && c > 0u) {  // (from registers: no LDS round trip before the gather)
         Found f;
-        const bool ok = pass_entry(A.fat + (size_t)fe * kFatStride4, px, py, pz, fr, f);
+        bool ok;
+        if (kSlot && pass == 0) {  // the slot's copy
+          f = {__float_as_uint(sm.z), record_path(__float_as_uint(sm.w), sm.x, sm.y, fr)};
+          ok = entry_passes(s0, s1, s2, sm, px, py, pz, fr);
+        } else {
+          ok = pass_entry(A.fat + (size_t)fe * kFatStride4, px, py, pz, fr, f);
+        }
         if (f.rec < flim) {  // scan_fat stops, uncounted, at the first record >= the limit
           ++specCand;
           if (ok) {
@@ -2419,6 +2450,7 @@ __global__ void __launch_bounds__(256) k_debug_locate(RenderArgs A, const float 
 // The same points through the cooperative kernel's wave-wide candidate scan
 // (Tracer::locate_wave; every lane of a wave calls it, lanes past n with want = false):
 // pins its dealt-out candidates and its second pass on radial bin edges to the serial path.
+template <int O>
 __global__ void __launch_bounds__(256) k_debug_locate_wave(RenderArgs A, const float *xyz, int n,
                                                            int *found, float *value) {
   __shared__ uint32_t s_sph[kSphBitWords];
@@ -2428,8 +2460,8 @@ __global__ void __launch_bounds__(256) k_debug_locate_wave(RenderArgs A, const f
   for (int i = threadIdx.x; i < kSphBitWords; i += 256) s_sph[i] = A.numSph ? A.sphBits[i] : 0u;
   if (threadIdx.x < kCnt) s_cnt[threadIdx.x] = 0;
   __syncthreads();
-  Tracer<kDefaultVariant & ~4096> T{{}, A, nullptr, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
-  static_assert(Tracer<kDefaultVariant & ~4096>::kWaveScan, "the default kernel scans wave-wide");
+  Tracer<O> T{{}, A, nullptr, s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
+  static_assert(Tracer<O>::kWaveScan, "the default kernel scans wave-wide");
   const int j = (int)(blockIdx.x * 256 + threadIdx.x);
   const bool want = j < n;
   float x = 0.f, y = 0.f, z = 0.f;
@@ -2449,8 +2481,11 @@ __global__ void __launch_bounds__(256) k_debug_locate_wave(RenderArgs A, const f
 void launch_debug_locate(const RenderArgs &A, const float *xyz, int n, int *found, float *value,
                          hipStream_t s, bool wave) {
   if (n <= 0) return;
-  if (wave)
-    hipLaunchKernelGGL(k_debug_locate_wave, dim3((n + 255) / 256), dim3(256), 0, s, A, xyz, n, found, value);
+  constexpr int D = kDefaultVariant & ~4096;
+  if (wave && A.slots)  // the scan from the slot table (OPT_SLOT), as the scene's launches run it
+    hipLaunchKernelGGL(k_debug_locate_wave<D | OPT_SLOT>, dim3((n + 255) / 256), dim3(256), 0, s, A, xyz, n, found, value);
+  else if (wave)
+    hipLaunchKernelGGL(k_debug_locate_wave<D>, dim3((n + 255) / 256), dim3(256), 0, s, A, xyz, n, found, value);
   else
     hipLaunchKernelGGL(k_debug_locate, dim3((n + 255) / 256), dim3(256), 0, s, A, xyz, n, found, value);
 }
@@ -2554,8 +2589,11 @@ RenderKernel kernel_for(const RenderArgs &A, int &threads) {
     if (A.queue) return k_render<K | OPT_QUEUE>;
 #endif
   // a single frame with measured-cost work items: the default kernels' split-capable form
-  if constexpr (K == (kDefaultVariant & ~OPT_MONO) || K == ((kDefaultVariant | kNoMissBit) & ~OPT_MONO))
+  // and a scene with a slot table: their OPT_SLOT form
+  if constexpr (K == (kDefaultVariant & ~OPT_MONO) || K == ((kDefaultVariant | kNoMissBit) & ~OPT_MONO)) {
+    if (A.slots) return A.numSplit ? k_render<K | OPT_SPLIT | OPT_SLOT> : k_render<K | OPT_SLOT>;
     if (A.numSplit) return k_render<K | OPT_SPLIT>;
+  }
   return k_render<K>;
 }
 
@@ -2613,7 +2651,13 @@ void prewarm_variant(hipStream_t s) {
   A.numSplit = 8;  // the split-capable form of the default kernels (never read: it returns first)
   const RenderKernel ks = kernel_for<N>(A, threads);
   if (ks != k) hipLaunchKernelGGL(ks, dim3(1), dim3(threads), 0, s, A);
+  A.slots = reinterpret_cast<const float4 *>(16);  // and the slot-table forms (never dereferenced)
+  const RenderKernel kts = kernel_for<N>(A, threads);
+  if (kts != ks) hipLaunchKernelGGL(kts, dim3(1), dim3(threads), 0, s, A);
   A.numSplit = 0;
+  const RenderKernel kt = kernel_for<N>(A, threads);
+  if (kt != k) hipLaunchKernelGGL(kt, dim3(1), dim3(threads), 0, s, A);
+  A.slots = nullptr;
   A.queue = reinterpret_cast<uint32_t *>(16);  // never dereferenced: the kernel returns first
   const RenderKernel kq = kernel_for<N>(A, threads);
   if (kq != kernel_for<N>(RenderArgs{}, threads)) hipLaunchKernelGGL(kq, dim3(1), dim3(256), 0, s, A);

@@ -447,14 +447,18 @@ def setup_frame(cells: np.ndarray, width: int, height: int, camera=None,
 # scene arrays the render kernel reads (irt_debug_context_array / irt_debug_scene_array)
 SCENE_ARRAYS = {"bin_hdr": 0, "fat": 1, "blocks": 2, "sph_r": 3, "sph_off": 4, "sph_rec": 5,
                 "sph_bits": 6}
+# ... and those only a context holds: the slot table (irt_common.h kSlot4; empty when the
+# scene's cells do not share their radial edges, or with IRT_SLOTS=0)
+CONTEXT_ARRAYS = {"slots": 7}
 
 
 def _array(fn, h, name):
+    which = SCENE_ARRAYS[name] if name in SCENE_ARRAYS else CONTEXT_ARRAYS[name]
     n = C.c_size_t()
-    _check(fn(h, SCENE_ARRAYS[name], None, 0, C.byref(n)), "scene array")
-    out = np.zeros(n.value, np.uint8)
-    _check(fn(h, SCENE_ARRAYS[name], _ptr(out), n.value, C.byref(n)), "scene array")
-    return out
+    _check(fn(h, which, None, 0, C.byref(n)), "scene array")
+    out = np.zeros(max(n.value, 1), np.uint8)
+    _check(fn(h, which, _ptr(out), n.value, C.byref(n)), "scene array")
+    return out[:n.value]
 
 
 # ----------------------------------------------------------------------- GPU context
@@ -513,6 +517,13 @@ class Context:
     def array(self, name: str) -> np.ndarray:
         """A scene array as the device built it (bytes; irt_debug_context_array)."""
         return _array(lib().irt_debug_context_array, self._h, name)
+
+    def array_bytes(self, name: str) -> int:
+        """The size of a scene array, without copying it."""
+        which = SCENE_ARRAYS[name] if name in SCENE_ARRAYS else CONTEXT_ARRAYS[name]
+        n = C.c_size_t()
+        _check(lib().irt_debug_context_array(self._h, which, None, 0, C.byref(n)), "scene array")
+        return n.value
 
     def close(self):
         if getattr(self, "_h", None):

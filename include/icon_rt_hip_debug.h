@@ -72,12 +72,14 @@ int irt_debug_intersect_wedge(const float *v24, irt_vec3f p, float *value);
  * only *bytes is set. */
 enum {
   IRT_DEBUG_ARRAY_BIN_HDR = 0,  /* cube-map cell headers, kBinHdrWords u32 each */
-  IRT_DEBUG_ARRAY_FAT = 1,      /* fat candidate entries, 80 B each */
+  IRT_DEBUG_ARRAY_FAT = 1,      /* fat candidate entries, 64 B each */
   IRT_DEBUG_ARRAY_BLOCKS = 2,   /* per-record height/value blocks, 256 B each */
   IRT_DEBUG_ARRAY_SPH_R = 3,    /* sphere radii (f32) */
   IRT_DEBUG_ARRAY_SPH_OFF = 4,  /* CSR offsets (u32) */
   IRT_DEBUG_ARRAY_SPH_REC = 5,  /* (record, numLayers) u32 pairs */
-  IRT_DEBUG_ARRAY_SPH_BITS = 6  /* radius hash bitmap (u32) */
+  IRT_DEBUG_ARRAY_SPH_BITS = 6, /* radius hash bitmap (u32) */
+  IRT_DEBUG_ARRAY_SLOTS = 7     /* the slot table (irt_common.h kSlot4), 128 B per (cell, sub-cell,
+                                   bin); 0 bytes when the scene has none (context only) */
 };
 int irt_debug_context_array(const irt_context *ctx, int which, void *dst, size_t capacity,
                             size_t *bytes);

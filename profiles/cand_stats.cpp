@@ -40,6 +40,7 @@ int main(int argc, char **argv) {
   std::uniform_real_distribution<double> U(0.0, 1.0);
   const float R = 6371229.f;
   long found = 0, hist[17] = {0}, tested = 0, admitted = 0, firstPass = 0;
+  long failRadial = 0, failPlane = 0, testedHalf = 0, admittedHalf = 0, binFirst = 0, quadFirst = 0;
   for (long i = 0; i < npts; ++i) {
     const double z = 2 * U(rng) - 1, ph = 2 * M_PI * U(rng), rr = sqrt(1 - z * z);
     const float r0 = R + (float)(U(rng) * top);
@@ -51,22 +52,56 @@ int main(int argc, char **argv) {
     const int b = bin_of(r, u2f(h[0]), u2f(h[1]), u2f(h[2]));
     const uint32_t beg = h[3] + (b ? h[4 + b - 1] : 0), end = h[3] + h[4 + b];
     const uint32_t mask = (h[8 + sub] >> (8 * b)) & 0xFFu;
-    int adm = 0, t = 0, hit = -1;
+    // a radial half mask: the bin split at the midpoint of its entries' radial extent (clipped
+    // to the bin); below it only candidates with h0 < mid, above only those with hN >= mid
+    float lo = INFINITY, hi = -INFINITY;
+    for (uint32_t q = beg; q < end; ++q) {
+      lo = fminf(lo, F[(size_t)q * 16 + 12]);
+      hi = fmaxf(hi, F[(size_t)q * 16 + 13]);
+    }
+    if (b > 0) lo = fmaxf(lo, u2f(h[b - 1]));
+    if (b < 3) hi = fminf(hi, u2f(h[b]));
+    const float mid = 0.5f * (lo + hi);
+    int adm = 0, t = 0, hit = -1, admH = 0, tH = 0, hitH = -1;
+    // the union of the masks of the sub-cell's 2 x 2 quad (kSub = 4: quads of sub-cells)
+    const uint32_t si = sub % kSub, sj = sub / kSub, q0 = (sj & ~1u) * kSub + (si & ~1u);
+    const uint32_t qmask = ((h[8 + q0] | h[8 + q0 + 1] | h[8 + q0 + kSub] | h[8 + q0 + kSub + 1]) >> (8 * b)) & 0xFFu;
+    int qj = -1;  // the quad's first admitted candidate
+    for (uint32_t j = 0; beg + j < end && qj < 0; ++j)
+      if (j >= (uint32_t)kMaskCand || ((qmask >> j) & 1u)) qj = (int)j;
     for (uint32_t j = 0; beg + j < end; ++j) {
       if (j < (uint32_t)kMaskCand && !((mask >> j) & 1u)) continue;
       ++adm;
       const float *e = &F[(size_t)(beg + j) * 16];
+      const bool rad = !(r < e[12] || r > e[13]);
+      bool ok = rad;
+      for (int k = 0; ok && k < 3; ++k)
+        if (eval_plane(e + 4 * k, px, py, pz) > 0.f) ok = false;
       if (hit < 0) {
         ++t;
-        bool ok = !(r < e[12] || r > e[13]);
-        for (int k = 0; ok && k < 3; ++k)
-          if (eval_plane(e + 4 * k, px, py, pz) > 0.f) ok = false;
+        if (!ok) ++(rad ? failPlane : failRadial);
         if (ok) hit = adm;
+      }
+      if (j == 0 && ok) ++binFirst;
+      if ((int)j == qj && ok) ++quadFirst;  // the bin's first candidate (unmasked) is the answer
+      const bool half = j >= (uint32_t)kMaskCand || (r < mid ? e[12] < mid : e[13] >= mid);
+      if (half) {
+        ++admH;
+        if (hitH < 0) {
+          ++tH;
+          if (ok) hitH = admH;
+        }
       }
     }
     if (hit < 0) continue;
     ++found;
+    if (hitH < 0) {
+      printf("half mask lost a hit\n");
+      return 1;
+    }
     tested += t;
+    testedHalf += tH;
+    admittedHalf += admH;
     admitted += adm;
     firstPass += hit == 1;
     ++hist[adm < 16 ? adm : 16];
@@ -75,6 +110,11 @@ int main(int argc, char **argv) {
          terrain, G, n, F.size() / 16, found, npts);
   printf("tested per sample %.3f, admitted per sample %.3f, first admitted passes %.3f\n",
          (double)tested / found, (double)admitted / found, (double)firstPass / found);
+  printf("failed tests per sample: radial %.3f, planes %.3f; with a radial half mask: tested %.3f, admitted %.3f\n",
+         (double)failRadial / found, (double)failPlane / found, (double)testedHalf / found,
+         (double)admittedHalf / found);
+  printf("the bin's first candidate is the answer: %.3f; the 2x2 quad's first admitted: %.3f\n",
+         (double)binFirst / found, (double)quadFirst / found);
   printf("admitted histogram:");
   for (int k = 0; k <= 16; ++k)
     if (hist[k]) printf(" %d:%.4f", k, (double)hist[k] / found);

@@ -777,12 +777,25 @@ def test_device_locator_matches_host_restatement(scene, entry):
     irt_debug_locate) and the cooperative kernel's wave-wide scan Tracer::locate_wave
     (irt_debug_locate_wave: dealt-out candidates and the bin-edge pass, many of them in
     one wave here)."""
+    _locator_check(scene, entry)
+
+
+@pytest.mark.parametrize("scene", ["r2b03_l90", "filtered"])
+def test_device_locator_slot_table(monkeypatch, scene):
+    """The same points through the wave-wide scan started from the slot table (OPT_SLOT,
+    irt_common.h kSlot4; forced on these small scenes with IRT_SLOTS=1)."""
+    monkeypatch.setenv("IRT_SLOTS", "1")
+    _locator_check(scene, "irt_debug_locate_wave", slots=True)
+
+
+def _locator_check(scene, entry, slots=False):
     from helpers import locator_points, terrain_cells
     cells = {"r2b03_l90": lambda: irt.synth_grid(2, 3, 90),
              "terrain": lambda: terrain_cells(11),
              "filtered": lambda: irt.filter_cells(irt.synth_grid(2, 3, 40), (-30, 60), (-90, 45))}[scene]()
     pts = locator_points(cells, 5)
     ctx = irt.Context(cells, 0)
+    assert (ctx.array("slots").size > 0) == slots
     D = irt.DebugScene(cells)
     L = irt.lib()
     fn = getattr(L, entry)

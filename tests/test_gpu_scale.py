@@ -88,12 +88,15 @@ def scene(request):
 def test_every_scene_runs_the_default_variant(scene):
     """The default raygen (5 waves/SIMD, no scratch) serves every scene size, the 39 GiB C5
     scene included (irt_context.hip, profiles/r03zg_waves/), in its hole-free form where the
-    scene has no holes (round 5); the frame is the one test_whole_frame_matches_oracle
-    checks."""
+    scene has no holes (round 5), and from the slot table where the headers outgrow the
+    last-level cache (C5; irt_common.h kSlot4); the frame is the one
+    test_whole_frame_matches_oracle checks."""
     import ctypes as C
     L = irt.lib()
     L.irt_debug_get_variant.argtypes = [C.c_void_p]
     v, d = L.irt_debug_get_variant(scene["ctx"]._h), L.irt_debug_default_variant()
+    if not os.environ.get("IRT_SLOTS"):
+        assert (scene["ctx"].array_bytes("slots") > 0) == (scene["name"] == "c5"), scene["name"]
     if os.environ.get("IRT_RENDER_VARIANT"):
         return
     # the hole-free form (no miss mode) on flat grids; the default itself over terrain, whose

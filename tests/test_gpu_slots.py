@@ -1,0 +1,123 @@
+"""The slot table (irt_common.h kSlot4, csrc/irt_build.hip k_slot_fill; Tracer::locate_wave's
+OPT_SLOT form): per (cube-map cell, sub-cell, radial bin) of a scene whose cells share their
+radial edges, the first candidate the sub-cell mask admits and the list's position, so that a
+sample's scan starts with one gather.
+
+Pinned here: the table the device builds equals a numpy restatement from the headers and fat
+entries byte for byte; frames, accumulators and every count equal a context without the table
+(IRT_SLOTS=0); scenes whose cells have their own edges (terrain) get no table; by default only
+scenes whose headers outgrow the last-level cache get one.  The small scenes here force it
+(IRT_SLOTS=1); tests/test_gpu_parity.py::test_device_locator_slot_table runs the wave-wide
+locate through it against the host restatement, test_gpu_scale.py's C5 frames run through it.
+"""
+import numpy as np
+import pytest
+
+import irt
+from helpers import FRAMING, bits
+
+pytestmark = pytest.mark.gpu
+
+_POP = np.array([bin(k).count("1") for k in range(256)], np.uint32)
+_CTZ = np.array([8] + [(k & -k).bit_length() - 1 for k in range(1, 256)], np.uint32)
+
+
+def restate_slots(hdr: np.ndarray, fat: np.ndarray) -> np.ndarray:
+    """irt_common.h slot_fill over every (cell, sub-cell, bin), from the scene's header and
+    fat-entry bytes (kBinHdrWords = 32 with 4 x 4 sub-cells, 16 words per entry)."""
+    H = hdr.view(np.uint32).reshape(-1, 32).astype(np.int64)
+    F = fat.view(np.uint32).reshape(-1, 16)
+    e = H[0, :3]
+    assert (H[:, :3] == e).all(), "cells with their own edges have no table"
+    nb = int(np.sum(e != 0x7F800000)) + 1
+    nsub = 16
+    out = np.zeros((H.shape[0], nsub, nb, 32), np.uint32)
+    for b in range(nb):
+        beg = H[:, 4 + b - 1] if b else np.zeros(H.shape[0], np.int64)
+        n = H[:, 4 + b] - beg
+        lenmask = np.where(n < 8, (1 << np.clip(n, 0, 8)) - 1, 0xFF)
+        for s in range(nsub):
+            m8 = (H[:, 8 + s] >> (8 * b)) & 0xFF & lenmask
+            c = _POP[m8].astype(np.int64) + np.where(n > 8, n - 8, 0)
+            first = H[:, 3] + beg + _CTZ[m8]
+            has = c > 0
+            out[has, s, b, :16] = F[first[has]]
+            out[:, s, b, 16] = c
+            out[:, s, b, 17] = H[:, 3] + beg
+            out[:, s, b, 18] = m8
+    return out.reshape(-1)
+
+
+@pytest.mark.parametrize("bis,levels,noise", [(2, 90, 0.0), (3, 47, 0.2), (3, 20, 0.0)])
+def test_slot_table_restated(monkeypatch, bis, levels, noise):
+    monkeypatch.setenv("IRT_SLOTS", "1")
+    cells = irt.synth_grid(2, bis, levels, noise=noise)
+    ctx = irt.Context(cells, 0)
+    slots = ctx.array("slots")
+    assert slots.size > 0, "a flat grid's cells share their edges"
+    want = restate_slots(ctx.array("bin_hdr"), ctx.array("fat"))
+    got = slots.view(np.uint32)
+    assert got.size == want.size
+    if not np.array_equal(got, want):
+        w = np.nonzero(got != want)[0]
+        raise AssertionError(f"{w.size} words differ, first at {w[0]}")
+    ctx.close()
+
+
+def test_cells_with_own_edges_have_no_table(monkeypatch):
+    monkeypatch.setenv("IRT_SLOTS", "1")
+    ctx = irt.Context(irt.synth_grid(2, 3, 90, terrain=4000.0), 0)
+    assert ctx.array("slots").size == 0
+    ctx.close()
+
+
+def test_slots_off_and_auto(monkeypatch):
+    cells = irt.synth_grid(2, 3, 90)
+    monkeypatch.setenv("IRT_SLOTS", "0")
+    ctx = irt.Context(cells, 0)
+    assert ctx.array("slots").size == 0
+    ctx.close()
+    monkeypatch.delenv("IRT_SLOTS")
+    ctx = irt.Context(cells, 0)  # 1,350 cells of headers: no table by default
+    assert ctx.array("slots").size == 0
+    ctx.close()
+
+
+def _frames(ctx, lp, W, n, batch):
+    import torch
+    fb = torch.zeros(W * W, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(W * W * 4, dtype=torch.float32, device="cuda")
+    out = []
+    for aid in range(0, n, batch):
+        lp.accumID = aid
+        if batch == 1:
+            ctx.render(lp, W, W, fb.data_ptr(), acc.data_ptr())
+        else:
+            ctx.render_accumulate(lp, W, W, batch, fb.data_ptr(), acc.data_ptr())
+        torch.cuda.synchronize()
+        st = ctx.stats()
+        out.append((fb.cpu().numpy().copy(), bits(acc.cpu().numpy()),
+                    (st.raysLaunched, st.raysInBox, st.locateCalls, st.samplesFound, st.candidatesTested)))
+    return out
+
+
+@pytest.mark.parametrize("bis,levels,batch", [(4, 90, 1), (4, 90, 4), (3, 47, 1)])
+def test_frames_equal_without_table(monkeypatch, bis, levels, batch):
+    cells = irt.synth_grid(2, bis, levels, noise=0.1 if levels == 47 else 0.0)
+    W = 320
+    setup = irt.setup_frame(cells, W, W, camera=FRAMING)
+    monkeypatch.setenv("IRT_SLOTS", "0")
+    ref_ctx = irt.Context(cells, 0)
+    monkeypatch.setenv("IRT_SLOTS", "1")
+    ctx = irt.Context(cells, 0)
+    assert ctx.array("slots").size > 0 and ref_ctx.array("slots").size == 0
+    for c in (ref_ctx, ctx):
+        c.set_transfunc(setup.lut, setup.value_range)
+    n = 8
+    ref = _frames(ref_ctx, setup.lp, W, n, batch)
+    got = _frames(ctx, setup.lp, W, n, batch)
+    for k in range(len(ref)):
+        assert np.array_equal(got[k][0], ref[k][0]) and np.array_equal(got[k][1], ref[k][1]), k
+        assert got[k][2] == ref[k][2], k
+    ref_ctx.close()
+    ctx.close()
