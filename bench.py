@@ -196,7 +196,8 @@ def profiled_traffic(kernel, config, frames=1):
             continue
         if s.get("config_name") != config or s.get("frames_per_launch", 1) != frames:
             continue
-        if not any(k.endswith(kernel) for k in s.get("kernels", {})):
+        # the profiled launches (not a context's one-workgroup prewarm dispatches of other forms)
+        if not any(k.endswith(kernel) and v.get("calls", 0) > 1 for k, v in s.get("kernels", {}).items()):
             continue
         if "traffic_bytes_per_launch_fetch_x2" in s:
             best = (s["traffic_bytes_per_launch_fetch_x2"], os.path.relpath(p, ROOT))

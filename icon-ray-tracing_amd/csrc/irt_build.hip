@@ -573,17 +573,31 @@ int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_
 }
 
 // ---------------------------------------------------------------- the slot table
-// every cell's radial edges (header words 0-2) against cell 0's
-__global__ void k_slot_uniform(const uint32_t *hdr, uint32_t numCells, uint32_t *differs) {
-  const uint32_t e0 = hdr[0], e1 = hdr[1], e2 = hdr[2];
+// The cells' distinct finite radial edges other than cell 0's (header words 0-2), into a set of
+// kSlotSet words (0: empty) by compare-and-swap; *full when more than that
+constexpr int kSlotSet = 8;
+__global__ void k_slot_edges(const uint32_t *hdr, uint32_t numCells, uint32_t *set, uint32_t *full) {
+  const uint32_t r0 = hdr[0], r1 = hdr[1], r2 = hdr[2];
   for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < numCells; c += gridDim.x * blockDim.x) {
     const uint32_t *H = hdr + (size_t)c * kBinHdrWords;
-    if (H[0] != e0 || H[1] != e1 || H[2] != e2) atomicOr(differs, 1u);
+    for (int j = 0; j < kMaxEdges; ++j) {
+      const uint32_t e = H[j];
+      if (e == r0 || e == r1 || e == r2 || __builtin_isinf(__uint_as_float(e))) continue;
+      bool in = false;
+      for (int q = 0; q < kSlotSet && !in; ++q) {
+        const uint32_t old = atomicCAS(&set[q], 0u, e);
+        in = old == 0u || old == e;
+      }
+      if (!in) atomicOr(full, 1u);
+    }
   }
 }
 
-// one thread per slot (cell, sub-cell, bin)
-__global__ void k_slot_fill(const uint32_t *hdr, const float *fat, uint32_t numCells, int bins, float4 *slots) {
+// one thread per slot (cell, sub-cell, table bin)
+__global__ void k_slot_fill(const uint32_t *hdr, const float *fat, uint32_t numCells, float u0, float u1, float u2,
+                            int ne, float4 *slots) {
+  const int bins = ne + 1;
+  const float U[kMaxEdges] = {u0, u1, u2};
   const uint64_t total = (uint64_t)numCells * kSubCells * kSubCells * bins;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
     const int b = (int)(i % bins);
@@ -591,7 +605,7 @@ __global__ void k_slot_fill(const uint32_t *hdr, const float *fat, uint32_t numC
     const int sc = (int)(cs % (kSubCells * kSubCells));
     const uint64_t c = cs / (kSubCells * kSubCells);
     float S[4 * kSlot4];
-    slot_fill(hdr + c * kBinHdrWords, fat, sc, b, S);
+    slot_fill(hdr + c * kBinHdrWords, fat, sc, b, U, ne, S);
     float4 *o = slots + i * kSlot4;
     for (int k = 0; k < kSlot4; ++k) o[k] = make_float4(S[4 * k], S[4 * k + 1], S[4 * k + 2], S[4 * k + 3]);
   }
@@ -605,17 +619,25 @@ int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells
   int rc;
   if ((rc = read_back(e, hdr, 3, s))) return rc;
   Scratch S;
-  uint32_t *differs;
-  BHIP(S.alloc(&differs, 1));
-  BHIP(hipMemsetAsync(differs, 0, sizeof(uint32_t), s));
-  hipLaunchKernelGGL(k_slot_uniform, dim3(grid_for(numCells)), dim3(256), 0, s, hdr, numCells, differs);
+  uint32_t *set;
+  BHIP(S.alloc(&set, kSlotSet + 1));
+  BHIP(hipMemsetAsync(set, 0, (kSlotSet + 1) * sizeof(uint32_t), s));
+  hipLaunchKernelGGL(k_slot_edges, dim3(grid_for(numCells)), dim3(256), 0, s, hdr, numCells, set, set + kSlotSet);
   BHIP(hipGetLastError());
-  uint32_t d = 0;
-  if ((rc = read_back(&d, differs, 1, s))) return rc;
-  if (d) return IRT_OK;
-  int ne = 0;
-  while (ne < kMaxEdges && !__builtin_isinf(u2f(e[ne]))) ++ne;
-  const int bins = ne + 1;
+  uint32_t h[kSlotSet + 1];
+  if ((rc = read_back(h, set, kSlotSet + 1, s))) return rc;
+  if (h[kSlotSet]) return IRT_OK;  // more distinct edges than the set holds
+  // the table's edges: cell 0's and the others', distinct and ascending
+  std::vector<float> U;
+  for (int j = 0; j < kMaxEdges; ++j)
+    if (!__builtin_isinf(u2f(e[j]))) U.push_back(u2f(e[j]));
+  for (int q = 0; q < kSlotSet; ++q)
+    if (h[q]) U.push_back(u2f(h[q]));
+  std::sort(U.begin(), U.end(), [](float a, float b) { return float_key(a) < float_key(b); });
+  U.erase(std::unique(U.begin(), U.end(), [](float a, float b) { return f2u(a) == f2u(b); }), U.end());
+  if ((int)U.size() > kMaxEdges) return IRT_OK;
+  const int ne = (int)U.size(), bins = ne + 1;
+  while ((int)U.size() < kMaxEdges) U.push_back(__builtin_inff());
   const size_t bytes = (size_t)numCells * kSubCells * kSubCells * bins * kSlot4 * sizeof(float4);
   if (bytes > maxBytes) return IRT_OK;
   float4 *slots = nullptr;
@@ -624,7 +646,7 @@ int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells
     return IRT_OK;
   }
   hipLaunchKernelGGL(k_slot_fill, dim3(std::min<uint64_t>(grid_for(bytes / (kSlot4 * sizeof(float4))), 1u << 20)),
-                     dim3(256), 0, s, hdr, reinterpret_cast<const float *>(fat), numCells, bins, slots);
+                     dim3(256), 0, s, hdr, reinterpret_cast<const float *>(fat), numCells, U[0], U[1], U[2], ne, slots);
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
     (void)hipFree(slots);
     set_error("slot table build failed");
@@ -633,7 +655,7 @@ int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells
   out.slots = slots;
   out.bins = bins;
   out.bytes = bytes;
-  for (int k = 0; k < kMaxEdges; ++k) out.edges[k] = u2f(e[k]);
+  for (int k = 0; k < kMaxEdges; ++k) out.edges[k] = U[k];
   return IRT_OK;
 }
 

@@ -406,31 +406,43 @@ IRT_HD uint32_t sph_hash(float r) {
 constexpr int kFat4 = 4;
 constexpr int kFatStride4 = 4;
 
-// Slot table (round 5; scenes whose cube-map cells all share their radial edges -- every
-// column with the same levels, as in C3/C4/C5): per (cell, sub-cell, bin) one 128-B line
-// holding what the header and the list's first candidate give a sample there, so a located
+// Slot table (round 5): for scenes whose cube-map cells' radial edges, all together, are at most
+// kMaxEdges distinct values U0 < U1 < U2 (every column with the same levels, as in C3/C4/C5;
+// cells with fewer entries may have fewer of them), the bin of a sample in the table's terms
+// follows from r alone, and per (cell, sub-cell, table bin) one 128-B line holds what the
+// cell's header and the list's first candidate give a sample there, so that a located
 // sample's scan starts with one gather instead of two dependent ones (header, then entry):
-//   [0..3]  the first candidate the sub-cell mask admits (its fat entry; zero when none)
-//   [4]     {admitted candidates c, the bin's list start (base + bin begin), the bin's
-//           8-bit sub-cell mask (masked to the list's length), 0}
+//   [0..3]  the first candidate the sub-cell mask admits in the cell's own bin k that holds the
+//           table bin (U_{b-1}, U_b] (its fat entry; zero when none)
+//   [4]     {admitted candidates c, bin k's list start (base + bin begin), bin k's 8-bit sub-cell
+//           mask (masked to the list's length), U_b if it is also the cell's edge e_k (a sample
+//           exactly there scans bin k + 1 too), else +inf}
 //   [5..7]  0
 // Slot (cell, s, b) sits at ((cell * kSubCells^2 + s) * bins + b) * kSlot4.  The rest of the
 // scan (the dealt-out candidates, the second pass on a bin edge) reads the header and the
 // lists as before.
 constexpr int kSlot4 = 8;
-// Fills slot (s, b) of a cell from its header H (kBinHdrWords) and the fat entries.
-IRT_HD void slot_fill(const uint32_t *H, const float *fat, int s, int b, float *S) {
+// Fills slot (s, b) of a cell from its header H (kBinHdrWords) and the fat entries; U: the
+// table's ne edges (ascending).
+IRT_HD void slot_fill(const uint32_t *H, const float *fat, int s, int b, const float *U, int ne, float *S) {
   for (int k = 0; k < 4 * kSlot4; ++k) S[k] = 0.f;
-  const uint32_t beg = b ? H[4 + b - 1] : 0u, end = H[4 + b], n = end - beg;
-  const uint32_t m8 = (H[8 + s] >> (8 * b)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
+  // the cell's bin holding (U_{b-1}, U_b]: its edges <= U_{b-1} (each is one of the U)
+  int k = 0;
+  if (b > 0)
+    for (int j = 0; j < kMaxEdges; ++j) k += u2f(H[j]) <= U[b - 1] ? 1 : 0;
+  const float up = b < ne ? U[b] : __builtin_inff();
+  const bool own = b < ne && k < kMaxEdges && u2f(H[k]) == up;
+  const uint32_t beg = k ? H[4 + k - 1] : 0u, end = H[4 + k], n = end - beg;
+  const uint32_t m8 = (H[8 + s] >> (8 * k)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
   const uint32_t c = (uint32_t)__builtin_popcount(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
   if (c) {
     const uint32_t first = H[3] + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
-    for (int k = 0; k < 4 * kFat4; ++k) S[k] = fat[(size_t)first * 4 * kFatStride4 + k];
+    for (int q = 0; q < 4 * kFat4; ++q) S[q] = fat[(size_t)first * 4 * kFatStride4 + q];
   }
   S[16] = u2f(c);
   S[17] = u2f(H[3] + beg);
   S[18] = u2f(m8);
+  S[19] = own ? up : __builtin_inff();
 }
 // Per-record height/value blocks (the render record without its planes/keys), kBlk4
 // float4 = 256 B: block b (4 float4) = {height[8b..8b+3]}, {height[8b+4..8b+7]},

@@ -128,8 +128,9 @@ struct RenderArgs {
   const uint32_t *splitList;
   const uint32_t *splitMask;
   uint32_t numSplit;
-  // the slot table (irt_common.h kSlot4; null: none -- the scene's cells do not share their
-  // radial edges, or IRT_SLOTS=0): slotEdge = the shared edges, slotBins = bins per sub-cell.
+  // the slot table (irt_common.h kSlot4; null: none -- the cells' radial edges are more than
+  // three values in all, the headers fit the last-level cache, or IRT_SLOTS=0): slotEdge = the
+  // table's edges (+inf past slotBins - 1), slotBins = table bins per sub-cell.
   // Launches with a table run the default kernels' OPT_SLOT form (kernel_for).
   const float4 *slots;
   float slotEdge[3];
@@ -217,8 +218,9 @@ struct DeviceScene {
 };
 int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_t n, size_t numRuns,
                        int G, hipStream_t s, DeviceScene &out);
-// The slot table (irt_common.h kSlot4) of a built scene whose cells all share their radial
-// edges, if it fits in maxBytes (and the device's free memory); otherwise slots stays null.
+// The slot table (irt_common.h kSlot4) of a built scene whose cells' radial edges are at most
+// three values in all, if it fits in maxBytes (and the device's free memory); otherwise slots
+// stays null.
 struct SlotTable {
   float4 *slots = nullptr;
   int bins = 0;

@@ -678,8 +678,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       s2 = S[2];
       sm = S[3];
       const uint4 info = reinterpret_cast<const uint4 *>(S)[4];
-      const float eb = b == 0 ? e0 : (b == 1 ? e1 : e2);
-      edge = b < kMaxEdges && r == eb;
+      edge = r == __uint_as_float(info.w);  // the cell's own bin edge (+inf: none)
       c = info.x;
       lds_st16(&W.pt[lane], make_float4(px, py, pz, r));
       lds_st16(&W.lst[lane], make_uint4(info.y, info.z, 0u, 0xFFFFFFFFu));

@@ -5,7 +5,8 @@ sample's scan starts with one gather.
 
 Pinned here: the table the device builds equals a numpy restatement from the headers and fat
 entries byte for byte; frames, accumulators and every count equal a context without the table
-(IRT_SLOTS=0); scenes whose cells have their own edges (terrain) get no table; by default only
+(IRT_SLOTS=0); scenes whose cells' edges are more than three distinct values (terrain) get no
+table; by default only
 scenes whose headers outgrow the last-level cache get one.  The small scenes here force it
 (IRT_SLOTS=1); tests/test_gpu_parity.py::test_device_locator_slot_table runs the wave-wide
 locate through it against the host restatement, test_gpu_scale.py's C5 frames run through it.
@@ -23,21 +24,29 @@ _CTZ = np.array([8] + [(k & -k).bit_length() - 1 for k in range(1, 256)], np.uin
 
 
 def restate_slots(hdr: np.ndarray, fat: np.ndarray) -> np.ndarray:
-    """irt_common.h slot_fill over every (cell, sub-cell, bin), from the scene's header and
-    fat-entry bytes (kBinHdrWords = 32 with 4 x 4 sub-cells, 16 words per entry)."""
+    """irt_common.h slot_fill over every (cell, sub-cell, table bin), from the scene's header
+    and fat-entry bytes (kBinHdrWords = 32 with 4 x 4 sub-cells, 16 words per entry); None when
+    the cells' edges are more than three distinct values."""
+    INF = 0x7F800000
     H = hdr.view(np.uint32).reshape(-1, 32).astype(np.int64)
     F = fat.view(np.uint32).reshape(-1, 16)
-    e = H[0, :3]
-    assert (H[:, :3] == e).all(), "cells with their own edges have no table"
-    nb = int(np.sum(e != 0x7F800000)) + 1
-    nsub = 16
+    E = H[:, :3]
+    U = np.unique(E[E != INF].astype(np.uint32).view(np.float32))
+    if U.size > 3:
+        return None
+    ne, nb, nsub = U.size, U.size + 1, 16
+    Ef = E.astype(np.uint32).view(np.float32)
     out = np.zeros((H.shape[0], nsub, nb, 32), np.uint32)
+    rows = np.arange(H.shape[0])
     for b in range(nb):
-        beg = H[:, 4 + b - 1] if b else np.zeros(H.shape[0], np.int64)
-        n = H[:, 4 + b] - beg
+        k = (Ef <= U[b - 1]).sum(1) if b else np.zeros(H.shape[0], np.int64)
+        up = np.float32(U[b]) if b < ne else np.float32(np.inf)
+        own = (b < ne) & (k < 3) & (Ef[rows, np.minimum(k, 2)] == up)
+        beg = np.where(k > 0, H[rows, 3 + k], 0)  # word 4 + k - 1
+        n = H[rows, 4 + k] - beg
         lenmask = np.where(n < 8, (1 << np.clip(n, 0, 8)) - 1, 0xFF)
         for s in range(nsub):
-            m8 = (H[:, 8 + s] >> (8 * b)) & 0xFF & lenmask
+            m8 = (H[:, 8 + s] >> (8 * k)) & 0xFF & lenmask
             c = _POP[m8].astype(np.int64) + np.where(n > 8, n - 8, 0)
             first = H[:, 3] + beg + _CTZ[m8]
             has = c > 0
@@ -45,19 +54,25 @@ def restate_slots(hdr: np.ndarray, fat: np.ndarray) -> np.ndarray:
             out[:, s, b, 16] = c
             out[:, s, b, 17] = H[:, 3] + beg
             out[:, s, b, 18] = m8
+            out[:, s, b, 19] = np.where(own, np.float32(up).view(np.uint32), INF)
     return out.reshape(-1)
 
 
-@pytest.mark.parametrize("bis,levels,noise", [(2, 90, 0.0), (3, 47, 0.2), (3, 20, 0.0)])
-def test_slot_table_restated(monkeypatch, bis, levels, noise):
+@pytest.mark.parametrize("scene", ["r2b02_l90", "r2b03_l47_noise", "r2b03_l20", "filtered"])
+def test_slot_table_restated(monkeypatch, scene):
+    """(filtered: cells at the region's border hold fewer records and fewer edges, a subset of
+    the others')"""
     monkeypatch.setenv("IRT_SLOTS", "1")
-    cells = irt.synth_grid(2, bis, levels, noise=noise)
+    cells = {"r2b02_l90": lambda: irt.synth_grid(2, 2, 90),
+             "r2b03_l47_noise": lambda: irt.synth_grid(2, 3, 47, noise=0.2),
+             "r2b03_l20": lambda: irt.synth_grid(2, 3, 20),
+             "filtered": lambda: irt.filter_cells(irt.synth_grid(2, 3, 40), (-30, 60), (-90, 45))}[scene]()
     ctx = irt.Context(cells, 0)
     slots = ctx.array("slots")
     assert slots.size > 0, "a flat grid's cells share their edges"
     want = restate_slots(ctx.array("bin_hdr"), ctx.array("fat"))
     got = slots.view(np.uint32)
-    assert got.size == want.size
+    assert want is not None and got.size == want.size
     if not np.array_equal(got, want):
         w = np.nonzero(got != want)[0]
         raise AssertionError(f"{w.size} words differ, first at {w[0]}")
@@ -68,6 +83,7 @@ def test_cells_with_own_edges_have_no_table(monkeypatch):
     monkeypatch.setenv("IRT_SLOTS", "1")
     ctx = irt.Context(irt.synth_grid(2, 3, 90, terrain=4000.0), 0)
     assert ctx.array("slots").size == 0
+    assert restate_slots(ctx.array("bin_hdr"), ctx.array("fat")) is None  # > 3 distinct edges
     ctx.close()
 
 
