@@ -40,7 +40,7 @@ int main(int argc, char **argv) {
   std::uniform_real_distribution<double> U(0.0, 1.0);
   const float R = 6371229.f;
   long found = 0, hist[17] = {0}, tested = 0, admitted = 0, firstPass = 0;
-  long failRadial = 0, failPlane = 0, testedHalf = 0, admittedHalf = 0, binFirst = 0, quadFirst = 0;
+  long failRadial = 0, failPlane = 0, testedHalf = 0, admittedHalf = 0, binFirst = 0, quadFirst = 0, secondPass = 0, secondSame = 0, needThird = 0;
   for (long i = 0; i < npts; ++i) {
     const double z = 2 * U(rng) - 1, ph = 2 * M_PI * U(rng), rr = sqrt(1 - z * z);
     const float r0 = R + (float)(U(rng) * top);
@@ -67,6 +67,7 @@ int main(int argc, char **argv) {
     const uint32_t si = sub % kSub, sj = sub / kSub, q0 = (sj & ~1u) * kSub + (si & ~1u);
     const uint32_t qmask = ((h[8 + q0] | h[8 + q0 + 1] | h[8 + q0 + kSub] | h[8 + q0 + kSub + 1]) >> (8 * b)) & 0xFFu;
     int qj = -1;  // the quad's first admitted candidate
+    const float *e1st = nullptr;
     for (uint32_t j = 0; beg + j < end && qj < 0; ++j)
       if (j >= (uint32_t)kMaskCand || ((qmask >> j) & 1u)) qj = (int)j;
     for (uint32_t j = 0; beg + j < end; ++j) {
@@ -83,7 +84,11 @@ int main(int argc, char **argv) {
         if (ok) hit = adm;
       }
       if (j == 0 && ok) ++binFirst;
-      if ((int)j == qj && ok) ++quadFirst;  // the bin's first candidate (unmasked) is the answer
+      if ((int)j == qj && ok) ++quadFirst;
+      if (adm == 1) e1st = e;
+      if (adm == 2 && t == 2) {  // the first admitted failed: is the second like it?
+        if (e[12] == e1st[12] && e[13] == e1st[13] && e[15] == e1st[15]) ++secondSame;
+      }  // the bin's first candidate (unmasked) is the answer
       const bool half = j >= (uint32_t)kMaskCand || (r < mid ? e[12] < mid : e[13] >= mid);
       if (half) {
         ++admH;
@@ -95,6 +100,8 @@ int main(int argc, char **argv) {
     }
     if (hit < 0) continue;
     ++found;
+    if (hit == 2) ++secondPass;
+    if (hit > 2) ++needThird;
     if (hitH < 0) {
       printf("half mask lost a hit\n");
       return 1;
@@ -113,6 +120,8 @@ int main(int argc, char **argv) {
   printf("failed tests per sample: radial %.3f, planes %.3f; with a radial half mask: tested %.3f, admitted %.3f\n",
          (double)failRadial / found, (double)failPlane / found, (double)testedHalf / found,
          (double)admittedHalf / found);
+  printf("the second admitted answers %.3f (its radial range and meta equal the first's when the first fails: %.3f); a third or later %.3f\n",
+         (double)secondPass / found, (double)secondSame / found, (double)needThird / found);
   printf("the bin's first candidate is the answer: %.3f; the 2x2 quad's first admitted: %.3f\n",
          (double)binFirst / found, (double)quadFirst / found);
   printf("admitted histogram:");
