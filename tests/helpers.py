@@ -145,3 +145,43 @@ def locator_points(cells, seed, n_random=400, n_cols=80):
                 for v in (cd.mean(0), cd[0] + cd[1], cd[0]):
                     pts.append(on_radius(v, rr))
     return np.array(pts, np.float32)
+
+
+# ---- the slot table (irt_common.h kSlot4), restated from a scene's header and entry bytes
+_POP = np.array([bin(k).count("1") for k in range(256)], np.uint32)
+_CTZ = np.array([8] + [(k & -k).bit_length() - 1 for k in range(1, 256)], np.uint32)
+
+
+def restate_slots(hdr: np.ndarray, fat: np.ndarray) -> np.ndarray:
+    """irt_common.h slot_fill over every (cell, sub-cell, table bin), from the scene's header
+    and fat-entry bytes (kBinHdrWords = 32 with 4 x 4 sub-cells, 16 words per entry); None when
+    the cells' edges are more than three distinct values."""
+    INF = 0x7F800000
+    H = hdr.view(np.uint32).reshape(-1, 32).astype(np.int64)
+    F = fat.view(np.uint32).reshape(-1, 16)
+    E = H[:, :3]
+    U = np.unique(E[E != INF].astype(np.uint32).view(np.float32))
+    if U.size > 3:
+        return None
+    ne, nb, nsub = U.size, U.size + 1, 16
+    Ef = E.astype(np.uint32).view(np.float32)
+    out = np.zeros((H.shape[0], nsub, nb, 32), np.uint32)
+    rows = np.arange(H.shape[0])
+    for b in range(nb):
+        k = (Ef <= U[b - 1]).sum(1) if b else np.zeros(H.shape[0], np.int64)
+        up = np.float32(U[b]) if b < ne else np.float32(np.inf)
+        own = (b < ne) & (k < 3) & (Ef[rows, np.minimum(k, 2)] == up)
+        beg = np.where(k > 0, H[rows, 3 + k], 0)  # word 4 + k - 1
+        n = H[rows, 4 + k] - beg
+        lenmask = np.where(n < 8, (1 << np.clip(n, 0, 8)) - 1, 0xFF)
+        for s in range(nsub):
+            m8 = (H[:, 8 + s] >> (8 * k)) & 0xFF & lenmask
+            c = _POP[m8].astype(np.int64) + np.where(n > 8, n - 8, 0)
+            first = H[:, 3] + beg + _CTZ[m8]
+            has = c > 0
+            out[has, s, b, :16] = F[first[has]]
+            out[:, s, b, 16] = c
+            out[:, s, b, 17] = H[:, 3] + beg
+            out[:, s, b, 18] = m8
+            out[:, s, b, 19] = np.where(own, np.float32(up).view(np.uint32), INF)
+    return out.reshape(-1)

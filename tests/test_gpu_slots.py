@@ -15,48 +15,9 @@ import numpy as np
 import pytest
 
 import irt
-from helpers import FRAMING, bits
+from helpers import FRAMING, bits, restate_slots
 
 pytestmark = pytest.mark.gpu
-
-_POP = np.array([bin(k).count("1") for k in range(256)], np.uint32)
-_CTZ = np.array([8] + [(k & -k).bit_length() - 1 for k in range(1, 256)], np.uint32)
-
-
-def restate_slots(hdr: np.ndarray, fat: np.ndarray) -> np.ndarray:
-    """irt_common.h slot_fill over every (cell, sub-cell, table bin), from the scene's header
-    and fat-entry bytes (kBinHdrWords = 32 with 4 x 4 sub-cells, 16 words per entry); None when
-    the cells' edges are more than three distinct values."""
-    INF = 0x7F800000
-    H = hdr.view(np.uint32).reshape(-1, 32).astype(np.int64)
-    F = fat.view(np.uint32).reshape(-1, 16)
-    E = H[:, :3]
-    U = np.unique(E[E != INF].astype(np.uint32).view(np.float32))
-    if U.size > 3:
-        return None
-    ne, nb, nsub = U.size, U.size + 1, 16
-    Ef = E.astype(np.uint32).view(np.float32)
-    out = np.zeros((H.shape[0], nsub, nb, 32), np.uint32)
-    rows = np.arange(H.shape[0])
-    for b in range(nb):
-        k = (Ef <= U[b - 1]).sum(1) if b else np.zeros(H.shape[0], np.int64)
-        up = np.float32(U[b]) if b < ne else np.float32(np.inf)
-        own = (b < ne) & (k < 3) & (Ef[rows, np.minimum(k, 2)] == up)
-        beg = np.where(k > 0, H[rows, 3 + k], 0)  # word 4 + k - 1
-        n = H[rows, 4 + k] - beg
-        lenmask = np.where(n < 8, (1 << np.clip(n, 0, 8)) - 1, 0xFF)
-        for s in range(nsub):
-            m8 = (H[:, 8 + s] >> (8 * k)) & 0xFF & lenmask
-            c = _POP[m8].astype(np.int64) + np.where(n > 8, n - 8, 0)
-            first = H[:, 3] + beg + _CTZ[m8]
-            has = c > 0
-            out[has, s, b, :16] = F[first[has]]
-            out[:, s, b, 16] = c
-            out[:, s, b, 17] = H[:, 3] + beg
-            out[:, s, b, 18] = m8
-            out[:, s, b, 19] = np.where(own, np.float32(up).view(np.uint32), INF)
-    return out.reshape(-1)
-
 
 @pytest.mark.parametrize("scene", ["r2b02_l90", "r2b03_l47_noise", "r2b03_l20", "filtered"])
 def test_slot_table_restated(monkeypatch, scene):
