@@ -507,6 +507,8 @@ def main():
                 "frames_per_launch": frames,
                 "bytes_per_launch_rank0": bytes_per_launch,
                 "chain_timeouts": chain_timeouts,
+                # the slot table (built when the headers outgrow the last-level cache)
+                "slot_table_bytes": ctx.array_bytes("slots"),
             },
             "roofline": {
                 "bound": "hbm",
