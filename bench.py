@@ -38,6 +38,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import sys
 import time
 
@@ -188,8 +189,12 @@ def profiled_traffic(kernel, config, frames=1):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 summary of the
     same workload (profiles/*/summary.json: FETCH_SIZE x 2 + WRITE_SIZE, per the gfx950
     correction of MI355X_MICROARCH.md), or None."""
+    def tag_order(p):  # profiles/rNN<tag>_*: tags run a..z, then aa..az (r05q before r05an)
+        m = re.match(r"r(\d+)([a-z]*)", os.path.basename(os.path.dirname(p)))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")), key=tag_order):
         try:
             s = json.load(open(p))
         except (OSError, ValueError):
