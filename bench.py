@@ -31,8 +31,12 @@ Frames are enqueued back to back: per-launch statistics come back through a ring
 stalling the host between launches.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c3s|c3t|c2|c4|c5]
-       [--mode progressive|frame]
+       [--mode progressive|frame] [--dist-backend nccl|gloo] [--verify] [--secondary LIST]
        torchrun --nproc-per-node N bench.py --gpus N ...
+With --gpus N > 1 and no launcher (WORLD_SIZE unset) bench.py starts the N ranks itself
+(torch.distributed.run as a child process, before this process touches a GPU) and relays rank
+0's JSON line; under a launcher --gpus must equal WORLD_SIZE.  On one GPU with the default c3,
+the line also carries "secondary": C3t, C3s and C5 measured the same way with a few steps each.
 """
 import argparse
 import glob
@@ -214,9 +218,48 @@ def orbit_camera(k):
     return ((1.4e7 * np.sin(th), 0.0, 1.4e7 * np.cos(th)), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0)
 
 
-def main():
+# the configs whose numbers DESIGN.md quotes besides the headline C3, measured in the same
+# run (a few steps each, after the primary line's timed region) so that they come under the
+# driver's clock too: terrain (the realistic-data layout), the sample-heavy TF and R2B09
+SECONDARY = ("c3t", "c3s", "c5")
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` (N > 1) started as a plain program: one rank per GPU, launched as
+    the driver's own `torch.distributed.run --nproc-per-node N` form does, from this process
+    before it imports torch or touches a GPU (it never execs: the launcher is a child).  The
+    children's stderr passes through; of their stdout only rank 0's JSON line is relayed to
+    ours, everything else goes to stderr.  Returns the launcher's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log(f"[launcher] {n} ranks: {' '.join(cmd)}")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    for line in p.stdout:
+        s = line.strip()
+        is_json = False
+        if s.startswith("{"):
+            try:
+                is_json = isinstance(json.loads(s), dict) and "metric" in json.loads(s)
+            except ValueError:
+                pass
+        (sys.stdout if is_json else sys.stderr).write(line)
+        (sys.stdout if is_json else sys.stderr).flush()
+    return p.wait()
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU).  Under torch.distributed.run it must equal "
+                         "WORLD_SIZE; started directly with N > 1, bench.py launches the N ranks "
+                         "itself")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
@@ -249,35 +292,32 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path with host-staged collectives "
                          "(ranks may share a GPU); nccl (RCCL) is the measured path")
-    args = ap.parse_args()
+    ap.add_argument("--verify", action="store_true",
+                    help="multi-rank: after the timed region rank 0 renders the same accumID "
+                         "sequence on its own context with irt_render_accumulate and compares "
+                         "the assembled framebuffer pixel for pixel (exit 3 on a mismatch)")
+    ap.add_argument("--secondary", default="auto",
+                    help="comma-separated configs measured after the primary line on one GPU "
+                         "(a few steps each, reported under \"secondary\"); auto: "
+                         + ",".join(SECONDARY) + " when the primary config is c3; none: skip")
+    ap.add_argument("--secondary-steps", type=int, default=10)
+    return ap.parse_args(argv)
 
+
+def run_config(args, config, steps, warmup, rank, world, dist_path, primary=True):
+    """Build `config`'s scene on this rank's GPU, render `warmup` + `steps` steps (timed
+    between barriers + synchronize), and return the result dict on rank 0 (None elsewhere)."""
     import torch
     import irt
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist_path = world > 1 or args.force_dist
-    device = local % max(torch.cuda.device_count(), 1) if dist_path else 0
-    json_out = sys.stdout
+    import resource
     if dist_path:
-        # RCCL (and the runtime under it) may print banners on fd 1: send everything
-        # native to stderr and keep stdout for the one JSON line
-        json_out = os.fdopen(os.dup(1), "w")
-        sys.stdout.flush()
-        os.dup2(2, 1)
         import torch.distributed as dist
-        torch.cuda.set_device(device)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{device}"))
-        else:
-            dist.init_process_group("gloo")
-    torch.cuda.set_device(device)
+    device = torch.cuda.current_device()
     dev = torch.device(f"cuda:{device}")
 
-    rn, bis, L, W, H, tf, orbit_cfg, desc = CONFIGS[args.config]
+    rn, bis, L, W, H, tf, orbit_cfg, desc = CONFIGS[config]
     t0 = time.time()
-    terrain = TERRAIN.get(args.config, 0.0)
+    terrain = TERRAIN.get(config, 0.0)
     # streamed into HBM, built on the device
     ctx = irt.Context.synth(rn, bis, L, device, terrain=terrain)
     info = ctx.info
@@ -287,10 +327,10 @@ def main():
     # duration): each timed launch adds ~4.7 us of event packets to its step (every launch
     # timed: +8 us per C3 step), so k = steps/4 (at most 32; four timed launches per run, one
     # at least when steps < 4) keeps them to ~1 % of the region
-    ctx.set_timing_interval(max(1, min(32, args.steps // 4)))
-    import resource
-    log(f"[rank {rank}] context: {info.numCells} records, {info.deviceBytes / 2**30:.2f} GiB HBM, "
-        f"locator G={info.locatorFaceRes} entries={info.locatorEntries} ({time.time() - t0:.1f} s, "
+    ctx.set_timing_interval(max(1, min(32, steps // 4)))
+    create_s = time.time() - t0
+    log(f"[rank {rank}] {config} context: {info.numCells} records, {info.deviceBytes / 2**30:.2f} GiB HBM, "
+        f"locator G={info.locatorFaceRes} entries={info.locatorEntries} ({create_s:.1f} s, "
         f"peak host RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.2f} GiB)")
 
     lp = setup.lp
@@ -368,15 +408,12 @@ def main():
         pipe.step(s, lambda buf: split.render(ctx, lp, frames, buf.data_ptr(),
                                               tiles_acc.data_ptr(), stream))
 
-    def drain():
-        pipe.drain()
-
-    for f in range(args.warmup):
+    for f in range(warmup):
         step(f)
     if dist_path:
-        drain()
+        pipe.drain()
     st = ctx.stats()
-    log(f"[rank {rank}] warmup: last launch kernel {st.kernelMs:.3f} ms, {st.samplesFound} "
+    log(f"[rank {rank}] {config} warmup: last launch kernel {st.kernelMs:.3f} ms, {st.samplesFound} "
         f"samples, {st.candidatesTested} candidates")
     ctx.reset_stats_total()
     ctx.set_statistics(args.stats == "on")
@@ -385,11 +422,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k)
+    for k in range(steps):
+        step(warmup + k)
     host_loop = time.perf_counter() - t_start  # host side of the loop (launches only)
     if dist_path:
-        drain()
+        pipe.drain()  # the gathers and rank 0's unpacks are inside the timed region
     torch.cuda.synchronize()
     if dist_path:
         dist.barrier()
@@ -401,21 +438,44 @@ def main():
         # counts), rendered again with counting on, untimed
         ctx.reset_stats_total()
         ctx.set_statistics(True)
-        for k in range(args.steps):
-            step(args.warmup + k)
+        for k in range(steps):
+            step(warmup + k)
         if dist_path:
-            drain()
+            pipe.drain()
         torch.cuda.synchronize()
         counted, _ = ctx.stats_total()
         counted.kernelMs = tot.kernelMs
         tot = counted
+    verify = None
+    if dist_path and args.verify and rank == 0:
+        # rank 0's assembled frame against its own context rendering every frame of every
+        # tile: the same accumID sequence (warmup + timed steps, then the counted re-run of the
+        # timed steps) through irt_render_accumulate on a fresh framebuffer
+        assert orbit is None, "--verify covers the progressive (non-orbit) configs"
+        ref_fb = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        ref_acc = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+        runs = [(0, (warmup + steps) * frames)]
+        if args.stats == "off":
+            runs.append((warmup * frames, steps * frames))
+        q = irt.LaunchParams.from_buffer_copy(lp)
+        for first, count in runs:
+            for a in range(first, first + count, batch):
+                q.accumID = a
+                ctx.render_accumulate(q, W, H, min(batch, first + count - a), ref_fb.data_ptr(),
+                                      ref_acc.data_ptr(), stream)
+        torch.cuda.synchronize()
+        bad = int((ref_fb != fb).sum().item())
+        verify = {"pixels": W * H, "mismatches": bad, "frames_per_pixel": sum(c for _, c in runs),
+                  "against": "irt_render_accumulate of the whole frame on rank 0's context, the "
+                             "same accumID sequence"}
+        log(f"[rank 0] verify: {bad} of {W * H} pixels differ from the single-context frame")
     single = None
     if not dist_path and frames > 1 and not args.no_single_compare:
         # the same workload at one launch per frame (irt_render), for comparison: the frames
         # that follow the timed steps' accumulation, statistics as in the timed loop
         ctx.set_statistics(args.stats == "on")
-        n1 = args.steps * frames
-        base = (args.warmup + args.steps) * frames
+        n1 = steps * frames
+        base = (warmup + steps) * frames
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for k in range(n1):
@@ -428,7 +488,7 @@ def main():
         e1 = time.perf_counter() - t1
         single = {"ms_per_frame": round(e1 / n1 * 1e3, 4), "value": round(W * H * n1 / e1 / 1e6, 3),
                   "frames": n1}
-    log(f"[rank {rank}] timed {args.steps} steps ({launches} launches) in {elapsed:.4f} s "
+    log(f"[rank {rank}] {config} timed {steps} steps ({launches} launches) in {elapsed:.4f} s "
         f"(host loop {host_loop:.4f} s); peak host RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.2f} GiB")
     samples, in_box = tot.samplesFound, tot.raysInBox
     if dist_path:
@@ -451,14 +511,15 @@ def main():
     if chain_timeouts:
         log(f"[rank {rank}] WARNING: {chain_timeouts} chained-frame waits timed out; frames may be wrong")
 
-    ms_per_step = elapsed / args.steps * 1e3
-    mray = W * H * frames * args.steps / elapsed / 1e6  # all ranks' rays
+    ms_per_step = elapsed / steps * 1e3
+    mray = W * H * frames * steps / elapsed / 1e6  # all ranks' rays
     # roofline of the dominant kernel on this rank: algorithmic bytes per launch over its
     # HIP-event-timed average duration (events on the stream the kernel runs on)
     avg_kernel_s = tot.kernelMs / 1e3 / max(launches, 1)
     bytes_per_launch = (BYTES_PER_SAMPLE * samples + BYTES_PER_RAY * in_box) / max(launches, 1)
     achieved = bytes_per_launch / avg_kernel_s if avg_kernel_s > 0 else float("nan")
 
+    out = None
     if rank == 0:
         if world == 1 and not dist_path:
             parallelism = "single GPU"
@@ -470,13 +531,15 @@ def main():
             parallelism = (f"{world} GPUs x 64x64 cost-balanced frame tiles, {frames} progressive "
                            f"frames per step in one launch per rank, RCCL gather of the final "
                            f"RGBA8 tiles to rank 0 overlapped with the next step")
+        if dist_path and args.dist_backend == "gloo":
+            parallelism += " (gloo rehearsal: host-staged gathers)"
         out = {
             "metric": METRIC,
             "value": round(mray, 3),
             "unit": "Mray/s",
             "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
+            "steps": steps,
+            "warmup": warmup,
             "ms_per_step": round(ms_per_step, 4),
             "frames_per_launch": frames,
             "higher_is_better": True,
@@ -485,7 +548,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "name": args.config,
+                "name": config,
                 "workload": desc + (", orbit camera (eye 1.4e7 (sin t, 0, cos t), -fovy 60), " +
                                     ("one orbit frame per step" if frames == 1 else
                                      f"{frames} consecutive orbit views per step (one launch)")
@@ -503,9 +566,9 @@ def main():
                 "accel": args.accel,
                 "parallelism": parallelism,
                 "frames_per_step": frames,
-                "ms_per_frame": round(elapsed / (args.steps * frames) * 1e3, 4),
-                "samples_per_frame": samples_all / args.steps / frames,
-                "rays_in_box_per_frame": in_box_all / args.steps / frames,
+                "ms_per_frame": round(elapsed / (steps * frames) * 1e3, 4),
+                "samples_per_frame": samples_all / steps / frames,
+                "rays_in_box_per_frame": in_box_all / steps / frames,
                 "candidates_per_sample": tot.candidatesTested / max(samples, 1),
                 "kernel_ms_rank0": round(avg_kernel_s * 1e3, 4),
                 "statistics_in_timed_loop": args.stats,
@@ -514,6 +577,7 @@ def main():
                 "chain_timeouts": chain_timeouts,
                 # the slot table (built when the headers outgrow the last-level cache)
                 "slot_table_bytes": ctx.array_bytes("slots"),
+                "context_create_s": round(create_s, 2),
             },
             "roofline": {
                 "bound": "hbm",
@@ -526,20 +590,112 @@ def main():
         }
         if single is not None:
             out["single_frame_launches"] = single  # the same frames, one launch each
-        prof = profiled_traffic(f"k_render<{irt.default_kernel_id(ctx)}>", args.config, frames)
+        if verify is not None:
+            out["verify"] = verify
+        prof = profiled_traffic(f"k_render<{irt.default_kernel_id(ctx)}>", config, frames)
         if prof and world == 1:
             out["roofline"]["traffic"] = prof[0]
             out["roofline"]["traffic_source"] = (
                 f"{prof[1]}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE per launch "
                 f"of the same kernel and workload")
-        if world == 1 and not args.no_cpu_baseline:
+        if primary and world == 1 and not args.no_cpu_baseline:
             cam = orbit_camera(0) if orbit is not None else FRAMING
             out["cpu_baseline"] = cpu_baseline(rn, bis, L, W, H, cam, tf, args.cpu_budget, terrain)
+    if dist_path:
+        dist.barrier()
+    del fb
+    if not dist_path:
+        del accum
+    ctx.close()
+    torch.cuda.empty_cache()
+    return out
+
+
+def secondary_entry(out):
+    """The fields of a secondary config's line that DESIGN.md quotes."""
+    c, r = out["config"], out["roofline"]
+    e = {"workload": c["workload"], "value": out["value"], "unit": out["unit"],
+         "ms_per_step": out["ms_per_step"], "ms_per_frame": c["ms_per_frame"],
+         "frames_per_launch": out["frames_per_launch"], "steps": out["steps"],
+         "warmup": out["warmup"], "records": c["records"],
+         "samples_per_frame": c["samples_per_frame"],
+         "candidates_per_sample": c["candidates_per_sample"],
+         "kernel_ms": c["kernel_ms_rank0"], "slot_table_bytes": c["slot_table_bytes"],
+         "context_create_s": c["context_create_s"], "chain_timeouts": c["chain_timeouts"],
+         "roofline": {k: r[k] for k in ("achieved", "unit", "frac", "traffic") if k in r}}
+    if "traffic_source" in r:
+        e["roofline"]["traffic_source"] = r["traffic_source"]
+    if "bytes_per_launch_rank0" in c and r.get("traffic"):
+        e["roofline"]["traffic_over_algorithmic"] = r["traffic"] / c["bytes_per_launch_rank0"]
+    if "single_frame_launches" in out:
+        e["single_frame_launches"] = out["single_frame_launches"]
+    return e
+
+
+def main():
+    args = parse_args()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        # no launcher: start the N ranks ourselves (before any GPU call in this process)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = int(world_env or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world} (one rank per GPU)")
+        sys.exit(2)
+
+    import torch
+
+    dist_path = world > 1 or args.force_dist
+    ndev = torch.cuda.device_count()  # counts without initialising the GPU on this image
+    if dist_path and args.dist_backend == "nccl" and ndev < world:
+        log(f"error: {world} RCCL ranks need {world} GPUs, {ndev} visible")
+        sys.exit(2)
+    device = local % max(ndev, 1) if dist_path else 0
+    json_out = sys.stdout
+    if dist_path:
+        # RCCL (and the runtime under it) may print banners on fd 1: send everything
+        # native to stderr and keep stdout for the one JSON line
+        json_out = os.fdopen(os.dup(1), "w")
+        sys.stdout.flush()
+        os.dup2(2, 1)
+        import torch.distributed as dist
+        torch.cuda.set_device(device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{device}"))
+        else:
+            dist.init_process_group("gloo")
+    torch.cuda.set_device(device)
+
+    out = run_config(args, args.config, args.steps, args.warmup, rank, world, dist_path)
+    if out is not None and not dist_path:
+        names = ([] if args.secondary == "none" else
+                 list(SECONDARY) if args.secondary == "auto" and args.config == "c3" else
+                 [] if args.secondary == "auto" else args.secondary.split(","))
+        sec = {}
+        for name in names:
+            if name not in CONFIGS or name == args.config:
+                continue
+            t = time.time()
+            try:
+                o = run_config(args, name, args.secondary_steps, 2, rank, world, dist_path,
+                               primary=False)
+                sec[name] = secondary_entry(o)
+                sec[name]["wall_s"] = round(time.time() - t, 1)
+            except Exception as e:  # a secondary config never costs the primary line
+                log(f"[rank 0] secondary {name} failed: {e!r}")
+                sec[name] = {"error": repr(e)}
+        if sec:
+            out["secondary"] = sec
+    if out is not None:
         print(json.dumps(out), file=json_out, flush=True)
+    bad = out is not None and out.get("verify", {}).get("mismatches", 0) > 0
     if dist_path:
         dist.barrier()
         dist.destroy_process_group()
-    ctx.close()
+    if bad:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

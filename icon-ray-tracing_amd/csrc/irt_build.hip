@@ -626,7 +626,10 @@ int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells
   BHIP(hipGetLastError());
   uint32_t h[kSlotSet + 1];
   if ((rc = read_back(h, set, kSlotSet + 1, s))) return rc;
-  if (h[kSlotSet]) return IRT_OK;  // more distinct edges than the set holds
+  if (h[kSlotSet]) {  // more distinct edges than the set holds
+    out.skipped = "the cells' radial edges are more than three values";
+    return IRT_OK;
+  }
   // the table's edges: cell 0's and the others', distinct and ascending
   std::vector<float> U;
   for (int j = 0; j < kMaxEdges; ++j)
@@ -635,14 +638,21 @@ int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells
     if (h[q]) U.push_back(u2f(h[q]));
   std::sort(U.begin(), U.end(), [](float a, float b) { return float_key(a) < float_key(b); });
   U.erase(std::unique(U.begin(), U.end(), [](float a, float b) { return f2u(a) == f2u(b); }), U.end());
-  if ((int)U.size() > kMaxEdges) return IRT_OK;
+  if ((int)U.size() > kMaxEdges) {
+    out.skipped = "the cells' radial edges are more than three values";
+    return IRT_OK;
+  }
   const int ne = (int)U.size(), bins = ne + 1;
   while ((int)U.size() < kMaxEdges) U.push_back(__builtin_inff());
   const size_t bytes = (size_t)numCells * kSubCells * kSubCells * bins * kSlot4 * sizeof(float4);
-  if (bytes > maxBytes) return IRT_OK;
+  if (bytes > maxBytes) {
+    out.skipped = "the table exceeds its memory cap (IRT_SLOTS_MAX_GB; default half the device's memory, and its free memory less 16 GiB)";
+    return IRT_OK;
+  }
   float4 *slots = nullptr;
   if (hipMalloc((void **)&slots, bytes) != hipSuccess) {
     (void)hipGetLastError();  // not enough memory: the scene renders without the table
+    out.skipped = "hipMalloc of the table failed";
     return IRT_OK;
   }
   hipLaunchKernelGGL(k_slot_fill, dim3(std::min<uint64_t>(grid_for(bytes / (kSlot4 * sizeof(float4))), 1u << 20)),

@@ -134,7 +134,7 @@ struct irt_context {
   uint32_t *d_schedOrder = nullptr, *d_schedCost = nullptr;  // 2 x stride, 4 cap
   uint32_t *h_schedCost = nullptr, *h_schedOrder = nullptr;  // pinned: kSlots x 4 cap, 2 x stride
   uint32_t schedSplit[2] = {0, 0};  // split packets in each order buffer
-  uint32_t lastNumSplit = 0;        // the last launch's split packets
+  uint32_t lastNumSplit = 0;        // the last launch's split work items (parts x packets, padded to 8)
   int splitLg = 2;                  // parts per split packet: 2^splitLg (IRT_SPLIT_LG; 0: no splits)
   float splitFactor = 1.f;          // a packet splits when its cost exceeds this x the frame's ideal span
   int schedBuf = 0;             // the order buffer launches read now
@@ -468,7 +468,8 @@ int sched_prepare(irt_context *c, int numBlocks, int W, int H, int packed, int t
   uint32_t *list = h + c->schedCap, *mask = list + kMaxSplit;
   memset(mask, 0, (4 * c->schedCap + 31) / 32 * sizeof(uint32_t));
   uint32_t ns = 0;
-  if (c->splitLg > 0 && c->splitFactor > 0.f && wavewg) {
+  // (a work item holds the packet index in 24 bits: no splits past 2^24 packets)
+  if (c->splitLg > 0 && c->splitFactor > 0.f && wavewg && 4 * (size_t)numBlocks < ((size_t)1 << 24)) {
     const size_t np = 4 * (size_t)numBlocks;
     double total = 0.0;
     for (size_t k = 0; k < np; ++k) total += cost[k];
@@ -1115,20 +1116,36 @@ int irt_create_end(irt_context *c) {
   c->binEntries = D.binEntries;
   mark("device scene build");
   // the slot table, when the cells share their radial edges, their headers outgrow the
-  // last-level cache (kSlotAutoHdrBytes) and it fits: at most IRT_SLOTS_MAX_GB (default: the
-  // device's free memory less 16 GiB); IRT_SLOTS=1: whatever the headers' size, 0: none
+  // last-level cache (kSlotAutoHdrBytes) and it fits: at most IRT_SLOTS_MAX_GB, by default half
+  // the device's memory and never more than its free memory less 16 GiB (a process sharing the
+  // GPU keeps the rest); IRT_SLOTS=1: whatever the headers' size, 0: none.  A built table is
+  // announced on stderr with its size; an explicit IRT_SLOTS=1 that builds none says why.
   {
     const char *e = getenv("IRT_SLOTS");
+    const bool forced = e && atoi(e) != 0;
     const size_t hdrBytes = (size_t)6 * c->G * c->G * kBinHdrWords * 4;
-    if (e ? atoi(e) != 0 : hdrBytes > kSlotAutoHdrBytes) {
+    // the kernel's slot index (cell * kSubCells^2 + sub) is 32-bit
+    const bool indexable = (uint64_t)6 * c->G * c->G * kSubCells * kSubCells < ((uint64_t)1 << 32);
+    if (e ? forced : hdrBytes > kSlotAutoHdrBytes) {
       size_t fr = 0, tot = 0;
       IRT_HIP(hipMemGetInfo(&fr, &tot));
       size_t cap = fr > ((size_t)16 << 30) ? fr - ((size_t)16 << 30) : 0;
+      cap = std::min(cap, tot / 2);
       if (const char *g = getenv("IRT_SLOTS_MAX_GB")) cap = std::min(cap, (size_t)(atof(g) * (double)(1ull << 30)));
-      if ((rc = build_slots_device(reinterpret_cast<const uint32_t *>(c->d_binHdr), c->d_fat, 6u * c->G * c->G, cap,
-                                   c->stream, c->slot)))
+      if (!indexable) {
+        c->slot = SlotTable{};
+        c->slot.skipped = "the cube map has 2^28 cells or more (32-bit slot index)";
+      } else if ((rc = build_slots_device(reinterpret_cast<const uint32_t *>(c->d_binHdr), c->d_fat,
+                                          6u * c->G * c->G, cap, c->stream, c->slot))) {
         return rc;
+      }
       c->bytes += c->slot.bytes;
+      if (c->slot.bytes)
+        fprintf(stderr, "icon_rt_hip: slot table built on device %d: %.1f GB of HBM (IRT_SLOTS=0: none)\n", c->device,
+                c->slot.bytes / 1e9);
+      else if (forced)
+        fprintf(stderr, "icon_rt_hip: IRT_SLOTS=1 but no slot table was built: %s\n",
+                c->slot.skipped ? c->slot.skipped : "unknown reason");
     }
   }
   mark("slot table");

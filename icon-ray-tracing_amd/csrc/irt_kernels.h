@@ -226,6 +226,7 @@ struct SlotTable {
   int bins = 0;
   float edges[3] = {0.f, 0.f, 0.f};
   size_t bytes = 0;
+  const char *skipped = nullptr;  // why no table was built (nullptr: built, or not asked for)
 };
 // Round 5: with the table C5 -9 %, C3s -3 %, but C3 +4 %, C4 +3 % (profiles/r05aa/): on by
 // default only when the headers exceed the 256-MB last-level cache (C5: 2.7 GB; C3: 167 MB)

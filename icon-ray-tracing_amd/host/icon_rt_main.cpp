@@ -13,6 +13,10 @@
 //                                                of the reference's hard-coded 512)
 //           [--accel sphere|grid]               (the "Accel mode" UI option,
 //                                                hostCode.cu:853-857, 170-199)
+//           [--gpus N]                          (N devices in this process: the frame's
+//                                                64x64 tiles dealt over them, RCCL gather
+//                                                to device 0; include/icon_rt_hip_multi.h)
+//           [--dump-fb file]                    (the final RGBA8 framebuffer, raw W*H u32)
 
 #include <math.h>
 #include <stdio.h>
@@ -27,6 +31,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "icon_rt_hip.h"
+#include "icon_rt_hip_multi.h"
 #include "pipeline.h"
 
 using namespace irt_host;
@@ -44,6 +49,8 @@ struct AppState {  // hostCode.cu:65-92 (the parts this backend uses)
   bool trueSize = false;
   int accelMode = IRT_ACCEL_SPHERE;  // g_appState.accelMode (hostCode.cu:75)
   int mode = IRT_MODE_USER_GEOM;     // g_appState.mode: the sampler (Params.h:29-31)
+  int gpus = 0;                      // > 0: the multi-GPU split over devices 0..gpus-1
+  std::string dumpFb;
 } g;
 
 bool endsWith(const std::string &s, const std::string &suffix) {
@@ -78,11 +85,20 @@ void parseCommandLine(int argc, char *argv[]) {  // hostCode.cu:106-129
       g.trueSize = true;
     else if (arg == "--accel" && i + 1 < argc)
       g.accelMode = std::string(argv[++i]) == "grid" ? IRT_ACCEL_GRID : IRT_ACCEL_SPHERE;
+    else if (arg == "--gpus" && i + 1 < argc)
+      g.gpus = atoi(argv[++i]);
+    else if (arg == "--dump-fb" && i + 1 < argc)
+      g.dumpFb = argv[++i];
   }
 }
 
 void die(const char *what) {
   fprintf(stderr, "%s: %s\n", what, irt_last_error());
+  exit(1);
+}
+
+void dieMulti(const char *what) {
+  fprintf(stderr, "%s: %s\n", what, irt_multi_last_error());
   exit(1);
 }
 
@@ -138,16 +154,30 @@ int main(int argc, char *argv[]) {
 
   // the accelerators (hostCode.cu:868-910): one HIP context replaces OptiX/cuBQL/shell
   irt_context *ctx = nullptr;
+  irt_multi *multi = nullptr;
   auto t0 = std::chrono::steady_clock::now();
-  if (irt_create(cells.data(), cells.size(), 0, &ctx)) die("irt_create");
+  if (g.gpus > 0) {  // one context per device, an RCCL communicator over them
+    std::vector<int> devs(g.gpus);
+    for (int d = 0; d < g.gpus; ++d) devs[d] = d;
+    if (irt_multi_create_cells(cells.data(), cells.size(), devs.data(), g.gpus, &multi))
+      dieMulti("irt_multi_create_cells");
+    ctx = irt_multi_context(multi, 0);
+    fprintf(stderr, "icon_rt: %d devices, frame tiles dealt by cost, RCCL gather to device 0\n", g.gpus);
+  } else if (irt_create(cells.data(), cells.size(), 0, &ctx)) {
+    die("irt_create");
+  }
   auto t1 = std::chrono::steady_clock::now();
   irt_get_volume_info(ctx, &info);
   fprintf(stderr, "icon_rt: %zu cells, %.2f GiB HBM, locator %d^2 x 6, build %.2f s\n",
           cells.size(), info.deviceBytes / 1073741824.0, info.locatorFaceRes,
           std::chrono::duration<double>(t1 - t0).count());
   pl.setTransfuncUpdateHandler([&](const Transfunc *tf, int) {
-    if (irt_set_transfunc(ctx, tf->lut.data(), tf->size(), tf->valueRange, tf->opacity))
+    if (multi) {
+      if (irt_multi_set_transfunc(multi, tf->lut.data(), tf->size(), tf->valueRange, tf->opacity))
+        dieMulti("irt_multi_set_transfunc");
+    } else if (irt_set_transfunc(ctx, tf->lut.data(), tf->size(), tf->valueRange, tf->opacity)) {
       die("irt_set_transfunc");
+    }
   });
 
   // camera (hostCode.cu:819-821 viewAll, pipeline.cu:444-454 cmdline override, 939-945)
@@ -166,7 +196,9 @@ int main(int argc, char *argv[]) {
   lp.accelMode = g.accelMode;         // toggleAccelMode (hostCode.cu:170-199)
   if (g.mode == IRT_MODE_CUBQL || g.mode == IRT_MODE_TRIANGLES) {
     // toggleMode (hostCode.cu:152-168): buildCuBQLAccel / buildTriangleAccel's geometry
-    if (irt_build_wedge_accel(ctx, cells.data(), cells.size())) die("irt_build_wedge_accel");
+    for (int d = 0; d < (multi ? g.gpus : 1); ++d)
+      if (irt_build_wedge_accel(multi ? irt_multi_context(multi, d) : ctx, cells.data(), cells.size()))
+        die("irt_build_wedge_accel");
     lp.mode = g.mode;
   } else if (g.mode != IRT_MODE_USER_GEOM) {
     fprintf(stderr, "icon_rt: unknown -mode %d; using the cell sampler (-mode 0)\n", g.mode);
@@ -177,6 +209,10 @@ int main(int argc, char *argv[]) {
       die("clear");
   };
   pl.setRayGen([&] {
+    if (multi) {
+      if (irt_multi_render(multi, &lp, fb.width, fb.height, 1, fb.fbPointer, nullptr)) dieMulti("irt_multi_render");
+      return;
+    }
     if (irt_render(ctx, &lp, fb.width, fb.height, fb.fbPointer, fb.accumBuffer, nullptr))
       die("irt_render");
     irt_render_stats st;
@@ -191,25 +227,47 @@ int main(int argc, char *argv[]) {
 
   if (g.benchFrames > 0) {
     // as bench.py: per-launch counting off, the launches back to back, one wait at the end
-    if (irt_set_statistics(ctx, 0)) die("irt_set_statistics");
+    for (int d = 0; d < (multi ? g.gpus : 1); ++d)
+      if (irt_set_statistics(multi ? irt_multi_context(multi, d) : ctx, 0)) die("irt_set_statistics");
     const int B = g.framesPerLaunch;
     auto render = [&](int k, int n) {  // B > 1: frames k .. k+n-1 of the accumulation in one launch
       lp.accumID = B > 1 ? k : 0;
+      if (multi) {
+        if (irt_multi_render(multi, &lp, fb.width, fb.height, n, fb.fbPointer, nullptr)) dieMulti("irt_multi_render");
+        return;
+      }
       const int rc = n > 1 ? irt_render_accumulate(ctx, &lp, fb.width, fb.height, n, fb.fbPointer,
                                                    fb.accumBuffer, nullptr)
                            : irt_render(ctx, &lp, fb.width, fb.height, fb.fbPointer, fb.accumBuffer, nullptr);
       if (rc) die("irt_render");
     };
+    auto sync = [&] {
+      if (multi && irt_multi_synchronize(multi)) dieMulti("irt_multi_synchronize");
+      if (hipDeviceSynchronize() != hipSuccess) die("hipDeviceSynchronize");
+    };
     render(0, B);  // warm-up
-    if (hipDeviceSynchronize() != hipSuccess) die("hipDeviceSynchronize");
+    sync();
     const auto a = std::chrono::steady_clock::now();
     for (int k = 0; k < g.benchFrames; k += B) render(B + k, std::min(B, g.benchFrames - k));
-    if (hipDeviceSynchronize() != hipSuccess) die("hipDeviceSynchronize");
+    sync();
     const double total = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
     const double px = (double)fb.width * fb.height * g.benchFrames;
-    printf("bench: %d frames %dx%d, %d per launch: %.4f ms/frame, %.1f Mray/s\n", g.benchFrames, fb.width,
-           fb.height, B, 1e3 * total / g.benchFrames, px / total / 1e6);
+    printf("bench: %d frames %dx%d, %d per launch, %d device(s): %.4f ms/frame, %.1f Mray/s\n", g.benchFrames,
+           fb.width, fb.height, B, multi ? g.gpus : 1, 1e3 * total / g.benchFrames, px / total / 1e6);
   }
-  irt_destroy(ctx);
+  if (!g.dumpFb.empty()) {  // the final framebuffer (after --bench's frames), raw (x + W*y, RGBA8 with r in the low byte)
+    if (multi && irt_multi_synchronize(multi)) dieMulti("irt_multi_synchronize");
+    std::vector<uint32_t> h((size_t)fb.width * fb.height);
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(h.data(), fb.fbPointer, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+      die("dump-fb copy");
+    FILE *f = fopen(g.dumpFb.c_str(), "wb");
+    if (!f || fwrite(h.data(), 4, h.size(), f) != h.size()) die("dump-fb write");
+    fclose(f);
+  }
+  if (multi)
+    irt_multi_destroy(multi);
+  else
+    irt_destroy(ctx);
   return 0;
 }

@@ -599,7 +599,8 @@ class Context:
         _check(L.irt_debug_set_chain_fault(self._h, spins, withhold_frame), "irt_debug_set_chain_fault")
 
     def sched_split(self):
-        """(packets split by the last launch, log2 of their parts) -- measured-cost scheduling."""
+        """(split work items of the last launch -- parts x split packets, padded with empty items to
+        a multiple of 8 -- and log2 of the parts per packet): measured-cost scheduling."""
         L = lib()
         L.irt_debug_sched_split.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         n, lg = C.c_int(), C.c_int()

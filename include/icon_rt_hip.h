@@ -198,7 +198,9 @@ int irt_render_tiles(irt_context *ctx, const irt_launch_params *lp, int width, i
  * next call on the context that sees it -- any irt_render* call, irt_get_render_stats*,
  * irt_reset_render_stats_total -- returns IRT_E_CHAIN, irt_last_error() names the launch, and
  * the context renders later multi-frame launches without chaining (per-frame sample buffer +
- * a lerp pass).  (The reference's launch either renders the frame or aborts,
+ * a lerp pass).  The call that returns IRT_E_CHAIN has NOT enqueued its own work: its frame(s)
+ * were not rendered, and the caller re-issues the call (or restarts the accumulation from
+ * accumID 0).  (The reference's launch either renders the frame or aborts,
  * pipeline.cu:1038-1075.)  Frames of 2^27 pixels or more are never chained. */
 int irt_render_accumulate(irt_context *ctx, const irt_launch_params *lp, int width, int height,
                           int numFrames, uint32_t *d_fb, irt_vec4f *d_accum, void *stream);

@@ -156,9 +156,11 @@ int irt_debug_set_wg_trace(irt_context *ctx, uint32_t *trace);
  * items, which come first; rows a launch does not use stay as they were). */
 long long irt_debug_launch_workgroups(const irt_context *ctx, int numTiles, int numFrames);
 /* Measured-cost scheduling (IRT_SCHED; on by default for scenes with holes): the last launch's
- * split packets -- those longer than IRT_SPLIT_FACTOR (1) x the frame's ideal span (the packets'
- * durations over the resident slots), rendered first in 2^splitLg parts of 64 >> splitLg rays
- * (IRT_SPLIT_LG, default 2; 0: no splits) -- and splitLg.  Frames are unchanged. */
+ * split WORK ITEMS in *numSplit -- every split packet (one longer than IRT_SPLIT_FACTOR (1) x
+ * the frame's ideal span, the packets' durations over the resident slots) is rendered first in
+ * 2^splitLg parts of 64 >> splitLg rays (IRT_SPLIT_LG, default 2; 0: no splits), one work item
+ * per part, and the items are padded with empty ones to a multiple of 8 (so *numSplit is parts x
+ * packets rounded up, not the packet count) -- and splitLg.  Frames are unchanged. */
 int irt_debug_sched_split(const irt_context *ctx, int *numSplit, int *splitLg);
 /* Chained progressive frames on (default; IRT_CHAIN=0 turns it off per context) or off: a
  * launch of several frames (irt_render_accumulate, irt_render_tiles_accumulate,

@@ -9,9 +9,18 @@ import irt
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_functions():
+# header -> the library that exports it (icon_rt_hip_multi.h: the RCCL multi-GPU layer,
+# a library of its own so that the product library never links a second RCCL into torch)
+LIBS = {"icon_rt_hip_multi.h": "libicon_rt_multi.so"}
+
+
+def declared_functions(header=None):
     names = set()
     for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        if header is not None and os.path.basename(h) != header:
+            continue
+        if header is None and os.path.basename(h) in LIBS:
+            continue
         src = open(h).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         for m in re.finditer(r"\b(irt_[a-z0-9_]+)\s*\(", src):
@@ -25,6 +34,21 @@ def test_library_exports_every_declared_symbol():
     lib = C.CDLL(irt.LIB_PATH)
     missing = [n for n in sorted(names) if not hasattr(lib, n)]
     assert not missing, missing
+
+
+def test_multi_library_exports_every_declared_symbol():
+    """libicon_rt_multi.so (one process, N devices, RCCL) loads without a GPU and exports
+    include/icon_rt_hip_multi.h; it rejects a null handle before touching a device."""
+    for header, so in LIBS.items():
+        names = declared_functions(header)
+        assert len(names) >= 8
+        lib = C.CDLL(os.path.join(os.path.dirname(irt.LIB_PATH), so))
+        missing = [n for n in sorted(names) if not hasattr(lib, n)]
+        assert not missing, missing
+    lib.irt_multi_last_error.restype = C.c_char_p
+    assert lib.irt_multi_set_transfunc(None, None, 0, irt.box1(0, 1), C.c_float(1.0)) == -1
+    assert b"null handle" in lib.irt_multi_last_error()
+    assert lib.irt_multi_num_devices(None) == 0
 
 
 def test_cell_record_layout():
