@@ -427,14 +427,41 @@ IRT_HD int cell_candidates(const E &en, int n, float *cand, double &rmin, double
 //   [4..7]   cumulative ends of bins 0..3 (relative to base)
 //   [8..23]  per sub-cell s (kSub x kSub, s = sj*kSub + si): byte k = which of the first
 //            kMaskCand candidates of bin k can reach sub-cell s
-//   [24..31] 0
-// The kernel loads words 0..7 and word 8+s from the same line.
+//   [24..31] per quad q of 2 x 2 sub-cells (kQuads of them, quad_of): words 24 + 2q, 25 + 2q =
+//            the highest height[numLayers] and the lowest height[0] of the cell's records whose
+//            column can reach the quad (-inf / +inf: none).  No point of the quad outside
+//            [lowest, highest] passes sample()'s radial test (ICONGrid.h:184) for any record
+//            listed here, and every record that can contain it is listed: such a sample is
+//            outside every cell without a candidate test.  convert_icon grids have such voids
+//            over every land column (its top H[j] = R + HHL - HSURF, convert_icon.cpp:371, lies
+//            HSURF below the ocean's) and under it (H[0] = R + HSURF, 361).
+// The kernel loads words 0..7 and word 8+s from the same line (and the quad's words 24..).
 //
 // Fills every word but the base from a cell's n entries (in record order: bottom/top
 // heights and sub-cell masks) and its ne edges; returns the cell's number of fat entries.
+IRT_HD uint32_t quad_mask(int q) {  // the sub-cells of quad q
+  uint32_t m = 0u;
+  for (uint32_t s = 0; s < (uint32_t)(kSub * kSub); ++s)
+    if (quad_of(s) == q) m |= 1u << s;
+  return m;
+}
+
 template <class E>
 IRT_HD uint32_t cell_header(const E &en, int n, const float *edges, int ne, uint32_t *H) {
   for (int w = 0; w < kBinHdrWords; ++w) H[w] = 0u;
+  // words 24..31: the radial range of the records that can reach each quad
+  for (int q = 0; q < kQuads; ++q) {
+    const uint32_t qm = quad_mask(q);
+    float hi = -__builtin_inff(), lo = __builtin_inff();
+    for (int e = 0; e < n; ++e) {
+      if (!(en.sub(e) & qm)) continue;
+      const float a = en.h0(e), b = en.hN(e);
+      hi = b > hi ? b : hi;
+      lo = a < lo ? a : lo;
+    }
+    H[kBoundWord + 2 * q] = f2u(hi);
+    H[kBoundWord + 1 + 2 * q] = f2u(lo);
+  }
   for (int k = 0; k < kMaxEdges; ++k) H[k] = f2u(k < ne ? edges[k] : __builtin_inff());
   uint32_t cum = 0;
   for (int k = 0; k <= kMaxEdges; ++k) {

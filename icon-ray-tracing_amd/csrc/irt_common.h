@@ -385,6 +385,14 @@ constexpr int kMaxEdges = 3;
 // Cell header (irt_build.h): {e0, e1, e2, base} {end0, end1, end2, end3}, then the sub-cell
 // candidate masks: 128 B per cell (64 B with 2 x 2 sub-cells)
 constexpr int kBinHdrWords = 8 + kSubCells * kSubCells <= 16 ? 16 : 32;
+// the header's per-quad radial bounds (irt_build.h cell_header): quads of 2 x 2 sub-cells
+constexpr int kQuadEdge = kSubCells > 1 ? kSubCells / 2 : 1;  // quads per cell edge
+constexpr int kQuads = kQuadEdge * kQuadEdge;
+constexpr int kBoundWord = 8 + kSubCells * kSubCells;  // after the masks (24 with 4 x 4 sub-cells)
+static_assert(kBoundWord + 2 * kQuads <= kBinHdrWords, "the quads' bounds fit the header line");
+IRT_HD int quad_of(uint32_t s) {  // sub-cell s = sj * kSubCells + si -> its 2 x 2 quad
+  return kSubCells > 1 ? (int)((s / kSubCells / 2) * kQuadEdge + (s % kSubCells) / 2) : 0;
+}
 IRT_HD int bin_of(float r, float e0, float e1, float e2) {
   return (e0 < r ? 1 : 0) + (e1 < r ? 1 : 0) + (e2 < r ? 1 : 0);
 }

@@ -81,6 +81,10 @@ enum : int {
   OPT_PAIR = 268435456,  // (A/B) the wave-wide scan's first step tests each lane's first two
                          // candidates (both entries gathered together), so the dealt-out step
                          // runs only for lanes whose first two fail
+  OPT_NOVOIDRUN = 2,   // (A/B) the miss-mode kernels without the solo lanes' void walk (woodcock_wave)
+  OPT_NOHOLESKIP = 4,  // (A/B) the miss-mode kernels without the quad-bound miss test (Tracer::locate_wave:
+                       // a sample outside its quad's radial range is outside every cell, no
+                       // candidate tested)
   OPT_SLOT = 128,  // the wave-wide scan starts from the slot table (RenderArgs::slots, irt_common.h
                    // kSlot4): the first admitted candidate and the list's position in one gather,
                    // instead of the header, then the entry; launches on a scene with a table run
@@ -308,6 +312,10 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // waves running ~1 ms: profiles/r05d_missmode/).  Flat grids almost never miss (C3: 707 of 1.01 M
   // samples).  The kernels with misses everywhere (wedges, grid) start with whole-wave groups.
   static constexpr bool kMiss = kCoop && (OPT & OPT_NOMISS) == 0;
+  // the void walk of woodcock_wave's solo miss-mode lanes (the user-geometry sampler from headers)
+  static constexpr bool kVoidRun =
+      kMiss && (OPT & (OPT_WEDGE | OPT_GRID | OPT_SCAN1 | OPT_SLOT | OPT_HDRLDS | OPT_NOHOLESKIP | OPT_NOVOIDRUN)) == 0;
+  static constexpr int kVoidRunMax = 32;  // samples one lane walks before the round goes on
   static constexpr bool kWideStart = (OPT & (OPT_WEDGE | OPT_GRID)) != 0;
 
   // one wave-aggregated LDS add per event site
@@ -660,6 +668,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     uint32_t tv = 0u;  // OPT_NEXTHDR's loaded word, consumed after the scan
     uint32_t fe2 = 0u; // OPT_PAIR: the pass's second candidate entry
     constexpr bool kSlot = (OPT & OPT_SLOT) != 0;
+    // the quad-bound miss test: scenes with holes (the miss-mode kernels) that start from headers
+    constexpr bool kHoleSkip = kMiss && !kSlot && (OPT & (OPT_HDRLDS | OPT_NOHOLESKIP)) == 0;
     static_assert(!kSlot || (OPT & (OPT_HDRLDS | OPT_PAIR | OPT_DEALALL | OPT_NEXTHDR)) == 0, "slot table: the default scan");
     float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, sm = s0;  // OPT_SLOT: the first candidate
     if constexpr ((OPT & OPT_HDRLDS) != 0) {
@@ -709,6 +719,18 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       const uint32_t n = end - beg;
       const uint32_t m8 = (M >> (8 * b)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
       c = (uint32_t)__popc(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
+      if constexpr (kHoleSkip) {
+        // the sample's quad's radial range (header words kBoundWord..): outside it no listed
+        // record passes the radial test (ICONGrid.h:184), so the scan would test every candidate
+        // and find none -- a void of the volume (convert_icon's land columns), decided from the
+        // header line alone
+        const uint2 bd = reinterpret_cast<const uint2 *>(A.binHdr + (size_t)cell * (kBinHdrWords / 4))
+            [kBoundWord / 2 + quad_of(sub)];
+        if (r > __uint_as_float(bd.x) || r < __uint_as_float(bd.y)) {
+          c = 0u;
+          edge = false;
+        }
+      }
       lds_st16(&W.pt[lane], make_float4(px, py, pz, r));
       lds_st16(&W.lst[lane], make_uint4(H0.w + beg, m8, 0u, 0xFFFFFFFFu));
       fe = H0.w + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
@@ -1027,7 +1049,45 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
           default: tk = coop_prefix<64>(rq.x, dg, k); break;
         }
       }
-      const bool past = used && tk > rq.y;
+      bool past = used && tk > rq.y;
+      if constexpr (kVoidRun) {
+        // A solo lane in miss mode walks the void its ray is in on its own: while its sample lies
+        // outside the radial range of every record that can reach the sample's quad (the cell
+        // header's bounds, the quad-bound test of locate_wave), the sample is outside every cell
+        // -- sampleVolume finds nothing and woodcockTracking takes its next step after one draw
+        // (deviceCode.cu:165-173) -- so the lane takes that step here, with no candidate test (the
+        // header's bound word, an L1 hit while the walk stays in one cell).  The round then scans the first sample
+        // that may be located.  convert_icon's voids (over and under every land column) are
+        // crossed in one round instead of one round per sample.
+        if (solo && mm && used && !past) {
+          const float3 O = cam_org(A, frame);
+#pragma nounroll
+          for (int it = 0; it < kVoidRunMax; ++it) {
+            const float px = O.x + ry.x * tk, py = O.y + ry.y * tk, pz = O.z + ry.z * tk;
+            const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
+            uint32_t sub;
+            const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G, sub);
+            // (the same header line as the last sample's while the walk stays in one cell: an L1 hit)
+            const uint2 bd = reinterpret_cast<const uint2 *>(A.binHdr + (size_t)cell * (kBinHdrWords / 4))
+                [kBoundWord / 2 + quad_of(sub)];
+            if (!(r > __uint_as_float(bd.x) || r < __uint_as_float(bd.y))) break;  // may be located: the round's scan decides
+            if (A.numSph) {  // a zero-thickness record at exactly r is not in the lists
+              const uint32_t h = sph_hash(r);
+              if ((s_sph[h >> 5] >> (h & 31)) & 1u) break;
+            }
+            // outside every cell: the sample is taken (a sampleVolume call), one draw
+            if (cntd) ++nLocate;
+            if constexpr ((OPT & OPT_STATS) != 0) ++cnt.steps;
+            rq.x = tk;
+            sk = lcg_next(sk);
+            tk = rq.x - woodcock_log(sk, s_logf) / rq.z;
+            if (tk > rq.y) {
+              past = true;
+              break;
+            }
+          }
+        }
+      }
       bool found = false, acc = false;
       float value = 0.f;
       tmark(2);  // round start: exchange, jumps, logf, prefix
@@ -2513,7 +2573,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73405728) X(73667872) X(73405760) X(73667904) X(73405712) X(73667856) X(73930016) X(74192160)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73405728) X(73667872) X(73405760) X(73667904) X(73405712) X(73667856) X(73930016) X(74192160) X(73405732) X(73405730)
 #else
 #define IRT_VARIANTS(X) X(73405728) X(73667872) X(5376) X(36864)
 #endif

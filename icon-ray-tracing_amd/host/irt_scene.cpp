@@ -347,7 +347,12 @@ int locate_bins_host(const HostScene &s, float px, float py, float pz, float &va
   int hit = 0;
   uint32_t best = 0;
   float bestV = 0.f;
-  const int last = (b < kMaxEdges && r == e[b]) ? b + 1 : b;  // exactly on an edge
+  // outside the radial range of every record that can reach the point's quad (the header's
+  // bounds, irt_build.h cell_header): no candidate can pass, none is tested (the miss-mode kernels'
+  // quad-bound test, irt_render.hip locate_wave)
+  const int q = quad_of(sub);
+  const bool outside = r > u2f(H[kBoundWord + 2 * q]) || r < u2f(H[kBoundWord + 1 + 2 * q]);
+  const int last = outside ? b - 1 : (b < kMaxEdges && r == e[b]) ? b + 1 : b;  // exactly on an edge
   for (int k = b; k <= last; ++k) {
     const uint32_t beg = H[3] + (k ? H[4 + k - 1] : 0), end = H[3] + H[4 + k];
     const uint32_t mask = (H[8 + sub] >> (8 * k)) & 0xFFu;

@@ -20,7 +20,7 @@ for cfg in $CONFIGS; do
         for a in "${kv[@]}"; do vars+=("$a"); v="${a#IRT_}"; [ "${a%%=*}" = IRT_RENDER_VARIANT ] && v="${a#*=}"; n="${n}_${v}"; done
       fi
       env IRT_LIB_PATH="$lib" "${vars[@]}" timeout -k 10 240 python3 bench.py --config $cfg --batch $B --steps $steps --no-single-compare \
-        --warmup 5 --no-cpu-baseline >> "$OUT/${n}_$cfg.jsonl" 2>> "$OUT/${n}_$cfg.err" || exit 1
+        --warmup 5 --no-cpu-baseline --secondary none >> "$OUT/${n}_$cfg.jsonl" 2>> "$OUT/${n}_$cfg.err" || exit 1
     done
   done
 done

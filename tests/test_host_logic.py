@@ -312,10 +312,13 @@ def test_binned_locator_on_terrain_following_columns(kind):
     assert zt
     for i in zt[:10]:
         pts.append(_on_radius(rng.normal(size=3), cells["height"][i][0]))
-    n_hit = n_sph = 0
+    n_hit = n_sph = n_void = 0
     zt = set(zt)
     for p in pts:
-        hb, vb, recb, _ = D.locate_binned(p)
+        hb, vb, recb, tested = D.locate_binned(p)
+        # outside the radial range of every record that can reach its quad (the header's bounds):
+        # decided without a candidate test -- and the brute-force scan below must agree
+        n_void += (not hb) and tested == 0
         val = C.c_float()
         found = None
         for i in range(cells.size):
@@ -328,6 +331,8 @@ def test_binned_locator_on_terrain_following_columns(kind):
             assert found[0] == recb and found[1] == np.float32(vb), (p, found, recb)
             n_sph += found[0] in zt
     assert n_hit > len(pts) // 3 and n_sph >= 3
+    # the convert_icon layout's voids over land (tops HSURF below the ocean's) and under it
+    assert kind != "convert_icon" or n_void > 20, n_void
 
 
 # ------------------------------------------------------------------ CUBQL_MODE wedges
