@@ -81,6 +81,9 @@ enum : int {
   OPT_PAIR = 268435456,  // (A/B) the wave-wide scan's first step tests each lane's first two
                          // candidates (both entries gathered together), so the dealt-out step
                          // runs only for lanes whose first two fail
+  OPT_CHAINPF = 1,  // (A/B, with OPT_LEAN) a chained frame's accum pixel fetched into LDS by LDS-DMA
+                    // (sc1) at the box test when frame f - 1 has already published it (the usual
+                    // case), not loaded (sc1) at the ray's end
   OPT_NOVOIDRUN = 2,   // (A/B) the miss-mode kernels without the solo lanes' void walk (woodcock_wave)
   OPT_NOHOLESKIP = 4,  // (A/B) the miss-mode kernels without the quad-bound miss test (Tracer::locate_wave:
                        // a sample outside its quad's radial range is outside every cell, no
@@ -1682,6 +1685,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   // array: the compiler's LDS-DMA tracking waits for it only where the slots are read, at the end)
   constexpr bool accPf = (OPT & OPT_ACCPF) != 0 && (OPT & OPT_LEAN) != 0;
   const bool accEarly = accPf && !toSample && !chainLate;
+  constexpr bool chainPf = (OPT & OPT_CHAINPF) != 0 && (OPT & OPT_LEAN) != 0;
   if (accEarly && px.active)
     __builtin_amdgcn_global_load_lds((const void *)(A.accum + px.outIdx),
                                      (__attribute__((address_space(3))) void *)(s_acc + (tid & ~63)), 16, 0, 0);
@@ -1737,7 +1741,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     }
   }
   const bool chainReady = !chainLate || __builtin_amdgcn_readfirstlane(chainSeen) == A.chainEpoch + (uint32_t)frame;
-  if ((OPT & OPT_LEAN) == 0 && chainLate && chainReady && inBox)
+  if (((OPT & OPT_LEAN) == 0 || chainPf) && chainLate && chainReady && inBox)
     __builtin_amdgcn_global_load_lds((const void *)(A.accum + px.outIdx),
                                      (__attribute__((address_space(3))) void *)(s_acc + (tid & ~63)), 16, 0, 16);  // sc1
   // GRID_ACCEL_MODE (deviceCode.cu:326-328): dda3 (DDA.h:35-136) over the 256^3 grid as
@@ -2097,8 +2101,11 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     const size_t outIdx = kRecompute ? pixel_of(A, (uint32_t)opaque_u((int)blk), ptid_late()).outIdx : px.outIdx;
     if (A.chain) {
       float4 old;
-      if (chainLate && (!chainReady || (OPT & OPT_LEAN) != 0)) {
+      if (chainLate && (!chainReady || ((OPT & OPT_LEAN) != 0 && !chainPf))) {
         old = chain_load_accum(A, outIdx);
+      } else if (chainPf && chainLate) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
+        old = lds_ld16(&s_acc[tl]);
       } else if constexpr (accPf) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
         old = lds_ld16(&s_acc[tl]);
@@ -2112,6 +2119,11 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       write_pixel_chain(A, outIdx, c.x, c.y, c.z, c.w, 1.f / (float)(accumID + 1), s_th, old,
                         frame < A.numSamples - 1);
     } else if constexpr ((OPT & OPT_LEAN) != 0 && !accPf) {
+      if (A.probeExit == 6) {  // measurement only: the lerp without its accum read (frames differ)
+        write_pixel(A, outIdx, c.x, c.y, c.z, c.w, s_th, make_float4(0.f, 0.f, 0.f, 0.f));
+        return;
+      }
+      if (A.probeExit == 7) return;  // measurement only: no accum read, no pixel stores
       write_pixel(A, outIdx, c.x, c.y, c.z, c.w, s_th);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
@@ -2183,7 +2195,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   __shared__ CoopWave s_coop[kW];   // the cooperative Woodcock loop (kCoop kernels)
   __shared__ ScanWave s_scan[Tracer<OPT>::kWaveScan ? kW : 1];  // its wave-wide candidate scan
   __shared__ HdrStage s_hdrs[(OPT & OPT_HDRLDS) ? kW : 1];       // OPT_HDRLDS: staged header lines
-  __shared__ float4 s_acc[lean ? ((OPT & OPT_ACCPF) ? 64 : 1) : 256];  // kCoop: the accum pixels, prefetched
+  __shared__ float4 s_acc[lean ? ((OPT & (OPT_ACCPF | OPT_CHAINPF)) ? 64 : 1) : 256];  // kCoop: the accum pixels, prefetched
   __shared__ uint2 s_jmp[kLcgJumps];  // lcg_jump's {mul, add} (kLcgJumpTab)
   const int tid = threadIdx.x;
   if (A.wgTrace && tid == 0) {  // measurement only: the workgroup's start, where it ran
@@ -2573,7 +2585,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73405728) X(73667872) X(73405760) X(73667904) X(73405712) X(73667856) X(73930016) X(74192160) X(73405732) X(73405730)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73405728) X(73667872) X(73405760) X(73667904) X(73405712) X(73667856) X(73930016) X(74192160) X(73405732) X(73405730) X(73405729) X(73667873) X(73405744) X(73667888) X(73405745) X(73667889)
 #else
 #define IRT_VARIANTS(X) X(73405728) X(73667872) X(5376) X(36864)
 #endif
