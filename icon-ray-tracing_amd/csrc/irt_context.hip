@@ -147,6 +147,7 @@ struct irt_context {
   // ramp, 2^coopMaxLg without (IRT_COOP_MAXLG, IRT_COOP_RAMP; profiles/r02e_dist/)
   int coopMaxLg = 0;
   int coopRamp = 1;
+  int voidLocFirst = 0;        // IRT_VOIDLOC_FIRST (OPT_VOIDLOC kernels, RenderArgs::voidLocFirst)
   int probeExit = 0;           // IRT_PROBE_EXIT (measurement only, RenderArgs::probeExit)
   uint32_t *wgTrace = nullptr; // irt_debug_set_wg_trace (measurement only, RenderArgs::wgTrace)
   // chained progressive frames (RenderArgs::chain; IRT_CHAIN=0 / irt_debug_set_chain: the
@@ -634,6 +635,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.lutSize = c->lutSize;
   A.coopMaxLg = c->coopMaxLg;
   A.coopRamp = c->coopRamp;
+  A.voidLocFirst = c->voidLocFirst;
   A.probeExit = c->probeExit;
   A.wgTrace = c->wgTrace;
   A.numCells = c->n;
@@ -689,7 +691,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   const size_t lanes = (size_t)numTiles * 4096;
   // persistent launch: the cooperative kernels, not for the measurement-only early exits
   // (every wave must reach the queue's done count)
-  const bool queued = c->queueOn && numTiles > 0 && c->probeExit == 0 && render_queue_ok(A, c->variant);
+  const bool queued = c->queueOn && numTiles > 0 && (c->probeExit == 0 || c->probeExit >= 16) && render_queue_ok(A, c->variant);
   int queueWG = 0;
   if (queued) {
     A.queue = c->d_queue + (size_t)kQueueWords * slot;
@@ -713,7 +715,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     const uint32_t *ob = c->d_schedOrder + (size_t)c->schedBuf * sched_stride(c->schedCap);
     A.schedOrder = c->schedOrderValid ? ob : nullptr;
     if (c->schedOrderValid && c->schedSplit[c->schedBuf] && render_split_ok(A, c->variant) &&
-        c->probeExit == 0) {
+        (c->probeExit == 0 || c->probeExit >= 16)) {
       A.splitList = ob + c->schedCap;
       A.splitMask = ob + c->schedCap + kMaxSplit;
       A.numSplit = c->schedSplit[c->schedBuf];
@@ -784,7 +786,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   // The hand-off's buffer resources address accum with 32-bit byte offsets: frames of 2^27
   // pixels or more (11,585^2) go through the sample buffer instead
   const uint64_t outPixels = packed ? (uint64_t)numTiles * 4096u : (uint64_t)W * (uint64_t)H;
-  A.chain = c->chainOn && numFrames > 1 && !queued && c->probeExit == 0 && (c->variant & 65536) == 0 &&
+  A.chain = c->chainOn && numFrames > 1 && !queued && (c->probeExit == 0 || c->probeExit >= 16) && (c->variant & 65536) == 0 &&
                     outPixels * 16u <= 0x7FFFFFFFull
                 ? 1
                 : 0;
@@ -1207,6 +1209,7 @@ int irt_create_end(irt_context *c) {
   if (const char *e = getenv("IRT_WG_COUNTS_MAX")) c->wgCountsMax = (size_t)std::max(0LL, atoll(e));
   if (const char *e = getenv("IRT_COOP_MAXLG")) c->coopMaxLg = std::min(6, std::max(0, atoi(e)));
   if (const char *e = getenv("IRT_COOP_RAMP")) c->coopRamp = std::min(6, std::max(0, atoi(e)));
+  if (const char *e = getenv("IRT_VOIDLOC_FIRST")) c->voidLocFirst = atoi(e) != 0;
   if (const char *e = getenv("IRT_PROBE_EXIT")) c->probeExit = atoi(e);
   if (const char *e = getenv("IRT_QUEUE")) c->queueOn = atoi(e) != 0 && render_queue_compiled();
   if (const char *e = getenv("IRT_QUEUE_WGS")) c->queuePerCU = std::max(0, atoi(e));
@@ -1479,7 +1482,7 @@ int render_sequence(irt_context *c, const irt_launch_params *lps, int numFrames,
       set_error("irt_render_sequence: frame %d differs from frame 0 in more than the camera and accumID", k);
       return IRT_E_INVALID;
     }
-  const bool chainable = c->chainOn && (c->variant & 65536) == 0 && !c->queueOn && c->probeExit == 0;
+  const bool chainable = c->chainOn && (c->variant & 65536) == 0 && !c->queueOn && (c->probeExit == 0 || c->probeExit >= 16);
   static const int32_t none = 0;
   const int32_t *list = tiles ? (numTiles > 0 ? tiles : &none) : nullptr;  // null: the whole frame
   const int packed = tiles ? 1 : 0;

@@ -81,6 +81,9 @@ enum : int {
   OPT_PAIR = 268435456,  // (A/B) the wave-wide scan's first step tests each lane's first two
                          // candidates (both entries gathered together), so the dealt-out step
                          // runs only for lanes whose first two fail
+  OPT_VOIDLOC = 1073741824,  // (A/B) the solo lanes' void walk also in located mode: a certain miss
+                             // at the round's sample switches the ray to miss mode there, not a
+                             // round later (RenderArgs::voidLocFirst: only in a call's first round)
   OPT_CHAINPF = 1,  // (A/B, with OPT_LEAN) a chained frame's accum pixel fetched into LDS by LDS-DMA
                     // (sc1) at the box test when frame f - 1 has already published it (the usual
                     // case), not loaded (sc1) at the ray's end
@@ -1062,7 +1065,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         // header's bound word, an L1 hit while the walk stays in one cell).  The round then scans the first sample
         // that may be located.  convert_icon's voids (over and under every land column) are
         // crossed in one round instead of one round per sample.
-        if (solo && mm && used && !past) {
+        constexpr bool kVoidLoc = (OPT & OPT_VOIDLOC) != 0;
+        if (solo && used && !past && (mm || (kVoidLoc && (wr == 0 || !A.voidLocFirst)))) {
           const float3 O = cam_org(A, frame);
 #pragma nounroll
           for (int it = 0; it < kVoidRunMax; ++it) {
@@ -1078,7 +1082,14 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
               const uint32_t h = sph_hash(r);
               if ((s_sph[h >> 5] >> (h & 31)) & 1u) break;
             }
-            // outside every cell: the sample is taken (a sampleVolume call), one draw
+            // outside every cell: the sample is taken (a sampleVolume call), one draw.  In
+            // located mode (OPT_VOIDLOC) this miss breaks the round's assumption: a solo lane's
+            // sample 0 takes its step draw first in either mode, so the ray switches to miss
+            // mode here and walks on
+            if (kVoidLoc && !mm) {
+              mm = true;
+              miss = true;
+            }
             if (cntd) ++nLocate;
             if constexpr ((OPT & OPT_STATS) != 0) ++cnt.steps;
             rq.x = tk;
@@ -1343,12 +1354,15 @@ __device__ __forceinline__ void write_pixel_chain(const RenderArgs &A, size_t ou
   nv.w = w * alpha + (1.f - w) * old.w;
   const uint32_t rgba = srgb_byte(s_th, nv.x) + (srgb_byte(s_th, nv.y) << 8) +
                         (srgb_byte(s_th, nv.z) << 16) + (make_8bit(nv.w) << 24);
-  if (publish) {
+  if (publish && A.probeExit != 17) {  // measurement only (17): plain stores to publish
     const uint32_t n = out_pixels(A);
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)A.accum, 0, (int)(n * 16u), 0x00020000);
     const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc((void *)A.fb, 0, (int)(n * 4u), 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, nv), ra, (int)(outIdx * 16u), 0, 16);
     __builtin_amdgcn_raw_buffer_store_b32(rgba, rf, (int)(outIdx * 4u), 0, 16);
+  } else if (publish) {
+    A.accum[outIdx] = nv;
+    A.fb[outIdx] = rgba;
   } else {
     typedef float f4v __attribute__((ext_vector_type(4)));
     const f4v t = {nv.x, nv.y, nv.z, nv.w};
@@ -2381,7 +2395,8 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
                                pblk, pw, frame, partSel);
         if (A.chain && frame < A.numSamples - 1 && frame != A.chainWithhold) {
           // chained frames: this wave's pixels are written through; tell frame + 1's wave
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (A.probeExit != 16)  // measurement only (16): the flag without the drain
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if (__lane_id() == 0)
             __hip_atomic_store(A.chainFlag + (size_t)pblk * 4u + (uint32_t)pw, A.chainEpoch + (uint32_t)frame + 1u,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2585,7 +2600,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73405728) X(73667872) X(73405760) X(73667904) X(73405712) X(73667856) X(73930016) X(74192160) X(73405732) X(73405730) X(73405729) X(73667873) X(73405744) X(73667888) X(73405745) X(73667889)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73405728) X(73667872) X(73405760) X(73667904) X(73405712) X(73667856) X(73930016) X(74192160) X(73405732) X(73405730) X(73405729) X(73667873) X(73405744) X(73667888) X(73405745) X(73667889) X(1147147552)
 #else
 #define IRT_VARIANTS(X) X(73405728) X(73667872) X(5376) X(36864)
 #endif
@@ -2619,7 +2634,8 @@ constexpr int kNoQueue = OPT_WAVEWG | OPT_WAVEWG2 | OPT_SERIAL | OPT_STATS | OPT
 // Persistent launches (OPT_QUEUE, 3-4x slower: DESIGN.md section 5) are compiled into the A/B
 // library only (make VARIANTS=all); the product library has no persistent kernel.
 bool render_split_ok(const RenderArgs &A, int variant) {
-  return (variant == kDefaultVariant || variant == (kDefaultVariant | kNoMissBit)) && render_wg_per_block(A, variant) == 4;
+  return (variant == kDefaultVariant || variant == (kDefaultVariant | kNoMissBit) || variant == (kDefaultVariant | OPT_VOIDLOC)) &&
+         render_wg_per_block(A, variant) == 4;
 }
 
 bool render_queue_compiled() {
@@ -2661,7 +2677,8 @@ RenderKernel kernel_for(const RenderArgs &A, int &threads) {
 #endif
   // a single frame with measured-cost work items: the default kernels' split-capable form
   // and a scene with a slot table: their OPT_SLOT form
-  if constexpr (K == (kDefaultVariant & ~OPT_MONO) || K == ((kDefaultVariant | kNoMissBit) & ~OPT_MONO)) {
+  if constexpr (K == (kDefaultVariant & ~OPT_MONO) || K == ((kDefaultVariant | kNoMissBit) & ~OPT_MONO) ||
+                K == ((kDefaultVariant | OPT_VOIDLOC) & ~OPT_MONO)) {
     if (A.slots) return A.numSplit ? k_render<K | OPT_SPLIT | OPT_SLOT> : k_render<K | OPT_SLOT>;
     if (A.numSplit) return k_render<K | OPT_SPLIT>;
   }
