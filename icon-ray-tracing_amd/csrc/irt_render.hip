@@ -225,6 +225,18 @@ __device__ __forceinline__ float dpp_prefix(float t0, float dk, int k) {
   return y;
 }
 
+// Measurement only, A/B library (make VARIANTS=all): IRT_PROBE_EXIT 8..13 end the first
+// woodcockFunc call inside its first round -- 8 after the samples' positions, 9 after the
+// header and bin, 10 after the first candidate test, 11 after the dealt-out candidates, 12 after
+// locate_wave (getValue included), 13 at the round's end -- so that the SQ counters of runs
+// with each exit give the instructions of every piece of a round (profiles/r06m_gpu.sh)
+#ifdef IRT_ALL_VARIANTS
+#define IRT_ROUND_PROBE(n, ...) \
+  if (A.probeExit == (n)) return __VA_ARGS__;
+#else
+#define IRT_ROUND_PROBE(n, ...)
+#endif
+
 // OPT_TIMING's per-wave region clocks (Tracer::tmark); empty in every other kernel
 struct TimeAccOff {};
 struct TimeAccOn {
@@ -743,6 +755,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       if constexpr (kPair) fe2 = H0.w + beg + list_entry(m8, 1u);
       fr = r;
     }
+    IRT_ROUND_PROBE(9, false)
     for (int pass = 0;; ++pass) {
       // every lane: its list's first candidate (OPT_DEALALL: none -- every candidate of
       // every lane goes through the deal below, so a round's samples wait for one entry
@@ -795,6 +808,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         }
       }
       tmark(3);  // header, first candidate
+      IRT_ROUND_PROBE(10, false)
       bool need = rem > 0u;
       for (uint64_t nm = __ballot(need); nm != 0ull; nm = __ballot(need)) {
         // deal the owners' untested candidates out to the lanes: exclusive prefix of rem
@@ -846,6 +860,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         __builtin_amdgcn_wave_barrier();
       }
       tmark(4);  // the dealt-out candidates
+      IRT_ROUND_PROBE(11, false)
       // the second pass: bin-edge samples, the next bin's list below the record found
       if (pass == 1 || __ballot(edge) == 0ull) break;
       c = 0u;
@@ -1102,6 +1117,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
           }
         }
       }
+      IRT_ROUND_PROBE(8)
       bool found = false, acc = false;
       float value = 0.f;
       tmark(2);  // round start: exchange, jumps, logf, prefix
@@ -1131,6 +1147,9 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         found = locate(O.x + ry.x * tk, O.y + ry.y * tk, O.z + ry.z * tk, value);
       }
       tmark(5);  // locate's tail: sphere, getValue
+#ifdef IRT_ALL_VARIANTS
+      if (A.probeExit >= 9 && A.probeExit <= 12) return;
+#endif
       if (found) {
         const float sw = classify_alpha(value);  // postClassify(value).w
         acc = sw >= lcg_float(lcg_next(sk)) * rq.w;
@@ -1205,6 +1224,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
           miss = !miss;  // the assumption broke: a miss, or (miss mode) a located sample
         }
       }
+      IRT_ROUND_PROBE(13)
     }
     if (req) t = fminf(t, tmax);
     tmark(7);  // the rounds' classify, LUT, ballots, outcomes
@@ -2076,7 +2096,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       }
     }
     T.woodcock_wave(req, dx, dy, dz, tw, tt1, st, maj, !zeroLen, s, miss, W, SW, jmp);
-    if (A.probeExit == 5) break;  // measurement only: the first woodcockFunc of every lane
+    if (A.probeExit == 5 || (A.probeExit >= 8 && A.probeExit < 16)) break;  // measurement only: the first woodcockFunc of every lane
     if (grid && req && phase == kWait && !ae) {
       if (tw > t && tw < tt1) {  // render_grid's hit test (deviceCode.cu:316)
         lds_st16(&s_entry[tid_late()], make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
@@ -2212,6 +2232,11 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   __shared__ float4 s_acc[lean ? ((OPT & (OPT_ACCPF | OPT_CHAINPF)) ? 64 : 1) : 256];  // kCoop: the accum pixels, prefetched
   __shared__ uint2 s_jmp[kLcgJumps];  // lcg_jump's {mul, add} (kLcgJumpTab)
   const int tid = threadIdx.x;
+#ifdef IRT_LDS_PAD
+  // measurement only (profiles/r06n_gpu.sh): IRT_LDS_PAD unused bytes of LDS per workgroup
+  __shared__ float4 s_pad[IRT_LDS_PAD / 16];
+  if (A.probeExit == 99) s_pad[tid % (IRT_LDS_PAD / 16)] = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
   if (A.wgTrace && tid == 0) {  // measurement only: the workgroup's start, where it ran
     uint32_t *w = A.wgTrace + 4 * (blockIdx.y * gridDim.x + blockIdx.x);
     w[0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
