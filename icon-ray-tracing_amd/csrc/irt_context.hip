@@ -147,7 +147,6 @@ struct irt_context {
   // ramp, 2^coopMaxLg without (IRT_COOP_MAXLG, IRT_COOP_RAMP; profiles/r02e_dist/)
   int coopMaxLg = 0;
   int coopRamp = 1;
-  int voidLocFirst = 0;        // IRT_VOIDLOC_FIRST (OPT_VOIDLOC kernels, RenderArgs::voidLocFirst)
   int probeExit = 0;           // IRT_PROBE_EXIT (measurement only, RenderArgs::probeExit)
   uint32_t *wgTrace = nullptr; // irt_debug_set_wg_trace (measurement only, RenderArgs::wgTrace)
   // chained progressive frames (RenderArgs::chain; IRT_CHAIN=0 / irt_debug_set_chain: the
@@ -635,7 +634,6 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.lutSize = c->lutSize;
   A.coopMaxLg = c->coopMaxLg;
   A.coopRamp = c->coopRamp;
-  A.voidLocFirst = c->voidLocFirst;
   A.probeExit = c->probeExit;
   A.wgTrace = c->wgTrace;
   A.numCells = c->n;
@@ -731,11 +729,21 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
       A.schedCost = c->d_schedCost;
     }
   }
+  // chained frames: the cooperative kernels (not the one-lane-per-ray A/B variant), grid
+  // launches, no measurement-only early exit
+  // The hand-off's buffer resources address accum with 32-bit byte offsets: frames of 2^27
+  // pixels or more (11,585^2) go through the sample buffer instead
+  const uint64_t outPixels = packed ? (uint64_t)numTiles * 4096u : (uint64_t)W * (uint64_t)H;
+  const bool chain = c->chainOn && numFrames > 1 && !queued && (c->probeExit == 0 || c->probeExit >= 16) &&
+                     (c->variant & 65536) == 0 && outPixels * 16u <= 0x7FFFFFFFull;
+  // two chained frames per wave (the OPT_FPAIR variants, bit 1): half the grid's frame rows
+  const int fpw = chain && (c->variant & 1) ? 2 : 1;
   // workgroups of this launch: 16 per 64x64 tile, x4 for the one-wave-workgroup variants
-  // (irt_render.hip OPT_WAVEWG, bit 4194304), per frame, + the split packets' parts; a
-  // persistent launch's resident ones
+  // (irt_render.hip OPT_WAVEWG, bit 4194304), per frame (per pair of frames), + the split
+  // packets' parts; a persistent launch's resident ones
   const size_t numWG = queued ? (size_t)queueWG
-                              : (size_t)numTiles * 16 * (size_t)render_wg_per_block(A, c->variant) * (size_t)numFrames +
+                              : (size_t)numTiles * 16 * (size_t)render_wg_per_block(A, c->variant) *
+                                        (size_t)((numFrames + fpw - 1) / fpw) +
                                     (size_t)A.numSplit;
   // Per-workgroup counts need kSlots x 32 B of pinned host memory per workgroup and frame
   // (1 KiB): a launch past kWgCountsMax workgroups (a large progressive batch) counts through
@@ -781,15 +789,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
     A.wgCounts = c->d_probeCounts;
   }
   A.numSamples = numFrames;
-  // chained frames: the cooperative kernels (not the one-lane-per-ray A/B variant), grid
-  // launches, no measurement-only early exit
-  // The hand-off's buffer resources address accum with 32-bit byte offsets: frames of 2^27
-  // pixels or more (11,585^2) go through the sample buffer instead
-  const uint64_t outPixels = packed ? (uint64_t)numTiles * 4096u : (uint64_t)W * (uint64_t)H;
-  A.chain = c->chainOn && numFrames > 1 && !queued && (c->probeExit == 0 || c->probeExit >= 16) && (c->variant & 65536) == 0 &&
-                    outPixels * 16u <= 0x7FFFFFFFull
-                ? 1
-                : 0;
+  A.chain = chain ? 1 : 0;
   if (A.chain) {
     const size_t words = (size_t)numTiles * 16 * 4;  // one per (block, wave)
     if (words > c->chainCap || c->chainEpoch > 0xF0000000u - (uint32_t)numFrames) {
@@ -1209,7 +1209,6 @@ int irt_create_end(irt_context *c) {
   if (const char *e = getenv("IRT_WG_COUNTS_MAX")) c->wgCountsMax = (size_t)std::max(0LL, atoll(e));
   if (const char *e = getenv("IRT_COOP_MAXLG")) c->coopMaxLg = std::min(6, std::max(0, atoi(e)));
   if (const char *e = getenv("IRT_COOP_RAMP")) c->coopRamp = std::min(6, std::max(0, atoi(e)));
-  if (const char *e = getenv("IRT_VOIDLOC_FIRST")) c->voidLocFirst = atoi(e) != 0;
   if (const char *e = getenv("IRT_PROBE_EXIT")) c->probeExit = atoi(e);
   if (const char *e = getenv("IRT_QUEUE")) c->queueOn = atoi(e) != 0 && render_queue_compiled();
   if (const char *e = getenv("IRT_QUEUE_WGS")) c->queuePerCU = std::max(0, atoi(e));

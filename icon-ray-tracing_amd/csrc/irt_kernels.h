@@ -85,9 +85,6 @@ struct RenderArgs {
   // setting gives the same frame)
   int coopMaxLg;
   int coopRamp;
-  // OPT_VOIDLOC kernels (A/B): the solo lanes' void walk also in located mode in every solo
-  // round (0) or only in a woodcockFunc call's first round (1) (IRT_VOIDLOC_FIRST)
-  int voidLocFirst;
   // measurement only (IRT_PROBE_EXIT, profiles/): 1 = every workgroup returns at once,
   // 2 = after the prologue, 3 = after ray generation and boxTest (no pixel written), 4 = at
   // the first woodcockFunc, 5 = after it

@@ -83,10 +83,12 @@ enum : int {
                          // runs only for lanes whose first two fail
   OPT_VOIDLOC = 1073741824,  // (A/B) the solo lanes' void walk also in located mode: a certain miss
                              // at the round's sample switches the ray to miss mode there, not a
-                             // round later (RenderArgs::voidLocFirst: only in a call's first round)
-  OPT_CHAINPF = 1,  // (A/B, with OPT_LEAN) a chained frame's accum pixel fetched into LDS by LDS-DMA
-                    // (sc1) at the box test when frame f - 1 has already published it (the usual
-                    // case), not loaded (sc1) at the ray's end
+                             // round later (profiles/r06h/: C3t chained -1 %, single frames even)
+  OPT_FPAIR = 1,  // (A/B) chained launches: a wave renders its packet for two consecutive frames,
+                  // one after the other (k_render: workgroup (b, y) frames 2y and 2y + 1): the second
+                  // frame's hand-off is the wave's own.  (Until profiles/r06f this bit was OPT_CHAINPF,
+                  // a chained frame's accum pixel by LDS-DMA at the box test: +6 % from its 1 KB of
+                  // LDS, profiles/r06f/ and r06n/.)
   OPT_NOVOIDRUN = 2,   // (A/B) the miss-mode kernels without the solo lanes' void walk (woodcock_wave)
   OPT_NOHOLESKIP = 4,  // (A/B) the miss-mode kernels without the quad-bound miss test (Tracer::locate_wave:
                        // a sample outside its quad's radial range is outside every cell, no
@@ -225,12 +227,13 @@ __device__ __forceinline__ float dpp_prefix(float t0, float dk, int k) {
   return y;
 }
 
-// Measurement only, A/B library (make VARIANTS=all): IRT_PROBE_EXIT 8..13 end the first
+// Measurement only, the probe build (profiles/build_probe_lib.sh, -DIRT_PROBE_BUILD):
+// IRT_PROBE_EXIT 8..13 end the first
 // woodcockFunc call inside its first round -- 8 after the samples' positions, 9 after the
 // header and bin, 10 after the first candidate test, 11 after the dealt-out candidates, 12 after
 // locate_wave (getValue included), 13 at the round's end -- so that the SQ counters of runs
 // with each exit give the instructions of every piece of a round (profiles/r06m_gpu.sh)
-#ifdef IRT_ALL_VARIANTS
+#ifdef IRT_PROBE_BUILD
 #define IRT_ROUND_PROBE(n, ...) \
   if (A.probeExit == (n)) return __VA_ARGS__;
 #else
@@ -1081,7 +1084,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         // that may be located.  convert_icon's voids (over and under every land column) are
         // crossed in one round instead of one round per sample.
         constexpr bool kVoidLoc = (OPT & OPT_VOIDLOC) != 0;
-        if (solo && used && !past && (mm || (kVoidLoc && (wr == 0 || !A.voidLocFirst)))) {
+        if (solo && used && !past && (mm || kVoidLoc)) {
           const float3 O = cam_org(A, frame);
 #pragma nounroll
           for (int it = 0; it < kVoidRunMax; ++it) {
@@ -1147,7 +1150,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         found = locate(O.x + ry.x * tk, O.y + ry.y * tk, O.z + ry.z * tk, value);
       }
       tmark(5);  // locate's tail: sphere, getValue
-#ifdef IRT_ALL_VARIANTS
+#ifdef IRT_PROBE_BUILD
       if (A.probeExit >= 9 && A.probeExit <= 12) return;
 #endif
       if (found) {
@@ -1374,15 +1377,19 @@ __device__ __forceinline__ void write_pixel_chain(const RenderArgs &A, size_t ou
   nv.w = w * alpha + (1.f - w) * old.w;
   const uint32_t rgba = srgb_byte(s_th, nv.x) + (srgb_byte(s_th, nv.y) << 8) +
                         (srgb_byte(s_th, nv.z) << 16) + (make_8bit(nv.w) << 24);
-  if (publish && A.probeExit != 17) {  // measurement only (17): plain stores to publish
+#ifdef IRT_PROBE_BUILD
+  if (publish && A.probeExit == 17) {  // measurement only (17, probe build): plain stores to publish
+    A.accum[outIdx] = nv;
+    A.fb[outIdx] = rgba;
+    return;
+  }
+#endif
+  if (publish) {
     const uint32_t n = out_pixels(A);
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)A.accum, 0, (int)(n * 16u), 0x00020000);
     const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc((void *)A.fb, 0, (int)(n * 4u), 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, nv), ra, (int)(outIdx * 16u), 0, 16);
     __builtin_amdgcn_raw_buffer_store_b32(rgba, rf, (int)(outIdx * 4u), 0, 16);
-  } else if (publish) {
-    A.accum[outIdx] = nv;
-    A.fb[outIdx] = rgba;
   } else {
     typedef float f4v __attribute__((ext_vector_type(4)));
     const f4v t = {nv.x, nv.y, nv.z, nv.w};
@@ -1667,7 +1674,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
                                                   const float *s_th, int4 *s_dda, float4 *s_entry,
                                                   float4 *s_acc, CoopWave &W, ScanWave *SW, const uint2 *jmp,
                                                   int tid, int accumID, uint32_t blk, int pwave, int frame,
-                                                  int partSel = -1) {
+                                                  int partSel = -1, int pairPos = 0) {
   // At 5+ waves/SIMD the pixel's output addresses are recomputed where they are used (from the
   // workgroup's uniform block index), not held in VGPRs through the rounds: a progressive
   // batch's sample slot (k_accumulate reads it) and the frame index.  (At 4 waves there is
@@ -1695,7 +1702,10 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   const bool toSample = A.numSamples > 1 && !A.chain;
   // chained frames: frame f > 0 of the launch reads its accum pixel at the end, once frame
   // f - 1's wave has published it (chain_wait); frame 0 prefetches it as a single frame does
-  const bool chainLate = A.chain && frame > 0;
+  // (pairPos, the OPT_FPAIR kernels: 1 = the first of two consecutive frames this wave
+  // renders -- no publish --, 2 = the second -- its previous frame is this wave's own, so no wait,
+  // and its accum pixel is read back, past this CU's L1, at the end)
+  const bool chainLate = A.chain && frame > 0 && pairPos != 2;
   // ... unless frame f - 1's wave has published by the time this wave's rays are set up (a
   // large frame's previous-frame workgroup ran numBlocks workgroups earlier): its publish word,
   // loaded now, compared after the box test, and then the accum pixel prefetched (sc1) as frame 0
@@ -1719,7 +1729,6 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   // array: the compiler's LDS-DMA tracking waits for it only where the slots are read, at the end)
   constexpr bool accPf = (OPT & OPT_ACCPF) != 0 && (OPT & OPT_LEAN) != 0;
   const bool accEarly = accPf && !toSample && !chainLate;
-  constexpr bool chainPf = (OPT & OPT_CHAINPF) != 0 && (OPT & OPT_LEAN) != 0;
   if (accEarly && px.active)
     __builtin_amdgcn_global_load_lds((const void *)(A.accum + px.outIdx),
                                      (__attribute__((address_space(3))) void *)(s_acc + (tid & ~63)), 16, 0, 0);
@@ -1775,7 +1784,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     }
   }
   const bool chainReady = !chainLate || __builtin_amdgcn_readfirstlane(chainSeen) == A.chainEpoch + (uint32_t)frame;
-  if (((OPT & OPT_LEAN) == 0 || chainPf) && chainLate && chainReady && inBox)
+  if ((OPT & OPT_LEAN) == 0 && chainLate && chainReady && inBox)
     __builtin_amdgcn_global_load_lds((const void *)(A.accum + px.outIdx),
                                      (__attribute__((address_space(3))) void *)(s_acc + (tid & ~63)), 16, 0, 16);  // sc1
   // GRID_ACCEL_MODE (deviceCode.cu:326-328): dda3 (DDA.h:35-136) over the 256^3 grid as
@@ -2096,7 +2105,10 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       }
     }
     T.woodcock_wave(req, dx, dy, dz, tw, tt1, st, maj, !zeroLen, s, miss, W, SW, jmp);
-    if (A.probeExit == 5 || (A.probeExit >= 8 && A.probeExit < 16)) break;  // measurement only: the first woodcockFunc of every lane
+    if (A.probeExit == 5) break;  // measurement only: the first woodcockFunc of every lane
+#ifdef IRT_PROBE_BUILD
+    if (A.probeExit >= 8 && A.probeExit < 16) break;  // (IRT_ROUND_PROBE)
+#endif
     if (grid && req && phase == kWait && !ae) {
       if (tw > t && tw < tt1) {  // render_grid's hit test (deviceCode.cu:316)
         lds_st16(&s_entry[tid_late()], make_float4(s.x * A.amb.x * A.ambRad, s.y * A.amb.y * A.ambRad,
@@ -2135,11 +2147,8 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     const size_t outIdx = kRecompute ? pixel_of(A, (uint32_t)opaque_u((int)blk), ptid_late()).outIdx : px.outIdx;
     if (A.chain) {
       float4 old;
-      if (chainLate && (!chainReady || ((OPT & OPT_LEAN) != 0 && !chainPf))) {
+      if (pairPos == 2 || (chainLate && (!chainReady || (OPT & OPT_LEAN) != 0))) {
         old = chain_load_accum(A, outIdx);
-      } else if (chainPf && chainLate) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
-        old = lds_ld16(&s_acc[tl]);
       } else if constexpr (accPf) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
         old = lds_ld16(&s_acc[tl]);
@@ -2151,13 +2160,15 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       }
       // 1.f / (float)(accumID + 1) of this frame, correctly rounded as the host's A.accumW
       write_pixel_chain(A, outIdx, c.x, c.y, c.z, c.w, 1.f / (float)(accumID + 1), s_th, old,
-                        frame < A.numSamples - 1);
+                        frame < A.numSamples - 1 && pairPos != 1);
     } else if constexpr ((OPT & OPT_LEAN) != 0 && !accPf) {
-      if (A.probeExit == 6) {  // measurement only: the lerp without its accum read (frames differ)
+#ifdef IRT_PROBE_BUILD
+      if (A.probeExit == 6) {  // measurement only (probe build): the lerp without its accum read
         write_pixel(A, outIdx, c.x, c.y, c.z, c.w, s_th, make_float4(0.f, 0.f, 0.f, 0.f));
         return;
       }
-      if (A.probeExit == 7) return;  // measurement only: no accum read, no pixel stores
+      if (A.probeExit == 7) return;  // measurement only (probe build): no accum read, no pixel stores
+#endif
       write_pixel(A, outIdx, c.x, c.y, c.z, c.w, s_th);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
@@ -2229,7 +2240,7 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
   __shared__ CoopWave s_coop[kW];   // the cooperative Woodcock loop (kCoop kernels)
   __shared__ ScanWave s_scan[Tracer<OPT>::kWaveScan ? kW : 1];  // its wave-wide candidate scan
   __shared__ HdrStage s_hdrs[(OPT & OPT_HDRLDS) ? kW : 1];       // OPT_HDRLDS: staged header lines
-  __shared__ float4 s_acc[lean ? ((OPT & (OPT_ACCPF | OPT_CHAINPF)) ? 64 : 1) : 256];  // kCoop: the accum pixels, prefetched
+  __shared__ float4 s_acc[lean ? ((OPT & OPT_ACCPF) ? 64 : 1) : 256];  // kCoop: the accum pixels, prefetched
   __shared__ uint2 s_jmp[kLcgJumps];  // lcg_jump's {mul, add} (kLcgJumpTab)
   const int tid = threadIdx.x;
 #ifdef IRT_LDS_PAD
@@ -2372,9 +2383,13 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
     QueueCursor qc = {(int)(blockIdx.x & (kQueueXcds - 1)), 0u};  // workgroup b runs on XCD b % 8
     uint32_t p = queued ? queue_take(A.queue, blocksAll, qc) : 0u;
     bool more = !queued || p != 0xFFFFFFFFu;
+    // chained frames two per wave (OPT_FPAIR): workgroup (b, y) renders frames
+    // 2y and 2y + 1 of its packet, one after the other
+    const int fpw = (OPT & OPT_FPAIR) != 0 && !queued && A.chain ? 2 : 1;
+    int fi = 0;
     while (more) {
       uint32_t pblk = blk, nx = 0u;
-      int pw = wwave + (tid >> 6), frame = (int)blockIdx.y;
+      int pw = wwave + (tid >> 6), frame = (int)blockIdx.y * fpw + fi;
       if constexpr (queued) {
         const uint32_t g = p >> 2;  // the packet's block over all frames
         frame = A.numSamples > 1 ? (int)(g / perFrame) : 0;
@@ -2408,6 +2423,31 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
                                &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, AL.accumID + frame,
                                pblk, pw, frame);
         TL.flush_coop();  // this packet's counts (nothing carried from packet to packet)
+      } else if constexpr ((OPT & OPT_FPAIR) != 0) {
+        // two chained frames per wave: as the persistent launch, the thread index and the
+        // launch's arguments are new to the compiler in each of the wave's frames, so nothing
+        // derived from them is held through both
+        asm volatile("" : "+v"(ltid));
+        typedef const __attribute__((address_space(4))) RenderArgs *KArgs;
+        KArgs kp = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kp));
+        const RenderArgs &AL = *(const RenderArgs *)kp;
+        Tracer<OPT> TL{{}, AL, s_logf, lean ? AL.sphBits : s_sph, s_cnt, {0, 0, 0, 0, 0, 0, 0}};
+        TL.s_gbits = s_gbits;
+        TL.frame = frame;
+        const Pixel ppx = pixel_of(AL, pblk, pw * 64 + (ltid & 63));
+        launched += (uint32_t)__popcll(__ballot(ppx.active));
+        const bool pairNext = fpw == 2 && fi == 0 && frame + 1 < AL.numSamples;  // this wave renders frame + 1 too
+        render_pixel_coop<OPT>(AL, TL, ppx, lean ? AL.srgbTh : s_th, s_dda, s_entry, s_acc, s_coop[ltid >> 6],
+                               &s_scan[Tracer<OPT>::kWaveScan ? ltid >> 6 : 0], s_jmp, ltid, cam_accum_id(AL, frame),
+                               pblk, pw, frame, -1, pairNext ? 1 : (fi == 1 ? 2 : 0));
+        TL.flush_coop();  // this frame's counts
+        if (AL.chain && frame < AL.numSamples - 1 && frame != AL.chainWithhold && !pairNext) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (__lane_id() == 0)
+            __hip_atomic_store(AL.chainFlag + (size_t)pblk * 4u + (uint32_t)pw, AL.chainEpoch + (uint32_t)frame + 1u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       } else {
         const int pl = partSel & 255, pn = 64 >> pl;  // a split packet's part: pn rays
         Pixel ppx = pixel_of(A, pblk, pw * 64 + (partSel < 0 ? (ltid & 63) : ((partSel >> 8) * pn) | (ltid & (pn - 1))));
@@ -2420,7 +2460,9 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
                                pblk, pw, frame, partSel);
         if (A.chain && frame < A.numSamples - 1 && frame != A.chainWithhold) {
           // chained frames: this wave's pixels are written through; tell frame + 1's wave
-          if (A.probeExit != 16)  // measurement only (16): the flag without the drain
+#ifdef IRT_PROBE_BUILD
+          if (A.probeExit != 16)  // measurement only (16, probe build): the flag without the drain
+#endif
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if (__lane_id() == 0)
             __hip_atomic_store(A.chainFlag + (size_t)pblk * 4u + (uint32_t)pw, A.chainEpoch + (uint32_t)frame + 1u,
@@ -2433,6 +2475,10 @@ __global__ void __launch_bounds__((OPT & OPT_WAVEWG) ? 64 : ((OPT & OPT_WAVEWG2)
       if constexpr (queued) nx = queue_take(A.queue, blocksAll, qc);
       p = nx;
       more = queued && p != 0xFFFFFFFFu;
+      if ((OPT & OPT_FPAIR) != 0 && !queued && fpw == 2 && fi == 0 && frame + 1 < A.numSamples) {
+        fi = 1;
+        more = true;
+      }
     }
     if constexpr (queued) queue_done(A.queue);
     T.flush_coop();
@@ -2625,7 +2671,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73405728) X(73667872) X(73405760) X(73667904) X(73405712) X(73667856) X(73930016) X(74192160) X(73405732) X(73405730) X(73405729) X(73667873) X(73405744) X(73667888) X(73405745) X(73667889) X(1147147552) X(107222304) X(106960160)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73405728) X(73667872) X(73405760) X(73667904) X(73405712) X(73667856) X(73930016) X(74192160) X(73405732) X(73405730) X(73405729) X(73667873) X(73405744) X(73667888) X(1147147552) X(107222304) X(106960160)
 #else
 #define IRT_VARIANTS(X) X(73405728) X(73667872) X(5376) X(36864)
 #endif
@@ -2719,7 +2765,8 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
     numBlocks = A.numTiles * 16;
   } else {
     const int split = A.numSplit ? (int)A.numSplit : 0;  // the listed work items first (kernel_for: OPT_SPLIT)
-    hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads) + split, A.numSamples), dim3(threads), 0, s, A);
+    const int fpw = (N & OPT_FPAIR) != 0 && A.chain ? 2 : 1;  // chained frames per wave
+    hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads) + split, (A.numSamples + fpw - 1) / fpw), dim3(threads), 0, s, A);
   }
   // progressive batch: the lerp chain over the frames' samples (chained frames lerp in k_render)
   if (A.numSamples > 1 && !A.chain) hipLaunchKernelGGL(k_accumulate, dim3(numBlocks), dim3(256), 0, s, A);
