@@ -737,7 +737,8 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   const bool chain = c->chainOn && numFrames > 1 && !queued && (c->probeExit == 0 || c->probeExit >= 16) &&
                      (c->variant & 65536) == 0 && outPixels * 16u <= 0x7FFFFFFFull;
   // two chained frames per wave (the OPT_FPAIR variants, bit 1): half the grid's frame rows
-  const int fpw = chain && (c->variant & 1) ? 2 : 1;
+  A.chain = chain ? 1 : 0;
+  const int fpw = render_frames_per_wave(A, c->variant);
   // workgroups of this launch: 16 per 64x64 tile, x4 for the one-wave-workgroup variants
   // (irt_render.hip OPT_WAVEWG, bit 4194304), per frame (per pair of frames), + the split
   // packets' parts; a persistent launch's resident ones

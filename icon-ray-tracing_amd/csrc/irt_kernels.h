@@ -173,6 +173,8 @@ int render_variants(int *out, int cap);  // the compiled variants (count; the fi
 // workgroups per 256-pixel block the launch of `variant` uses for these arguments (4 only for
 // the one-wave-workgroup A/B variants on the user-geometry sphere path)
 int render_wg_per_block(const RenderArgs &A, int variant);
+// chained frames per wave (2: the OPT_FPAIR variants, irt_render.hip)
+int render_frames_per_wave(const RenderArgs &A, int variant);
 // whether `variant` can run as a persistent launch (RenderArgs::queue) with these arguments:
 // the cooperative user-geometry sphere-accel kernels with 256-thread workgroups
 bool render_queue_ok(const RenderArgs &A, int variant);

@@ -2695,6 +2695,15 @@ bool render_variant_available(int v) {
   return false;
 }
 
+// chained frames per wave of a launch: 2 for the OPT_FPAIR variants' own user-geometry kernels
+// (kernel_for: the grid-accel and wedge kernels carry no variant bits), else 1
+int render_frames_per_wave(const RenderArgs &A, int variant) {
+  return (variant & OPT_FPAIR) != 0 && A.chain && render_variant_available(variant) &&
+                 A.sampler == IRT_MODE_USER_GEOM && A.accelMode != IRT_ACCEL_GRID
+             ? 2
+             : 1;
+}
+
 int render_wg_per_block(const RenderArgs &A, int variant) {
   const int per = (variant & OPT_WAVEWG) ? 4 : ((variant & OPT_WAVEWG2) ? 2 : 1);
   return render_variant_available(variant) && A.sampler == IRT_MODE_USER_GEOM && A.accelMode != IRT_ACCEL_GRID ? per : 1;
@@ -2765,7 +2774,7 @@ void launch_variant(const RenderArgs &A, int numBlocks, hipStream_t s) {
     numBlocks = A.numTiles * 16;
   } else {
     const int split = A.numSplit ? (int)A.numSplit : 0;  // the listed work items first (kernel_for: OPT_SPLIT)
-    const int fpw = (N & OPT_FPAIR) != 0 && A.chain ? 2 : 1;  // chained frames per wave
+    const int fpw = render_frames_per_wave(A, N);  // chained frames per wave
     hipLaunchKernelGGL(k, dim3(numBlocks * (256 / threads) + split, (A.numSamples + fpw - 1) / fpw), dim3(threads), 0, s, A);
   }
   // progressive batch: the lerp chain over the frames' samples (chained frames lerp in k_render)
