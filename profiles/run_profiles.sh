@@ -13,7 +13,7 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-ARGS=(--steps 20 --warmup 2 --no-cpu-baseline --no-single-compare "$@")
+ARGS=(--steps 20 --warmup 2 --no-cpu-baseline --no-single-compare --secondary none "$@")
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run \
   -- python3 "$ROOT/bench.py" "${ARGS[@]}" > "$OUT/bench_stats.json" 2> "$OUT/bench_stats.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
