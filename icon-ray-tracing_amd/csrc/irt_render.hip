@@ -1124,6 +1124,13 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       bool found = false, acc = false;
       float value = 0.f;
       tmark(2);  // round start: exchange, jumps, logf, prefix
+#ifdef IRT_PROBE_BUILD
+      // measurement only (31): 100 extra VALU instructions per Woodcock round
+      if (A.probeExit == 31) {
+#pragma nounroll
+        for (int k = 0; k < 25; ++k) asm volatile("v_nop\n v_nop\n v_nop\n v_nop" ::: "memory");
+      }
+#endif
       if constexpr (kWaveScan) {
         const uint32_t *tp = nullptr;
         if constexpr ((OPT & OPT_NEXTHDR) != 0) {
@@ -1744,6 +1751,14 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     const Ray ray = {O.x, O.y, O.z, 0.f, dx, dy, dz, 1e10f};
     float t0, t1;
     const bool boxHit = box_test(ray, A, t0, t1);
+#ifdef IRT_PROBE_BUILD
+    // measurement only (30): 200 extra VALU instructions per wave in the ray setup -- is the
+    // frame's time sensitive to VALU work at all?
+    if (A.probeExit == 30) {
+#pragma nounroll
+      for (int k = 0; k < 50; ++k) asm volatile("v_nop\n v_nop\n v_nop\n v_nop" ::: "memory");
+    }
+#endif
     if (A.probeExit == 3) {  // measurement only: ray generation and boxTest, nothing written
       if (boxHit && t0 == -1.2345f) A.fb[0] = 0u;  // keeps the work live
       return;
