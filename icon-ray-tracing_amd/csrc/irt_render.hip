@@ -1676,6 +1676,24 @@ __device__ __forceinline__ bool spherical_fast(const RenderArgs &A, float x, flo
 // (kDone); then the wave tracks every waiting lane's leaf at once, and each lane resumes
 // with the leaf's outcome.  Every lane of the wave calls it (those without a pixel start
 // finished).  Same ranges, leaves, draws and results as render_pixel, step for step.
+// The ray's per-lane state machine reads RenderArgs through fresh_args(): k_render's only
+// argument reached through a pointer the compiler cannot follow, so the fields it uses are
+// loaded (scalar loads, scalar-cache hits) where it uses them instead of held in SGPRs -- or
+// spilled to VGPR lanes -- through the Woodcock rounds: 108 -> 78 spilled SGPRs on flat grids,
+// 120 -> 92 over terrain; C3 -1.8 %, C5 -1.1 %, one launch per frame -1.1 % (profiles/r06s/).
+// -DIRT_HELD_ARGS builds the held form for A/B; -DIRT_FRESH_TAIL (A/B) also the ray's end.
+#ifndef IRT_HELD_ARGS
+__device__ __forceinline__ const RenderArgs &fresh_args() {
+  typedef const __attribute__((address_space(4))) RenderArgs *KArgs;
+  KArgs kp = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(kp));
+  return *(const RenderArgs *)kp;
+}
+#define IRT_SM_ARGS fresh_args()
+#else
+#define IRT_SM_ARGS A
+#endif
+
 template <int OPT>
 __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
                                                   const float *s_th, int4 *s_dda, float4 *s_entry,
@@ -1838,7 +1856,10 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   }
   // sceneEPS (ShellAccel.h:121-127), recomputed where it is used (a VALU product the
   // compiler would otherwise hold in a VGPR through every loop)
-  auto sceneEPS = [&]() { return opaque_u(A.sbLo.x) * 1e-6f; };
+  auto sceneEPS = [&]() {
+    const RenderArgs &SA = IRT_SM_ARGS;
+    return opaque_u(SA.sbLo.x) * 1e-6f;
+  };
   int i = 0, iter = 0, cx = 0, cy = 0, cz = 0;
   float t = 0.f, upper = 0.f, tt1 = 0.f, maj = 0.f;
   bool lastRange = true, zeroLen = false, hit = false;
@@ -1847,6 +1868,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   // after a leaf without a hit: the next leaf of the range, or the next range
   // (render_pixel's loop tail, ShellAccel.h:201-226)
   auto next_leaf = [&]() {
+    const RenderArgs &SA = IRT_SM_ARGS;
     if (lastRange) {  // every later leaf of the last range is zero-length
       ++i;
       phase = kRange;
@@ -1861,7 +1883,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       float r2, la2, lo2;
       int cy2 = 0, cz2 = 0;
       bool ok2 = false;
-      const float3 O = cam_org(A, frame);
+      const float3 O = cam_org(SA, frame);
       if constexpr (kFastSph)
         ok2 = spherical_fast(A, O.x + dx * e2, O.y + dy * e2, O.z + dz * e2, r2, la2, lo2, cy2, cz2);
       else
@@ -1873,8 +1895,8 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       if constexpr (!kFastSph) {
         sy = en.y < la2 ? 1 : -1;
         sz = en.z < lo2 ? 1 : -1;
-        cy2 = project_axis_inv(la2, A.sbLo.y, A.invSb[1], A.dims.y);
-        cz2 = project_axis_inv(lo2, A.sbLo.z, A.invSb[2], A.dims.z);
+        cy2 = project_axis_inv(la2, SA.sbLo.y, SA.invSb[1], SA.dims.y);
+        cz2 = project_axis_inv(lo2, SA.sbLo.z, SA.invSb[2], SA.dims.z);
       } else {
         sy = sign_certified(en.y, la2, kLatErr);
         sz = sign_certified(en.z, lo2, kLonErr);
@@ -1896,11 +1918,11 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
         }
         sy = la1 < la2 ? 1 : -1;
         sz = lo1 < lo2 ? 1 : -1;
-        cy2 = project_axis_inv(la2, A.sbLo.y, A.invSb[1], A.dims.y);
-        cz2 = project_axis_inv(lo2, A.sbLo.z, A.invSb[2], A.dims.z);
+        cy2 = project_axis_inv(la2, SA.sbLo.y, SA.invSb[1], SA.dims.y);
+        cz2 = project_axis_inv(lo2, SA.sbLo.z, SA.invSb[2], SA.dims.z);
       }
       dd.x = (sx > 0 ? 1 : 0) | (sy > 0 ? 2 : 0) | (sz > 0 ? 4 : 0);
-      dd.y = (int)((uint32_t)project_axis_inv(r2, A.sbLo.x, A.invSb[0], A.dims.x) + (uint32_t)sx);
+      dd.y = (int)((uint32_t)project_axis_inv(r2, SA.sbLo.x, SA.invSb[0], SA.dims.x) + (uint32_t)sx);
       dd.z = (int)((uint32_t)cy2 + (uint32_t)sy);
       dd.w = (int)((uint32_t)cz2 + (uint32_t)sz);
       lds_st16(&s_entry[tid_late()], __builtin_bit_cast(float4, dd));  // the entry point is not needed again
@@ -1983,6 +2005,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
     }
     // this lane, on its own: up to its next woodcockFunc, or to the end
     while (phase == kRange || phase == kLeaf) {
+      const RenderArgs &SA = IRT_SM_ARGS;
       if (phase == kRange) {
         if (i >= numRanges) {
           phase = kDone;
@@ -1998,16 +2021,16 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
         cx = cy = cz = 0;
         if (!ae) {  // cellID of the entry point (ShellAccel.h:121-124)
           const float e1 = lower + sceneEPS();
-          const float3 O = cam_org(A, frame);
+          const float3 O = cam_org(SA, frame);
           const float x1 = O.x + dx * e1, y1 = O.y + dy * e1, z1 = O.z + dz * e1;
           float r1, la1, lo1;
           // OPT_FASTSPH: the certified fast lat/lon, glibc-exact when not certified
           if (!(kFastSph && spherical_fast(A, x1, y1, z1, r1, la1, lo1, cy, cz))) {
             to_spherical(x1, y1, z1, r1, la1, lo1);
-            cy = project_axis_inv(la1, A.sbLo.y, A.invSb[1], A.dims.y);
-            cz = project_axis_inv(lo1, A.sbLo.z, A.invSb[2], A.dims.z);
+            cy = project_axis_inv(la1, SA.sbLo.y, SA.invSb[1], SA.dims.y);
+            cz = project_axis_inv(lo1, SA.sbLo.z, SA.invSb[2], SA.dims.z);
           }
-          cx = project_axis_inv(r1, A.sbLo.x, A.invSb[0], A.dims.x);
+          cx = project_axis_inv(r1, SA.sbLo.x, SA.invSb[0], SA.dims.x);
           // for the exit's step (sign_certified) and its exact fallback (`lower`)
           if (!lastRange) lds_st16(&s_entry[tid_late()], make_float4(r1, la1, lo1, lower));
         }
@@ -2044,23 +2067,23 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
         if (ky >= 1 && kz >= 1 && iter + min(ky, kz) < (1 << 22)) {
           constexpr int kWalk = 8;
           const int n = min(min(ky, kz), kWalk);
-          const int dimx = opaque_u(A.dims.x), dimy = opaque_u(A.dims.y);
+          const int dimx = opaque_u(SA.dims.x), dimy = opaque_u(SA.dims.y);
           const uint32_t wx = (uint32_t)wrap_coord(cx, dimx);
           float mj[kWalk];
 #pragma unroll
           for (int j = 0; j < kWalk; ++j) {
             mj[j] = 0.f;
             if (j < n) {
-              const uint32_t leaf = (uint32_t)wrap_coord(cz + j * sz, A.dims.z) * (uint32_t)dimx * (uint32_t)dimy +
+              const uint32_t leaf = (uint32_t)wrap_coord(cz + j * sz, SA.dims.z) * (uint32_t)dimx * (uint32_t)dimy +
                                     (uint32_t)wrap_coord(cy + j * sy, dimy) * (uint32_t)dimx + wx;
-              mj[j] = A.maxOp[leaf];
+              mj[j] = SA.maxOp[leaf];
             }
           }
           int done = n;  // leaves taken by the fast path
 #pragma unroll
           for (int j = 0; j < kWalk; ++j) {
             if (j < done) {
-              const float q = mj[j] / A.unitDistance;
+              const float q = mj[j] / SA.unitDistance;
               const uint32_t nx = lcg_next(st);
               if (!(mj[j] > 0.f)) {
               } else if (q > 0.f && q <= 1e30f && (nx & 0x00FFFFFFu) != 0u) {
@@ -2085,14 +2108,14 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
       if constexpr ((OPT & OPT_STATS) != 0) T.cnt.deg += zeroLen ? 1u : 0u;
       maj = 1.f;
       if (!ae) {
-        const uint32_t leaf = (uint32_t)wrap_coord(cz, A.dims.z) * (uint32_t)A.dims.x * (uint32_t)A.dims.y +
-                              (uint32_t)wrap_coord(cy, A.dims.y) * (uint32_t)A.dims.x +
-                              (uint32_t)wrap_coord(cx, A.dims.x);
-        maj = A.maxOp[leaf];
+        const uint32_t leaf = (uint32_t)wrap_coord(cz, SA.dims.z) * (uint32_t)SA.dims.x * (uint32_t)SA.dims.y +
+                              (uint32_t)wrap_coord(cy, SA.dims.y) * (uint32_t)SA.dims.x +
+                              (uint32_t)wrap_coord(cx, SA.dims.x);
+        maj = SA.maxOp[leaf];
       }
       bool fast = false;
       if (zeroLen) {
-        const float q = maj / A.unitDistance;
+        const float q = maj / SA.unitDistance;
         const uint32_t nx = lcg_next(st);
         if (!(maj > 0.f)) {
           fast = true;
@@ -2148,7 +2171,12 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   // chained frames: every wave of frame f > 0 waits for frame f - 1's wave of its pixels -- also
   // a wave none of whose rays hit the box, so that the publish words advance in frame order and
   // frame f - 1's word covers every earlier frame's stores
-  if (chainLate && !chainReady) chain_wait(A, blk, pwave, frame);
+#ifdef IRT_FRESH_TAIL
+  const RenderArgs &TA = IRT_SM_ARGS;  // the ray's end: chain wait, pixel write
+#else
+  const RenderArgs &TA = A;
+#endif
+  if (chainLate && !chainReady) chain_wait(TA, blk, pwave, frame);
   {
     const uint64_t ib = __ballot(inBox);  // rays in the box (T.count(1) at the box test)
     if (ib && __lane_id() == (unsigned)__builtin_ctzll(ib)) atomicAdd(&T.s_cnt[1], (uint32_t)__popcll(ib));
@@ -2159,35 +2187,35 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   if (toSample) {
     *sample_slot() = c;
   } else {
-    const size_t outIdx = kRecompute ? pixel_of(A, (uint32_t)opaque_u((int)blk), ptid_late()).outIdx : px.outIdx;
-    if (A.chain) {
+    const size_t outIdx = kRecompute ? pixel_of(TA, (uint32_t)opaque_u((int)blk), ptid_late()).outIdx : px.outIdx;
+    if (TA.chain) {
       float4 old;
       if (pairPos == 2 || (chainLate && (!chainReady || (OPT & OPT_LEAN) != 0))) {
-        old = chain_load_accum(A, outIdx);
+        old = chain_load_accum(TA, outIdx);
       } else if constexpr (accPf) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
         old = lds_ld16(&s_acc[tl]);
       } else if constexpr ((OPT & OPT_LEAN) != 0) {
-        old = A.accum[outIdx];
+        old = TA.accum[outIdx];
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
         old = lds_ld16(&s_acc[tl]);
       }
-      // 1.f / (float)(accumID + 1) of this frame, correctly rounded as the host's A.accumW
-      write_pixel_chain(A, outIdx, c.x, c.y, c.z, c.w, 1.f / (float)(accumID + 1), s_th, old,
-                        frame < A.numSamples - 1 && pairPos != 1);
+      // 1.f / (float)(accumID + 1) of this frame, correctly rounded as the host's TA.accumW
+      write_pixel_chain(TA, outIdx, c.x, c.y, c.z, c.w, 1.f / (float)(accumID + 1), s_th, old,
+                        frame < TA.numSamples - 1 && pairPos != 1);
     } else if constexpr ((OPT & OPT_LEAN) != 0 && !accPf) {
 #ifdef IRT_PROBE_BUILD
-      if (A.probeExit == 6) {  // measurement only (probe build): the lerp without its accum read
-        write_pixel(A, outIdx, c.x, c.y, c.z, c.w, s_th, make_float4(0.f, 0.f, 0.f, 0.f));
+      if (TA.probeExit == 6) {  // measurement only (probe build): the lerp without its accum read
+        write_pixel(TA, outIdx, c.x, c.y, c.z, c.w, s_th, make_float4(0.f, 0.f, 0.f, 0.f));
         return;
       }
-      if (A.probeExit == 7) return;  // measurement only (probe build): no accum read, no pixel stores
+      if (TA.probeExit == 7) return;  // measurement only (probe build): no accum read, no pixel stores
 #endif
-      write_pixel(A, outIdx, c.x, c.y, c.z, c.w, s_th);
+      write_pixel(TA, outIdx, c.x, c.y, c.z, c.w, s_th);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the accum prefetch has landed
-      write_pixel<kRecompute>(A, outIdx, c.x, c.y, c.z, c.w, s_th, lds_ld16(&s_acc[tl]));
+      write_pixel<kRecompute>(TA, outIdx, c.x, c.y, c.z, c.w, s_th, lds_ld16(&s_acc[tl]));
     }
   }
 }
