@@ -274,6 +274,32 @@ __device__ __forceinline__ int cam_accum_id(const RenderArgs &A, int frame) {
   return A.accumID + frame;
 }
 
+// The ray's per-lane state machine reads RenderArgs through fresh_args(): k_render's only
+// argument reached through a pointer the compiler cannot follow, so the fields it uses are
+// loaded (scalar loads, scalar-cache hits) where it uses them instead of held in SGPRs -- or
+// spilled to VGPR lanes -- through the Woodcock rounds; so does the ray's end (chain wait, pixel
+// write).  108 -> 65 spilled SGPRs on flat grids, 120 -> 87 and no scratch over terrain; C3
+// -1.5 %, C3t -2.4 % (one launch per frame -4.3 %), C3s -0.6 %, C5 even (profiles/r06s/, r06t/).
+// -DIRT_HELD_ARGS builds the held form for A/B.
+#ifndef IRT_HELD_ARGS
+__device__ __forceinline__ const RenderArgs &fresh_args() {
+  typedef const __attribute__((address_space(4))) RenderArgs *KArgs;
+  KArgs kp = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(kp));
+  return *(const RenderArgs *)kp;
+}
+#define IRT_SM_ARGS fresh_args()
+#else
+#define IRT_SM_ARGS A
+#endif
+// IRT_FRESH_TRACER (A/B build): each woodcockFunc call re-reads the arguments the Tracer uses
+// through fresh_args(), so they are live during the call only, not through the state machine
+#if defined(IRT_FRESH_TRACER) && !defined(IRT_HELD_ARGS)
+#define IRT_TR_ARGS (&fresh_args())
+#else
+#define IRT_TR_ARGS (&A)
+#endif
+
 template <int OPT>
 struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOff> {
   const RenderArgs &A;
@@ -287,6 +313,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // candidate tests), added into s_cnt at the end by flush_coop
   uint32_t nLocate = 0, nFound = 0, nCand = 0;
   int frame = 0;  // the launch's frame this wave renders (its camera: cam_org)
+  const RenderArgs *Ap = &A;  // the arguments its methods read (IRT_TR_ARGS: re-read per call)
   // OPT_TIMING: shader clocks per region (wave-uniform), in the TimeAcc base
   __device__ __forceinline__ void tmark(int region) {
     if constexpr ((OPT & OPT_TIMING) != 0) {
@@ -395,7 +422,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         j = m ? j + (uint32_t)__builtin_ctz(m) : (uint32_t)kMaskCand;
       }
       if (j >= n) break;
-      const float4 *F = A.fat + (size_t)(q + j) * kFatStride4;
+      const float4 *F = (*Ap).fat + (size_t)(q + j) * kFatStride4;
       const float4 a0 = F[0], a1 = F[1], a2 = F[2], am = F[3];
       if (__float_as_uint(am.z) >= limit) return false;
       if (pass_fat(a0, a1, a2, am, px, py, pz, r)) {
@@ -411,7 +438,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // the exact keys from the record's lines first), others the literal binary search
   __device__ __forceinline__ float record_value(const Found &f, float r) {
     const int nl = (int)(f.path & 31u);
-    const float4 *B = A.blocks + (size_t)f.rec * kBlk4;
+    const float4 *B = (*Ap).blocks + (size_t)f.rec * kBlk4;
     if (f.path & kPathBlock) {
       int b = (int)((f.path >> 5) & 3u);
       if (f.path & kPathExactKeys) {
@@ -430,15 +457,15 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // A zero-thickness record at exactly radius r (a sphere, host/irt_scene.cpp), if any:
   // the lowest such record and its getValue.
   __device__ __forceinline__ bool sphere_at(float r, float &value, uint32_t &rec) {
-    uint32_t lo = 0, hi = A.numSph;
+    uint32_t lo = 0, hi = (*Ap).numSph;
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
-      if (A.sphR[mid] < r) lo = mid + 1;
+      if ((*Ap).sphR[mid] < r) lo = mid + 1;
       else hi = mid;
     }
-    if (lo >= A.numSph || !(A.sphR[lo] == r)) return false;
-    const uint2 q = A.sphRec[A.sphOff[lo]];
-    value = find_value_literal(A.blocks + (size_t)q.x * kBlk4, (int)q.y, r);
+    if (lo >= (*Ap).numSph || !((*Ap).sphR[lo] == r)) return false;
+    const uint2 q = (*Ap).sphRec[(*Ap).sphOff[lo]];
+    value = find_value_literal((*Ap).blocks + (size_t)q.x * kBlk4, (int)q.y, r);
     rec = q.x;
     return true;
   }
@@ -452,17 +479,17 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // registers from the record's corner trig and heights exactly as buildCuBQLAccel makes
   // them (hostCode.cu:557-590); a record's union box rejects it first.
   __device__ __forceinline__ bool locate_wedge(float px, float py, float pz, float &value) {
-    const uint32_t cell = cubemap_cell_fast(px, py, pz, A.wG);
-    const uint32_t qe = A.wOff[cell + 1];
-    for (uint32_t q = A.wOff[cell]; q < qe; ++q) {
-      const uint32_t rec = A.wRec[q];
-      const float4 lo = A.wBox[2 * (size_t)rec], hi = A.wBox[2 * (size_t)rec + 1];
+    const uint32_t cell = cubemap_cell_fast(px, py, pz, (*Ap).wG);
+    const uint32_t qe = (*Ap).wOff[cell + 1];
+    for (uint32_t q = (*Ap).wOff[cell]; q < qe; ++q) {
+      const uint32_t rec = (*Ap).wRec[q];
+      const float4 lo = (*Ap).wBox[2 * (size_t)rec], hi = (*Ap).wBox[2 * (size_t)rec + 1];
       if (!(lo.x <= px && px <= hi.x && lo.y <= py && py <= hi.y && lo.z <= pz && pz <= hi.z))
         continue;
       const int nl = (int)__float_as_uint(lo.w);
-      const float4 t0 = A.wTrig[3 * (size_t)rec], t1 = A.wTrig[3 * (size_t)rec + 1],
-                   t2 = A.wTrig[3 * (size_t)rec + 2];
-      const float4 *B = A.blocks + (size_t)rec * kBlk4;
+      const float4 t0 = (*Ap).wTrig[3 * (size_t)rec], t1 = (*Ap).wTrig[3 * (size_t)rec + 1],
+                   t2 = (*Ap).wTrig[3 * (size_t)rec + 2];
+      const float4 *B = (*Ap).blocks + (size_t)rec * kBlk4;
       const float *Bf = reinterpret_cast<const float *>(B);
       for (int h = 0; h < nl; ++h) {
         const float hb = Bf[blk_height_pos(h)], ht = Bf[blk_height_pos(h + 1)];
@@ -503,15 +530,15 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   __device__ __forceinline__ bool locate_tri(float px, float py, float pz, float &value) {
     const float len = sqrtf(dot3(px, py, pz, px, py, pz));
     const float dx = -(px / len), dy = -(py / len), dz = -(pz / len);
-    const uint32_t cell = cubemap_cell_fast(px, py, pz, A.wG);
-    const uint32_t qe = A.wOff[cell + 1];
+    const uint32_t cell = cubemap_cell_fast(px, py, pz, (*Ap).wG);
+    const uint32_t qe = (*Ap).wOff[cell + 1];
     float best = __builtin_inff();
     uint32_t hit = 0xFFFFFFFFu;
-    for (uint32_t q = A.wOff[cell]; q < qe; ++q) {
-      const uint32_t rec = A.wRec[q];
-      const float4 t0 = A.wTrig[3 * (size_t)rec], t1 = A.wTrig[3 * (size_t)rec + 1],
-                   t2 = A.wTrig[3 * (size_t)rec + 2];
-      const float h0 = reinterpret_cast<const float *>(A.blocks + (size_t)rec * kBlk4)[blk_height_pos(0)];
+    for (uint32_t q = (*Ap).wOff[cell]; q < qe; ++q) {
+      const uint32_t rec = (*Ap).wRec[q];
+      const float4 t0 = (*Ap).wTrig[3 * (size_t)rec], t1 = (*Ap).wTrig[3 * (size_t)rec + 1],
+                   t2 = (*Ap).wTrig[3 * (size_t)rec + 2];
+      const float h0 = reinterpret_cast<const float *>((*Ap).blocks + (size_t)rec * kBlk4)[blk_height_pos(0)];
       const float v0[3] = {(h0 * t0.x) * t0.z, (h0 * t0.x) * t0.w, h0 * t0.y};
       const float v1[3] = {(h0 * t1.x) * t1.z, (h0 * t1.x) * t1.w, h0 * t1.y};
       const float v2[3] = {(h0 * t2.x) * t2.z, (h0 * t2.x) * t2.w, h0 * t2.y};
@@ -522,25 +549,25 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       }
     }
     if (hit == 0xFFFFFFFFu) return false;
-    const float4 *B = A.blocks + (size_t)hit * kBlk4;
+    const float4 *B = (*Ap).blocks + (size_t)hit * kBlk4;
     const float *Bf = reinterpret_cast<const float *>(B);
-    const int nl = (int)__float_as_uint(A.wBox[2 * (size_t)hit].w);
+    const int nl = (int)__float_as_uint((*Ap).wBox[2 * (size_t)hit].w);
     if (len < Bf[blk_height_pos(0)] || len > Bf[blk_height_pos(nl)]) return false;
     value = find_value_literal(B, nl, len);
     return true;
   }
 
   __device__ __forceinline__ bool locate(float px, float py, float pz, float &value) {
-    if (A.numCells == 0) return false;
+    if ((*Ap).numCells == 0) return false;
     if constexpr ((OPT & OPT_WEDGE) != 0) {
-      if (A.sampler == IRT_MODE_TRIANGLES) return locate_tri(px, py, pz, value);
+      if ((*Ap).sampler == IRT_MODE_TRIANGLES) return locate_tri(px, py, pz, value);
       return locate_wedge(px, py, pz, value);
     }
     const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
     uint32_t sub;
-    const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G, sub);
+    const uint32_t cell = cubemap_cell_fast(px, py, pz, (*Ap).G, sub);
     // the cell header's words 0..7 and the sub-cell's mask word: one 128-B line
-    const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
+    const uint4 *Hc = (*Ap).binHdr + (size_t)cell * (kBinHdrWords / 4);
     const uint4 H0 = Hc[0], H1 = Hc[1];
     const uint32_t M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
     return locate_hdr(px, py, pz, r, H0, H1, M, value);
@@ -573,7 +600,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       qb = qe;
       qe = H0.w + end2;
     }
-    if (A.numSph) {
+    if ((*Ap).numSph) {
       const uint32_t h = sph_hash(r);
       if ((s_sph[h >> 5] >> (h & 31)) & 1u) {
         float v2;
@@ -648,7 +675,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       const int k = 2 * p + (lane >> 5);
       v[p] = 0u;
       if (k < ns && (lane & 31) < kBinHdrWords)
-        v[p] = reinterpret_cast<const uint32_t *>(A.binHdr)[(size_t)S.cell[k] * kBinHdrWords + (lane & 31)];
+        v[p] = reinterpret_cast<const uint32_t *>((*Ap).binHdr)[(size_t)S.cell[k] * kBinHdrWords + (lane & 31)];
     }
 #pragma unroll
     for (int p = 0; p < kHdrStage / 2; ++p) {
@@ -661,7 +688,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       H1 = lds_ld16(reinterpret_cast<const uint4 *>(&S.w[slot][4]));
       M = S.w[slot][8 + sub];
     } else if (want) {
-      const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
+      const uint4 *Hc = (*Ap).binHdr + (size_t)cell * (kBinHdrWords / 4);
       H0 = Hc[0];
       H1 = Hc[1];
       M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
@@ -670,7 +697,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   }
   __device__ __forceinline__ bool locate_wave(bool want, float px, float py, float pz, float &value,
                                               CoopWave &CW, ScanWave &W, const uint32_t *touch = nullptr) {
-    want = want && A.numCells != 0;
+    want = want && (*Ap).numCells != 0;
     const int lane = (int)__lane_id();
     // The scan's state lives in the wave's LDS (fewer live VGPRs across it):
     //   W.pt[l]  the sample {point, r} of lane l
@@ -694,16 +721,16 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     static_assert(!kSlot || (OPT & (OPT_HDRLDS | OPT_PAIR | OPT_DEALALL | OPT_NEXTHDR)) == 0, "slot table: the default scan");
     float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, sm = s0;  // OPT_SLOT: the first candidate
     if constexpr ((OPT & OPT_HDRLDS) != 0) {
-      if (want) cell = cubemap_cell_fast(px, py, pz, A.G, sub);
+      if (want) cell = cubemap_cell_fast(px, py, pz, (*Ap).G, sub);
       stage_headers(want, cell, sub, H0, H1, M);
     }
     if (kSlot && want) {
       // the slot of the sample's (cell, sub-cell, bin): the bins from the scene's shared edges
       const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
-      cell = cubemap_cell_fast(px, py, pz, A.G, sub);
-      const float e0 = A.slotEdge[0], e1 = A.slotEdge[1], e2 = A.slotEdge[2];
+      cell = cubemap_cell_fast(px, py, pz, (*Ap).G, sub);
+      const float e0 = (*Ap).slotEdge[0], e1 = (*Ap).slotEdge[1], e2 = (*Ap).slotEdge[2];
       const int b = bin_of(r, e0, e1, e2);
-      const float4 *S = A.slots + ((size_t)(cell * (uint32_t)(kSubCells * kSubCells) + sub) * (uint32_t)A.slotBins + (uint32_t)b) * kSlot4;
+      const float4 *S = (*Ap).slots + ((size_t)(cell * (uint32_t)(kSubCells * kSubCells) + sub) * (uint32_t)(*Ap).slotBins + (uint32_t)b) * kSlot4;
       s0 = S[0];
       s1 = S[1];
       s2 = S[2];
@@ -717,8 +744,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     } else if (want) {
       const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
       if constexpr ((OPT & OPT_HDRLDS) == 0) {
-        cell = cubemap_cell_fast(px, py, pz, A.G, sub);
-        const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
+        cell = cubemap_cell_fast(px, py, pz, (*Ap).G, sub);
+        const uint4 *Hc = (*Ap).binHdr + (size_t)cell * (kBinHdrWords / 4);
         H0 = Hc[0];
         H1 = Hc[1];
         M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
@@ -727,7 +754,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         // issued after this sample's header words: waiting for them leaves it in flight
         // (unconditional -- this sample's own line when there is none: a load under a branch
         // makes the compiler wait for it before the header words)
-        tv = *(touch ? touch : reinterpret_cast<const uint32_t *>(A.binHdr + (size_t)cell * (kBinHdrWords / 4)));
+        tv = *(touch ? touch : reinterpret_cast<const uint32_t *>((*Ap).binHdr + (size_t)cell * (kBinHdrWords / 4)));
       }
       const int b = bin_of(r, __uint_as_float(H0.x), __uint_as_float(H0.y), __uint_as_float(H0.z));
       const uint32_t m1 = b > 0 ? ~0u : 0u, m2 = b > 1 ? ~0u : 0u, m3 = b > 2 ? ~0u : 0u;
@@ -745,7 +772,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         // record passes the radial test (ICONGrid.h:184), so the scan would test every candidate
         // and find none -- a void of the volume (convert_icon's land columns), decided from the
         // header line alone
-        const uint2 bd = reinterpret_cast<const uint2 *>(A.binHdr + (size_t)cell * (kBinHdrWords / 4))
+        const uint2 bd = reinterpret_cast<const uint2 *>((*Ap).binHdr + (size_t)cell * (kBinHdrWords / 4))
             [kBoundWord / 2 + quad_of(sub)];
         if (r > __uint_as_float(bd.x) || r < __uint_as_float(bd.y)) {
           c = 0u;
@@ -767,8 +794,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       if (kPair && c > 0u) {
         // both entries gathered before either is tested; the second counts only if the
         // first fails (the serial scan's order)
-        const float4 *F1 = A.fat + (size_t)fe * kFatStride4;
-        const float4 *F2 = A.fat + (size_t)(c > 1u ? fe2 : fe) * kFatStride4;
+        const float4 *F1 = (*Ap).fat + (size_t)fe * kFatStride4;
+        const float4 *F2 = (*Ap).fat + (size_t)(c > 1u ? fe2 : fe) * kFatStride4;
         const float4 a0 = F1[0], a1 = F1[1], a2 = F1[2], am = F1[3];
         const float4 b0 = F2[0], b1 = F2[1], b2 = F2[2], bm = F2[3];
         const bool ok1 = entry_passes(a0, a1, a2, am, px, py, pz, fr);
@@ -797,7 +824,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
           f = {__float_as_uint(sm.z), record_path(__float_as_uint(sm.w), sm.x, sm.y, fr)};
           ok = entry_passes(s0, s1, s2, sm, px, py, pz, fr);
         } else {
-          ok = pass_entry(A.fat + (size_t)fe * kFatStride4, px, py, pz, fr, f);
+          ok = pass_entry((*Ap).fat + (size_t)fe * kFatStride4, px, py, pz, fr, f);
         }
         if (f.rec < flim) {  // scan_fat stops, uncounted, at the first record >= the limit
           ++specCand;
@@ -834,7 +861,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         if (task) {
           const float4 po = lds_ld16(&W.pt[o]);
           const uint4 d = lds_ld16(&W.lst[o]);
-          tp = pass_entry(A.fat + (size_t)(d.x + list_entry(d.y, d.z + (t - s0))) * kFatStride4, po.x, po.y,
+          tp = pass_entry((*Ap).fat + (size_t)(d.x + list_entry(d.y, d.z + (t - s0))) * kFatStride4, po.x, po.y,
                           po.z, po.w, g);
           tl = g.rec >= d.w;  // past the limit: the serial scan stops there
           tp = tp && !tl;
@@ -870,8 +897,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       if (edge) {
         const float4 p = lds_ld16(&W.pt[lane]);
         uint32_t sub;
-        const uint32_t cell = cubemap_cell_fast(p.x, p.y, p.z, A.G, sub);
-        const uint4 *Hc = A.binHdr + (size_t)cell * (kBinHdrWords / 4);
+        const uint32_t cell = cubemap_cell_fast(p.x, p.y, p.z, (*Ap).G, sub);
+        const uint4 *Hc = (*Ap).binHdr + (size_t)cell * (kBinHdrWords / 4);
         const uint4 H0 = Hc[0], H1 = Hc[1];
         const uint32_t M = reinterpret_cast<const uint32_t *>(Hc)[8 + sub];
         const int b = bin_of(p.w, __uint_as_float(H0.x), __uint_as_float(H0.y), __uint_as_float(H0.z)) + 1;
@@ -895,7 +922,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       const uint2 rm = frm[lane];
       f = {rm.x, rm.y};
     }
-    if (A.numSph) {
+    if ((*Ap).numSph) {
       const uint32_t h = sph_hash(r);
       if ((s_sph[h >> 5] >> (h & 31)) & 1u) {
         float v2;
@@ -913,33 +940,33 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // postClassify's alpha only (the acceptance test needs nothing else); the colour comes
   // from post_classify on acceptance
   __device__ __forceinline__ float classify_alpha(float v) {
-    v = div_uniform(v - A.tfLo, A.invTf);  // (v - tfLo) / (tfHi - tfLo), correctly rounded
-    const int size = opaque_u(A.lutSize);
+    v = div_uniform(v - (*Ap).tfLo, (*Ap).invTf);  // (v - tfLo) / (tfHi - tfLo), correctly rounded
+    const int size = opaque_u((*Ap).lutSize);
     const int idx = f2i_x86(v * (float)size);
     const float frac = (v * (float)size) - (float)idx;
     const int i1 = idx < 0 ? 0 : (idx > size - 1 ? size - 1 : idx);
     const int idx2 = (int)((uint32_t)idx + 1u);
     const int i2 = idx2 < 0 ? 0 : (idx2 > size - 1 ? size - 1 : idx2);
-    const float a = A.lut[i1].w, b = A.lut[i2].w;
-    return a * frac + b * (1.f - frac) * A.opacityScale;
+    const float a = (*Ap).lut[i1].w, b = (*Ap).lut[i2].w;
+    return a * frac + b * (1.f - frac) * (*Ap).opacityScale;
   }
 
   // postClassify (deviceCode.cu:127-135): weights reversed, opacityScale on 2nd term only
   __device__ __forceinline__ float4 post_classify(float v) {
-    v = div_uniform(v - A.tfLo, A.invTf);  // (v - tfLo) / (tfHi - tfLo), correctly rounded
-    const int size = opaque_u(A.lutSize);
+    v = div_uniform(v - (*Ap).tfLo, (*Ap).invTf);  // (v - tfLo) / (tfHi - tfLo), correctly rounded
+    const int size = opaque_u((*Ap).lutSize);
     const int idx = f2i_x86(v * (float)size);
     const float frac = (v * (float)size) - (float)idx;
     const int i1 = idx < 0 ? 0 : (idx > size - 1 ? size - 1 : idx);
     const int idx2 = (int)((uint32_t)idx + 1u);
     const int i2 = idx2 < 0 ? 0 : (idx2 > size - 1 ? size - 1 : idx2);
-    const float4 a = A.lut[i1], b = A.lut[i2];
+    const float4 a = (*Ap).lut[i1], b = (*Ap).lut[i2];
     const float om = 1.f - frac;
     float4 o;
     o.x = a.x * frac + b.x * om * 1.f;
     o.y = a.y * frac + b.y * om * 1.f;
     o.z = a.z * frac + b.z * om * 1.f;
-    o.w = a.w * frac + b.w * om * A.opacityScale;
+    o.w = a.w * frac + b.w * om * (*Ap).opacityScale;
     return o;
   }
 
@@ -950,13 +977,13 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
                                             bool counted) {
     float t = tmin;
     if (majorant <= 0.f) return fminf(t, tmax);
-    const float q = majorant / A.unitDistance;  // the same value every iteration (165)
+    const float q = majorant / (*Ap).unitDistance;  // the same value every iteration (165)
     while (true) {
       if constexpr ((OPT & OPT_STATS) != 0) ++cnt.steps;
       st = lcg_next(st);
       t -= (woodcock_log(st, s_logf) / q);
       if (t > tmax) break;
-      const float3 O = cam_org(A, frame);
+      const float3 O = cam_org((*Ap), frame);
       const float px = O.x + dx * t, py = O.y + dy * t, pz = O.z + dz * t;
       float value = 0.f;
       if (counted) count(2);
@@ -991,9 +1018,10 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
                                                 float tmax, uint32_t &st, float majorant,
                                                 bool counted, float4 &sampleOut, bool &miss,
                                                 CoopWave &W, ScanWave *SW, const uint2 *jmp) {
+    Ap = IRT_TR_ARGS;
     const int lane = (int)__lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
-    const float q = majorant / A.unitDistance;
+    const float q = majorant / (*Ap).unitDistance;
     bool active = req && !(majorant <= 0.f);  // majorant <= 0: return at once (161-162)
     // speculation ramps up: a ray gets at most 2^lgCap lanes this round, and lgCap grows
     // each round it stays undecided.  Most chains end within a few samples (default TF:
@@ -1001,9 +1029,9 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     // (sparse TFs) reach whole-wave groups after six rounds.  The miss-mode kernels (wedge
     // samplers, grid accel) keep whole-wave groups from the start: their misses come in
     // runs that wide groups cross in one round (2 % faster there, profiles/r02e_coop_cap).
-    int lgCap = kWideStart ? 6 : A.coopMaxLg;
+    int lgCap = kWideStart ? 6 : (*Ap).coopMaxLg;
     tmark(6);  // between woodcockFunc calls (sdda leaves, ranges)
-    for (int wr = 0;; lgCap = min(lgCap + A.coopRamp, 6), ++wr) {
+    for (int wr = 0;; lgCap = min(lgCap + (*Ap).coopRamp, 6), ++wr) {
       const uint64_t am = __ballot(active);
       if (am == 0ull) break;
       if constexpr ((OPT & OPT_STATS) != 0) ++cnt.rounds;
@@ -1085,18 +1113,18 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         // crossed in one round instead of one round per sample.
         constexpr bool kVoidLoc = (OPT & OPT_VOIDLOC) != 0;
         if (solo && used && !past && (mm || kVoidLoc)) {
-          const float3 O = cam_org(A, frame);
+          const float3 O = cam_org((*Ap), frame);
 #pragma nounroll
           for (int it = 0; it < kVoidRunMax; ++it) {
             const float px = O.x + ry.x * tk, py = O.y + ry.y * tk, pz = O.z + ry.z * tk;
             const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
             uint32_t sub;
-            const uint32_t cell = cubemap_cell_fast(px, py, pz, A.G, sub);
+            const uint32_t cell = cubemap_cell_fast(px, py, pz, (*Ap).G, sub);
             // (the same header line as the last sample's while the walk stays in one cell: an L1 hit)
-            const uint2 bd = reinterpret_cast<const uint2 *>(A.binHdr + (size_t)cell * (kBinHdrWords / 4))
+            const uint2 bd = reinterpret_cast<const uint2 *>((*Ap).binHdr + (size_t)cell * (kBinHdrWords / 4))
                 [kBoundWord / 2 + quad_of(sub)];
             if (!(r > __uint_as_float(bd.x) || r < __uint_as_float(bd.y))) break;  // may be located: the round's scan decides
-            if (A.numSph) {  // a zero-thickness record at exactly r is not in the lists
+            if ((*Ap).numSph) {  // a zero-thickness record at exactly r is not in the lists
               const uint32_t h = sph_hash(r);
               if ((s_sph[h >> 5] >> (h & 31)) & 1u) break;
             }
@@ -1126,7 +1154,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       tmark(2);  // round start: exchange, jumps, logf, prefix
 #ifdef IRT_PROBE_BUILD
       // measurement only (31): 100 extra VALU instructions per Woodcock round
-      if (A.probeExit == 31) {
+      if ((*Ap).probeExit == 31) {
 #pragma nounroll
         for (int k = 0; k < 25; ++k) asm volatile("v_nop\n v_nop\n v_nop\n v_nop" ::: "memory");
       }
@@ -1140,25 +1168,25 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
             const float t1 = tk - woodcock_log(lcg_next(lcg_next(sk)), s_logf) * __builtin_amdgcn_rcpf(rq.z);
             if (t1 <= rq.y) {
               uint32_t sb;
-              const float3 O = cam_org(A, frame);
+              const float3 O = cam_org((*Ap), frame);
               const uint32_t c1 = cubemap_cell_fast(O.x + ry.x * t1, O.y + ry.y * t1, O.z + ry.z * t1,
-                                                    A.G, sb);
-              tp = reinterpret_cast<const uint32_t *>(A.binHdr + (size_t)c1 * (kBinHdrWords / 4));
+                                                    (*Ap).G, sb);
+              tp = reinterpret_cast<const uint32_t *>((*Ap).binHdr + (size_t)c1 * (kBinHdrWords / 4));
             }
           }
         } else {
           (void)wr;
         }
-        const float3 O = cam_org(A, frame);
+        const float3 O = cam_org((*Ap), frame);
         found = locate_wave(used && !past, O.x + ry.x * tk, O.y + ry.y * tk, O.z + ry.z * tk,
                             value, W, *SW, tp);
       } else if (used && !past) {
-        const float3 O = cam_org(A, frame);
+        const float3 O = cam_org((*Ap), frame);
         found = locate(O.x + ry.x * tk, O.y + ry.y * tk, O.z + ry.z * tk, value);
       }
       tmark(5);  // locate's tail: sphere, getValue
 #ifdef IRT_PROBE_BUILD
-      if (A.probeExit >= 9 && A.probeExit <= 12) return;
+      if ((*Ap).probeExit >= 9 && (*Ap).probeExit <= 12) return;
 #endif
       if (found) {
         const float sw = classify_alpha(value);  // postClassify(value).w
@@ -1676,23 +1704,6 @@ __device__ __forceinline__ bool spherical_fast(const RenderArgs &A, float x, flo
 // (kDone); then the wave tracks every waiting lane's leaf at once, and each lane resumes
 // with the leaf's outcome.  Every lane of the wave calls it (those without a pixel start
 // finished).  Same ranges, leaves, draws and results as render_pixel, step for step.
-// The ray's per-lane state machine reads RenderArgs through fresh_args(): k_render's only
-// argument reached through a pointer the compiler cannot follow, so the fields it uses are
-// loaded (scalar loads, scalar-cache hits) where it uses them instead of held in SGPRs -- or
-// spilled to VGPR lanes -- through the Woodcock rounds: 108 -> 78 spilled SGPRs on flat grids,
-// 120 -> 92 over terrain; C3 -1.8 %, C5 -1.1 %, one launch per frame -1.1 % (profiles/r06s/).
-// -DIRT_HELD_ARGS builds the held form for A/B; -DIRT_FRESH_TAIL (A/B) also the ray's end.
-#ifndef IRT_HELD_ARGS
-__device__ __forceinline__ const RenderArgs &fresh_args() {
-  typedef const __attribute__((address_space(4))) RenderArgs *KArgs;
-  KArgs kp = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(kp));
-  return *(const RenderArgs *)kp;
-}
-#define IRT_SM_ARGS fresh_args()
-#else
-#define IRT_SM_ARGS A
-#endif
 
 template <int OPT>
 __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OPT> &T, const Pixel &px,
@@ -2171,11 +2182,7 @@ __device__ __forceinline__ void render_pixel_coop(const RenderArgs &A, Tracer<OP
   // chained frames: every wave of frame f > 0 waits for frame f - 1's wave of its pixels -- also
   // a wave none of whose rays hit the box, so that the publish words advance in frame order and
   // frame f - 1's word covers every earlier frame's stores
-#ifdef IRT_FRESH_TAIL
   const RenderArgs &TA = IRT_SM_ARGS;  // the ray's end: chain wait, pixel write
-#else
-  const RenderArgs &TA = A;
-#endif
   if (chainLate && !chainReady) chain_wait(TA, blk, pwave, frame);
   {
     const uint64_t ib = __ballot(inBox);  // rays in the box (T.count(1) at the box test)

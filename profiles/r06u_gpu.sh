@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 6 (u): each woodcockFunc call also re-reads the Tracer's arguments through fresh_args()
+# (-DIRT_FRESH_TRACER: 42 spilled SGPRs on flat grids, 48 over terrain) against the new default
+# (state machine and ray's end fresh: 65 / 87) and the committed round-6 kernel ("old", 108 / 120);
+# frames with the tracer build first, then the A/B
+set -o pipefail
+O=gpurun_out/r06u
+mkdir -p $O
+P=icon-ray-tracing_amd
+export IRT_LIB_PATH=$(pwd)/$P/libicon_rt_hip_tracer.so
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_chain.py tests/test_gpu_split.py > $O/tests_tracer_chain.log 2>&1 || exit 1
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_scale.py -k "(c3 or c3t) and (whole or eight)" > $O/tests_tracer_scale.log 2>&1 || exit 1
+unset IRT_LIB_PATH
+BATCH=8 ROUNDS=3 timeout -k 10 600 bash profiles/ab_multi.sh $O/ab8 "c3 c3t" $P/libicon_rt_hip_old.so $P/libicon_rt_hip.so $P/libicon_rt_hip_tracer.so || exit 1
+BATCH=1 ROUNDS=3 timeout -k 10 400 bash profiles/ab_multi.sh $O/ab1 "c3 c3t" $P/libicon_rt_hip_old.so $P/libicon_rt_hip.so $P/libicon_rt_hip_tracer.so || exit 1
+BATCH=8 ROUNDS=2 timeout -k 10 600 bash profiles/ab_multi.sh $O/ab8 "c3s c5" $P/libicon_rt_hip_old.so $P/libicon_rt_hip.so $P/libicon_rt_hip_tracer.so || exit 1
