@@ -437,8 +437,13 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // 64-B height/value block the quantised keys pick (one gather; r within a unit of a key:
   // the exact keys from the record's lines first), others the literal binary search
   __device__ __forceinline__ float record_value(const Found &f, float r) {
+#if defined(IRT_FRESH_LATE) && !defined(IRT_HELD_ARGS)
+    const RenderArgs &LA = fresh_args();  // read where used (IRT_FRESH_LATE)
+#else
+    const RenderArgs &LA = *Ap;
+#endif
     const int nl = (int)(f.path & 31u);
-    const float4 *B = (*Ap).blocks + (size_t)f.rec * kBlk4;
+    const float4 *B = LA.blocks + (size_t)f.rec * kBlk4;
     if (f.path & kPathBlock) {
       int b = (int)((f.path >> 5) & 3u);
       if (f.path & kPathExactKeys) {
@@ -457,15 +462,20 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // A zero-thickness record at exactly radius r (a sphere, host/irt_scene.cpp), if any:
   // the lowest such record and its getValue.
   __device__ __forceinline__ bool sphere_at(float r, float &value, uint32_t &rec) {
-    uint32_t lo = 0, hi = (*Ap).numSph;
+#if defined(IRT_FRESH_LATE) && !defined(IRT_HELD_ARGS)
+    const RenderArgs &LA = fresh_args();  // read where used (IRT_FRESH_LATE)
+#else
+    const RenderArgs &LA = *Ap;
+#endif
+    uint32_t lo = 0, hi = LA.numSph;
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
-      if ((*Ap).sphR[mid] < r) lo = mid + 1;
+      if (LA.sphR[mid] < r) lo = mid + 1;
       else hi = mid;
     }
-    if (lo >= (*Ap).numSph || !((*Ap).sphR[lo] == r)) return false;
-    const uint2 q = (*Ap).sphRec[(*Ap).sphOff[lo]];
-    value = find_value_literal((*Ap).blocks + (size_t)q.x * kBlk4, (int)q.y, r);
+    if (lo >= LA.numSph || !(LA.sphR[lo] == r)) return false;
+    const uint2 q = LA.sphRec[LA.sphOff[lo]];
+    value = find_value_literal(LA.blocks + (size_t)q.x * kBlk4, (int)q.y, r);
     rec = q.x;
     return true;
   }
@@ -940,33 +950,43 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // postClassify's alpha only (the acceptance test needs nothing else); the colour comes
   // from post_classify on acceptance
   __device__ __forceinline__ float classify_alpha(float v) {
-    v = div_uniform(v - (*Ap).tfLo, (*Ap).invTf);  // (v - tfLo) / (tfHi - tfLo), correctly rounded
-    const int size = opaque_u((*Ap).lutSize);
+#if defined(IRT_FRESH_LATE) && !defined(IRT_HELD_ARGS)
+    const RenderArgs &LA = fresh_args();  // read where used (IRT_FRESH_LATE)
+#else
+    const RenderArgs &LA = *Ap;
+#endif
+    v = div_uniform(v - LA.tfLo, LA.invTf);  // (v - tfLo) / (tfHi - tfLo), correctly rounded
+    const int size = opaque_u(LA.lutSize);
     const int idx = f2i_x86(v * (float)size);
     const float frac = (v * (float)size) - (float)idx;
     const int i1 = idx < 0 ? 0 : (idx > size - 1 ? size - 1 : idx);
     const int idx2 = (int)((uint32_t)idx + 1u);
     const int i2 = idx2 < 0 ? 0 : (idx2 > size - 1 ? size - 1 : idx2);
-    const float a = (*Ap).lut[i1].w, b = (*Ap).lut[i2].w;
-    return a * frac + b * (1.f - frac) * (*Ap).opacityScale;
+    const float a = LA.lut[i1].w, b = LA.lut[i2].w;
+    return a * frac + b * (1.f - frac) * LA.opacityScale;
   }
 
   // postClassify (deviceCode.cu:127-135): weights reversed, opacityScale on 2nd term only
   __device__ __forceinline__ float4 post_classify(float v) {
-    v = div_uniform(v - (*Ap).tfLo, (*Ap).invTf);  // (v - tfLo) / (tfHi - tfLo), correctly rounded
-    const int size = opaque_u((*Ap).lutSize);
+#if defined(IRT_FRESH_LATE) && !defined(IRT_HELD_ARGS)
+    const RenderArgs &LA = fresh_args();  // read where used (IRT_FRESH_LATE)
+#else
+    const RenderArgs &LA = *Ap;
+#endif
+    v = div_uniform(v - LA.tfLo, LA.invTf);  // (v - tfLo) / (tfHi - tfLo), correctly rounded
+    const int size = opaque_u(LA.lutSize);
     const int idx = f2i_x86(v * (float)size);
     const float frac = (v * (float)size) - (float)idx;
     const int i1 = idx < 0 ? 0 : (idx > size - 1 ? size - 1 : idx);
     const int idx2 = (int)((uint32_t)idx + 1u);
     const int i2 = idx2 < 0 ? 0 : (idx2 > size - 1 ? size - 1 : idx2);
-    const float4 a = (*Ap).lut[i1], b = (*Ap).lut[i2];
+    const float4 a = LA.lut[i1], b = LA.lut[i2];
     const float om = 1.f - frac;
     float4 o;
     o.x = a.x * frac + b.x * om * 1.f;
     o.y = a.y * frac + b.y * om * 1.f;
     o.z = a.z * frac + b.z * om * 1.f;
-    o.w = a.w * frac + b.w * om * (*Ap).opacityScale;
+    o.w = a.w * frac + b.w * om * LA.opacityScale;
     return o;
   }
 
