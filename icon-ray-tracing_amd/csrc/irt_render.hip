@@ -280,7 +280,9 @@ __device__ __forceinline__ int cam_accum_id(const RenderArgs &A, int frame) {
 // spilled to VGPR lanes -- through the Woodcock rounds; so does the ray's end (chain wait, pixel
 // write).  108 -> 65 spilled SGPRs on flat grids, 120 -> 87 and no scratch over terrain; C3
 // -1.5 %, C3t -2.4 % (one launch per frame -4.3 %), C3s -0.6 %, C5 even (profiles/r06s/, r06t/).
-// -DIRT_HELD_ARGS builds the held form for A/B.
+// The Tracer's late reads (classify_alpha, record_value, sphere_at, the sphere test) too: 62 and
+// 73 spilled SGPRs, C3t -1.2 %, C5 -0.9 %, C3 and C3s even (profiles/r06v/; -DIRT_HELD_LATE
+// reads them through Ap).  -DIRT_HELD_ARGS builds the held form for A/B.
 #ifndef IRT_HELD_ARGS
 __device__ __forceinline__ const RenderArgs &fresh_args() {
   typedef const __attribute__((address_space(4))) RenderArgs *KArgs;
@@ -437,8 +439,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // 64-B height/value block the quantised keys pick (one gather; r within a unit of a key:
   // the exact keys from the record's lines first), others the literal binary search
   __device__ __forceinline__ float record_value(const Found &f, float r) {
-#if defined(IRT_FRESH_LATE) && !defined(IRT_HELD_ARGS)
-    const RenderArgs &LA = fresh_args();  // read where used (IRT_FRESH_LATE)
+#if !defined(IRT_HELD_ARGS) && !defined(IRT_HELD_LATE)
+    const RenderArgs &LA = fresh_args();  // read where used (-DIRT_HELD_LATE: through Ap)
 #else
     const RenderArgs &LA = *Ap;
 #endif
@@ -462,8 +464,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // A zero-thickness record at exactly radius r (a sphere, host/irt_scene.cpp), if any:
   // the lowest such record and its getValue.
   __device__ __forceinline__ bool sphere_at(float r, float &value, uint32_t &rec) {
-#if defined(IRT_FRESH_LATE) && !defined(IRT_HELD_ARGS)
-    const RenderArgs &LA = fresh_args();  // read where used (IRT_FRESH_LATE)
+#if !defined(IRT_HELD_ARGS) && !defined(IRT_HELD_LATE)
+    const RenderArgs &LA = fresh_args();  // read where used (-DIRT_HELD_LATE: through Ap)
 #else
     const RenderArgs &LA = *Ap;
 #endif
@@ -950,8 +952,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // postClassify's alpha only (the acceptance test needs nothing else); the colour comes
   // from post_classify on acceptance
   __device__ __forceinline__ float classify_alpha(float v) {
-#if defined(IRT_FRESH_LATE) && !defined(IRT_HELD_ARGS)
-    const RenderArgs &LA = fresh_args();  // read where used (IRT_FRESH_LATE)
+#if !defined(IRT_HELD_ARGS) && !defined(IRT_HELD_LATE)
+    const RenderArgs &LA = fresh_args();  // read where used (-DIRT_HELD_LATE: through Ap)
 #else
     const RenderArgs &LA = *Ap;
 #endif
@@ -968,8 +970,8 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
 
   // postClassify (deviceCode.cu:127-135): weights reversed, opacityScale on 2nd term only
   __device__ __forceinline__ float4 post_classify(float v) {
-#if defined(IRT_FRESH_LATE) && !defined(IRT_HELD_ARGS)
-    const RenderArgs &LA = fresh_args();  // read where used (IRT_FRESH_LATE)
+#if !defined(IRT_HELD_ARGS) && !defined(IRT_HELD_LATE)
+    const RenderArgs &LA = fresh_args();  // read where used (-DIRT_HELD_LATE: through Ap)
 #else
     const RenderArgs &LA = *Ap;
 #endif

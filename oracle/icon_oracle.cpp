@@ -35,6 +35,7 @@
 #include <cmath>
 #include <cstring>
 #include <thread>
+#include <string>
 #include <vector>
 
 namespace {
@@ -673,6 +674,9 @@ void buildFast(Scene &S, int nthreads) {
 
 struct ThreadStats {
   uint64_t launched = 0, inBox = 0, locate = 0, found = 0, draws = 0, leaves = 0;
+  // analysis only (oracle_trace_pixels): one letter per counted sampleVolume call -- 'm' outside
+  // every cell, 'l' located and rejected, 'A' accepted -- 'E' for a call ending past its tmax
+  std::string *trace = nullptr;
 };
 
 // sampleVolume, CPU branch: first cell index wins (deviceCode.cu:116-123)
@@ -839,14 +843,21 @@ inline float woodcockTracking(const Scene &S, const oc_params &p, const Ray &ray
   while (1) {
     if (majorant <= 0.f) break;
     t -= (logf(1.f - rnd()) / (majorant / p.unitDistance));
-    if (t > ray.tmax) break;
+    if (t > ray.tmax) {
+      if (ts.trace) ts.trace->push_back('E');
+      break;
+    }
     V3 P = ray.org + ray.dir * t;
     float value{0.f};
     ++ts.locate;
-    if (!sampleVolume(S, P, value)) continue;
+    if (!sampleVolume(S, P, value)) {
+      if (ts.trace) ts.trace->push_back('m');
+      continue;
+    }
     ++ts.found;
     V4 sample = postClassify(p, value);
     float u = rnd();
+    if (ts.trace) ts.trace->push_back(sample.w >= u * majorant ? 'A' : 'l');
     if (sample.w >= u * majorant) {
       albedo = {sample.x, sample.y, sample.z};
       extinction = sample.w;
@@ -925,6 +936,7 @@ void raygen(const Scene &S, const oc_params &p, int x, int y, int W, int H, floa
       // since the reference's lat/lon planes are degenerate) can never change the pixel and
       // are not counted; the GPU kernel skips those it does not need for the RNG state.
       ThreadStats uncounted;
+      if (ts.trace && tt0 != tt1) ts.trace->push_back('|');
       float t = woodcockTracking(S, p, ray, rnd, majorant, albedo, extinction,
                                  tt0 == tt1 ? uncounted : ts);
       if (t > tt0 && t < tt1) {
@@ -1352,6 +1364,40 @@ int oracle_render_pixels(const oc_cell *cells, size_t n, const oc_params *p, int
       stats->leaves += ts.leaves;
     }
   }
+  return 0;
+}
+
+// Analysis only (profiles/sample_pattern.py): the sample outcomes of each pixel's ray, as
+// letters (ThreadStats::trace) with '|' before each counted woodcockFunc call; pixel i's string
+// at out + i * stride, NUL-terminated, cut at stride - 1 letters.
+int oracle_trace_pixels(const oc_cell *cells, size_t n, const oc_params *p, int W, int H,
+                        const int32_t *xy, int numPixels, char *out, int stride, int nthreads) {
+  if (!p || W <= 0 || H <= 0 || numPixels < 0 || stride < 1) return -1;
+  Scene S{cells, n, 2, {}, {}, {}, false, {}, {}, false};
+  prepare(S, p, nthreads);
+  std::atomic<int> counter{0};
+  if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
+  if (nthreads <= 0) nthreads = 1;
+  std::vector<float> acc(4 * (size_t)W * H);
+  std::vector<uint32_t> fb((size_t)W * H);
+  auto worker = [&]() {
+    ThreadStats ts;
+    std::string tr;
+    ts.trace = &tr;
+    for (;;) {
+      int i = counter.fetch_add(1);
+      if (i >= numPixels) break;
+      tr.clear();
+      raygen(S, *p, xy[2 * i], xy[2 * i + 1], W, H, acc.data(), fb.data(), ts);
+      const size_t m = std::min(tr.size(), (size_t)stride - 1);
+      memcpy(out + (size_t)i * stride, tr.data(), m);
+      out[(size_t)i * stride + m] = 0;
+    }
+  };
+  std::vector<std::thread> threads;
+  for (int t = 1; t < nthreads; ++t) threads.emplace_back(worker);
+  worker();
+  for (auto &t : threads) t.join();
   return 0;
 }
 

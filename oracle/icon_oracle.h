@@ -139,6 +139,11 @@ void oracle_scene_free(oc_scene *s);
 int oracle_render_pixels(const oc_cell *cells, size_t n, const oc_params *p, int W, int H,
                          const int32_t *xy, int numPixels, float *accum, uint32_t *fb,
                          int nthreads, int fast, oc_stats *stats);
+/* Analysis only: each pixel's sample outcomes as letters ('|' a woodcockFunc call, 'm' outside
+ * every cell, 'l' located and rejected, 'A' accepted, 'E' past tmax), NUL-terminated at
+ * out + i * stride (profiles/sample_pattern.py). */
+int oracle_trace_pixels(const oc_cell *cells, size_t n, const oc_params *p, int W, int H,
+                        const int32_t *xy, int numPixels, char *out, int stride, int nthreads);
 
 /* ---- known-answer helpers (single functions) ---- */
 void oracle_lcg(uint32_t seed0, uint32_t seed1, int n, float *out);            /* dvr_course-common-both.h:41-86 */
