@@ -593,26 +593,29 @@ __global__ void k_slot_edges(const uint32_t *hdr, uint32_t numCells, uint32_t *s
   }
 }
 
-// one thread per slot (cell, sub-cell, table bin)
+// one thread per slot (cell, slot unit of `subs` sub-cells, table bin); *bad when a bin's unmasked
+// candidates do not fit the slot's 24-bit count
 __global__ void k_slot_fill(const uint32_t *hdr, const float *fat, uint32_t numCells, float u0, float u1, float u2,
-                            int ne, float4 *slots) {
+                            int ne, int subs, float4 *slots, uint32_t *bad) {
   const int bins = ne + 1;
+  const int units = kSubCells * kSubCells / subs;
   const float U[kMaxEdges] = {u0, u1, u2};
-  const uint64_t total = (uint64_t)numCells * kSubCells * kSubCells * bins;
+  const uint64_t total = (uint64_t)numCells * units * bins;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
     const int b = (int)(i % bins);
-    const uint64_t cs = i / bins;
-    const int sc = (int)(cs % (kSubCells * kSubCells));
-    const uint64_t c = cs / (kSubCells * kSubCells);
+    const uint64_t cu = i / bins;
+    const int u = (int)(cu % units);
+    const uint64_t c = cu / units;
     float S[4 * kSlot4];
-    slot_fill(hdr + c * kBinHdrWords, fat, sc, b, U, ne, S);
+    slot_fill(hdr + c * kBinHdrWords, fat, u, b, U, ne, subs, S);
+    if ((__float_as_uint(S[16]) & 0xFFFFFFu) == 0xFFFFFFu) atomicOr(bad, 1u);
     float4 *o = slots + i * kSlot4;
     for (int k = 0; k < kSlot4; ++k) o[k] = make_float4(S[4 * k], S[4 * k + 1], S[4 * k + 2], S[4 * k + 3]);
   }
 }
 
-int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells, size_t maxBytes, hipStream_t s,
-                       SlotTable &out) {
+int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells, size_t maxBytes, int subs,
+                       size_t autoBytes, hipStream_t s, SlotTable &out) {
   out = SlotTable{};
   if (numCells == 0) return IRT_OK;
   uint32_t e[3];
@@ -644,7 +647,17 @@ int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells
   }
   const int ne = (int)U.size(), bins = ne + 1;
   while ((int)U.size() < kMaxEdges) U.push_back(__builtin_inff());
-  const size_t bytes = (size_t)numCells * kSubCells * kSubCells * bins * kSlot4 * sizeof(float4);
+  // sub-cells per slot unit: as asked, or (0) the finest unit whose table is at most autoBytes
+  auto table_bytes = [&](int u) { return (size_t)numCells * (kSubCells * kSubCells / u) * bins * kSlot4 * sizeof(float4); };
+  if (subs != 1 && subs != 2 && subs != 4) {
+    subs = 4;
+    for (int u : {1, 2})
+      if (table_bytes(u) <= autoBytes && table_bytes(u) <= maxBytes) {
+        subs = u;
+        break;
+      }
+  }
+  const size_t bytes = table_bytes(subs);
   if (bytes > maxBytes) {
     out.skipped = "the table exceeds its memory cap (IRT_SLOTS_MAX_GB; default half the device's memory, and its free memory less 16 GiB)";
     return IRT_OK;
@@ -656,14 +669,25 @@ int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells
     return IRT_OK;
   }
   hipLaunchKernelGGL(k_slot_fill, dim3(std::min<uint64_t>(grid_for(bytes / (kSlot4 * sizeof(float4))), 1u << 20)),
-                     dim3(256), 0, s, hdr, reinterpret_cast<const float *>(fat), numCells, U[0], U[1], U[2], ne, slots);
+                     dim3(256), 0, s, hdr, reinterpret_cast<const float *>(fat), numCells, U[0], U[1], U[2], ne, subs,
+                     slots, set + kSlotSet);
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
     (void)hipFree(slots);
     set_error("slot table build failed");
     return IRT_E_HIP;
   }
+  if ((rc = read_back(h, set, kSlotSet + 1, s))) {
+    (void)hipFree(slots);
+    return rc;
+  }
+  if (h[kSlotSet]) {  // (never at any scene size this library has seen)
+    (void)hipFree(slots);
+    out.skipped = "a radial bin's list exceeds the slot's 24-bit count";
+    return IRT_OK;
+  }
   out.slots = slots;
   out.bins = bins;
+  out.subs = subs;
   out.bytes = bytes;
   for (int k = 0; k < kMaxEdges; ++k) out.edges[k] = U[k];
   return IRT_OK;

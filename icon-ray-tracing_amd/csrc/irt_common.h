@@ -417,22 +417,45 @@ constexpr int kFatStride4 = 4;
 // Slot table (round 5): for scenes whose cube-map cells' radial edges, all together, are at most
 // kMaxEdges distinct values U0 < U1 < U2 (every column with the same levels, as in C3/C4/C5;
 // cells with fewer entries may have fewer of them), the bin of a sample in the table's terms
-// follows from r alone, and per (cell, sub-cell, table bin) one 128-B line holds what the
+// follows from r alone, and per (cell, slot unit, table bin) one 128-B line holds what the
 // cell's header and the list's first candidate give a sample there, so that a located
-// sample's scan starts with one gather instead of two dependent ones (header, then entry):
-//   [0..3]  the first candidate the sub-cell mask admits in the cell's own bin k that holds the
-//           table bin (U_{b-1}, U_b] (its fat entry; zero when none)
-//   [4]     {admitted candidates c, bin k's list start (base + bin begin), bin k's 8-bit sub-cell
-//           mask (masked to the list's length), U_b if it is also the cell's edge e_k (a sample
-//           exactly there scans bin k + 1 too), else +inf}
+// sample's scan usually starts with one gather instead of two dependent ones (header, then entry).
+// A slot unit is `subs` sub-cells of the cell: 1 (round 5: 129 GB at C5), 2 (the pairs s, s + 1 of a
+// sub-cell row) or 4 (the 2 x 2 quads of quad_of; the default since round 6: 32 GB at C5):
+//   [0..3]  the first candidate the unit's sub-cells admit, together, in the cell's own bin k
+//           that holds the table bin (U_{b-1}, U_b] (its fat entry; zero when none)
+//   [4]     {the bin's unmasked candidates (list length less kMaskCand, at least 0) | that first
+//           candidate's list position j_U << 24, bin k's list start (base + bin begin), the unit's
+//           sub-cells' 8-bit masks (masked to the list's length; sub-cell i of the unit in bits
+//           8i..8i+7, slot_sub), U_b if it is also the cell's edge e_k (a sample exactly there
+//           scans bin k + 1 too), else +inf}
 //   [5..7]  0
-// Slot (cell, s, b) sits at ((cell * kSubCells^2 + s) * bins + b) * kSlot4.  The rest of the
+// A sample in sub-cell i of the unit admits c = popc(m8_i) + unmasked candidates, the first at
+// list position j = ctz(m8_i) (kMaskCand when m8_i = 0): when j == j_U the slot's copy is that
+// candidate, otherwise the scan gathers it from the list (one line, as from the header).
+// Slot (cell, u, b) sits at ((cell * kSubCells^2 / subs + u) * bins + b) * kSlot4.  The rest of the
 // scan (the dealt-out candidates, the second pass on a bin edge) reads the header and the
 // lists as before.
 constexpr int kSlot4 = 8;
-// Fills slot (s, b) of a cell from its header H (kBinHdrWords) and the fat entries; U: the
-// table's ne edges (ascending).
-IRT_HD void slot_fill(const uint32_t *H, const float *fat, int s, int b, const float *U, int ne, float *S) {
+constexpr uint32_t kSlotNoFirst = 15u;  // j_U when no sub-cell of the unit admits a candidate
+// sub-cell s = sj * kSubCells + si -> its slot unit and its index within the unit
+IRT_HD uint32_t slot_unit(uint32_t s, int subs) {
+  return subs == 4 ? (uint32_t)quad_of(s) : (subs == 2 ? s >> 1 : s);
+}
+IRT_HD uint32_t slot_sub(uint32_t s, int subs) {
+  return subs == 4 ? (((s / kSubCells) & 1u) << 1) | (s & 1u) : (subs == 2 ? s & 1u : 0u);
+}
+// sub-cell i of unit u
+IRT_HD uint32_t slot_member(uint32_t u, uint32_t i, int subs) {
+  if (subs == 4) {
+    const uint32_t qe = (uint32_t)kSubCells / 2;
+    return (2u * (u / qe) + (i >> 1)) * (uint32_t)kSubCells + 2u * (u % qe) + (i & 1u);
+  }
+  return subs == 2 ? 2u * u + i : u;
+}
+// Fills slot (u, b) of a cell from its header H (kBinHdrWords) and the fat entries; U: the
+// table's ne edges (ascending); subs: sub-cells per unit.
+IRT_HD void slot_fill(const uint32_t *H, const float *fat, int u, int b, const float *U, int ne, int subs, float *S) {
   for (int k = 0; k < 4 * kSlot4; ++k) S[k] = 0.f;
   // the cell's bin holding (U_{b-1}, U_b]: its edges <= U_{b-1} (each is one of the U)
   int k = 0;
@@ -441,15 +464,23 @@ IRT_HD void slot_fill(const uint32_t *H, const float *fat, int s, int b, const f
   const float up = b < ne ? U[b] : __builtin_inff();
   const bool own = b < ne && k < kMaxEdges && u2f(H[k]) == up;
   const uint32_t beg = k ? H[4 + k - 1] : 0u, end = H[4 + k], n = end - beg;
-  const uint32_t m8 = (H[8 + s] >> (8 * k)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
-  const uint32_t c = (uint32_t)__builtin_popcount(m8) + (n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u);
-  if (c) {
-    const uint32_t first = H[3] + beg + (m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand);
+  uint32_t mu = 0u, masks = 0u;
+  for (int i = 0; i < subs; ++i) {
+    const uint32_t s = slot_member((uint32_t)u, (uint32_t)i, subs);
+    const uint32_t m8 = (H[8 + s] >> (8 * k)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
+    mu |= m8;
+    masks |= m8 << (8 * i);
+  }
+  const uint32_t nx = n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u;
+  uint32_t jU = kSlotNoFirst;
+  if (mu || nx) {
+    jU = mu ? (uint32_t)__builtin_ctz(mu) : (uint32_t)kMaskCand;
+    const uint32_t first = H[3] + beg + jU;
     for (int q = 0; q < 4 * kFat4; ++q) S[q] = fat[(size_t)first * 4 * kFatStride4 + q];
   }
-  S[16] = u2f(c);
+  S[16] = u2f(nx | (jU << 24));
   S[17] = u2f(H[3] + beg);
-  S[18] = u2f(m8);
+  S[18] = u2f(masks);
   S[19] = own ? up : __builtin_inff();
 }
 // Per-record height/value blocks (the render record without its planes/keys), kBlk4

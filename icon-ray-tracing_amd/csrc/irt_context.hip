@@ -655,6 +655,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.blocks = c->d_blocks;
   A.slots = c->slot.slots;
   A.slotBins = c->slot.bins;
+  A.slotSubs = c->slot.subs;
   for (int k = 0; k < 3; ++k) A.slotEdge[k] = c->slot.edges[k];
   A.numSph = c->numSph;
   A.sphR = c->d_sphR;
@@ -1129,6 +1130,11 @@ int irt_create_end(irt_context *c) {
     const size_t hdrBytes = (size_t)6 * c->G * c->G * kBinHdrWords * 4;
     // the kernel's slot index (cell * kSubCells^2 + sub) is 32-bit
     const bool indexable = (uint64_t)6 * c->G * c->G * kSubCells * kSubCells < ((uint64_t)1 << 32);
+    // sub-cells per slot unit (irt_common.h slot_unit): by default the finest unit -- 1 sub-cell,
+    // a pair or a quad -- whose table is at most the scene's own bytes (C5: quads, 32 GB for a
+    // 39-GB scene); IRT_SLOT_SUBS=1, 2 or 4 asks for one
+    int slotSubs = 0;
+    if (const char *v = getenv("IRT_SLOT_SUBS")) slotSubs = atoi(v);
     if (e ? forced : hdrBytes > kSlotAutoHdrBytes) {
       size_t fr = 0, tot = 0;
       IRT_HIP(hipMemGetInfo(&fr, &tot));
@@ -1139,13 +1145,13 @@ int irt_create_end(irt_context *c) {
         c->slot = SlotTable{};
         c->slot.skipped = "the cube map has 2^28 cells or more (32-bit slot index)";
       } else if ((rc = build_slots_device(reinterpret_cast<const uint32_t *>(c->d_binHdr), c->d_fat,
-                                          6u * c->G * c->G, cap, c->stream, c->slot))) {
+                                          6u * c->G * c->G, cap, slotSubs, c->bytes, c->stream, c->slot))) {
         return rc;
       }
       c->bytes += c->slot.bytes;
       if (c->slot.bytes)
-        fprintf(stderr, "icon_rt_hip: slot table built on device %d: %.1f GB of HBM (IRT_SLOTS=0: none)\n", c->device,
-                c->slot.bytes / 1e9);
+        fprintf(stderr, "icon_rt_hip: slot table built on device %d: %.1f GB of HBM, %d sub-cells per slot (IRT_SLOTS=0: none)\n",
+                c->device, c->slot.bytes / 1e9, c->slot.subs);
       else if (forced)
         fprintf(stderr, "icon_rt_hip: IRT_SLOTS=1 but no slot table was built: %s\n",
                 c->slot.skipped ? c->slot.skipped : "unknown reason");
@@ -1860,6 +1866,7 @@ static int debug_locate(irt_context *c, const float *xyz, int n, int *found, flo
   A.blocks = c->d_blocks;
   A.slots = c->slot.slots;
   A.slotBins = c->slot.bins;
+  A.slotSubs = c->slot.subs;
   for (int k = 0; k < 3; ++k) A.slotEdge[k] = c->slot.edges[k];
   A.numSph = c->numSph;
   A.sphR = c->d_sphR;

@@ -130,11 +130,13 @@ struct RenderArgs {
   uint32_t numSplit;
   // the slot table (irt_common.h kSlot4; null: none -- the cells' radial edges are more than
   // three values in all, the headers fit the last-level cache, or IRT_SLOTS=0): slotEdge = the
-  // table's edges (+inf past slotBins - 1), slotBins = table bins per sub-cell.
+  // table's edges (+inf past slotBins - 1), slotBins = table bins per slot unit, slotSubs =
+  // sub-cells per slot unit (1, 2 or 4).
   // Launches with a table run the default kernels' OPT_SLOT form (kernel_for).
   const float4 *slots;
   float slotEdge[3];
   int slotBins;
+  int slotSubs;
 };
 // a persistent launch's queue words (irt_render.hip queue_take): 8 per-XCD counters and the
 // done count, each on its own 128-B line
@@ -226,15 +228,21 @@ int build_scene_device(const irt_icon_cell *d_cells, const float4 *d_trig, size_
 struct SlotTable {
   float4 *slots = nullptr;
   int bins = 0;
+  int subs = 0;  // sub-cells per slot unit (irt_common.h slot_unit; IRT_SLOT_SUBS=1|2|4)
   float edges[3] = {0.f, 0.f, 0.f};
   size_t bytes = 0;
   const char *skipped = nullptr;  // why no table was built (nullptr: built, or not asked for)
 };
 // Round 5: with the table C5 -9 %, C3s -3 %, but C3 +4 %, C4 +3 % (profiles/r05aa/): on by
-// default only when the headers exceed the 256-MB last-level cache (C5: 2.7 GB; C3: 167 MB)
+// default only when the headers exceed the 256-MB last-level cache (C5: 2.7 GB; C3: 167 MB).
+// Round 6: slot units of 2 or 4 sub-cells (a half or a quarter of the table): C5 -7.6 % / -6.0 %
+// against no table, one sub-cell -7.5 to -9 % (profiles/r06x/); the default unit keeps the
+// table within the scene's own bytes (C5: quads, 32 GB)
 constexpr size_t kSlotAutoHdrBytes = (size_t)256 << 20;
-int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells, size_t maxBytes, hipStream_t s,
-                       SlotTable &out);
+// subs: sub-cells per slot unit (irt_common.h slot_unit), 1, 2 or 4; any other value: the finest
+// unit whose table is at most autoBytes (and maxBytes), else 4
+int build_slots_device(const uint32_t *hdr, const float4 *fat, uint32_t numCells, size_t maxBytes, int subs,
+                       size_t autoBytes, hipStream_t s, SlotTable &out);
 void launch_unpack(const uint32_t *gathered, int numRanks, int maxTiles, int W, int H,
                    uint32_t *fb, hipStream_t s, const int32_t *table = nullptr);
 

@@ -732,6 +732,7 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
     constexpr bool kHoleSkip = kMiss && !kSlot && (OPT & (OPT_HDRLDS | OPT_NOHOLESKIP)) == 0;
     static_assert(!kSlot || (OPT & (OPT_HDRLDS | OPT_PAIR | OPT_DEALALL | OPT_NEXTHDR)) == 0, "slot table: the default scan");
     float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, sm = s0;  // OPT_SLOT: the first candidate
+    bool slotCopy = false;  // OPT_SLOT: the slot's copy is this sample's first admitted candidate
     if constexpr ((OPT & OPT_HDRLDS) != 0) {
       if (want) cell = cubemap_cell_fast(px, py, pz, (*Ap).G, sub);
       stage_headers(want, cell, sub, H0, H1, M);
@@ -742,16 +743,24 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
       cell = cubemap_cell_fast(px, py, pz, (*Ap).G, sub);
       const float e0 = (*Ap).slotEdge[0], e1 = (*Ap).slotEdge[1], e2 = (*Ap).slotEdge[2];
       const int b = bin_of(r, e0, e1, e2);
-      const float4 *S = (*Ap).slots + ((size_t)(cell * (uint32_t)(kSubCells * kSubCells) + sub) * (uint32_t)(*Ap).slotBins + (uint32_t)b) * kSlot4;
+      const int subs = (*Ap).slotSubs;
+      const uint32_t unit = slot_unit(sub, subs);
+      const float4 *S = (*Ap).slots + ((size_t)(cell * ((uint32_t)(kSubCells * kSubCells) >> (subs >> 1)) + unit) * (uint32_t)(*Ap).slotBins + (uint32_t)b) * kSlot4;
       s0 = S[0];
       s1 = S[1];
       s2 = S[2];
       sm = S[3];
       const uint4 info = reinterpret_cast<const uint4 *>(S)[4];
       edge = r == __uint_as_float(info.w);  // the cell's own bin edge (+inf: none)
-      c = info.x;
+      // this sub-cell's mask and first admitted candidate; the slot's copy is that candidate when
+      // its list position is the unit's first (j_U), otherwise it is gathered from the list
+      const uint32_t m8 = (info.z >> (8 * slot_sub(sub, subs))) & 0xFFu;
+      const uint32_t j = m8 ? (uint32_t)__builtin_ctz(m8) : (uint32_t)kMaskCand;
+      c = (uint32_t)__popc(m8) + (info.x & 0xFFFFFFu);
+      slotCopy = j == (info.x >> 24);
+      fe = info.y + j;
       lds_st16(&W.pt[lane], make_float4(px, py, pz, r));
-      lds_st16(&W.lst[lane], make_uint4(info.y, info.z, 0u, 0xFFFFFFFFu));
+      lds_st16(&W.lst[lane], make_uint4(info.y, m8, 0u, 0xFFFFFFFFu));
       fr = r;
     } else if (want) {
       const float r = sqrtf(dot3(px, py, pz, px, py, pz));  // toSpherical(pos).x
@@ -838,7 +847,12 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
         } else {
           ok = pass_entry((*Ap).fat + (size_t)fe * kFatStride4, px, py, pz, fr, f);
         }
-        if (f.rec < flim) {  // scan_fat stops, uncounted, at the first record >= the limit
+        if (kSlot && pass == 0 && !slotCopy) {
+          // the unit's first candidate is not one this sub-cell admits (a slot unit of several
+          // sub-cells): it cannot hold the sample, and the sample's own candidates, its first
+          // included, go to the dealt-out step -- no gather of its own on the round's chain
+          rem = c;
+        } else if (f.rec < flim) {  // scan_fat stops, uncounted, at the first record >= the limit
           ++specCand;
           if (ok) {
             hit = true;

@@ -152,10 +152,24 @@ _POP = np.array([bin(k).count("1") for k in range(256)], np.uint32)
 _CTZ = np.array([8] + [(k & -k).bit_length() - 1 for k in range(1, 256)], np.uint32)
 
 
-def restate_slots(hdr: np.ndarray, fat: np.ndarray) -> np.ndarray:
-    """irt_common.h slot_fill over every (cell, sub-cell, table bin), from the scene's header
-    and fat-entry bytes (kBinHdrWords = 32 with 4 x 4 sub-cells, 16 words per entry); None when
-    the cells' edges are more than three distinct values."""
+def slot_member(u, i, subs):
+    """irt_common.h slot_member: sub-cell i of slot unit u (4 x 4 sub-cells)."""
+    if subs == 4:
+        return (2 * (u // 2) + (i >> 1)) * 4 + 2 * (u % 2) + (i & 1)
+    return 2 * u + i if subs == 2 else u
+
+
+def slot_unit_sub(s, subs):
+    """irt_common.h slot_unit, slot_sub: sub-cell s's unit and its index in the unit."""
+    if subs == 4:
+        return (s // 8) * 2 + (s % 4) // 2, (((s // 4) & 1) << 1) | (s & 1)
+    return (s >> 1, s & 1) if subs == 2 else (s, 0)
+
+
+def restate_slots(hdr: np.ndarray, fat: np.ndarray, subs: int = 4) -> np.ndarray:
+    """irt_common.h slot_fill over every (cell, slot unit of `subs` sub-cells, table bin), from
+    the scene's header and fat-entry bytes (kBinHdrWords = 32 with 4 x 4 sub-cells, 16 words per
+    entry); None when the cells' edges are more than three distinct values."""
     INF = 0x7F800000
     H = hdr.view(np.uint32).reshape(-1, 32).astype(np.int64)
     F = fat.view(np.uint32).reshape(-1, 16)
@@ -163,9 +177,9 @@ def restate_slots(hdr: np.ndarray, fat: np.ndarray) -> np.ndarray:
     U = np.unique(E[E != INF].astype(np.uint32).view(np.float32))
     if U.size > 3:
         return None
-    ne, nb, nsub = U.size, U.size + 1, 16
+    ne, nb, units = U.size, U.size + 1, 16 // subs
     Ef = E.astype(np.uint32).view(np.float32)
-    out = np.zeros((H.shape[0], nsub, nb, 32), np.uint32)
+    out = np.zeros((H.shape[0], units, nb, 32), np.uint32)
     rows = np.arange(H.shape[0])
     for b in range(nb):
         k = (Ef <= U[b - 1]).sum(1) if b else np.zeros(H.shape[0], np.int64)
@@ -174,14 +188,20 @@ def restate_slots(hdr: np.ndarray, fat: np.ndarray) -> np.ndarray:
         beg = np.where(k > 0, H[rows, 3 + k], 0)  # word 4 + k - 1
         n = H[rows, 4 + k] - beg
         lenmask = np.where(n < 8, (1 << np.clip(n, 0, 8)) - 1, 0xFF)
-        for s in range(nsub):
-            m8 = (H[:, 8 + s] >> (8 * k)) & 0xFF & lenmask
-            c = _POP[m8].astype(np.int64) + np.where(n > 8, n - 8, 0)
-            first = H[:, 3] + beg + _CTZ[m8]
-            has = c > 0
-            out[has, s, b, :16] = F[first[has]]
-            out[:, s, b, 16] = c
-            out[:, s, b, 17] = H[:, 3] + beg
-            out[:, s, b, 18] = m8
-            out[:, s, b, 19] = np.where(own, np.float32(up).view(np.uint32), INF)
+        nx = np.where(n > 8, n - 8, 0)
+        for u in range(units):
+            mu = np.zeros(H.shape[0], np.int64)
+            masks = np.zeros(H.shape[0], np.int64)
+            for i in range(subs):
+                m8 = (H[:, 8 + slot_member(u, i, subs)] >> (8 * k)) & 0xFF & lenmask
+                mu |= m8
+                masks |= m8 << (8 * i)
+            has = (mu > 0) | (nx > 0)
+            jU = np.where(has, _CTZ[mu], 15)
+            first = H[:, 3] + beg + jU
+            out[has, u, b, :16] = F[first[has]]
+            out[:, u, b, 16] = nx | (jU << 24)
+            out[:, u, b, 17] = H[:, 3] + beg
+            out[:, u, b, 18] = masks
+            out[:, u, b, 19] = np.where(own, np.float32(up).view(np.uint32), INF)
     return out.reshape(-1)

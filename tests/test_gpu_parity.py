@@ -795,11 +795,14 @@ def test_device_locator_matches_host_restatement(scene, entry):
     _locator_check(scene, entry)
 
 
+@pytest.mark.parametrize("subs", [4, 1])
 @pytest.mark.parametrize("scene", ["r2b03_l90", "filtered"])
-def test_device_locator_slot_table(monkeypatch, scene):
+def test_device_locator_slot_table(monkeypatch, scene, subs):
     """The same points through the wave-wide scan started from the slot table (OPT_SLOT,
-    irt_common.h kSlot4; forced on these small scenes with IRT_SLOTS=1)."""
+    irt_common.h kSlot4; forced on these small scenes with IRT_SLOTS=1), with quads (the
+    default) and one sub-cell per slot unit."""
     monkeypatch.setenv("IRT_SLOTS", "1")
+    monkeypatch.setenv("IRT_SLOT_SUBS", str(subs))
     _locator_check(scene, "irt_debug_locate_wave", slots=True)
 
 

@@ -1,7 +1,8 @@
 """The slot table (irt_common.h kSlot4, csrc/irt_build.hip k_slot_fill; Tracer::locate_wave's
-OPT_SLOT form): per (cube-map cell, sub-cell, radial bin) of a scene whose cells share their
-radial edges, the first candidate the sub-cell mask admits and the list's position, so that a
-sample's scan starts with one gather.
+OPT_SLOT form): per (cube-map cell, slot unit of 4 sub-cells -- 2 or 1 with IRT_SLOT_SUBS --,
+radial bin) of a scene whose cells share their radial edges, the first candidate the unit's
+sub-cell masks admit, the masks and the list's position, so that a sample's scan starts with one
+gather (the slot's copy, when it is the sample's own first admitted candidate).
 
 Pinned here: the table the device builds equals a numpy restatement from the headers and fat
 entries byte for byte; frames, accumulators and every count equal a context without the table
@@ -19,11 +20,13 @@ from helpers import FRAMING, bits, restate_slots
 
 pytestmark = pytest.mark.gpu
 
+@pytest.mark.parametrize("subs", [4, 2, 1])
 @pytest.mark.parametrize("scene", ["r2b02_l90", "r2b03_l47_noise", "r2b03_l20", "filtered"])
-def test_slot_table_restated(monkeypatch, scene):
+def test_slot_table_restated(monkeypatch, scene, subs):
     """(filtered: cells at the region's border hold fewer records and fewer edges, a subset of
     the others')"""
     monkeypatch.setenv("IRT_SLOTS", "1")
+    monkeypatch.setenv("IRT_SLOT_SUBS", str(subs))
     cells = {"r2b02_l90": lambda: irt.synth_grid(2, 2, 90),
              "r2b03_l47_noise": lambda: irt.synth_grid(2, 3, 47, noise=0.2),
              "r2b03_l20": lambda: irt.synth_grid(2, 3, 20),
@@ -31,7 +34,7 @@ def test_slot_table_restated(monkeypatch, scene):
     ctx = irt.Context(cells, 0)
     slots = ctx.array("slots")
     assert slots.size > 0, "a flat grid's cells share their edges"
-    want = restate_slots(ctx.array("bin_hdr"), ctx.array("fat"))
+    want = restate_slots(ctx.array("bin_hdr"), ctx.array("fat"), subs)
     got = slots.view(np.uint32)
     assert want is not None and got.size == want.size
     if not np.array_equal(got, want):
@@ -78,14 +81,16 @@ def _frames(ctx, lp, W, n, batch):
     return out
 
 
-@pytest.mark.parametrize("bis,levels,batch", [(4, 90, 1), (4, 90, 4), (3, 47, 1)])
-def test_frames_equal_without_table(monkeypatch, bis, levels, batch):
+@pytest.mark.parametrize("bis,levels,batch,subs", [(4, 90, 1, 4), (4, 90, 4, 4), (3, 47, 1, 4), (4, 90, 1, 2),
+                                                   (3, 47, 1, 1)])
+def test_frames_equal_without_table(monkeypatch, bis, levels, batch, subs):
     cells = irt.synth_grid(2, bis, levels, noise=0.1 if levels == 47 else 0.0)
     W = 320
     setup = irt.setup_frame(cells, W, W, camera=FRAMING)
     monkeypatch.setenv("IRT_SLOTS", "0")
     ref_ctx = irt.Context(cells, 0)
     monkeypatch.setenv("IRT_SLOTS", "1")
+    monkeypatch.setenv("IRT_SLOT_SUBS", str(subs))
     ctx = irt.Context(cells, 0)
     assert ctx.array("slots").size > 0 and ref_ctx.array("slots").size == 0
     for c in (ref_ctx, ctx):
