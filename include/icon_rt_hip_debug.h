@@ -156,7 +156,7 @@ int irt_debug_set_wg_trace(irt_context *ctx, uint32_t *trace);
  * items, which come first; rows a launch does not use stay as they were). */
 long long irt_debug_launch_workgroups(const irt_context *ctx, int numTiles, int numFrames);
 /* Measured-cost scheduling (IRT_SCHED; on by default for scenes with holes): the last launch's
- * split WORK ITEMS in *numSplit -- every split packet (one longer than IRT_SPLIT_FACTOR (1) x
+ * split WORK ITEMS in *numSplit -- every split packet (one longer than IRT_SPLIT_FACTOR (0.35 with holes, else 1) x
  * the frame's ideal span, the packets' durations over the resident slots) is rendered first in
  * 2^splitLg parts of 64 >> splitLg rays (IRT_SPLIT_LG, default 2; 0: no splits), one work item
  * per part, and the items are padded with empty ones to a multiple of 8 (so *numSplit is parts x

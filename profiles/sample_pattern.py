@@ -28,7 +28,7 @@ CONFIGS = {"c3": (2, 7, 90, 1024, 0.0), "c3t": (2, 7, 90, 1024, 4000.0),
 FRAMING = ((0.0, 0.0, 1.4e7), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0)
 
 
-def traces(cfg, step, stride=8192):
+def traces(cfg, step, stride=8192, rows=None):
     import irt
     import oracle as O
     rn, bis, L, W, terrain = CONFIGS[cfg]
@@ -39,7 +39,7 @@ def traces(cfg, step, stride=8192):
     cam = S.camera(W, W, FRAMING)
     params = S.params(cam, accum_id=0, raygen=0)
     pk = []
-    for py in range(0, W // 8, step):
+    for py in (range(0, W // 8, step) if rows is None else rows):
         for px in range(0, W // 8, step):
             pk.append((px, py))
     xy = np.array([(8 * px + (l & 7), 8 * py + (l >> 3)) for px, py in pk for l in range(64)],
@@ -97,11 +97,12 @@ def simulate(packets, rule="kernel", voidwalk=True, maxlg0=0, ramp=1):
     voidwalk: a solo lane in miss mode crosses its run of misses in the same round (the kernel
     does so only for misses its quad-bound test certifies; this bounds it from below).
     rule "both": a group's lanes also speculate the other assumption (two half groups)."""
-    per_wave = []
+    per_wave, walks = [], []
     for P in packets:
         calls = [calls_of(s) for s in P]
         idx = [0] * 64
         rounds = 0
+        walk_steps = 0
         while True:
             joined = [i for i in range(64) if idx[i] < len(calls[i])]
             if not joined:
@@ -112,6 +113,7 @@ def simulate(packets, rule="kernel", voidwalk=True, maxlg0=0, ramp=1):
             lg_cap = maxlg0
             while live:
                 rounds += 1
+                walk_round = 0
                 R = len(live)
                 lgR = 0 if R > 32 else 1 if R > 16 else 2 if R > 8 else 3 if R > 4 else 4 if R > 2 else 5 if R > 1 else 6
                 lg = min(lg_cap, lgR)
@@ -132,18 +134,23 @@ def simulate(packets, rule="kernel", voidwalk=True, maxlg0=0, ramp=1):
                             miss[i] = (not mm) if sw else mm
                         continue
                     if voidwalk and G == 1 and miss[i]:
+                        p0 = p
                         while p < len(c) and c[p] == "m":
                             p += 1
+                        walk_round = max(walk_round, p - p0)
                     adv, done, sw = advance(c, p, G, miss[i])
                     pos[i] = p + adv
                     if done:
                         live.discard(i)
                     elif sw:
                         miss[i] = not miss[i]
+                walk_steps += walk_round
                 lg_cap = min(lg_cap + ramp, 6)
             for i in joined:
                 idx[i] += 1
         per_wave.append(rounds)
+        walks.append(walk_steps)
+    simulate.walk_steps = np.array(walks)
     return np.array(per_wave)
 
 
@@ -166,8 +173,19 @@ def main():
     ap.add_argument("--config", default="c3t", choices=sorted(CONFIGS))
     ap.add_argument("--step", type=int, default=4, help="every step-th packet in x and y")
     ap.add_argument("--json")
+    ap.add_argument("--stride", type=int, default=8192, help="trace letters per ray (cut)")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="all packets of every step-th packet row, this many rows per trace call")
     args = ap.parse_args()
-    packets = traces(args.config, args.step)
+    if args.chunks:
+        # every packet row step-th, in chunks of packet rows (bounded memory), then pooled
+        W = CONFIGS[args.config][3]
+        packets = []
+        rows = list(range(0, W // 8, args.step))
+        for i in range(0, len(rows), args.chunks):
+            packets += traces(args.config, 1, stride=args.stride, rows=rows[i:i + args.chunks])
+    else:
+        packets = traces(args.config, args.step, stride=args.stride)
     res = {"config": args.config, "packets": len(packets)}
     res.update(outcome_stats(packets))
     for name, kw in (("kernel", {}), ("kernel_novoid", {"voidwalk": False}), ("both", {"rule": "both"})):
@@ -175,6 +193,9 @@ def main():
         res["rounds_" + name] = {"mean": float(r.mean()), "p50": float(np.median(r)),
                                  "p90": float(np.percentile(r, 90)), "max": int(r.max()),
                                  "sum": int(r.sum())}
+        w = simulate.walk_steps  # the longest solo walk of each round, summed per wave
+        res["walk_steps_" + name] = {"mean": float(w.mean()), "p90": float(np.percentile(w, 90)),
+                                     "max": int(w.max())}
     print(json.dumps(res, indent=1))
     if args.json:
         json.dump(res, open(args.json, "w"), indent=1)
