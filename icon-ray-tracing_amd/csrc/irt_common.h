@@ -422,8 +422,11 @@ constexpr int kFatStride4 = 4;
 // sample's scan usually starts with one gather instead of two dependent ones (header, then entry).
 // A slot unit is `subs` sub-cells of the cell: 1 (round 5: 129 GB at C5), 2 (the pairs s, s + 1 of a
 // sub-cell row) or 4 (the 2 x 2 quads of quad_of; the default since round 6: 32 GB at C5):
-//   [0..3]  the first candidate the unit's sub-cells admit, together, in the cell's own bin k
-//           that holds the table bin (U_{b-1}, U_b] (its fat entry; zero when none)
+//   [0..3]  in the cell's own bin k that holds the table bin (U_{b-1}, U_b], the candidate that
+//           is the first admitted one of the most of the unit's sub-cells, the lowest list
+//           position on a tie (its fat entry; zero when no sub-cell admits one).  Quads: 79 % of
+//           (sub-cell, bin) pairs find their own first candidate there, 72 % with the unit's
+//           lowest admitted one (R2B05)
 //   [4]     {the bin's unmasked candidates (list length less kMaskCand, at least 0) | that first
 //           candidate's list position j_U << 24, bin k's list start (base + bin begin), the unit's
 //           sub-cells' 8-bit masks (masked to the list's length; sub-cell i of the unit in bits
@@ -464,17 +467,28 @@ IRT_HD void slot_fill(const uint32_t *H, const float *fat, int u, int b, const f
   const float up = b < ne ? U[b] : __builtin_inff();
   const bool own = b < ne && k < kMaxEdges && u2f(H[k]) == up;
   const uint32_t beg = k ? H[4 + k - 1] : 0u, end = H[4 + k], n = end - beg;
-  uint32_t mu = 0u, masks = 0u;
+  const uint32_t nx = n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u;
+  // the unit's masks, and the list position that is the first admitted candidate of the most of
+  // its sub-cells (the lowest such position on a tie): the slot's copy
+  uint32_t masks = 0u, firstOf = 0u;  // firstOf: 4 bits per sub-cell, kSlotNoFirst when none
   for (int i = 0; i < subs; ++i) {
     const uint32_t s = slot_member((uint32_t)u, (uint32_t)i, subs);
     const uint32_t m8 = (H[8 + s] >> (8 * k)) & 0xFFu & (n < 8u ? (1u << n) - 1u : 0xFFu);
-    mu |= m8;
     masks |= m8 << (8 * i);
+    const uint32_t j = m8 ? (uint32_t)__builtin_ctz(m8) : (nx ? (uint32_t)kMaskCand : kSlotNoFirst);
+    firstOf |= j << (4 * i);
   }
-  const uint32_t nx = n > (uint32_t)kMaskCand ? n - (uint32_t)kMaskCand : 0u;
   uint32_t jU = kSlotNoFirst;
-  if (mu || nx) {
-    jU = mu ? (uint32_t)__builtin_ctz(mu) : (uint32_t)kMaskCand;
+  int most = 0;
+  for (uint32_t j = 0; j <= (uint32_t)kMaskCand; ++j) {
+    int cnt = 0;
+    for (int i = 0; i < subs; ++i) cnt += ((firstOf >> (4 * i)) & 15u) == j ? 1 : 0;
+    if (cnt > most) {
+      most = cnt;
+      jU = j;
+    }
+  }
+  if (jU != kSlotNoFirst) {
     const uint32_t first = H[3] + beg + jU;
     for (int q = 0; q < 4 * kFat4; ++q) S[q] = fat[(size_t)first * 4 * kFatStride4 + q];
   }

@@ -1142,10 +1142,12 @@ int irt_create_end(irt_context *c) {
     // the kernel's slot index (cell * kSubCells^2 + sub) is 32-bit
     const bool indexable = (uint64_t)6 * c->G * c->G * kSubCells * kSubCells < ((uint64_t)1 << 32);
     // sub-cells per slot unit (irt_common.h slot_unit): by default the finest unit -- 1 sub-cell,
-    // a pair or a quad -- whose table is at most the scene's own bytes (C5: quads, 32 GB for a
-    // 39-GB scene); IRT_SLOT_SUBS=1, 2 or 4 asks for one
+    // a pair or a quad -- whose table is at most the scene's own bytes (C5: quads, 32 GB beside
+    // 38.7 GB of headers, entries and blocks); IRT_SLOT_SUBS=1, 2 or 4 asks for one
     int slotSubs = 0;
     if (const char *v = getenv("IRT_SLOT_SUBS")) slotSubs = atoi(v);
+    // the scene's own bytes: the locator and the records it indexes (headers, entries, blocks)
+    const size_t sceneBytes = hdrBytes + c->binEntries * kFatStride4 * 16 + (size_t)c->n * kBlk4 * 16;
     if (e ? forced : hdrBytes > kSlotAutoHdrBytes) {
       size_t fr = 0, tot = 0;
       IRT_HIP(hipMemGetInfo(&fr, &tot));
@@ -1156,7 +1158,7 @@ int irt_create_end(irt_context *c) {
         c->slot = SlotTable{};
         c->slot.skipped = "the cube map has 2^28 cells or more (32-bit slot index)";
       } else if ((rc = build_slots_device(reinterpret_cast<const uint32_t *>(c->d_binHdr), c->d_fat,
-                                          6u * c->G * c->G, cap, slotSubs, c->bytes, c->stream, c->slot))) {
+                                          6u * c->G * c->G, cap, slotSubs, sceneBytes, c->stream, c->slot))) {
         return rc;
       }
       c->bytes += c->slot.bytes;

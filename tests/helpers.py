@@ -190,14 +190,21 @@ def restate_slots(hdr: np.ndarray, fat: np.ndarray, subs: int = 4) -> np.ndarray
         lenmask = np.where(n < 8, (1 << np.clip(n, 0, 8)) - 1, 0xFF)
         nx = np.where(n > 8, n - 8, 0)
         for u in range(units):
-            mu = np.zeros(H.shape[0], np.int64)
             masks = np.zeros(H.shape[0], np.int64)
+            firsts = []
             for i in range(subs):
                 m8 = (H[:, 8 + slot_member(u, i, subs)] >> (8 * k)) & 0xFF & lenmask
-                mu |= m8
                 masks |= m8 << (8 * i)
-            has = (mu > 0) | (nx > 0)
-            jU = np.where(has, _CTZ[mu], 15)
+                firsts.append(np.where(m8 > 0, _CTZ[m8], np.where(nx > 0, 8, 15)))
+            # the position that is the most sub-cells' first admitted candidate (lowest on a tie)
+            jU = np.full(H.shape[0], 15, np.int64)
+            most = np.zeros(H.shape[0], np.int64)
+            for j in range(9):
+                cnt = sum((f == j).astype(np.int64) for f in firsts)
+                upd = cnt > most
+                jU = np.where(upd, j, jU)
+                most = np.where(upd, cnt, most)
+            has = jU != 15
             first = H[:, 3] + beg + jU
             out[has, u, b, :16] = F[first[has]]
             out[:, u, b, 16] = nx | (jU << 24)

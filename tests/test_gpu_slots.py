@@ -46,15 +46,15 @@ def test_slot_table_restated(monkeypatch, scene, subs):
 @pytest.mark.parametrize("bis", [3, 4])
 def test_default_unit_fits_the_scene(monkeypatch, bis):
     """Without IRT_SLOT_SUBS the context takes the finest slot unit (1, 2, then 4 sub-cells)
-    whose table is at most the scene's own device bytes (quads otherwise): the table equals
-    that unit's restatement."""
+    whose table is at most the scene's own bytes -- its headers, fat entries and blocks -- and
+    quads otherwise: the table equals that unit's restatement."""
     monkeypatch.setenv("IRT_SLOTS", "1")
     monkeypatch.delenv("IRT_SLOT_SUBS", raising=False)
     ctx = irt.Context(irt.synth_grid(2, bis, 90), 0)
     got = ctx.array("slots").view(np.uint32)
     hdr, fat = ctx.array("bin_hdr"), ctx.array("fat")
     tables = {u: restate_slots(hdr, fat, u) for u in (1, 2, 4)}
-    scene = ctx.info.deviceBytes - got.nbytes
+    scene = sum(ctx.array_bytes(a) for a in ("bin_hdr", "fat", "blocks"))
     sizes = {u: t.nbytes for u, t in tables.items()}
     if any(abs(sizes[u] - scene) < 0.05 * scene for u in (1, 2)):
         pytest.skip("a unit's table is within 5 % of the scene's bytes")
