@@ -2757,7 +2757,7 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 // (libicon_rt_hip_all.so, loaded through IRT_LIB_PATH by the profiles/ tools and by
 // tests/test_gpu_parity.py::test_all_render_variants_identical when present).
 #ifdef IRT_ALL_VARIANTS
-#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73405728) X(73667872) X(73405760) X(73667904) X(73405712) X(73667856) X(73930016) X(74192160) X(73405732) X(73405730) X(73405729) X(73667873) X(73405744) X(73667888) X(1147147552) X(107222304) X(106960160)
+#define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73405728) X(73667872) X(73405760) X(73667904) X(73405712) X(73667856) X(73930016) X(74192160) X(73405732) X(73405730) X(73405729) X(73667873) X(73405744) X(73667888) X(1147147552) X(107222304) X(106960160) X(73438496) X(73700640)
 #else
 #define IRT_VARIANTS(X) X(73405728) X(73667872) X(5376) X(36864)
 #endif

@@ -677,6 +677,7 @@ struct ThreadStats {
   // analysis only (oracle_trace_pixels): one letter per counted sampleVolume call -- 'm' outside
   // every cell, 'l' located and rejected, 'A' accepted -- 'E' for a call ending past its tmax
   std::string *trace = nullptr;
+  std::vector<float> *missPos = nullptr;  // (analysis) each 'm' sample's point, xyz
 };
 
 // sampleVolume, CPU branch: first cell index wins (deviceCode.cu:116-123)
@@ -852,6 +853,7 @@ inline float woodcockTracking(const Scene &S, const oc_params &p, const Ray &ray
     ++ts.locate;
     if (!sampleVolume(S, P, value)) {
       if (ts.trace) ts.trace->push_back('m');
+      if (ts.missPos) ts.missPos->insert(ts.missPos->end(), {P.x, P.y, P.z});
       continue;
     }
     ++ts.found;
@@ -1399,6 +1401,40 @@ int oracle_trace_pixels(const oc_cell *cells, size_t n, const oc_params *p, int 
   worker();
   for (auto &t : threads) t.join();
   return 0;
+}
+
+// Analysis only: the points of the counted samples outside every cell of the listed pixels'
+// rays (xyz floats into out, at most cap points); returns the number of points (all of them,
+// even past cap), -1 on bad arguments.
+long oracle_trace_misses(const oc_cell *cells, size_t n, const oc_params *p, int W, int H,
+                         const int32_t *xy, int numPixels, float *out, long cap, int nthreads) {
+  if (!p || W <= 0 || H <= 0 || numPixels < 0) return -1;
+  Scene S{cells, n, 2, {}, {}, {}, false, {}, {}, false};
+  prepare(S, p, nthreads);
+  std::atomic<int> counter{0};
+  if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
+  if (nthreads <= 0) nthreads = 1;
+  std::vector<float> acc(4 * (size_t)W * H);
+  std::vector<uint32_t> fb((size_t)W * H);
+  std::vector<std::vector<float>> pts(nthreads);
+  auto worker = [&](int tid) {
+    ThreadStats ts;
+    ts.missPos = &pts[tid];
+    for (;;) {
+      int i = counter.fetch_add(1);
+      if (i >= numPixels) break;
+      raygen(S, *p, xy[2 * i], xy[2 * i + 1], W, H, acc.data(), fb.data(), ts);
+    }
+  };
+  std::vector<std::thread> threads;
+  for (int t = 1; t < nthreads; ++t) threads.emplace_back(worker, t);
+  worker(0);
+  for (auto &t : threads) t.join();
+  long k = 0;
+  for (auto &v : pts)
+    for (size_t j = 0; j + 2 < v.size(); j += 3, ++k)
+      if (k < cap) memcpy(out + 3 * k, &v[j], 3 * sizeof(float));
+  return k;
 }
 
 // ------------------------------------------------------------------ KATs

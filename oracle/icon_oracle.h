@@ -144,6 +144,9 @@ int oracle_render_pixels(const oc_cell *cells, size_t n, const oc_params *p, int
  * out + i * stride (profiles/sample_pattern.py). */
 int oracle_trace_pixels(const oc_cell *cells, size_t n, const oc_params *p, int W, int H,
                         const int32_t *xy, int numPixels, char *out, int stride, int nthreads);
+/* Analysis only: the points (xyz) of the traced rays' samples outside every cell. */
+long oracle_trace_misses(const oc_cell *cells, size_t n, const oc_params *p, int W, int H,
+                         const int32_t *xy, int numPixels, float *out, long cap, int nthreads);
 
 /* ---- known-answer helpers (single functions) ---- */
 void oracle_lcg(uint32_t seed0, uint32_t seed1, int n, float *out);            /* dvr_course-common-both.h:41-86 */
