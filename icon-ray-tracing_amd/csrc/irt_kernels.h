@@ -169,7 +169,12 @@ constexpr int kNoMissBit = 262144;
 // measured-cost scheduling (irt_context.hip sched_prepare): at most this many work items run first
 // in a single frame (RenderArgs::splitList), a multiple of 8
 constexpr uint32_t kMaxSplit = 4096;
-inline int scene_variant(bool holes) { return holes ? kDefaultVariant : kDefaultVariant | kNoMissBit; }
+// Round 6: a scene with holes also walks a certain miss in located mode (bit 1073741824,
+// OPT_VOIDLOC: a solo lane whose sample is outside its quad's records switches its ray to the miss
+// mode in the same round and walks on): C3t 8 chained frames -1.7 %, one per launch even
+// (profiles/r06zg/)
+constexpr int kVoidLocBit = 1073741824;
+inline int scene_variant(bool holes) { return holes ? kDefaultVariant | kVoidLocBit : kDefaultVariant | kNoMissBit; }
 bool render_variant_available(int variant);
 int render_variants(int *out, int cap);  // the compiled variants (count; the first cap into out)
 // workgroups per 256-pixel block the launch of `variant` uses for these arguments (4 only for

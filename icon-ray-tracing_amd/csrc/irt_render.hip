@@ -81,9 +81,10 @@ enum : int {
   OPT_PAIR = 268435456,  // (A/B) the wave-wide scan's first step tests each lane's first two
                          // candidates (both entries gathered together), so the dealt-out step
                          // runs only for lanes whose first two fail
-  OPT_VOIDLOC = 1073741824,  // (A/B) the solo lanes' void walk also in located mode: a certain miss
-                             // at the round's sample switches the ray to miss mode there, not a
-                             // round later (profiles/r06h/: C3t chained -1 %, single frames even)
+  OPT_VOIDLOC = 1073741824,  // the solo lanes' void walk also in located mode: a certain miss at
+                             // the round's sample switches the ray to miss mode there, not a round
+                             // later; scenes with holes run it since round 6 (scene_variant:
+                             // profiles/r06zg/ C3t chained -1.7 %, single frames even)
   OPT_FPAIR = 1,  // (A/B) chained launches: a wave renders its packet for two consecutive frames,
                   // one after the other (k_render: workgroup (b, y) frames 2y and 2y + 1): the second
                   // frame's hand-off is the wave's own.  (Until profiles/r06f this bit was OPT_CHAINPF,
@@ -2759,10 +2760,11 @@ static_assert((kDefaultVariant & OPT_MONO) != 0, "variant numbering");
 #ifdef IRT_ALL_VARIANTS
 #define IRT_VARIANTS(X) X(4096) X(5120) X(5376) X(36864) X(70656) X(136192) X(529408) X(1053696) X(2102272) X(2102528) X(8393728) X(8393984) X(6296576) X(6296832) X(529664) X(2102784) X(33559808) X(134223104) X(268440832) X(39851264) X(538973440) X(6297088) X(6558976) X(73405696) X(73667840) X(73405728) X(73667872) X(73405760) X(73667904) X(73405712) X(73667856) X(73930016) X(74192160) X(73405732) X(73405730) X(73405729) X(73667873) X(73405744) X(73667888) X(1147147552) X(107222304) X(106960160) X(73438496) X(73700640)
 #else
-#define IRT_VARIANTS(X) X(73405728) X(73667872) X(5376) X(36864)
+#define IRT_VARIANTS(X) X(73405728) X(73667872) X(1147147552) X(5376) X(36864)
 #endif
-static_assert(kDefaultVariant == 73405728 && (kDefaultVariant | kNoMissBit) == 73667872 && kNoMissBit == OPT_NOMISS,
-              "the product build's variant list names the default and its hole-free form");
+static_assert(kDefaultVariant == 73405728 && (kDefaultVariant | kNoMissBit) == 73667872 && kNoMissBit == OPT_NOMISS &&
+                  (kDefaultVariant | kVoidLocBit) == 1147147552 && kVoidLocBit == OPT_VOIDLOC,
+              "the product build's variant list names the default and its scene forms (scene_variant)");
 
 int render_variants(int *out, int cap) {
   int n = 0;

@@ -377,12 +377,14 @@ def test_convert_icon_terrain_bit_exact_with_and_without_miss_mode(levels):
     L.irt_debug_set_variant.argtypes = [C.c_void_p, C.c_int]
     L.irt_debug_get_variant.argtypes = [C.c_void_p]
     d = L.irt_debug_default_variant()
+    VOIDLOC = 1073741824
     if os.environ.get("IRT_RENDER_VARIANT"):  # a forced variant (A/B runs of the suite)
-        d = int(os.environ["IRT_RENDER_VARIANT"]) & ~262144
-    assert L.irt_debug_get_variant(ctx._h) in (d, d | 262144)  # holes: the miss mode, unless forced
+        d = int(os.environ["IRT_RENDER_VARIANT"]) & ~(262144 | VOIDLOC)
+    # holes: the miss mode with the located-mode void walk (scene_variant), unless forced
+    assert L.irt_debug_get_variant(ctx._h) in (d, d | 262144, d | VOIDLOC)
     if not os.environ.get("IRT_RENDER_VARIANT"):
-        assert L.irt_debug_get_variant(ctx._h) == d
-    for v in (d, d | 262144):
+        assert L.irt_debug_get_variant(ctx._h) == d | VOIDLOC
+    for v in (d | VOIDLOC, d, d | 262144):
         assert L.irt_debug_set_variant(ctx._h, v) == 0
         fr = GpuFrame(ctx, W, W)
         st = fr.render(setup.lp)

@@ -99,9 +99,9 @@ def test_every_scene_runs_the_default_variant(scene):
         assert (scene["ctx"].array_bytes("slots") > 0) == (scene["name"] == "c5"), scene["name"]
     if os.environ.get("IRT_RENDER_VARIANT"):
         return
-    # the hole-free form (no miss mode) on flat grids; the default itself over terrain, whose
-    # land columns start at R + HSURF (voids below them: runs of misses)
-    assert v == (d if SCALE[scene["name"]][5] else d | 262144), (scene["name"], v, d)
+    # the hole-free form (no miss mode) on flat grids; over terrain, whose land columns start at
+    # R + HSURF (voids below them: runs of misses), the default with the located-mode void walk
+    assert v == (d | 1073741824 if SCALE[scene["name"]][5] else d | 262144), (scene["name"], v, d)
 
 
 def test_whole_frame_matches_oracle(scene):
