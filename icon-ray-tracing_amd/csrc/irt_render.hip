@@ -366,7 +366,10 @@ struct Tracer : std::conditional_t<(OPT & OPT_TIMING) != 0, TimeAccOn, TimeAccOf
   // the void walk of woodcock_wave's solo miss-mode lanes (the user-geometry sampler from headers)
   static constexpr bool kVoidRun =
       kMiss && (OPT & (OPT_WEDGE | OPT_GRID | OPT_SCAN1 | OPT_SLOT | OPT_HDRLDS | OPT_NOHOLESKIP | OPT_NOVOIDRUN)) == 0;
-  static constexpr int kVoidRunMax = 32;  // samples one lane walks before the round goes on
+#ifndef IRT_VOID_RUN_MAX
+#define IRT_VOID_RUN_MAX 32  // (A/B builds may set it)
+#endif
+  static constexpr int kVoidRunMax = IRT_VOID_RUN_MAX;  // samples one lane walks before the round goes on
   static constexpr bool kWideStart = (OPT & (OPT_WEDGE | OPT_GRID)) != 0;
 
   // one wave-aggregated LDS add per event site
