@@ -47,6 +47,19 @@ def test_bench_gpus2_spawns_two_ranks(mode):
     assert len([l for l in r.stdout.splitlines() if l.strip()]) == 1
 
 
+@pytest.mark.parametrize("n", [4, 8])
+def test_bench_more_ranks_progressive(n):
+    """The driver's scaling run at N = 4 and 8 rehearsed on the one GPU (gloo): the deal of the
+    frame's 64x64 tiles over N ranks, the launcher, and rank 0's assembled frame against a
+    single-context render (--verify)."""
+    r, out = _bench(["--gpus", str(n), "--dist-backend", "gloo", "--config", "c2", "--steps", "2",
+                     "--warmup", "1", "--verify", "--no-cpu-baseline"], timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert out is not None and out["n_gpus"] == n, r.stderr[-3000:]
+    assert out["verify"]["mismatches"] == 0 and out["config"]["chain_timeouts"] == 0
+    assert out["frames_per_launch"] == 8 * n
+
+
 def test_bench_secondary_block():
     """The primary line carries the secondary configs' measurements (C2 primary, C3t second)."""
     r, out = _bench(["--config", "c2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
