@@ -492,7 +492,7 @@ IRT_HD void slot_fill(const uint32_t *H, const float *fat, int u, int b, const f
     const uint32_t first = H[3] + beg + jU;
     for (int q = 0; q < 4 * kFat4; ++q) S[q] = fat[(size_t)first * 4 * kFatStride4 + q];
   }
-  S[16] = u2f(nx | (jU << 24));
+  S[16] = u2f((nx < 0xFFFFFFu ? nx : 0xFFFFFFu) | (jU << 24));  // 0xFFFFFF: too long (k_slot_fill drops the table)
   S[17] = u2f(H[3] + beg);
   S[18] = u2f(masks);
   S[19] = own ? up : __builtin_inff();

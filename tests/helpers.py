@@ -207,7 +207,7 @@ def restate_slots(hdr: np.ndarray, fat: np.ndarray, subs: int = 4) -> np.ndarray
             has = jU != 15
             first = H[:, 3] + beg + jU
             out[has, u, b, :16] = F[first[has]]
-            out[:, u, b, 16] = nx | (jU << 24)
+            out[:, u, b, 16] = np.minimum(nx, 0xFFFFFF) | (jU << 24)
             out[:, u, b, 17] = H[:, 3] + beg
             out[:, u, b, 18] = masks
             out[:, u, b, 19] = np.where(own, np.float32(up).view(np.uint32), INF)
