@@ -32,6 +32,12 @@ using namespace irt;
 
 // the split threshold of single frames of scenes with holes (irt_context::splitFactor)
 constexpr float kSplitFactorHoles = 0.35f;
+// A transfer function whose mean Woodcock samples per acceptance over the shell's macrocells
+// (k_accept_stat) is at least this is sparse: launches on a scene whose headers fit the
+// last-level cache then start their candidate scan from the slot table (built on the first such
+// TF), which the dense default TF does not pay for.  Quads on the C3 grid (2.0 GB): the comb TF
+// (32 samples per acceptance) -3.8 %, the default TF (1.3) +3.0 % (profiles/r06zl/).
+constexpr double kSparseTfSamples = 8.0;
 
 struct irt_context {
   int device = 0;
@@ -44,6 +50,11 @@ struct irt_context {
   float4 *d_fat = nullptr;
   float4 *d_blocks = nullptr;
   SlotTable slot;              // the slot table (irt_common.h kSlot4; IRT_SLOTS=0: none)
+  bool slotAlways = false;     // every launch starts its scan from it (large scenes, IRT_SLOTS=1)
+  bool slotLazy = false;       // a smaller scene builds it for a sparse transfer function
+  bool slotTried = false;      // a build was attempted (never again)
+  bool slotSparse = false;     // the current transfer function is sparse (kSparseTfSamples)
+  double tfSamples = 0.0;      // its mean Woodcock samples per acceptance (k_accept_stat)
   size_t binEntries = 0;       // fat entries
   uint32_t numSph = 0;         // zero-thickness records (spheres): distinct radii
   uint32_t numSphRec = 0;      // ... and records
@@ -658,7 +669,7 @@ int render_impl(irt_context *c, const irt_launch_params *lp, int W, int H, int p
   A.binHdr = c->d_binHdr;
   A.fat = c->d_fat;
   A.blocks = c->d_blocks;
-  A.slots = c->slot.slots;
+  A.slots = c->slotAlways || c->slotSparse ? c->slot.slots : nullptr;
   A.slotBins = c->slot.bins;
   A.slotSubs = c->slot.subs;
   for (int k = 0; k < 3; ++k) A.slotEdge[k] = c->slot.edges[k];
@@ -1082,6 +1093,43 @@ int irt_create_append(irt_context *c, const irt_icon_cell *cells, size_t n) {
   return append_chunk(c, cells, n, nullptr);
 }
 
+// The slot table of a built scene (irt_kernels.h build_slots_device), if its cells share their
+// radial edges and it fits: at most IRT_SLOTS_MAX_GB, half the device's memory and its free memory
+// less 16 GiB.  Sub-cells per slot unit (irt_common.h slot_unit): by default the finest unit -- 1
+// sub-cell, a pair or a quad -- whose table is at most the scene's own bytes (C5: quads, 32 GB
+// beside 38.7 GB of headers, entries and blocks); IRT_SLOT_SUBS=1, 2 or 4 asks for one.
+int build_slot_table(irt_context *c, bool forced) {
+  c->slotTried = true;
+  // the kernel's slot index (cell * kSubCells^2 + sub) is 32-bit
+  const bool indexable = (uint64_t)6 * c->G * c->G * kSubCells * kSubCells < ((uint64_t)1 << 32);
+  int slotSubs = 0;
+  if (const char *v = getenv("IRT_SLOT_SUBS")) slotSubs = atoi(v);
+  // the scene's own bytes: the locator and the records it indexes (headers, entries, blocks)
+  const size_t hdrBytes = (size_t)6 * c->G * c->G * kBinHdrWords * 4;
+  const size_t sceneBytes = hdrBytes + c->binEntries * kFatStride4 * 16 + (size_t)c->n * kBlk4 * 16;
+  size_t fr = 0, tot = 0;
+  IRT_HIP(hipMemGetInfo(&fr, &tot));
+  size_t cap = fr > ((size_t)16 << 30) ? fr - ((size_t)16 << 30) : 0;
+  cap = std::min(cap, tot / 2);
+  if (const char *g = getenv("IRT_SLOTS_MAX_GB")) cap = std::min(cap, (size_t)(atof(g) * (double)(1ull << 30)));
+  if (!indexable) {
+    c->slot = SlotTable{};
+    c->slot.skipped = "the cube map has 2^28 cells or more (32-bit slot index)";
+  } else if (int rc = build_slots_device(reinterpret_cast<const uint32_t *>(c->d_binHdr), c->d_fat, 6u * c->G * c->G,
+                                         cap, slotSubs, sceneBytes, c->stream, c->slot)) {
+    return rc;
+  }
+  c->bytes += c->slot.bytes;
+  c->info.deviceBytes = c->bytes;
+  if (c->slot.bytes)
+    fprintf(stderr, "icon_rt_hip: slot table built on device %d: %.1f GB of HBM, %d sub-cells per slot (IRT_SLOTS=0: none)\n",
+            c->device, c->slot.bytes / 1e9, c->slot.subs);
+  else if (forced)
+    fprintf(stderr, "icon_rt_hip: IRT_SLOTS=1 but no slot table was built: %s\n",
+            c->slot.skipped ? c->slot.skipped : "unknown reason");
+  return IRT_OK;
+}
+
 int irt_create_end(irt_context *c) {
   if (!c || !c->building) {
     set_error("irt_create_end: no context being created");
@@ -1133,41 +1181,18 @@ int irt_create_end(irt_context *c) {
   // the slot table, when the cells share their radial edges, their headers outgrow the
   // last-level cache (kSlotAutoHdrBytes) and it fits: at most IRT_SLOTS_MAX_GB, by default half
   // the device's memory and never more than its free memory less 16 GiB (a process sharing the
-  // GPU keeps the rest); IRT_SLOTS=1: whatever the headers' size, 0: none.  A built table is
-  // announced on stderr with its size; an explicit IRT_SLOTS=1 that builds none says why.
+  // GPU keeps the rest); IRT_SLOTS=1: whatever the headers' size, 0: none.  Without IRT_SLOTS a
+  // smaller scene gets it when a sparse transfer function is set (irt_set_transfunc).  A built
+  // table is announced on stderr with its size; an explicit IRT_SLOTS=1 that builds none says why.
   {
     const char *e = getenv("IRT_SLOTS");
     const bool forced = e && atoi(e) != 0;
+    const char *sp = getenv("IRT_SLOTS_SPARSE_TF");  // 0: not for sparse transfer functions either
+    c->slotLazy = !e && (!sp || atoi(sp) != 0);
     const size_t hdrBytes = (size_t)6 * c->G * c->G * kBinHdrWords * 4;
-    // the kernel's slot index (cell * kSubCells^2 + sub) is 32-bit
-    const bool indexable = (uint64_t)6 * c->G * c->G * kSubCells * kSubCells < ((uint64_t)1 << 32);
-    // sub-cells per slot unit (irt_common.h slot_unit): by default the finest unit -- 1 sub-cell,
-    // a pair or a quad -- whose table is at most the scene's own bytes (C5: quads, 32 GB beside
-    // 38.7 GB of headers, entries and blocks); IRT_SLOT_SUBS=1, 2 or 4 asks for one
-    int slotSubs = 0;
-    if (const char *v = getenv("IRT_SLOT_SUBS")) slotSubs = atoi(v);
-    // the scene's own bytes: the locator and the records it indexes (headers, entries, blocks)
-    const size_t sceneBytes = hdrBytes + c->binEntries * kFatStride4 * 16 + (size_t)c->n * kBlk4 * 16;
     if (e ? forced : hdrBytes > kSlotAutoHdrBytes) {
-      size_t fr = 0, tot = 0;
-      IRT_HIP(hipMemGetInfo(&fr, &tot));
-      size_t cap = fr > ((size_t)16 << 30) ? fr - ((size_t)16 << 30) : 0;
-      cap = std::min(cap, tot / 2);
-      if (const char *g = getenv("IRT_SLOTS_MAX_GB")) cap = std::min(cap, (size_t)(atof(g) * (double)(1ull << 30)));
-      if (!indexable) {
-        c->slot = SlotTable{};
-        c->slot.skipped = "the cube map has 2^28 cells or more (32-bit slot index)";
-      } else if ((rc = build_slots_device(reinterpret_cast<const uint32_t *>(c->d_binHdr), c->d_fat,
-                                          6u * c->G * c->G, cap, slotSubs, sceneBytes, c->stream, c->slot))) {
-        return rc;
-      }
-      c->bytes += c->slot.bytes;
-      if (c->slot.bytes)
-        fprintf(stderr, "icon_rt_hip: slot table built on device %d: %.1f GB of HBM, %d sub-cells per slot (IRT_SLOTS=0: none)\n",
-                c->device, c->slot.bytes / 1e9, c->slot.subs);
-      else if (forced)
-        fprintf(stderr, "icon_rt_hip: IRT_SLOTS=1 but no slot table was built: %s\n",
-                c->slot.skipped ? c->slot.skipped : "unknown reason");
+      if ((rc = build_slot_table(c, forced))) return rc;
+      c->slotAlways = c->slot.slots != nullptr;
     }
   }
   mark("slot table");
@@ -1453,6 +1478,31 @@ int irt_set_transfunc(irt_context *c, const irt_vec4f *lut, int size, irt_box1f 
     launch_grid_bits(c->d_gridMaxOp, c->d_gridBits, c->stream);
   }
   IRT_HIP(hipGetLastError());
+  // a sparse transfer function (many samples per acceptance) on a scene whose table is not used
+  // by every launch: the slot table, built on the first such TF (irt_context::slotSparse)
+  c->slotSparse = false;
+  if (!c->slotAlways && (c->slot.slots || (c->slotLazy && !c->slotTried)) && c->numMCs > 0) {
+    double *d_stat = nullptr;
+    IRT_HIP(hipMalloc((void **)&d_stat, 2 * sizeof(double)));
+    double h[2] = {0.0, 0.0};
+    hipError_t err = hipMemsetAsync(d_stat, 0, 2 * sizeof(double), c->stream);
+    if (err == hipSuccess) {
+      launch_accept_stat(c->d_valueRanges, c->d_maxOp, c->numMCs, c->d_lut, size, valueRange.lower,
+                         valueRange.upper, d_stat, c->stream);
+      err = hipMemcpyAsync(h, d_stat, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+    }
+    if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_stat);
+    IRT_HIP(err);
+    c->tfSamples = h[1] > 0.0 ? h[0] / h[1] : 0.0;
+    if (c->tfSamples >= kSparseTfSamples) {
+      if (!c->slot.slots && !c->slotTried) {
+        int rc = build_slot_table(c, false);
+        if (rc) return rc;
+      }
+      c->slotSparse = c->slot.slots != nullptr;
+    }
+  }
   IRT_HIP(hipStreamSynchronize(c->stream));
   c->tfSet = true;
   c->info.deviceBytes = c->bytes;
@@ -1936,6 +1986,14 @@ extern "C" int irt_debug_counters(irt_context *c, unsigned long long *out16) {
 }
 
 extern "C" int irt_debug_default_variant(void) { return kDefaultVariant; }
+// 1 when the context's launches start their candidate scan from the slot table (the OPT_SLOT
+// kernels), 0 otherwise; -1 without a context.  *tfSamples (if given): the current transfer
+// function's mean Woodcock samples per acceptance (k_accept_stat; 0 when not computed).
+extern "C" int irt_debug_slot_use(const irt_context *c, double *tfSamples) {
+  if (!c) return -1;
+  if (tfSamples) *tfSamples = c->tfSamples;
+  return c->slot.slots && (c->slotAlways || c->slotSparse) ? 1 : 0;
+}
 
 extern "C" int irt_debug_context_array(const irt_context *c, int which, void *dst, size_t capacity,
                                        size_t *bytes) {

@@ -206,6 +206,10 @@ void launch_shell_build(const irt_icon_cell *cells, size_t n, int3 dims, float3 
 void launch_grid_build(const float4 *blocks, const uint32_t *meta, const float4 *trig, size_t n,
                        float3 lo, float3 hi, float *valueRanges, hipStream_t s);
 void launch_grid_bits(const float *maxOp, uint32_t *bits, hipStream_t s);
+// the TF's mean Woodcock samples per acceptance over the macrocells: out[0] += sum, out[1] += count
+// (k_accept_stat, irt_kernels.hip)
+void launch_accept_stat(const float *valueRanges, const float *maxOp, size_t numMCs, const float4 *lut, int size,
+                        float lo, float hi, double *out, hipStream_t s);
 void launch_max_opacities(const float *valueRanges, size_t numMCs, const float4 *lut, int size,
                           float lo, float hi, float *maxOp, hipStream_t s);
 void launch_clear(uint32_t *fb, float4 *accum, size_t n, hipStream_t s);

@@ -300,6 +300,49 @@ __global__ void k_max_opacities(const float2 *valueRanges, size_t numMCs, const 
   maxOp[mc] = m;
 }
 
+// The transfer function's expected Woodcock samples per acceptance, over the shell's macrocells
+// with a positive majorant: per macrocell 1 / p, p = the mean LUT alpha over its value range's
+// entries (the range k_max_opacities scans) over the majorant -- postClassify's alpha against the
+// majorant, deviceCode.cu:174-176 -- capped at 1000; out[0] += sum, out[1] += count (one atomic
+// pair per workgroup).  A dense TF (the reference's default: ~1.3) takes about one located sample
+// per ray, a sparse one many (bench.py's comb: ~32), which decides whether launches start their
+// candidate scan from the slot table (irt_context.hip).
+__global__ void k_accept_stat(const float2 *valueRanges, const float *maxOp, size_t numMCs, const float4 *lut,
+                              int size, float tfLo, float tfHi, double *out) {
+  __shared__ double s_sum[256];
+  __shared__ double s_cnt[256];
+  const size_t mc = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  double inv = 0.0, cnt = 0.0;
+  if (mc < numMCs && maxOp[mc] > 0.f) {
+    float2 vr = valueRanges[mc];
+    vr.x = (vr.x - tfLo) / (tfHi - tfLo);
+    vr.y = (vr.y - tfLo) / (tfHi - tfLo);
+    int lo = f2i_x86(vr.x * (float)(size - 1));
+    int hi = (int)((uint32_t)f2i_x86(vr.y * (float)(size - 1)) + 1u);
+    lo = lo < 0 ? 0 : (lo > size - 1 ? size - 1 : lo);
+    hi = hi < 0 ? 0 : (hi > size - 1 ? size - 1 : hi);
+    float a = 0.f;
+    for (int i = lo; i <= hi; ++i) a += lut[i].w;
+    const float p = a / (float)(hi - lo + 1) / maxOp[mc];
+    inv = p > 1e-3f ? 1.0 / (double)p : 1000.0;
+    cnt = 1.0;
+  }
+  s_sum[threadIdx.x] = inv;
+  s_cnt[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      s_sum[threadIdx.x] += s_sum[threadIdx.x + w];
+      s_cnt[threadIdx.x] += s_cnt[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && s_cnt[0] > 0.0) {
+    atomicAdd(&out[0], s_sum[0]);
+    atomicAdd(&out[1], s_cnt[0]);
+  }
+}
+
 // clearFramebuffer (common/pipeline.cu:171-199)
 __global__ void k_clear(uint32_t *fb, float4 *accum, size_t n) {
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -441,6 +484,11 @@ void launch_max_opacities(const float *vr, size_t numMCs, const float4 *lut, int
                           float hi, float *maxOp, hipStream_t s) {
   hipLaunchKernelGGL(k_max_opacities, dim3((unsigned)((numMCs + 255) / 256)), dim3(256), 0, s,
                      (const float2 *)vr, numMCs, lut, size, lo, hi, maxOp);
+}
+void launch_accept_stat(const float *vr, const float *maxOp, size_t numMCs, const float4 *lut, int size, float lo,
+                        float hi, double *out, hipStream_t s) {
+  hipLaunchKernelGGL(k_accept_stat, dim3((unsigned)((numMCs + 255) / 256)), dim3(256), 0, s,
+                     (const float2 *)vr, maxOp, numMCs, lut, size, lo, hi, out);
 }
 void launch_stats_out(const unsigned long long *cur, unsigned long long *host,
                       unsigned long long *next, unsigned long long *buckets, hipStream_t s) {

@@ -237,14 +237,15 @@ def default_kernel_id(ctx=None) -> int:
     """Template id of the raygen kernel (k_render<id>, as rocprofv3 names it) that `ctx`
     launches -- the default variant, its hole-free form (bit 262144) on scenes without holes
     or its located-mode void walk (bit 1073741824) on scenes with holes, with bit 128 (OPT_SLOT)
-    where the scene has a slot table -- or, without a context,
+    where the launches use the slot table (irt_debug_slot_use) -- or, without a context,
     that of the default variant."""
     L = lib()
     if ctx is not None:
         L.irt_debug_get_variant.argtypes = [C.c_void_p]
         v = int(L.irt_debug_get_variant(ctx._h)) & ~4096
         d = int(L.irt_debug_default_variant())
-        if v in ((d & ~4096), (d | 262144) & ~4096, (d | 1073741824) & ~4096) and ctx.array_bytes("slots"):
+        L.irt_debug_slot_use.argtypes = [C.c_void_p, C.c_void_p]
+        if v in ((d & ~4096), (d | 262144) & ~4096, (d | 1073741824) & ~4096) and L.irt_debug_slot_use(ctx._h, None) == 1:
             v |= 128  # kernel_for: the default kernels' OPT_SLOT form
         return v
     return int(L.irt_debug_default_variant()) & ~4096  # OPT_MONO: one kernel per frame

@@ -91,6 +91,12 @@ int irt_debug_scene_array(const irt_debug_scene *s, int which, void *dst, size_t
 int irt_debug_set_variant(irt_context *ctx, int variant);
 /* The variant a new context launches (IRT_RENDER_VARIANT overrides it per context). */
 int irt_debug_default_variant(void);
+/* 1 when the context's launches start their candidate scan from the slot table (the OPT_SLOT
+ * kernels: every launch on scenes whose headers outgrow the last-level cache or with IRT_SLOTS=1;
+ * otherwise while a sparse transfer function is set), 0 otherwise, -1 without a context.
+ * *tfSamples (if not null): the transfer function's mean Woodcock samples per acceptance over the
+ * shell's macrocells, the measure of "sparse" (>= 8; 0 when it was not computed). */
+int irt_debug_slot_use(const irt_context *ctx, double *tfSamples);
 /* The variant this context launches: the default on scenes with holes (columns starting at
  * different radii, as convert_icon's terrain does, or gaps inside columns: the raygen's miss
  * mode), the default | 262144 (no miss mode) on scenes without, unless IRT_RENDER_VARIANT or

@@ -123,3 +123,47 @@ def test_frames_equal_without_table(monkeypatch, bis, levels, batch, subs):
         assert got[k][2] == ref[k][2], k
     ref_ctx.close()
     ctx.close()
+
+
+def _comb(lut):
+    """bench.py's sparse "comb" TF: alpha 0.01, every 50th entry 1.0"""
+    lut = np.array(lut, dtype=np.float32, copy=True)
+    lut[:, 3] = 0.01
+    lut[::50, 3] = 1.0
+    return lut
+
+
+def test_sparse_transfer_function_uses_the_table(monkeypatch):
+    """A scene whose headers fit the last-level cache builds the table on its first sparse TF
+    (mean Woodcock samples per acceptance >= 8) and its launches start from it while that TF is
+    set; the dense default TF does not use it.  Frames and counts equal a context without the
+    table either way."""
+    import ctypes as C
+    monkeypatch.delenv("IRT_SLOTS", raising=False)
+    monkeypatch.delenv("IRT_SLOT_SUBS", raising=False)
+    cells = irt.synth_grid(2, 4, 90)
+    W = 256
+    setup = irt.setup_frame(cells, W, W, camera=FRAMING)
+    L = irt.lib()
+    L.irt_debug_slot_use.argtypes = [C.c_void_p, C.c_void_p]
+    ctx = irt.Context(cells, 0)
+    monkeypatch.setenv("IRT_SLOTS", "0")
+    ref = irt.Context(cells, 0)
+    monkeypatch.delenv("IRT_SLOTS")
+    samples = C.c_double()
+    ctx.set_transfunc(setup.lut, setup.value_range)
+    assert L.irt_debug_slot_use(ctx._h, C.byref(samples)) == 0 and 0 < samples.value < 8
+    assert ctx.array("slots").size == 0  # not built for a dense TF
+    comb = _comb(setup.lut)
+    for c in (ctx, ref):
+        c.set_transfunc(comb, setup.value_range)
+    assert L.irt_debug_slot_use(ctx._h, C.byref(samples)) == 1 and samples.value >= 8
+    assert ctx.array("slots").size > 0 and L.irt_debug_slot_use(ref._h, None) == 0
+    a, b = _frames(ctx, setup.lp, W, 4, 2), _frames(ref, setup.lp, W, 4, 2)
+    for k in range(len(a)):
+        assert np.array_equal(a[k][0], b[k][0]) and np.array_equal(a[k][1], b[k][1]) and a[k][2] == b[k][2], k
+    ctx.set_transfunc(setup.lut, setup.value_range)  # dense again: the table stays, unused
+    assert L.irt_debug_slot_use(ctx._h, None) == 0 and ctx.array("slots").size > 0
+    ctx.close()
+    ref.close()
+
