@@ -89,7 +89,7 @@ def outcome_stats(packets):
     return {"samples": n, "mode_switches": switches, "run_hist_capped16": hist}
 
 
-def simulate(packets, rule="kernel", voidwalk=True, maxlg0=0, ramp=1):
+def simulate(packets, rule="kernel", voidwalk=True, maxlg0=0, ramp=1, groupwalk=False, cap=32):
     """Rounds per wave of Tracer::woodcock_wave over the traced outcomes.  A wave runs its
     rays' counted calls in wave calls: every ray with a call pending joins; the wave call runs
     rounds until each joined ray's call is decided.  rule "kernel": a group's lanes assume all
@@ -135,10 +135,18 @@ def simulate(packets, rule="kernel", voidwalk=True, maxlg0=0, ramp=1):
                         continue
                     if voidwalk and G == 1 and miss[i]:
                         p0 = p
-                        while p < len(c) and c[p] == "m":
+                        while p < len(c) and c[p] == "m" and p - p0 < cap:
                             p += 1
                         walk_round = max(walk_round, p - p0)
                     adv, done, sw = advance(c, p, G, miss[i])
+                    if groupwalk and G > 1 and miss[i] and adv == G and not done and not sw:
+                        # the group's last lane walks on through the void (all G samples missed)
+                        q0 = p + adv
+                        q = q0
+                        while q < len(c) and c[q] == "m" and q - q0 < cap:
+                            q += 1
+                        walk_round = max(walk_round, q - q0)
+                        adv += q - q0
                     pos[i] = p + adv
                     if done:
                         live.discard(i)
@@ -188,7 +196,8 @@ def main():
         packets = traces(args.config, args.step, stride=args.stride)
     res = {"config": args.config, "packets": len(packets)}
     res.update(outcome_stats(packets))
-    for name, kw in (("kernel", {}), ("kernel_novoid", {"voidwalk": False}), ("both", {"rule": "both"})):
+    for name, kw in (("kernel", {}), ("kernel_novoid", {"voidwalk": False}), ("both", {"rule": "both"}),
+                     ("groupwalk", {"groupwalk": True})):
         r = simulate(packets, **kw)
         res["rounds_" + name] = {"mean": float(r.mean()), "p50": float(np.median(r)),
                                  "p90": float(np.percentile(r, 90)), "max": int(r.max()),
