@@ -55,6 +55,7 @@ struct irt_context {
   bool slotTried = false;      // a build was attempted (never again)
   bool slotSparse = false;     // the current transfer function is sparse (kSparseTfSamples)
   double tfSamples = 0.0;      // its mean Woodcock samples per acceptance (k_accept_stat)
+  double *d_tfStat = nullptr;  // k_accept_stat's sum and count
   size_t binEntries = 0;       // fat entries
   uint32_t numSph = 0;         // zero-thickness records (spheres): distinct radii
   uint32_t numSphRec = 0;      // ... and records
@@ -258,7 +259,7 @@ void free_all(irt_context *c) {
   void *ptrs[] = {c->d_binHdr, c->d_fat, c->slot.slots, c->d_blocks, c->d_sphR, c->d_sphOff, c->d_sphRec,
                   c->d_sphBits, c->d_samples, c->d_maxOp, c->d_gridVR, c->d_gridMaxOp, c->d_gridBits, c->d_wOff, c->d_wRec, c->d_wBox, c->d_wTrig, c->d_schedOrder, c->d_schedCost, c->d_srgb, c->d_valueRanges,
                   c->d_lut, c->d_counters, c->d_counterBuckets, c->d_meta, c->d_queue, c->d_chainFlag,
-                  c->d_frameCams};
+                  c->d_frameCams, c->d_tfStat};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->d_cells) (void)hipFree(c->d_cells);
@@ -1482,18 +1483,17 @@ int irt_set_transfunc(irt_context *c, const irt_vec4f *lut, int size, irt_box1f 
   // by every launch: the slot table, built on the first such TF (irt_context::slotSparse)
   c->slotSparse = false;
   if (!c->slotAlways && (c->slot.slots || (c->slotLazy && !c->slotTried)) && c->numMCs > 0) {
-    double *d_stat = nullptr;
-    IRT_HIP(hipMalloc((void **)&d_stat, 2 * sizeof(double)));
-    double h[2] = {0.0, 0.0};
-    hipError_t err = hipMemsetAsync(d_stat, 0, 2 * sizeof(double), c->stream);
-    if (err == hipSuccess) {
-      launch_accept_stat(c->d_valueRanges, c->d_maxOp, c->numMCs, c->d_lut, size, valueRange.lower,
-                         valueRange.upper, d_stat, c->stream);
-      err = hipMemcpyAsync(h, d_stat, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+    if (!c->d_tfStat) {  // once per context (a hipFree per TF change would synchronise the device)
+      int rc = dalloc(c, &c->d_tfStat, 2);
+      if (rc) return rc;
     }
-    if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
-    (void)hipFree(d_stat);
-    IRT_HIP(err);
+    double h[2] = {0.0, 0.0};
+    IRT_HIP(hipMemsetAsync(c->d_tfStat, 0, 2 * sizeof(double), c->stream));
+    launch_accept_stat(c->d_valueRanges, c->d_maxOp, c->numMCs, c->d_lut, size, valueRange.lower,
+                       valueRange.upper, c->d_tfStat, c->stream);
+    IRT_HIP(hipGetLastError());
+    IRT_HIP(hipMemcpyAsync(h, c->d_tfStat, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    IRT_HIP(hipStreamSynchronize(c->stream));
     c->tfSamples = h[1] > 0.0 ? h[0] / h[1] : 0.0;
     if (c->tfSamples >= kSparseTfSamples) {
       if (!c->slot.slots && !c->slotTried) {
